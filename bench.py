@@ -1,0 +1,238 @@
+"""bench.py — segments fitted per second, MI355X DFMI NLS readout (BASELINE.json metric).
+
+One step = one pass of the hot path (StandardNLSFitter._fit_parallel semantics,
+fitters.py:395-428) over one batch of synthetic input resident in HBM:
+demodulation of every segment, the seed LM fit of buffer 0, and the LM fits of
+all remaining segments seeded from it — i.e. (amp, m, phi, psi, dc, ssq, fitok)
+for every segment. Workload at N=1: BASELINE config 2 — 100,000 segments of
+R = 4000 samples (200 kS/s, f_mod = 1 kHz, n = 20), ndata = 10, fp64.
+
+Multi-GPU (torchrun, one process per GPU): every rank owns a contiguous shard of
+`--segments` segments of one long record (weak scaling, no data-path collective);
+each rank also demodulates/fits the record's buffer 0 to get the seed, exactly
+what every reference Pool worker receives. Timing: barrier + synchronize on both
+sides of exactly K steps, MAX over ranks (all_reduce MAX of the elapsed time).
+
+Extra JSON fields: roofline (demod kernel, HIP events on the launch stream),
+cpu_baseline (oracle restatement of _fit_parallel with a Pool on the host's
+cores, rank 0 at N=1 only, bounded sample), parity (max |dphi| of the GPU vs that
+oracle on the same sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "segments fitted/sec (m,phi,psi,amp) @200 kS/s, 1/2/4/8 GPU; max|Δphi| vs ref"
+F_SAMP, F_MOD, N_CYC, NDATA = 200000.0, 1000.0, 20, 10
+M_TRUE, SNR_DB = 6.0, 40.0
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--segments", type=int, default=100_000, help="segments per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=8000, help="segments in the CPU-baseline sample")
+    ap.add_argument("--cpu-procs", type=int, default=16, help="Pool size of the CPU baseline (box share: 16)")
+    ap.add_argument("--demod-only", action="store_true", help="profile helper: time only the demod kernel")
+    return ap.parse_args()
+
+
+def gen_shard(torch, dev, seg0, nseg, R, seed, chunk=8192):
+    """snr-mode signal (physics.py:493-530 formula) for global segments [seg0, seg0+nseg)
+    generated on the device: y = 1 + cos(m cos(w t)), white noise at SNR_DB."""
+    x = torch.empty(nseg * R, dtype=torch.float64, device=dev)
+    w = 2 * np.pi * F_MOD
+    # noise power from the (periodic) clean signal power: mean((y - mean y)^2)
+    t1 = torch.arange(R, dtype=torch.float64, device=dev) / F_SAMP
+    y1 = 1.0 + torch.cos(M_TRUE * torch.cos(w * t1))
+    std = float(torch.sqrt(((y1 - y1.mean()) ** 2).mean() / 10 ** (SNR_DB / 10.0)))
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    for s in range(0, nseg, chunk):
+        n = min(chunk, nseg - s)
+        t = (torch.arange(n * R, dtype=torch.float64, device=dev) + float((seg0 + s) * R)) / F_SAMP
+        y = 1.0 + torch.cos(M_TRUE * torch.cos(w * t))
+        y += std * torch.randn(n * R, dtype=torch.float64, device=dev, generator=g)
+        x[s * R:(s + n) * R] = y
+    return x
+
+
+def cpu_baseline(args):
+    """Oracle restatement of StandardNLSFitter._fit_parallel (Pool over np.array_split
+    chunks, fitters.py:395-428) timed on this host. Runs BEFORE the GPU is touched
+    (the Pool forks). Returns the sample, the oracle result and the baseline record."""
+    from multiprocessing import get_context
+
+    import deepfmkit_amd as dfm
+    from oracle import nls_oracle as O
+
+    R = int(F_SAMP / F_MOD * N_CYC)
+    nseg = args.cpu_sample
+    laser, ifo = dfm.LaserConfig(), dfm.InterferometerConfig()
+    dfm.set_laser_df_for_effect(laser, ifo, M_TRUE)
+    sim = dfm.DFMIObject("cpu", laser, ifo, f_samp=F_SAMP)
+    raw = dfm.SignalGenerator().generate(sim, nseg * R / F_SAMP, mode="snr", snr_db=SNR_DB, trial_num=0)["main"]
+    x = raw.samples()
+    procs = max(1, min(args.cpu_procs, os.cpu_count() or 1))
+    with get_context("fork").Pool(procs) as pool:
+        O.fit_record_parallel(x[: 4 * R * procs], F_SAMP, F_MOD, N_CYC, n_cores=procs, pool=pool)  # warm
+        t0 = time.perf_counter()
+        ref = O.fit_record_parallel(x, F_SAMP, F_MOD, N_CYC, n_cores=procs, pool=pool)
+        dt = time.perf_counter() - t0
+    base = {"value": round(nseg / dt, 1), "unit": "segments/s", "cores": procs, "kind": "port",
+            "sample": f"{nseg} segments of config 2 (R=4000, ndata=10, m=6, 40 dB), numpy restatement of "
+                      f"StandardNLSFitter._fit_parallel with multiprocessing.Pool({procs}); {dt:.2f} s wall"}
+    return raw, ref, procs, base
+
+
+def parity_vs_oracle(df, ref):
+    st_ok = (df["fitok"].to_numpy() == ref[:, 6]) & (ref[:, 6] == 0)
+    dphi = np.abs((df["phi"].to_numpy() - ref[:, 2] + np.pi) % (2 * np.pi) - np.pi)[st_ok]
+    dm = np.abs(df["m"].to_numpy() - ref[:, 1])[st_ok]
+    da = np.abs(df["amp"].to_numpy() - ref[:, 0])[st_ok]
+    dpsi = np.abs(df["psi"].to_numpy() - ref[:, 3])[st_ok]
+    return {"segments": int(ref.shape[0]), "max_dphi": float(dphi.max()), "max_dm": float(dm.max()),
+            "max_damp": float(da.max()), "max_dpsi": float(dpsi.max()),
+            "status_match": float(np.mean(df["fitok"].to_numpy() == ref[:, 6])),
+            "vs": "oracle restatement of fit.py/fitters.py, pinned to the reference by tests/golden"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    want_base = rank == 0 and world == 1 and not args.no_cpu_baseline and not args.demod_only
+    pre = cpu_baseline(args) if want_base else None
+    if world > 1:
+        dist.init_process_group("gloo" if not torch.cuda.is_available() else "nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from deepfmkit_amd import _lib
+    from deepfmkit_amd import fit as F
+    from deepfmkit_amd.fitters import StandardNLSFitter, w0_of
+
+    lib = _lib.load()
+    R = int(F_SAMP / F_MOD * N_CYC)
+    nseg = args.segments
+    seg0 = rank * nseg
+    # rank 0's shard starts with the record's buffer 0; the others prepend it (the seed)
+    body = gen_shard(torch, dev, seg0, nseg, R, seed=1234 + rank)
+    if rank == 0:
+        x = body
+        nbuf = nseg
+    else:
+        head = gen_shard(torch, dev, 0, 1, R, seed=1234)
+        x = torch.cat([head, body])
+        nbuf = nseg + 1
+        del head
+    del body
+    torch.cuda.synchronize()
+    w0 = w0_of(F_MOD, F_SAMP)
+    cfg = F.lm_config()
+    guess = np.array([1.6, 6.0, 0.0, 0.0])
+    out = torch.empty((6, nbuf), dtype=torch.float64, device=dev)
+    ok = torch.empty(nbuf, dtype=torch.int32, device=dev)
+    qi = torch.empty((2 * NDATA, nbuf), dtype=torch.float64, device=dev)
+    dcb = torch.empty(nbuf, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        rc = lib.dfmi_nls_record(x.data_ptr(), 1, nbuf * R, nbuf, R, NDATA, w0, 0, _lib.ptr(guess), 1, nbuf - 1,
+                                 cfg, out.data_ptr(), ok.data_ptr(), _lib.DFMI_MEM_DEVICE, stream.cuda_stream)
+        _lib.check(rc, "dfmi_nls_record")
+
+    def demod():
+        rc = lib.dfmi_demod(x.data_ptr(), nbuf, R, R, NDATA, w0, 0, qi.data_ptr(), dcb.data_ptr(),
+                            _lib.DFMI_MEM_DEVICE, stream.cuda_stream)
+        _lib.check(rc, "dfmi_demod")
+
+    fn = demod if args.demod_only else step
+    for _ in range(args.warmup):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    ms = el / args.steps * 1e3
+    total_segments = nseg * world  # units of work; the seed replicas on ranks > 0 are not counted
+    value = total_segments * args.steps / el
+
+    # ---- roofline of the dominant kernel (demod), HIP events on the launch stream ----
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    demod()
+    nrep = max(5, args.steps)
+    ev0.record(stream)
+    for _ in range(nrep):
+        demod()
+    ev1.record(stream)
+    ev1.synchronize()
+    demod_ms = ev0.elapsed_time(ev1) / nrep
+    bytes_per_seg = 8 * R + 8 * (2 * NDATA + 1)  # read the segment, write QI + dc
+    achieved = nbuf * bytes_per_seg / (demod_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_demod_r01.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+    roof = {"kernel": "demod_fold_kernel<2,2,true>", "bound": "hbm", "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "avg_launch_ms": round(demod_ms, 4), "algorithmic_bytes_per_launch": nbuf * bytes_per_seg}
+
+    # parity on the timed batch itself: status-0 fraction and a sanity check of the estimates
+    st = ok.cpu().numpy()
+    res = out.cpu().numpy()
+
+    line = {"metric": METRIC, "value": round(value, 1), "unit": "segments/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic snr-mode DFMI (m=6, 40 dB white noise) generated on device",
+            "config": {"workload": f"config2: {nseg} segments/GPU x R={R} @200 kS/s, ndata={NDATA}, 1 channel, "
+                                   f"_fit_parallel chunk size 1",
+                       "segments_per_gpu": nseg, "R": R, "ndata": NDATA, "parallelism": f"shard{world}"},
+            "roofline": roof,
+            "batch_status0_frac": float(np.mean(st == 0)),
+            "batch_m_mean": float(res[1].mean())}
+    if args.demod_only:
+        line["metric"] = "demod only (profile helper)"
+    if pre is not None:
+        raw, ref, procs, base = pre
+        df = StandardNLSFitter({"n": N_CYC}).fit(raw, parallel=True, n_cores=procs)  # same chunking, on GPU
+        line["cpu_baseline"] = base
+        line["parity"] = parity_vs_oracle(df, ref)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

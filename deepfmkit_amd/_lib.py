@@ -1,0 +1,98 @@
+"""ctypes binding of libdfmi.so (the C ABI in include/dfmi.h).
+
+The library is built in-tree (deepfmkit_amd/libdfmi.so, see __graft_entry__.build
+or `make -C deepfmkit_amd`). There is NO CPU fallback: if the library or a GPU
+is missing, every compute call raises DFMIError.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdfmi.so")
+
+DFMI_MEM_HOST = 0
+DFMI_MEM_DEVICE = 1
+MAX_LAMBDA = 16
+
+SYMBOLS = ("dfmi_lm_config_default", "dfmi_demod", "dfmi_lm", "dfmi_nls_record", "dfmi_ekf",
+           "dfmi_detect_period", "dfmi_device_count", "dfmi_last_error", "dfmi_version")
+
+
+class DFMIError(RuntimeError):
+    pass
+
+
+class LMConfig(ctypes.Structure):
+    """Mirror of dfmi_lm_config (include/dfmi.h)."""
+    _fields_ = [
+        ("max_lma_steps", ctypes.c_int32),
+        ("n_lambda", ctypes.c_int32),
+        ("lambdas", ctypes.c_double * MAX_LAMBDA),
+        ("min_step_norm", ctypes.c_double),
+        ("conv_improve", ctypes.c_double),
+        ("conv_param_change", ctypes.c_double),
+        ("fitok_threshold", ctypes.c_double),
+        ("m_grid_min", ctypes.c_double),
+        ("m_grid_max", ctypes.c_double),
+        ("m_grid_step", ctypes.c_double),
+        ("bessel_amp_threshold", ctypes.c_double),
+        ("sincos_amp_threshold", ctypes.c_double),
+    ]
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load():
+    """Load libdfmi.so once (lazy: HIP itself is initialised on the first compute call)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise DFMIError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        lib = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        i64, i32, dbl = ctypes.c_int64, ctypes.c_int32, ctypes.c_double
+        lib.dfmi_lm_config_default.argtypes = [ctypes.POINTER(LMConfig)]
+        lib.dfmi_lm_config_default.restype = None
+        lib.dfmi_demod.argtypes = [P, i64, i64, i32, i32, dbl, i32, P, P, i32, P]
+        lib.dfmi_demod.restype = ctypes.c_int
+        lib.dfmi_lm.argtypes = [P, i64, i32, P, i32, i64, ctypes.POINTER(LMConfig), P, P, P, i32, P]
+        lib.dfmi_lm.restype = ctypes.c_int
+        lib.dfmi_nls_record.argtypes = [P, i64, i64, i64, i32, i32, dbl, i32, P, i32, i64,
+                                        ctypes.POINTER(LMConfig), P, P, i32, P]
+        lib.dfmi_nls_record.restype = ctypes.c_int
+        lib.dfmi_ekf.argtypes = [P, i64, i64, i64, P, P, P, P, dbl, dbl, i32, i64, P, i32, P]
+        lib.dfmi_ekf.restype = ctypes.c_int
+        lib.dfmi_detect_period.argtypes = [dbl, i32, i32]
+        lib.dfmi_detect_period.restype = i32
+        lib.dfmi_device_count.argtypes = []
+        lib.dfmi_device_count.restype = ctypes.c_int
+        lib.dfmi_last_error.argtypes = []
+        lib.dfmi_last_error.restype = ctypes.c_char_p
+        lib.dfmi_version.argtypes = []
+        lib.dfmi_version.restype = ctypes.c_char_p
+        _lib = lib
+        return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load().dfmi_last_error().decode(errors="replace")
+        raise DFMIError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(a):
+    """Raw pointer of a numpy array or a torch tensor (data_ptr)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return a.data_ptr()

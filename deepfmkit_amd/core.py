@@ -1,0 +1,217 @@
+"""DeepFitFramework — the reference's drop-in facade (core.py:22-588), hot-path subset.
+
+Kept: the containers (raws, sims, fits, fits_df), simulate (snr mode; asd mode
+for zero/white noise), new_sim / load_sim, create_witness_channel, fit_init,
+fit (strategy dispatch, tau column, DeepFitObject), and fit_many — several
+equal-length channels fitted as ONE GPU batch (config 3).
+
+Out of scope (SURVEY.md §2 "OUT"): file loaders, LPSD, plotting.
+"""
+from __future__ import annotations
+
+import logging
+import time
+
+import numpy as np
+import scipy.constants as sc
+
+from . import fitters as _fitters
+from .data import DeepFitObject
+from .physics import DFMIObject, InterferometerConfig, SignalGenerator
+
+log = logging.getLogger(__name__)
+
+
+def vectorized_downsample(signal, R):
+    """dsp.py:3-55: boxcar mean over blocks of R (used for phi_sim only)."""
+    if not isinstance(R, int) or R <= 0:
+        return np.array([])
+    signal = np.asarray(signal)
+    n = (len(signal) // R) * R
+    if n == 0:
+        return np.array([])
+    return signal[:n].reshape(-1, R).mean(axis=1)
+
+
+class DeepFitFramework:
+    def __init__(self, raw_file=None, fit_file=None, raw_labels=None, fit_labels=None):
+        self.raw_file = raw_file
+        self.fit_file = fit_file
+        self.lasers = {}
+        self.ifos = {}
+        self.sims = {}
+        self.raws = {}
+        self.fits = {}
+        self.fits_df = {}
+        self.channr = None
+        self.n = None
+        self.t0 = None
+        self.R = None
+        self.fs = None
+        self.f_samp = None
+        self.f_mod = None
+        self.ndata = 10
+        self.init_a = 1.6
+        self.init_m = 6.0
+        if raw_file is not None or fit_file is not None:
+            raise NotImplementedError("raw/fit file loaders are outside the readout engine's scope")
+
+    # --- simulation ---------------------------------------------------------
+    def load_sim(self, sim):
+        self.sims[sim.label] = sim
+
+    def new_sim(self, label=None):
+        if label is None:
+            from datetime import datetime
+            label = datetime.now().strftime("%Y%m%d_%H%M%S")
+        from .physics import LaserConfig
+        sim = DFMIObject(label=label, laser_config=LaserConfig(), ifo_config=InterferometerConfig())
+        self.sims[sim.label] = sim
+        return label
+
+    def simulate(self, main_label, n_seconds, mode="asd", witness_label=None, snr_db=None, trial_num=0,
+                 verbose=False):
+        """core.py:176-243."""
+        t0 = time.time()
+        if main_label not in self.sims:
+            log.error(f"Main simulation label '{main_label}' not found!")
+            return
+        main_config = self.sims[main_label]
+        witness_config = None
+        if witness_label:
+            if witness_label not in self.sims:
+                log.error(f"Witness simulation label '{witness_label}' not found!")
+                return
+            witness_config = self.sims[witness_label]
+        chans = SignalGenerator().generate(main_config=main_config, n_seconds=n_seconds, mode=mode,
+                                           trial_num=trial_num, witness_config=witness_config, snr_db=snr_db)
+        if not chans:
+            log.error("Simulation failed to generate data.")
+            return
+        for _, raw in chans.items():
+            self.raws[raw.label] = raw
+        main_config.simtime = time.time() - t0
+
+    def create_witness_channel(self, main_channel_label, witness_channel_label, m_witness=None,
+                               delta_l_witness=None):
+        """core.py:519-588: a static witness sharing the main channel's laser."""
+        if main_channel_label not in self.sims:
+            raise KeyError(f"Main channel '{main_channel_label}' not found in framework.")
+        if delta_l_witness is not None and m_witness is not None:
+            raise ValueError("Please specify either delta_l_witness or m_witness, but not both.")
+        main = self.sims[main_channel_label]
+        laser = main.laser
+        if m_witness is None and delta_l_witness is None:
+            m_target = 0.1
+        elif m_witness is not None:
+            m_target = m_witness
+        else:
+            m_target = (2 * np.pi * laser.df * delta_l_witness) / sc.c
+        ifo = InterferometerConfig(label=f"{witness_channel_label}_ifo")
+        ifo.arml_mod_amp = 0.0
+        ifo.arml_mod_n = 0.0
+        if laser.df == 0:
+            raise ValueError("Cannot set 'm_witness' when laser 'df' is zero.")
+        dl = (m_target * sc.c) / (2 * np.pi * laser.df)
+        ifo.ref_arml = 0.01
+        ifo.meas_arml = ifo.ref_arml + dl
+        f0 = sc.c / laser.wavelength
+        static_phase = (2 * np.pi * f0 * dl) / sc.c
+        ifo.phi = ((np.pi / 2.0) + static_phase) % (2 * np.pi)
+        w = DFMIObject(label=witness_channel_label, laser_config=laser, ifo_config=ifo, f_samp=main.f_samp)
+        w.fit_n = main.fit_n
+        self.sims[witness_channel_label] = w
+        return w
+
+    # --- fitting ------------------------------------------------------------
+    def fit_init(self, label, n):
+        """core.py:390-422."""
+        raw = self.raws[label]
+        R = int(raw.f_samp / raw.f_mod * n)
+        fs = raw.f_samp / R
+        nbuf = int(raw.n_samples() / R)
+        if nbuf == 0:
+            log.error("Check buffer size !! Calculated nbuf is zero.")
+        return R, fs, nbuf
+
+    def _n_cycles(self, raw, main_label, kwargs):
+        n = kwargs.get("n")
+        if n is None:
+            sim = self.sims.get(raw.sim.label if raw.sim else main_label)
+            n = sim.fit_n if sim else 20
+        return n
+
+    def fit(self, main_label, method="nls", fit_label=None, **kwargs):
+        """core.py:424-517: strategy dispatch -> DataFrame -> DeepFitObject."""
+        fitter_map = _fitters.FITTER_MAP
+        if method not in fitter_map:
+            log.error(f"Unknown fit method: '{method}'. Available: {list(fitter_map.keys())}")
+            return
+        if main_label not in self.raws:
+            log.error(f"Invalid raw data label: '{main_label}' !!")
+            return
+        raw = self.raws[main_label]
+        if fit_label is None:
+            fit_label = f"{main_label}_{method}"
+        n = self._n_cycles(raw, main_label, kwargs)
+        R, fs, nbuf = self.fit_init(main_label, n)
+        if getattr(raw, "phi_sim", None) is not None and len(raw.phi_sim) > 0:
+            raw.phi_sim_downsamp = vectorized_downsample(raw.phi_sim, R)
+        fit_config = {"n": n}
+        df = fitter_map[method](fit_config).fit(main_raw=raw, **kwargs)
+        if df is None or df.empty:
+            log.error(f"{fitter_map[method].__name__} returned no results.")
+            return None
+        return self._finish(fit_label, main_label, raw, method, df, n, R, fs, nbuf)
+
+    def _finish(self, fit_label, main_label, raw, method, df, n, R, fs, nbuf):
+        if method in ("nls", "ekf"):
+            df["tau"] = df["m"] / (2 * np.pi * raw.sim.laser.df) if raw.sim else 0.0
+        self.fits_df[fit_label] = df
+        fit = DeepFitObject()
+        # core.py:511-514 records ndata/init_a/init_m as 0 in the fit object
+        fit.n, fit.R, fit.fs, fit.nbuf, fit.ndata, fit.init_a, fit.init_m = n, R, fs, nbuf, 0, 0, 0
+        fit.t0, fit.f_samp, fit.f_mod = raw.t0, raw.f_samp, raw.f_mod
+        for k in ("ssq", "amp", "m", "tau", "phi", "psi", "dc"):
+            setattr(fit, k, df[k].to_numpy())
+        fit.time = np.arange(0, fit.ssq.shape[0] / fit.fs, 1.0 / fit.fs)
+        fit.label = fit_label
+        self.fits[fit_label] = fit
+        return fit
+
+    def fit_many(self, labels, method="nls", **kwargs):
+        """Fit several channels in ONE engine call (lane/segment batch across channels).
+
+        Equivalent to `for l in labels: self.fit(l, method, **kwargs)` (which is how
+        notebooks/0.1_quickstart-2-ch fits its two channels); channels must share
+        f_samp, f_mod and length. Returns {label: DeepFitObject}."""
+        raws = [self.raws[l] for l in labels]
+        r0 = raws[0]
+        if any(r.f_samp != r0.f_samp or r.f_mod != r0.f_mod or r.n_samples() != r0.n_samples() for r in raws):
+            return {l: self.fit(l, method=method, **kwargs) for l in labels}
+        n = self._n_cycles(r0, labels[0], kwargs)
+        R, fs, nbuf = self.fit_init(labels[0], n)
+        out = {}
+        if method == "ekf":
+            states = _fitters.ekf_records(raws, n, **kwargs)
+            for l, raw, st in zip(labels, raws, states):
+                import pandas as pd
+                df = pd.DataFrame({"amp": st[:, 0], "m": st[:, 1], "phi": st[:, 2], "psi": st[:, 3], "dc": st[:, 4],
+                                   "ssq": np.zeros(nbuf), "fitok": np.ones(nbuf, dtype=int)})
+                out[l] = self._finish(f"{l}_{method}", l, raw, method, df, n, R, fs, nbuf)
+            return out
+        if method != "nls":
+            return {l: self.fit(l, method=method, **kwargs) for l in labels}
+        ndata = int(kwargs.get("ndata", 10))
+        N = r0.n_samples()
+        if N % R != 0:
+            raise ValueError(f"cannot reshape array of size {N} into shape ({R})")
+        parallel = kwargs.get("parallel", True)
+        g = (kwargs.get("init_a", 1.6), kwargs.get("init_m", 6.0), 0.0, kwargs.get("init_psi", 0.0))
+        cols, ok = _fitters.nls_records([r.samples() for r in raws], r0.f_samp, r0.f_mod, R, nbuf, ndata, g,
+                                        parallel=parallel, n_cores=kwargs.get("n_cores") if parallel else None)
+        df_all = _fitters.frame_from(cols, ok)
+        for i, (l, raw) in enumerate(zip(labels, raws)):
+            df = df_all.iloc[i * nbuf:(i + 1) * nbuf].reset_index(drop=True)
+            out[l] = self._finish(f"fit_{l}", l, raw, method, df, n, R, fs, nbuf)
+        return out

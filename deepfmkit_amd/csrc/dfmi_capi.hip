@@ -1,0 +1,544 @@
+// dfmi_capi.hip — host side of libdfmi.so: the C ABI declared in include/dfmi.h.
+//
+// Owns: lazy HIP initialisation, per-device grow-only workspaces, the cached
+// demodulation basis tables and m-grid Bessel tables, kernel selection and
+// launch geometry. No torch, no Python.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <cstdint>
+#include <map>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/dfmi.h"
+#include "demod.h"
+#include "dfmi_math.h"
+#include "ekf.h"
+#include "lm.h"
+
+namespace {
+
+thread_local std::string g_err;
+std::mutex g_mu;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                       \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    if (_e != hipSuccess)                                                                  \
+      return fail(DFMI_ERR_HIP, std::string(#expr " failed: ") + hipGetErrorString(_e));   \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+};
+
+struct DeviceState {
+  bool init = false;
+  int n_cu = 0;
+  size_t lds_per_block = 0;
+  std::map<std::string, DevBuf> ws;                                  // named workspaces
+  std::map<std::tuple<int, int, uint64_t>, DevBuf> basis;            // (L, ndata, w0 bits)
+  std::map<std::tuple<int, uint64_t, uint64_t, uint64_t>, DevBuf> gridtab;  // (ndata, min, max, step)
+};
+
+std::map<int, DeviceState> g_dev;
+int g_ndev = -1;
+
+int ensure_init(int* dev_out) {
+  if (g_ndev < 0) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) {
+      g_ndev = 0;
+      return fail(DFMI_ERR_NODEV, "no HIP device visible (hipGetDeviceCount: " +
+                                      std::string(hipGetErrorString(e)) + ")");
+    }
+    g_ndev = n;
+  }
+  if (g_ndev == 0) return fail(DFMI_ERR_NODEV, "no HIP device visible");
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  DeviceState& ds = g_dev[dev];
+  if (!ds.init) {
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, dev));
+    ds.n_cu = prop.multiProcessorCount;
+    ds.lds_per_block = prop.sharedMemPerBlock;
+    ds.init = true;
+  }
+  *dev_out = dev;
+  return DFMI_OK;
+}
+
+int workspace(int dev, const char* name, size_t bytes, void** out) {
+  DevBuf& b = g_dev[dev].ws[name];
+  if (b.n < bytes) {
+    if (b.p) HIPCHK(hipFree(b.p));
+    b.p = nullptr;
+    b.n = 0;
+    HIPCHK(hipMalloc(&b.p, bytes));
+    b.n = bytes;
+  }
+  *out = b.p;
+  return DFMI_OK;
+}
+
+uint64_t bits(double v) {
+  uint64_t u;
+  memcpy(&u, &v, 8);
+  return u;
+}
+
+// Basis table for the fold kernel: row c < ndata = cos(fl((c+1) w0) p), row
+// ndata + c = sin(...), p < L. fit.py:55-64 forms the angle as ((n+1)*w0)*t.
+int basis_table(int dev, int L, int ndata, double w0, hipStream_t st, const double** out) {
+  auto key = std::make_tuple(L, ndata, bits(w0));
+  DevBuf& b = g_dev[dev].basis[key];
+  if (!b.p) {
+    std::vector<double> h((size_t)2 * ndata * L);
+    for (int c = 0; c < ndata; ++c) {
+      const double wh = (double)(c + 1) * w0;
+      for (int p = 0; p < L; ++p) {
+        const double ang = wh * (double)p;
+        h[(size_t)c * L + p] = cos(ang);
+        h[(size_t)(ndata + c) * L + p] = sin(ang);
+      }
+    }
+    HIPCHK(hipMalloc(&b.p, h.size() * 8));
+    b.n = h.size() * 8;
+    HIPCHK(hipMemcpy(b.p, h.data(), b.n, hipMemcpyHostToDevice));
+  }
+  (void)st;
+  *out = (const double*)b.p;
+  return DFMI_OK;
+}
+
+// numpy.arange(min, max + step, step): length ceil((stop - start)/step),
+// values start + i*((start + step) - start).
+void grid_geometry(const dfmi_lm_config& c, int* n, double* delta) {
+  const double stop = c.m_grid_max + c.m_grid_step;
+  const double len = ceil((stop - c.m_grid_min) / c.m_grid_step);
+  *n = len > 0 ? (int)len : 0;
+  *delta = (c.m_grid_min + c.m_grid_step) - c.m_grid_min;
+}
+
+int grid_table(int dev, int ndata, const dfmi_lm_config& c, const double** out) {
+  auto key = std::make_tuple(ndata, bits(c.m_grid_min), bits(c.m_grid_max), bits(c.m_grid_step));
+  DevBuf& b = g_dev[dev].gridtab[key];
+  if (!b.p) {
+    int n;
+    double delta;
+    grid_geometry(c, &n, &delta);
+    std::vector<double> h((size_t)(n > 0 ? n : 1) * ndata, 0.0);
+    std::vector<double> row(ndata + 2);
+    for (int g = 0; g < n; ++g) {
+      const double mtry = c.m_grid_min + (double)g * delta;
+      dfmi_bessel_table(mtry, ndata, row.data());
+      for (int i = 0; i < ndata; ++i) h[(size_t)g * ndata + i] = row[i + 1];
+    }
+    HIPCHK(hipMalloc(&b.p, h.size() * 8));
+    b.n = h.size() * 8;
+    HIPCHK(hipMemcpy(b.p, h.data(), b.n, hipMemcpyHostToDevice));
+  }
+  *out = (const double*)b.p;
+  return DFMI_OK;
+}
+
+int to_lmconst(const dfmi_lm_config* cfg, dfmi::LMConst* c) {
+  dfmi_lm_config d;
+  if (!cfg) {
+    dfmi_lm_config_default(&d);
+    cfg = &d;
+  }
+  if (cfg->n_lambda < 0 || cfg->n_lambda > DFMI_MAX_LAMBDA) return fail(DFMI_ERR_ARG, "n_lambda out of range");
+  if (cfg->max_lma_steps < 0) return fail(DFMI_ERR_ARG, "max_lma_steps < 0");
+  if (!(cfg->m_grid_step > 0)) return fail(DFMI_ERR_ARG, "m_grid_step must be > 0");
+  memset(c, 0, sizeof(*c));
+  c->max_steps = cfg->max_lma_steps;
+  c->n_lambda = cfg->n_lambda;
+  for (int i = 0; i < cfg->n_lambda; ++i) c->lambdas[i] = cfg->lambdas[i];
+  c->min_step_norm = cfg->min_step_norm;
+  c->conv_improve = cfg->conv_improve;
+  c->conv_param_change = cfg->conv_param_change;
+  c->fitok_threshold = cfg->fitok_threshold;
+  c->bessel_amp_thr = cfg->bessel_amp_threshold;
+  c->sincos_amp_thr = cfg->sincos_amp_threshold;
+  grid_geometry(*cfg, &c->n_grid, &c->grid_delta);
+  c->grid_min = cfg->m_grid_min;
+  return DFMI_OK;
+}
+
+constexpr int kMaxSlotCap = 8;
+
+int32_t detect_period_impl(double w0, int32_t R, int32_t ndata) {
+  if (!(w0 > 0) || R <= 0 || ndata <= 0) return 0;
+  const double two_pi = 6.283185307179586;
+  const int Lmax = 64 * 2 * kMaxSlotCap;
+  for (int L = 1; L <= Lmax; ++L) {
+    const double v = (double)L * w0 / two_pi;
+    const double n = nearbyint(v);
+    if (n < 1) continue;
+    // periodicity error of the basis, accumulated over R/L cycles at the top harmonic
+    const double err = two_pi * fabs(v - n) * (double)ndata * ((double)R / (double)L + 1.0);
+    if (err <= 1e-11) return L;
+  }
+  return 0;
+}
+
+template <int VEC, int MS, bool LDS>
+int launch_fold_t(const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tab,
+                  double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu) {
+  const size_t lds = LDS ? (size_t)2 * ndata * L * sizeof(double) : 0;
+  auto kern = dfmi::demod_fold_kernel<VEC, MS, LDS>;
+  int per_cu = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, dfmi::kBlockThreads, lds));
+  if (per_cu < 1) per_cu = 1;
+  int64_t need = (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock;
+  int64_t grid = (int64_t)n_cu * per_cu;
+  if (grid > need) grid = need;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(dfmi::kBlockThreads), lds, st, x, nseg, stride, R, L, ndata,
+                     tab, qi, qi_ld, dc);
+  HIPCHK(hipGetLastError());
+  return DFMI_OK;
+}
+
+template <int VEC, bool LDS>
+int launch_fold_ms(int ms, const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tab,
+                   double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu) {
+  switch (ms) {
+    case 1: return launch_fold_t<VEC, 1, LDS>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
+    case 2: return launch_fold_t<VEC, 2, LDS>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
+    case 4: return launch_fold_t<VEC, 4, LDS>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
+    default: return launch_fold_t<VEC, 8, LDS>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
+  }
+}
+
+// Device-pointer demodulation (all pointers on the current device).
+int demod_device(int dev, const double* x, int64_t nseg, int64_t stride, int R, int ndata, double w0, int period,
+                 double* qi, int64_t qi_ld, double* dc, hipStream_t st) {
+  if (nseg == 0) return DFMI_OK;
+  int L = period;
+  if (L == 0) L = detect_period_impl(w0, R, ndata);
+  const DeviceState& ds = g_dev[dev];
+  if (L > 0) {
+    const bool vec2 = (L % 2 == 0) && (stride % 2 == 0) && (((uintptr_t)x & 15) == 0);
+    const int VEC = vec2 ? 2 : 1;
+    int nslot = (L + 64 * VEC - 1) / (64 * VEC);
+    if (nslot <= kMaxSlotCap) {
+      int ms = 1;
+      while (ms < nslot) ms <<= 1;
+      const double* tab = nullptr;
+      int rc = basis_table(dev, L, ndata, w0, st, &tab);
+      if (rc) return rc;
+      const size_t lds = (size_t)2 * ndata * L * sizeof(double);
+      const bool use_lds = lds <= 64 * 1024 && lds <= ds.lds_per_block;
+      if (vec2) {
+        return use_lds ? launch_fold_ms<2, true>(ms, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, ds.n_cu)
+                       : launch_fold_ms<2, false>(ms, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, ds.n_cu);
+      }
+      return use_lds ? launch_fold_ms<1, true>(ms, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, ds.n_cu)
+                     : launch_fold_ms<1, false>(ms, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, ds.n_cu);
+    }
+  }
+  // direct kernel
+  int64_t need = (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock;
+  int64_t grid = (int64_t)ds.n_cu * 8;
+  if (grid > need) grid = need;
+  hipLaunchKernelGGL(dfmi::demod_direct_kernel, dim3((unsigned)grid), dim3(dfmi::kBlockThreads), 0, st, x, nseg,
+                     stride, R, ndata, w0, qi, qi_ld, dc);
+  HIPCHK(hipGetLastError());
+  return DFMI_OK;
+}
+
+int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec, int64_t nbuf, int64_t first,
+              int64_t nitems, int64_t nchunk, const double* guess_dev, int64_t g_rec, int64_t g_comp,
+              const double* guess_host /* nrec*4, used when nrec <= 8 and guess_dev == null */,
+              const dfmi::LMConst& c, const double* jtab, double* out, int64_t out_ld, int32_t* status,
+              hipStream_t st) {
+  if (nrec == 0 || nitems == 0) return DFMI_OK;
+  if (nchunk < 1) nchunk = 1;
+  if (nchunk > nitems) nchunk = nitems;  // np.array_split chunks beyond nitems are empty
+  dfmi::GuessInline ginl;
+  memset(&ginl, 0, sizeof(ginl));
+  int use_inline = 0;
+  if (!guess_dev) {
+    if (nrec > 8) return fail(DFMI_ERR_ARG, "inline guesses support at most 8 records");
+    for (int64_t r = 0; r < nrec; ++r)
+      for (int i = 0; i < 4; ++i) ginl.v[r][i] = guess_host[r * 4 + i];
+    use_inline = 1;
+  }
+  const int64_t lanes = nrec * nchunk;
+  const int block = 64;
+  const int64_t grid = (lanes + block - 1) / block;
+  hipLaunchKernelGGL(dfmi::lm_chunks_kernel, dim3((unsigned)grid), dim3(block), 0, st, qi, qi_ld, ndata, nrec, nbuf,
+                     first, nitems, nchunk, guess_dev, g_rec, g_comp, ginl, use_inline, jtab, c, out, out_ld, status);
+  HIPCHK(hipGetLastError());
+  return DFMI_OK;
+}
+
+// Whole record pipeline on device pointers (fitters.py:370-428).
+int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride, int64_t nbuf, int R, int ndata,
+                      double w0, int period, const double* init_guess_host, int parallel, int64_t nchunk,
+                      const dfmi_lm_config& cfg, const dfmi::LMConst& c, double* out, int32_t* fitok,
+                      hipStream_t st) {
+  const int64_t nseg = nrec * nbuf;
+  if (nseg == 0) return DFMI_OK;
+  void* qiw = nullptr;
+  int rc = workspace(dev, "qi", (size_t)2 * ndata * nseg * sizeof(double), &qiw);
+  if (rc) return rc;
+  double* qi = (double*)qiw;
+  const double* jtab = nullptr;
+  rc = grid_table(dev, ndata, cfg, &jtab);
+  if (rc) return rc;
+  const int64_t out_ld = nseg;
+  double* dc = out + 4 * out_ld;
+  if (rec_stride == nbuf * (int64_t)R) {
+    rc = demod_device(dev, x, nseg, R, R, ndata, w0, period, qi, nseg, dc, st);
+    if (rc) return rc;
+  } else {
+    for (int64_t r = 0; r < nrec; ++r) {
+      rc = demod_device(dev, x + r * rec_stride, nbuf, R, R, ndata, w0, period, qi + r * nbuf, nseg, dc + r * nbuf,
+                        st);
+      if (rc) return rc;
+    }
+  }
+  // guesses: inline kernel arguments for up to 8 records, a device table otherwise
+  const double* gdev = nullptr;
+  if (nrec > 8) {
+    void* gw = nullptr;
+    rc = workspace(dev, "guess", (size_t)nrec * 4 * sizeof(double), &gw);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(gw, init_guess_host, (size_t)nrec * 4 * sizeof(double), hipMemcpyHostToDevice, st));
+    gdev = (const double*)gw;
+  }
+  if (!parallel) {
+    return lm_device(dev, qi, nseg, ndata, nrec, nbuf, 0, nbuf, 1, gdev, 4, 1, init_guess_host, c, jtab, out, out_ld,
+                     fitok, st);
+  }
+  // seed step: buffer 0 of every record from the default seed
+  rc = lm_device(dev, qi, nseg, ndata, nrec, nbuf, 0, 1, 1, gdev, 4, 1, init_guess_host, c, jtab, out, out_ld, fitok,
+                 st);
+  if (rc || nbuf <= 1) return rc;
+  // the rest, seeded with each record's buffer-0 result (read on device: no host sync)
+  return lm_device(dev, qi, nseg, ndata, nrec, nbuf, 1, nbuf - 1, nchunk, out, nbuf, out_ld, nullptr, c, jtab, out,
+                   out_ld, fitok, st);
+}
+
+}  // namespace
+
+extern "C" {
+
+void dfmi_lm_config_default(dfmi_lm_config* cfg) {
+  if (!cfg) return;
+  memset(cfg, 0, sizeof(*cfg));
+  cfg->max_lma_steps = 100;
+  const double lam[8] = {0.0, 1e-7, 1e-5, 1e-3, 1e-1, 1.0, 10.0, 100.0};
+  cfg->n_lambda = 8;
+  for (int i = 0; i < 8; ++i) cfg->lambdas[i] = lam[i];
+  cfg->min_step_norm = 1e-15;
+  cfg->conv_improve = 1e-9;
+  cfg->conv_param_change = 1e-9;
+  cfg->fitok_threshold = 1e-3;
+  cfg->m_grid_min = 5.0;
+  cfg->m_grid_max = 30.0;
+  cfg->m_grid_step = 0.5;
+  cfg->bessel_amp_threshold = 0.05;
+  cfg->sincos_amp_threshold = 0.1;
+}
+
+int32_t dfmi_detect_period(double w0, int32_t R, int32_t ndata) { return detect_period_impl(w0, R, ndata); }
+
+int dfmi_device_count(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int dev;
+  int rc = ensure_init(&dev);
+  if (rc) return 0;
+  return g_ndev;
+}
+
+const char* dfmi_last_error(void) { return g_err.c_str(); }
+
+const char* dfmi_version(void) { return "dfmi 0.1 gfx950"; }
+
+int dfmi_demod(const double* x, int64_t nseg, int64_t seg_stride, int32_t R, int32_t ndata, double w0,
+               int32_t period, double* qi, double* dc, int32_t mem, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_err.clear();
+  if (nseg < 0 || R <= 0 || ndata <= 0 || seg_stride < R) return fail(DFMI_ERR_ARG, "bad demod geometry");
+  if (nseg > 0 && (!x || !qi || !dc)) return fail(DFMI_ERR_ARG, "null pointer");
+  int dev;
+  int rc = ensure_init(&dev);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (mem == DFMI_MEM_DEVICE) return demod_device(dev, x, nseg, seg_stride, R, ndata, w0, period, qi, nseg, dc, st);
+  if (nseg == 0) return DFMI_OK;
+  const size_t xb = (size_t)((nseg - 1) * seg_stride + R) * sizeof(double);
+  void *dx, *dq, *dd;
+  if ((rc = workspace(dev, "h_x", xb, &dx))) return rc;
+  if ((rc = workspace(dev, "h_qi", (size_t)2 * ndata * nseg * 8, &dq))) return rc;
+  if ((rc = workspace(dev, "h_dc", (size_t)nseg * 8, &dd))) return rc;
+  HIPCHK(hipMemcpyAsync(dx, x, xb, hipMemcpyHostToDevice, st));
+  rc = demod_device(dev, (const double*)dx, nseg, seg_stride, R, ndata, w0, period, (double*)dq, nseg, (double*)dd, st);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(qi, dq, (size_t)2 * ndata * nseg * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(dc, dd, (size_t)nseg * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return DFMI_OK;
+}
+
+int dfmi_lm(const double* qi, int64_t nseg, int32_t ndata, const double* guess, int32_t guess_per_segment,
+            int64_t nchunk, const dfmi_lm_config* cfg, double* params, double* ssq, int32_t* status, int32_t mem,
+            void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_err.clear();
+  if (nseg < 0 || ndata <= 0) return fail(DFMI_ERR_ARG, "bad lm geometry");
+  if (nseg > 0 && (!qi || !guess || !params || !ssq || !status)) return fail(DFMI_ERR_ARG, "null pointer");
+  dfmi_lm_config dcfg;
+  if (!cfg) {
+    dfmi_lm_config_default(&dcfg);
+    cfg = &dcfg;
+  }
+  dfmi::LMConst c;
+  int rc = to_lmconst(cfg, &c);
+  if (rc) return rc;
+  int dev;
+  if ((rc = ensure_init(&dev))) return rc;
+  if (nseg == 0) return DFMI_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const double* jtab = nullptr;
+  if ((rc = grid_table(dev, ndata, *cfg, &jtab))) return rc;
+  // the kernel writes 6 columns (col 4 = dc is untouched); stage through a workspace
+  void *dq = nullptr, *dg = nullptr, *dout = nullptr, *dst = nullptr;
+  const size_t qib = (size_t)2 * ndata * nseg * 8;
+  const size_t gb = (size_t)(guess_per_segment ? nseg : 1) * 4 * 8;
+  if ((rc = workspace(dev, "lm_out", (size_t)6 * nseg * 8, &dout))) return rc;
+  if ((rc = workspace(dev, "lm_status", (size_t)nseg * 4, &dst))) return rc;
+  if (mem == DFMI_MEM_DEVICE) {
+    dq = (void*)qi;
+    dg = (void*)guess;
+  } else {
+    if ((rc = workspace(dev, "h_qi", qib, &dq))) return rc;
+    if ((rc = workspace(dev, "h_guess", gb, &dg))) return rc;
+    HIPCHK(hipMemcpyAsync(dq, qi, qib, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dg, guess, gb, hipMemcpyHostToDevice, st));
+  }
+  double* o = (double*)dout;
+  if (guess_per_segment) {
+    rc = lm_device(dev, (const double*)dq, nseg, ndata, nseg, 1, 0, 1, 1, (const double*)dg, 4, 1, nullptr, c, jtab, o,
+                   nseg, (int32_t*)dst, st);
+  } else {
+    rc = lm_device(dev, (const double*)dq, nseg, ndata, 1, nseg, 0, nseg, nchunk, (const double*)dg, 4, 1, nullptr,
+                   c, jtab, o, nseg, (int32_t*)dst, st);
+  }
+  if (rc) return rc;
+  const hipMemcpyKind kind = (mem == DFMI_MEM_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  HIPCHK(hipMemcpyAsync(params, o, (size_t)4 * nseg * 8, kind, st));
+  HIPCHK(hipMemcpyAsync(ssq, o + 5 * nseg, (size_t)nseg * 8, kind, st));
+  HIPCHK(hipMemcpyAsync(status, dst, (size_t)nseg * 4, kind, st));
+  if (mem != DFMI_MEM_DEVICE) HIPCHK(hipStreamSynchronize(st));
+  return DFMI_OK;
+}
+
+int dfmi_nls_record(const double* x, int64_t nrec, int64_t rec_stride, int64_t nbuf, int32_t R, int32_t ndata,
+                    double w0, int32_t period, const double* init_guess, int32_t parallel, int64_t nchunk,
+                    const dfmi_lm_config* cfg, double* out, int32_t* fitok, int32_t mem, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_err.clear();
+  if (nrec < 0 || nbuf < 0 || R <= 0 || ndata <= 0) return fail(DFMI_ERR_ARG, "bad record geometry");
+  if (nrec > 1 && rec_stride < nbuf * (int64_t)R) return fail(DFMI_ERR_ARG, "rec_stride < nbuf*R");
+  if (nrec * nbuf > 0 && (!x || !init_guess || !out || !fitok)) return fail(DFMI_ERR_ARG, "null pointer");
+  dfmi_lm_config dcfg;
+  if (!cfg) {
+    dfmi_lm_config_default(&dcfg);
+    cfg = &dcfg;
+  }
+  dfmi::LMConst c;
+  int rc = to_lmconst(cfg, &c);
+  if (rc) return rc;
+  int dev;
+  if ((rc = ensure_init(&dev))) return rc;
+  const int64_t nseg = nrec * nbuf;
+  if (nseg == 0) return DFMI_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (mem == DFMI_MEM_DEVICE)
+    return nls_record_device(dev, x, nrec, rec_stride, nbuf, R, ndata, w0, period, init_guess, parallel, nchunk, *cfg,
+                             c, out, fitok, st);
+  const int64_t rs = (nrec > 1) ? rec_stride : nbuf * (int64_t)R;
+  const size_t xb = (size_t)((nrec - 1) * rs + nbuf * (int64_t)R) * 8;
+  void *dx, *dout, *dst;
+  if ((rc = workspace(dev, "h_x", xb, &dx))) return rc;
+  if ((rc = workspace(dev, "h_out", (size_t)6 * nseg * 8, &dout))) return rc;
+  if ((rc = workspace(dev, "h_status", (size_t)nseg * 4, &dst))) return rc;
+  HIPCHK(hipMemcpyAsync(dx, x, xb, hipMemcpyHostToDevice, st));
+  rc = nls_record_device(dev, (const double*)dx, nrec, rs, nbuf, R, ndata, w0, period, init_guess, parallel, nchunk,
+                         *cfg, c, (double*)dout, (int32_t*)dst, st);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(out, dout, (size_t)6 * nseg * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(fitok, dst, (size_t)nseg * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return DFMI_OK;
+}
+
+int dfmi_ekf(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, const double* x0,
+             const double* p0_diag, const double* q_diag, const double* r_val, double w_m, double f_samp, int32_t R,
+             int64_t nbuf, double* states, int32_t mem, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_err.clear();
+  if (nrec < 0 || n_samp < 0 || R <= 0 || nbuf < 0) return fail(DFMI_ERR_ARG, "bad ekf geometry");
+  if (nrec > 1 && rec_stride < n_samp) return fail(DFMI_ERR_ARG, "rec_stride < n_samp");
+  int dev;
+  int rc = ensure_init(&dev);
+  if (rc) return rc;
+  if (nrec == 0) return DFMI_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t rs = nrec > 1 ? rec_stride : n_samp;
+  const double *dx = x, *dx0 = x0, *dp0 = p0_diag, *dq = q_diag, *dr = r_val;
+  double* dstates = states;
+  const size_t sb = (size_t)nrec * nbuf * 5 * 8;
+  if (mem != DFMI_MEM_DEVICE) {
+    void *a, *b, *c2, *d, *e, *f;
+    const size_t xb = (size_t)((nrec - 1) * rs + n_samp) * 8;
+    if ((rc = workspace(dev, "e_x", xb > 0 ? xb : 8, &a))) return rc;
+    if ((rc = workspace(dev, "e_x0", (size_t)nrec * 5 * 8, &b))) return rc;
+    if ((rc = workspace(dev, "e_p0", 5 * 8, &c2))) return rc;
+    if ((rc = workspace(dev, "e_q", 5 * 8, &d))) return rc;
+    if ((rc = workspace(dev, "e_r", (size_t)nrec * 8, &e))) return rc;
+    if ((rc = workspace(dev, "e_st", sb > 0 ? sb : 8, &f))) return rc;
+    if (xb) HIPCHK(hipMemcpyAsync(a, x, xb, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(b, x0, (size_t)nrec * 5 * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(c2, p0_diag, 5 * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d, q_diag, 5 * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(e, r_val, (size_t)nrec * 8, hipMemcpyHostToDevice, st));
+    dx = (const double*)a;
+    dx0 = (const double*)b;
+    dp0 = (const double*)c2;
+    dq = (const double*)d;
+    dr = (const double*)e;
+    dstates = (double*)f;
+  }
+  if (sb) HIPCHK(hipMemsetAsync(dstates, 0, sb, st));
+  const int block = 64;
+  const int64_t grid = (nrec + block - 1) / block;
+  hipLaunchKernelGGL(dfmi::ekf_kernel, dim3((unsigned)grid), dim3(block), 0, st, dx, nrec, rs, n_samp, dx0, dp0, dq,
+                     dr, w_m, f_samp, (int)R, nbuf, dstates);
+  HIPCHK(hipGetLastError());
+  if (mem != DFMI_MEM_DEVICE) {
+    if (sb) HIPCHK(hipMemcpyAsync(states, dstates, sb, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  return DFMI_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,105 @@
+// ekf.h — per-sample Extended Kalman Filter (fitters.py:214-320), one lane per channel.
+//
+// The EKF is a serial chain over samples inside a channel (each update depends
+// on the previous state), so the only parallelism is across independent
+// channels/trials: lane = channel, the 5-vector state and the full 5×5
+// covariance live in that lane's registers, and the sample loop runs in
+// order. Operation order follows the numpy expressions of fitters.py:276-302:
+//   P = F P F^T + Q (F = I: exact, so P + Q), H from fitters.py:287-293,
+//   S = (H P) H^T + R, K = (P H^T) · (1/S), x += K y, P = (I − K H) P.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dfmi {
+
+__global__ __launch_bounds__(64) void ekf_kernel(const double* __restrict__ x, int64_t nrec, int64_t rec_stride,
+                                                  int64_t n_samp, const double* __restrict__ x0,
+                                                  const double* __restrict__ p0, const double* __restrict__ qd,
+                                                  const double* __restrict__ rv, double w_m, double f_samp, int R,
+                                                  int64_t nbuf, double* __restrict__ states) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrec) return;
+  const double* __restrict__ xr = x + r * rec_stride;
+  double st[5];
+  double P[5][5];
+  double Q[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    st[i] = x0[r * 5 + i];
+    Q[i] = qd[i];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) P[i][j] = (i == j) ? p0[i] : 0.0;
+  }
+  const double Rv = rv[r];
+  for (int64_t k = 0; k < n_samp; ++k) {
+    // predict: P = F P F^T + Q with F = I
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+      for (int j = 0; j < 5; ++j) P[i][j] = P[i][j] + (i == j ? Q[i] : 0.0);
+    const double a = st[0], m = st[1], phi = st[2], psi = st[3], dc = st[4];
+    const double t = (double)k / f_samp;
+    const double th = w_m * t + psi;
+    double sth, cth;
+    sincos(th, &sth, &cth);
+    const double arg = phi + m * cth;
+    double sa, ca;
+    sincos(arg, &sa, &ca);
+    const double h = a * ca + dc;
+    double H[5] = {ca, -a * sa * cth, -a * sa, a * m * sa * sth, 1.0};
+    const double y = xr[k] - h;
+    double HP[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) acc = fma(H[i], P[i][j], acc);
+      HP[j] = acc;
+    }
+    double S = 0.0;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) S = fma(HP[j], H[j], S);
+    S = S + Rv;
+    const double invS = 1.0 / S;
+    double K[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) acc = fma(P[i][j], H[j], acc);
+      K[i] = acc * invS;
+    }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) st[i] = st[i] + K[i] * y;
+    // P = (I - K H) P
+    double Mt[5][5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+      for (int j = 0; j < 5; ++j) Mt[i][j] = (i == j ? 1.0 : 0.0) - K[i] * H[j];
+    double Pn[5][5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        double acc = 0.0;
+#pragma unroll
+        for (int l = 0; l < 5; ++l) acc = fma(Mt[i][l], P[l][j], acc);
+        Pn[i][j] = acc;
+      }
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+      for (int j = 0; j < 5; ++j) P[i][j] = Pn[i][j];
+    if ((k + 1) % R == 0) {
+      const int64_t b = (k + 1) / R - 1;
+      if (b < nbuf) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) states[(r * nbuf + b) * 5 + i] = st[i];
+      }
+    }
+  }
+}
+
+}  // namespace dfmi

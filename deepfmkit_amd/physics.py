@@ -1,0 +1,203 @@
+"""Simulation configuration objects and the synthetic-input generator.
+
+Only what the NLS readout path needs as INPUT is restated here (SURVEY.md §8a row
+a16): the configuration containers and the snr-mode generator of
+physics.py:475-530, plus the zero/white-noise subset of the asd mode used by
+workers.run_single_trial (physics.py:423-473, 615-722).  Coloured (1/f^alpha)
+noise needs `pyplnoise`, which is absent from this image: requesting it raises.
+
+The snr-mode restatement keeps the reference's numpy operation order, so for a
+given seed the generated record is bit-identical to the reference's (pinned by
+the SHA-256 values in tests/golden/manifest.json).
+"""
+from __future__ import annotations
+
+import logging
+from typing import Any, Callable, Dict, Optional
+
+import numpy as np
+import scipy.constants as sc
+
+from .data import DeepRawObject
+
+log = logging.getLogger(__name__)
+
+
+class LaserConfig:
+    """Laser source parameters (reference physics.py:15-51)."""
+
+    def __init__(self, label="laser_source", psi=None):
+        self.label = label
+        self.wavelength = 1.064e-6
+        self.amp = 1.0
+        self.visibility = 1.0
+        self.f_mod = 1000
+        self.df = 3e9
+        self.psi = psi if psi else 0.0
+        self.waveform_func: Callable[..., np.ndarray] = lambda t_phase: np.cos(t_phase)
+        self.waveform_kwargs: Dict[str, Any] = {}
+        self.f_n = 0.0
+        self.df_n = 0.0
+        self.amp_n = 0.0
+
+
+class InterferometerConfig:
+    """Optical path parameters (reference physics.py:213-237)."""
+
+    def __init__(self, label="interferometer_path"):
+        self.label = label
+        self.phi = 0.0
+        self.ref_arml = 0.1
+        self.meas_arml = 0.3
+        self.arml_mod_f = 5.0
+        self.arml_mod_amp = 0.0
+        self.arml_mod_psi = 0.0
+        self.arml_mod_n = 0.0
+
+
+class DFMIObject:
+    """One simulation channel = laser + interferometer (reference physics.py:239-296)."""
+
+    def __init__(self, label, laser_config, ifo_config, f_samp=200000):
+        self.label = label
+        self.laser = laser_config
+        self.ifo = ifo_config
+        self.f_samp = float(f_samp)
+        self.N = 0
+        self.simtime = None
+        self.fit_n = 20
+        self.f_fit = float(self.laser.f_mod / self.fit_n)
+
+    @property
+    def m(self):
+        delta_l = self.ifo.meas_arml - self.ifo.ref_arml
+        if delta_l == 0:
+            return 0.0
+        return 2 * np.pi * self.laser.df * delta_l / sc.c
+
+
+def set_laser_df_for_effect(laser: LaserConfig, ifo: InterferometerConfig, m):
+    """helpers.py:10-14: choose laser.df so that the channel's m equals `m`."""
+    opd = np.abs(ifo.meas_arml - ifo.ref_arml)
+    laser.df = (m * sc.c) / (2 * sc.pi * opd)
+
+
+class SignalGenerator:
+    """Synthetic DFMI time series (reference physics.py:362-530)."""
+
+    def generate(self, main_config, n_seconds, mode="asd", trial_num=0, witness_config=None, snr_db=None,
+                 external_noise: Optional[dict] = None):
+        if mode == "asd":
+            return self._generate_with_asd(main_config, n_seconds, trial_num, witness_config, external_noise)
+        if mode == "snr":
+            if snr_db is None:
+                log.error("SNR mode requires a value for 'snr_db'.")
+                return {}
+            return self._generate_with_snr(main_config, n_seconds, trial_num, snr_db)
+        log.error(f"Unknown simulation mode: '{mode}'")
+        return {}
+
+    # --- snr mode: physics.py:475-530 ---------------------------------------
+    def _generate_with_snr(self, cfg, n_seconds, trial_num, snr_db):
+        num_samples = int(n_seconds * cfg.f_samp)
+        t = np.arange(num_samples) / cfg.f_samp
+        cfg.N = len(t)
+        y = ideal_signal(cfg, t)
+        y = add_white_noise(y, snr_db, trial_num)
+        raw = DeepRawObject(data=y)
+        raw.label = cfg.label
+        raw.f_samp = cfg.f_samp
+        raw.f_mod = cfg.laser.f_mod
+        raw.t0 = 0
+        raw.sim = cfg
+        return {"main": raw}
+
+    # --- asd mode, zero/white-noise subset: physics.py:423-473, 532-722 ------
+    def _generate_with_asd(self, cfg, n_seconds, trial_num, witness_config, external_noise=None):
+        num_samples = int(n_seconds * cfg.f_samp)
+        t = np.arange(num_samples) / cfg.f_samp
+        cfg.N = len(t)
+        if external_noise:
+            noise = {k: external_noise.get(k, 0.0) for k in ("laser_frequency", "amplitude", "df", "armlength")}
+        else:
+            noise = asd_noise_arrays(cfg, len(t), trial_num)
+        out = {}
+        for key, c, dyn in (("main", cfg, True), ("witness", witness_config, False)):
+            if c is None:
+                continue
+            sig, phase, truth = exact_model_signal(c, t, noise, dyn)
+            raw = DeepRawObject(data=sig)
+            raw.label = c.label
+            raw.f_samp = c.f_samp
+            raw.f_mod = c.laser.f_mod
+            raw.sim = c
+            raw.phi = phase
+            raw.phi_sim = truth
+            out[key] = raw
+        return out
+
+
+def ideal_signal(cfg, t):
+    """physics.py:493-518 with is_dynamic=False: A(1 + C cos(phi + m cos(w t + psi)))."""
+    laser, ifo = cfg.laser, cfg.ifo
+    omega_mod = 2 * np.pi * laser.f_mod
+    phitot = ifo.phi + cfg.m * np.cos(omega_mod * t + laser.psi)
+    return laser.amp * (1 + laser.visibility * np.cos(phitot))
+
+
+def add_white_noise(clean, snr_db, trial_num):
+    """physics.py:520-530: white Gaussian noise from RandomState(trial_num)."""
+    ac = clean - np.mean(clean)
+    power = np.mean(ac ** 2)
+    std = np.sqrt(power / 10 ** (snr_db / 10.0))
+    rng = np.random.RandomState(seed=trial_num)
+    return clean + rng.randn(len(clean)) * std
+
+
+def asd_noise_arrays(cfg, n_samples, trial_num=0):
+    """physics.py:532-613, white/zero sources only (coloured needs pyplnoise)."""
+    fs = cfg.f_samp
+    params = [("laser_frequency", cfg.laser.f_n, 2.0), ("amplitude", cfg.laser.amp_n, 0.0),
+              ("df", cfg.laser.df_n, 0.0), ("armlength", cfg.ifo.arml_mod_n, 2.0)]
+    rng = np.random.RandomState(seed=1 + trial_num * len(params))
+    out = {}
+    for name, asd, alpha in params:
+        if asd == 0.0:
+            out[name] = 0.0
+        elif name in ("amplitude", "df"):
+            out[name] = rng.normal(scale=asd * np.sqrt(fs / 2.0), size=int(n_samples))
+        else:
+            raise NotImplementedError(
+                f"coloured '{name}' noise (alpha={alpha}) needs pyplnoise, which is not installed")
+    return out
+
+
+def exact_model_signal(cfg, t, noise, is_dynamic):
+    """physics.py:615-722: exact-delay model via the integrated FM waveform."""
+    laser, ifo = cfg.laser, cfg.ifo
+    omega_mod = 2 * np.pi * laser.f_mod
+    g = laser.waveform_func(omega_mod * t + laser.psi, **laser.waveform_kwargs)
+    gmax = np.max(np.abs(g))
+    g = g / gmax if gmax != 0 else np.zeros_like(g)
+    df_noisy = laser.df + noise.get("df", 0.0)
+    dt = t[1] - t[0]
+    fs = 1 / dt
+    phi_mod = (2 * np.pi / fs) * np.cumsum(df_noisy * g)
+    tau_r = ifo.ref_arml / sc.c
+    tau_m = ifo.meas_arml / sc.c
+    if not is_dynamic:
+        dl = ifo.phi * laser.wavelength / (2 * np.pi)
+    else:
+        dl = (ifo.arml_mod_amp * np.sin(2 * np.pi * ifo.arml_mod_f * t + ifo.arml_mod_psi)
+              + noise.get("armlength", 0.0) + ifo.phi * laser.wavelength / (2 * np.pi))
+    tau_dl = dl / sc.c
+    pm_meas = np.interp(t - (tau_m + tau_dl), t, phi_mod)
+    pm_ref = np.interp(t - tau_r, t, phi_mod)
+    f0 = (sc.c / laser.wavelength) + noise.get("laser_frequency", 0.0)
+    phase = 2 * np.pi * f0 * ((tau_m + tau_dl) - tau_r) + (pm_meas - pm_ref)
+    amp = laser.amp + noise.get("amplitude", 0.0)
+    sig = amp * (1 + laser.visibility * np.cos(phase))
+    truth = (2 * np.pi * sc.c / laser.wavelength) * ((tau_m + tau_dl) - tau_r)
+    if np.isscalar(truth):
+        truth = np.full_like(t, truth, dtype=float)
+    return sig, phase, truth

@@ -1,0 +1,128 @@
+/* dfmi.h — C ABI of libdfmi.so, the MI355X (gfx950) DFMI per-segment NLS readout.
+ *
+ * Every entry point takes plain pointers and sizes; nothing here knows about
+ * torch or numpy. A pointer argument is a HOST pointer when `mem` is
+ * DFMI_MEM_HOST (the library stages it through device memory it owns and
+ * returns after the results are back on the host) or a DEVICE pointer when
+ * `mem` is DFMI_MEM_DEVICE (the library only enqueues kernels on `stream`, a
+ * hipStream_t or NULL for the null stream, and returns without synchronising).
+ * The library keeps no caller pointer after a call returns. HIP is initialised
+ * lazily on the first call (never at load time), so the .so is safe to load in
+ * a process that later forks (fitters.py:422 / experiments.py:381 Pools).
+ *
+ * Return value: 0 on success, a negative DFMI_ERR_* code otherwise; the
+ * message is in dfmi_last_error(). Numerical non-convergence is NOT an error:
+ * it is the per-segment status 0/1/2 of fit.py:334-349, and a singular damped
+ * system yields a zero step exactly as fit.py:197-204.
+ *
+ * Reference interfaces replaced (file:line in mdovale/DeepFMKit):
+ *   dfmi_demod       calculate_quadratures (fit.py:18-66) + the per-buffer means of
+ *                    fitters.py:45-49/380-384/436-440 and dc = mean(buffer)
+ *                    (fitters.py:57/391/446)
+ *   dfmi_lm          fit.fit (fit.py:322-361) incl. _run_lma_fit, msolve, coeffs,
+ *                    ssqf, _find_best_initial_guess (fit.py:68-320), applied per
+ *                    chunk with the warm start of _process_fit_chunk (fitters.py:13-60)
+ *   dfmi_nls_record  StandardNLSFitter._fit_sequential / _fit_parallel
+ *                    (fitters.py:370-428) for one or more records (channels)
+ */
+#ifndef DFMI_H
+#define DFMI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DFMI_OK 0
+#define DFMI_ERR_ARG (-1)
+#define DFMI_ERR_HIP (-2)
+#define DFMI_ERR_NODEV (-3)
+#define DFMI_ERR_UNSUPPORTED (-4)
+
+#define DFMI_MEM_HOST 0
+#define DFMI_MEM_DEVICE 1
+
+#define DFMI_MAX_LAMBDA 16
+
+/* Numerical constants of fit.py:5-16 and the lambda ladder of fit.py:222.
+ * The Python shim fills this from the live `deepfmkit_amd.fit` module globals
+ * at call time (the reference's benchmark notebook overwrites them). */
+typedef struct dfmi_lm_config {
+  int32_t max_lma_steps;          /* MAX_LMA_STEPS (100) */
+  int32_t n_lambda;               /* <= DFMI_MAX_LAMBDA */
+  double lambdas[DFMI_MAX_LAMBDA];/* [0,1e-7,1e-5,1e-3,1e-1,1,10,100] */
+  double min_step_norm;           /* 1e-15 (fit.py:230) */
+  double conv_improve;            /* LMA_CONVERGENCE_IMPROVE (1e-9) */
+  double conv_param_change;       /* LMA_CONVERGENCE_PARAM_CHANGE (1e-9) */
+  double fitok_threshold;         /* FITOK_THRESHOLD (1e-3) */
+  double m_grid_min;              /* M_GRID_MIN (5.0) */
+  double m_grid_max;              /* M_GRID_MAX (30.0) */
+  double m_grid_step;             /* M_GRID_STEP (0.5) */
+  double bessel_amp_threshold;    /* BESSEL_AMP_THRESHOLD (0.05) */
+  double sincos_amp_threshold;    /* SINCOS_AMP_THRESHOLD (0.1) */
+} dfmi_lm_config;
+
+/* Fill `cfg` with the reference defaults (fit.py:5-16, 222, 230). */
+void dfmi_lm_config_default(dfmi_lm_config* cfg);
+
+/* Demodulate nseg segments of R samples each.
+ *   x[s*seg_stride + t], t < R           input samples (float64)
+ *   qi[c*nseg + s], c < 2*ndata          output, component-major: c < ndata is
+ *                                        Q_{c+1} = mean(x cos((c+1) w0 t)),
+ *                                        c >= ndata is I_{c-ndata+1} (sin)
+ *   dc[s]                                output, mean(x) of the segment
+ * period: samples per basis period L (L*w0 = 2*pi*integer), 0 = detect from
+ * w0, -1 = force the direct (per-sample sincos) kernel. */
+int dfmi_demod(const double* x, int64_t nseg, int64_t seg_stride, int32_t R, int32_t ndata, double w0,
+               int32_t period, double* qi, double* dc, int32_t mem, void* stream);
+
+/* Fit nseg demodulated segments.
+ *   qi[c*nseg + s]                       input, layout of dfmi_demod
+ *   guess_per_segment != 0: guess[s*4+i] seeds segment s (every segment its own chunk)
+ *   guess_per_segment == 0: guess[0..3] seeds nchunk np.array_split chunks of the
+ *                           nseg segments, warm start within a chunk
+ *   params[i*nseg + s], i < 4            output amp, m, phi, psi (normalised)
+ *   ssq[s], status[s]                    output */
+int dfmi_lm(const double* qi, int64_t nseg, int32_t ndata, const double* guess, int32_t guess_per_segment,
+            int64_t nchunk, const dfmi_lm_config* cfg, double* params, double* ssq, int32_t* status,
+            int32_t mem, void* stream);
+
+/* Whole StandardNLSFitter pass over nrec records (channels) of nbuf buffers.
+ *   x[r*rec_stride + b*R + t]            input samples
+ *   init_guess[r*4 + i]                  per-record default seed [init_a, init_m, 0, init_psi]
+ *   parallel == 0: one warm-start chain over all nbuf buffers (fitters.py:370-393)
+ *   parallel != 0: buffer 0 fitted from init_guess, then buffers 1..nbuf-1 split
+ *                  into nchunk chunks seeded with buffer 0's result
+ *                  (fitters.py:395-428; nchunk >= nbuf-1 = every buffer its own chunk)
+ *   out[col*(nrec*nbuf) + r*nbuf + b]    col = 0 amp, 1 m, 2 phi, 3 psi, 4 dc, 5 ssq
+ *   fitok[r*nbuf + b]                    status 0/1/2 */
+int dfmi_nls_record(const double* x, int64_t nrec, int64_t rec_stride, int64_t nbuf, int32_t R, int32_t ndata,
+                    double w0, int32_t period, const double* init_guess, int32_t parallel, int64_t nchunk,
+                    const dfmi_lm_config* cfg, double* out, int32_t* fitok, int32_t mem, void* stream);
+
+/* Per-sample EKF (fitters.py:214-320) over nrec independent channels, one lane per
+ * channel. x[r*rec_stride + k], k < n_samp. x0[r*5+i] initial state (dc included),
+ * p0_diag[5], q_diag[5], r_val[r] measurement variance, w_m = 2*pi*f_mod,
+ * f_samp; snapshots every R samples into states[(r*nbuf + b)*5 + i]. */
+int dfmi_ekf(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, const double* x0,
+             const double* p0_diag, const double* q_diag, const double* r_val, double w_m, double f_samp,
+             int32_t R, int64_t nbuf, double* states, int32_t mem, void* stream);
+
+/* Period (samples) the fold kernel would use for this w0, R, ndata; 0 if none. */
+int32_t dfmi_detect_period(double w0, int32_t R, int32_t ndata);
+
+/* Number of visible HIP devices (initialises HIP). */
+int dfmi_device_count(void);
+
+/* Message of the last failed call on this thread ("" if none). */
+const char* dfmi_last_error(void);
+
+/* Library/ABI version, e.g. "dfmi 0.1 gfx950". */
+const char* dfmi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DFMI_H */

@@ -1,0 +1,50 @@
+// hostcheck.hip — TEST-ONLY host build of the product's fp64 numerics.
+//
+// Compiles deepfmkit_amd/csrc/dfmi_math.h and lm.h (whose numerics are
+// __host__ __device__) for the CPU so the CPU test suite can check the Bessel
+// walk and the per-segment LM against the golden vectors without a GPU. The
+// product library never links this; the GPU parity tests (tests/test_gpu_*.py)
+// exercise the real kernels.
+#include <vector>
+#include "../../deepfmkit_amd/csrc/dfmi_math.h"
+#include "../../deepfmkit_amd/csrc/lm.h"
+
+extern "C" {
+
+void hc_bessel_table(double x, int N, double* out) { dfmi_bessel_table(x, N, out); }
+
+// qi component-major (qi[c*n + s]); guess n x 4; constants in the reference order.
+int hc_fit_segments(const double* qi, long n, int ndata, const double* guess, const double* consts,
+                    const double* lambdas, int n_lambda, double* p_out, double* ssq_out, int* status_out) {
+  dfmi::LMConst c{};
+  c.max_steps = (int)consts[0];
+  c.conv_improve = consts[1];
+  c.conv_param_change = consts[2];
+  c.fitok_threshold = consts[3];
+  const double gmin = consts[4], gmax = consts[5], gstep = consts[6];
+  c.bessel_amp_thr = consts[7];
+  c.sincos_amp_thr = consts[8];
+  c.min_step_norm = consts[9];
+  c.n_lambda = n_lambda;
+  for (int i = 0; i < n_lambda; ++i) c.lambdas[i] = lambdas[i];
+  const double stop = gmax + gstep;
+  const double len = ceil((stop - gmin) / gstep);
+  c.n_grid = len > 0 ? (int)len : 0;
+  c.grid_min = gmin;
+  c.grid_delta = (gmin + gstep) - gmin;
+  std::vector<double> tab((size_t)(c.n_grid > 0 ? c.n_grid : 1) * ndata);
+  std::vector<double> row(ndata + 2);
+  for (int g = 0; g < c.n_grid; ++g) {
+    dfmi_bessel_table(gmin + g * c.grid_delta, ndata, row.data());
+    for (int i = 0; i < ndata; ++i) tab[(size_t)g * ndata + i] = row[i + 1];
+  }
+  for (long s = 0; s < n; ++s) {
+    double p[4] = {guess[s * 4], guess[s * 4 + 1], guess[s * 4 + 2], guess[s * 4 + 3]};
+    double ssq;
+    status_out[s] = dfmi::fit_segment(qi + s, n, ndata, tab.data(), c, p, ssq);
+    for (int i = 0; i < 4; ++i) p_out[s * 4 + i] = p[i];
+    ssq_out[s] = ssq;
+  }
+  return 0;
+}
+}

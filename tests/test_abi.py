@@ -1,0 +1,91 @@
+"""The C-ABI library loads and exports every symbol include/dfmi.h declares
+(no compute calls: this runs on the CPU-only container)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    with open(os.path.join(ROOT, "include", "dfmi.h")) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dfmi_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_entry_points():
+    syms = declared_symbols()
+    for s in ("dfmi_demod", "dfmi_lm", "dfmi_nls_record", "dfmi_ekf", "dfmi_last_error", "dfmi_device_count"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    from deepfmkit_amd import _lib
+    lib = _lib.load()
+    nm = ctypes.CDLL(_lib.LIB_PATH)
+    for s in declared_symbols():
+        assert hasattr(nm, s), s
+    assert set(declared_symbols()) == set(_lib.SYMBOLS)
+    assert lib.dfmi_version().decode().startswith("dfmi")
+
+
+def test_library_is_gfx950_code_object():
+    from deepfmkit_amd import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        blob = f.read()
+    assert b"gfx950" in blob
+
+
+def test_default_config_matches_fit_constants():
+    """dfmi_lm_config_default == the reference constants fit.py:5-16, 222, 230."""
+    from deepfmkit_amd import _lib
+    from deepfmkit_amd import fit as F
+    lib = _lib.load()
+    c = _lib.LMConfig()
+    lib.dfmi_lm_config_default(ctypes.byref(c))
+    p = F.lm_config()
+    for name, _ in _lib.LMConfig._fields_:
+        a, b = getattr(c, name), getattr(p, name)
+        if name == "lambdas":
+            assert list(a) == list(b)
+        else:
+            assert a == b, name
+    assert c.n_lambda == 8 and list(c.lambdas)[:8] == [0.0, 1e-7, 1e-5, 1e-3, 1e-1, 1.0, 10.0, 100.0]
+
+
+def test_lm_config_reads_live_module_globals():
+    """Overwriting deepfmkit_amd.fit constants (as notebooks/0.0_benchmark cell 1 does
+    for the reference) changes what the next engine call receives."""
+    from deepfmkit_amd import fit as F
+    old = F.MAX_LMA_STEPS
+    try:
+        F.MAX_LMA_STEPS = 7
+        assert F.lm_config().max_lma_steps == 7
+    finally:
+        F.MAX_LMA_STEPS = old
+
+
+def test_period_detection_host_function():
+    """dfmi_detect_period is pure host code (no GPU): L = f_samp/f_mod when integral."""
+    from deepfmkit_amd import _lib
+    from deepfmkit_amd.fitters import w0_of
+    lib = _lib.load()
+    assert lib.dfmi_detect_period(w0_of(1000.0, 200000.0), 4000, 10) == 200
+    assert lib.dfmi_detect_period(w0_of(400.0, 30000.0), 1500, 10) == 75
+    assert lib.dfmi_detect_period(w0_of(1500.0, 200000.0), 2666, 10) == 400
+    assert lib.dfmi_detect_period(w0_of(1000.0, 199999.7), 4000, 10) == 0
+
+
+def test_no_gpu_here_is_a_loud_error():
+    """Without a GPU the engine must fail loudly (no silent CPU fallback)."""
+    import pytest
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from deepfmkit_amd import fit as F
+    from deepfmkit_amd._lib import DFMIError
+    with pytest.raises(DFMIError):
+        F.demodulate(np.zeros((2, 400)), 10, w0=2 * np.pi / 200)

@@ -1,0 +1,84 @@
+"""CPU pre-validation of the product's fp64 numerics (Bessel walk, per-segment LM)
+through a TEST-ONLY host build of the same headers (tests/hostcheck). The GPU
+parity tests are the real gate; these catch numerics regressions without a GPU."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from conftest import wrapped
+
+HC = os.path.join(os.path.dirname(__file__), "hostcheck", "libhostcheck.so")
+
+
+@pytest.fixture(scope="module")
+def hc():
+    if not os.path.exists(HC):
+        pytest.skip("hostcheck not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(HC)
+    P = ctypes.c_void_p
+    lib.hc_bessel_table.argtypes = [ctypes.c_double, ctypes.c_int, P]
+    lib.hc_fit_segments.argtypes = [P, ctypes.c_long, ctypes.c_int, P, P, P, ctypes.c_int, P, P, P]
+    return lib
+
+
+def test_bessel_vs_scipy_table(hc):
+    """Miller two-pass walk vs scipy.special.jv (the reference's Bessel), n <= 64, |x| <= 64."""
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "bessel.npz"))
+    n, x, jv = d["n"], d["x"], d["jv"]
+    N = int(n.max())
+    out = np.zeros(N + 1)
+    ours = np.zeros_like(jv)
+    for i, xv in enumerate(x):
+        hc.hc_bessel_table(float(xv), N, out.ctypes.data)
+        ours[:, i] = out
+    err = np.abs(ours - jv)
+    assert err[:13].max() <= 1e-15          # orders used at ndata = 10
+    assert err.max() <= 3e-15               # every order <= 64
+    assert (err.max(0) / np.abs(jv).max(0)).max() <= 2e-14
+
+
+def _fit(hc, qi, guess):
+    n, nd2 = qi.shape
+    consts = np.array([100, 1e-9, 1e-9, 1e-3, 5.0, 30.0, 0.5, 0.05, 0.1, 1e-15])
+    lams = np.array([0.0, 1e-7, 1e-5, 1e-3, 1e-1, 1.0, 10.0, 100.0])
+    qcm = np.ascontiguousarray(qi.T)
+    g = np.ascontiguousarray(guess)
+    p = np.zeros((n, 4))
+    ssq = np.zeros(n)
+    st = np.zeros(n, np.int32)
+    hc.hc_fit_segments(qcm.ctypes.data, n, nd2 // 2, g.ctypes.data, consts.ctypes.data, lams.ctypes.data, 8,
+                       p.ctypes.data, ssq.ctypes.data, st.ctypes.data)
+    return st, p, ssq
+
+
+@pytest.mark.parametrize("group", ["10", "5", "20", "30", "62", "edge10"])
+def test_host_lm_vectors(hc, lm_npz, group):
+    qi, g = lm_npz[f"g{group}_qi"], lm_npz[f"g{group}_guess"]
+    st, p, ssq = _fit(hc, qi, g)
+    rs, rp = lm_npz[f"g{group}_status"], lm_npz[f"g{group}_p"]
+    assert (st == rs).all()
+    # a == 0 (all-zero data) leaves m, phi, psi undetermined (ssq = 0 for any value):
+    # only the amplitude is compared there
+    degenerate = np.abs(rp[:, 0]) < 1e-100
+    ok = (rs == 0) & ~degenerate
+    assert np.all(np.abs(p[degenerate, 0]) < 1e-100)
+    d = np.abs(p - rp)
+    d[:, 2] = wrapped(p[:, 2] - rp[:, 2])
+    assert d[ok].max(initial=0) <= 1e-8
+    assert np.mean(d[ok].max(1) <= 1e-9) >= 0.98
+
+
+def test_host_lm_on_reference_qi(hc, records_npz, manifest):
+    """LM on the reference's own QI of the config-1 record, chunk size 1, vs the
+    reference's _fit_parallel(chunk size 1) outputs: the BASELINE tolerance 1e-9."""
+    qi = records_npz["config1_qi"]
+    s0 = np.array([records_npz["config1_c1_" + k][0] for k in ("amp", "m", "phi", "psi")])
+    g = np.tile(s0, (qi.shape[0], 1))
+    g[0] = [1.6, 6.0, 0.0, 0.0]
+    st, p, ssq = _fit(hc, qi, g)
+    assert (st == records_npz["config1_c1_fitok"]).all()
+    for i, k in ((0, "amp"), (1, "m"), (3, "psi")):
+        assert np.abs(p[:, i] - records_npz["config1_c1_" + k]).max() <= 1e-9, k
+    assert wrapped(p[:, 2] - records_npz["config1_c1_phi"]).max() <= 1e-9

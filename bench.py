@@ -196,6 +196,24 @@ def main():
     ev1.record(stream)
     ev1.synchronize()
     demod_ms = ev0.elapsed_time(ev1) / nrep
+    # the LM kernel alone over the same QI (every segment its own chunk), for the record
+    lm_out = torch.empty((4, nbuf), dtype=torch.float64, device=dev)
+    lm_ssq = torch.empty(nbuf, dtype=torch.float64, device=dev)
+    lm_st = torch.empty(nbuf, dtype=torch.int32, device=dev)
+    gdev = torch.tensor([1.0, 6.0, 0.0, 0.0], dtype=torch.float64, device=dev)
+
+    def lm_only():
+        rc = lib.dfmi_lm(qi.data_ptr(), nbuf, NDATA, gdev.data_ptr(), 0, nbuf, cfg, lm_out.data_ptr(),
+                         lm_ssq.data_ptr(), lm_st.data_ptr(), _lib.DFMI_MEM_DEVICE, stream.cuda_stream)
+        _lib.check(rc, "dfmi_lm")
+
+    lm_only()
+    ev0.record(stream)
+    for _ in range(nrep):
+        lm_only()
+    ev1.record(stream)
+    ev1.synchronize()
+    lm_ms = ev0.elapsed_time(ev1) / nrep
     bytes_per_seg = 8 * R + 8 * (2 * NDATA + 1)  # read the segment, write QI + dc
     achieved = nbuf * bytes_per_seg / (demod_ms * 1e-3) / 1e9
     traffic = None
@@ -219,6 +237,7 @@ def main():
                                    f"_fit_parallel chunk size 1",
                        "segments_per_gpu": nseg, "R": R, "ndata": NDATA, "parallelism": f"shard{world}"},
             "roofline": roof,
+            "kernels_ms": {"demod": round(demod_ms, 4), "lm_all_segments": round(lm_ms, 4)},
             "batch_status0_frac": float(np.mean(st == 0)),
             "batch_m_mean": float(res[1].mean())}
     if args.demod_only:

@@ -20,7 +20,7 @@ DFMI_MEM_DEVICE = 1
 MAX_LAMBDA = 16
 
 SYMBOLS = ("dfmi_lm_config_default", "dfmi_demod", "dfmi_lm", "dfmi_nls_record", "dfmi_ekf",
-           "dfmi_detect_period", "dfmi_device_count", "dfmi_last_error", "dfmi_version")
+           "dfmi_detect_period", "dfmi_device_count", "dfmi_last_error", "dfmi_version", "dfmi_set_tuning")
 
 
 class DFMIError(RuntimeError):
@@ -77,6 +77,8 @@ def load():
         lib.dfmi_device_count.restype = ctypes.c_int
         lib.dfmi_last_error.argtypes = []
         lib.dfmi_last_error.restype = ctypes.c_char_p
+        lib.dfmi_set_tuning.argtypes = [ctypes.c_char_p, i64]
+        lib.dfmi_set_tuning.restype = ctypes.c_int
         lib.dfmi_version.argtypes = []
         lib.dfmi_version.restype = ctypes.c_char_p
         _lib = lib

@@ -193,7 +193,7 @@ class DeepFitFramework:
         R, fs, nbuf = self.fit_init(labels[0], n)
         out = {}
         if method == "ekf":
-            states = _fitters.ekf_records(raws, n, **kwargs)
+            states = _fitters.ekf_records(raws, n, **{k: v for k, v in kwargs.items() if k != "n"})
             for l, raw, st in zip(labels, raws, states):
                 import pandas as pd
                 df = pd.DataFrame({"amp": st[:, 0], "m": st[:, 1], "phi": st[:, 2], "psi": st[:, 3], "dc": st[:, 4],

@@ -83,12 +83,21 @@ template <>
 struct VecT<1> {
   using T = double;
   __device__ static __forceinline__ void load(const double* p, double (&o)[1]) { o[0] = *p; }
+  __device__ static __forceinline__ void load_nt(const double* p, double (&o)[1]) {
+    o[0] = __builtin_nontemporal_load(p);
+  }
 };
 template <>
 struct VecT<2> {
   using T = double2;
   __device__ static __forceinline__ void load(const double* p, double (&o)[2]) {
     const double2 v = *reinterpret_cast<const double2*>(p);
+    o[0] = v.x;
+    o[1] = v.y;
+  }
+  __device__ static __forceinline__ void load_nt(const double* p, double (&o)[2]) {
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(p));
     o[0] = v.x;
     o[1] = v.y;
   }
@@ -107,8 +116,114 @@ __device__ __forceinline__ void store_block(const double (&v)[16], int lane, int
   }
 }
 
-// MAXSLOT: compile-time bound on nslot = ceil(L / (64·VEC)).
-template <int VEC, int MAXSLOT, bool LDS_TAB>
+// One segment, one wavefront: fold + dc + contraction (see the header comment).
+// T: basis table (LDS or global), col: the segment's column in qi / dc.
+// MAXSLOT: compile-time bound on nslot = ceil(L / (64·VEC)); LOADS: vector loads
+// kept in flight per lane in the fold loop; NT: non-temporal (streaming) loads.
+template <int VEC, int MAXSLOT, int LOADS = 8, bool NT = true>
+__device__ __forceinline__ void fold_segment(const double* __restrict__ xs, int R, int L, int ndata,
+                                             const double* __restrict__ T, int lane, double* __restrict__ qi,
+                                             int64_t qi_ld, int64_t col, double* __restrict__ dc) {
+  const int nslot = (L + 64 * VEC - 1) / (64 * VEC);
+  const int ncyc = R / L;
+  const int rem = R - ncyc * L;
+  constexpr int UNR = (MAXSLOT >= LOADS) ? 1 : (LOADS / MAXSLOT);
+  const int nblk = (ndata + kHarmBlock - 1) / kHarmBlock;
+  int pbase[MAXSLOT];
+  bool pval[MAXSLOT];
+#pragma unroll
+  for (int j = 0; j < MAXSLOT; ++j) {
+    pbase[j] = VEC * (lane + 64 * j);
+    pval[j] = (j < nslot) && (pbase[j] < L);
+  }
+  double y[MAXSLOT][VEC];
+#pragma unroll
+  for (int j = 0; j < MAXSLOT; ++j)
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) y[j][e] = 0.0;
+
+  // ---- fold: y[p] += x[p + k L] over the full cycles ----
+  int k = 0;
+  for (; k + UNR <= ncyc; k += UNR) {
+    double v[UNR][MAXSLOT][VEC];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+#pragma unroll
+      for (int j = 0; j < MAXSLOT; ++j) {
+        if (pval[j]) {
+          if constexpr (NT) VecT<VEC>::load_nt(xs + (int64_t)(k + u) * L + pbase[j], v[u][j]);
+          else VecT<VEC>::load(xs + (int64_t)(k + u) * L + pbase[j], v[u][j]);
+        }
+        else {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) v[u][j][e] = 0.0;
+        }
+      }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+#pragma unroll
+      for (int j = 0; j < MAXSLOT; ++j)
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) y[j][e] += v[u][j][e];
+  }
+  for (; k < ncyc; ++k) {
+#pragma unroll
+    for (int j = 0; j < MAXSLOT; ++j) {
+      if (pval[j]) {
+        double v[VEC];
+        VecT<VEC>::load(xs + (int64_t)k * L + pbase[j], v);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) y[j][e] += v[e];
+      }
+    }
+  }
+  if (rem) {  // ragged last cycle: element-wise bounds
+    const double* xr = xs + (int64_t)ncyc * L;
+#pragma unroll
+    for (int j = 0; j < MAXSLOT; ++j)
+#pragma unroll
+      for (int e = 0; e < VEC; ++e)
+        if (pval[j] && pbase[j] + e < rem) y[j][e] += xr[pbase[j] + e];
+  }
+
+  // ---- dc = mean(x) ----
+  double tot = 0.0;
+#pragma unroll
+  for (int j = 0; j < MAXSLOT; ++j)
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) tot += y[j][e];
+  tot = wave_sum(tot);
+  if (lane == 0) dc[col] = tot / (double)R;
+
+  // ---- contraction with the basis, 8 harmonics per block ----
+  for (int hb = 0; hb < nblk; ++hb) {
+    double acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0;
+#pragma unroll
+    for (int j = 0; j < MAXSLOT; ++j) {
+      if (!pval[j]) continue;
+#pragma unroll
+      for (int h = 0; h < kHarmBlock; ++h) {
+        const int hh = hb * kHarmBlock + h;
+        if (hh < ndata) {
+          double bc[VEC], bs[VEC];
+          VecT<VEC>::load(T + (int64_t)hh * L + pbase[j], bc);
+          VecT<VEC>::load(T + (int64_t)(ndata + hh) * L + pbase[j], bs);
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) {
+            acc[h] = fma(y[j][e], bc[e], acc[h]);
+            acc[8 + h] = fma(y[j][e], bs[e], acc[8 + h]);
+          }
+        }
+      }
+    }
+    butterfly16(acc, lane);
+    store_block(acc, lane, hb, ndata, qi, qi_ld, col, R);
+  }
+}
+
+template <int VEC, int MAXSLOT, bool LDS_TAB, int LOADS = 8, bool NT = true>
 __global__ __launch_bounds__(kBlockThreads) void demod_fold_kernel(
     const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
     const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc) {
@@ -121,147 +236,56 @@ __global__ __launch_bounds__(kBlockThreads) void demod_fold_kernel(
   const double* __restrict__ T = LDS_TAB ? lds_tab : tab;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int nslot = (L + 64 * VEC - 1) / (64 * VEC);
-  const int ncyc = R / L;
-  const int rem = R - ncyc * L;
-  constexpr int UNR = (MAXSLOT >= 8) ? 1 : (8 / MAXSLOT);
-  const int nblk = (ndata + kHarmBlock - 1) / kHarmBlock;
-
-  int pbase[MAXSLOT];
-  bool pval[MAXSLOT];
-#pragma unroll
-  for (int j = 0; j < MAXSLOT; ++j) {
-    pbase[j] = VEC * (lane + 64 * j);
-    pval[j] = (j < nslot) && (pbase[j] < L);
-  }
-
   for (int64_t s = (int64_t)blockIdx.x * kWavesPerBlock + wave; s < nseg;
        s += (int64_t)gridDim.x * kWavesPerBlock) {
-    const double* __restrict__ xs = x + s * seg_stride;
-    double y[MAXSLOT][VEC];
-#pragma unroll
-    for (int j = 0; j < MAXSLOT; ++j)
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) y[j][e] = 0.0;
-
-    // ---- fold: y[p] += x[p + k L] over the full cycles ----
-    int k = 0;
-    for (; k + UNR <= ncyc; k += UNR) {
-      double v[UNR][MAXSLOT][VEC];
-#pragma unroll
-      for (int u = 0; u < UNR; ++u)
-#pragma unroll
-        for (int j = 0; j < MAXSLOT; ++j) {
-          if (pval[j]) VecT<VEC>::load(xs + (int64_t)(k + u) * L + pbase[j], v[u][j]);
-          else {
-#pragma unroll
-            for (int e = 0; e < VEC; ++e) v[u][j][e] = 0.0;
-          }
-        }
-#pragma unroll
-      for (int u = 0; u < UNR; ++u)
-#pragma unroll
-        for (int j = 0; j < MAXSLOT; ++j)
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) y[j][e] += v[u][j][e];
-    }
-    for (; k < ncyc; ++k) {
-#pragma unroll
-      for (int j = 0; j < MAXSLOT; ++j) {
-        if (pval[j]) {
-          double v[VEC];
-          VecT<VEC>::load(xs + (int64_t)k * L + pbase[j], v);
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) y[j][e] += v[e];
-        }
-      }
-    }
-    if (rem) {  // ragged last cycle: element-wise bounds
-      const double* xr = xs + (int64_t)ncyc * L;
-#pragma unroll
-      for (int j = 0; j < MAXSLOT; ++j)
-#pragma unroll
-        for (int e = 0; e < VEC; ++e)
-          if (pval[j] && pbase[j] + e < rem) y[j][e] += xr[pbase[j] + e];
-    }
-
-    // ---- dc = mean(x) ----
-    double tot = 0.0;
-#pragma unroll
-    for (int j = 0; j < MAXSLOT; ++j)
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) tot += y[j][e];
-    tot = wave_sum(tot);
-    if (lane == 0) dc[s] = tot / (double)R;
-
-    // ---- contraction with the basis, 8 harmonics per block ----
-    for (int hb = 0; hb < nblk; ++hb) {
-      double acc[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] = 0.0;
-#pragma unroll
-      for (int j = 0; j < MAXSLOT; ++j) {
-        if (!pval[j]) continue;
-#pragma unroll
-        for (int h = 0; h < kHarmBlock; ++h) {
-          const int hh = hb * kHarmBlock + h;
-          if (hh < ndata) {
-            double bc[VEC], bs[VEC];
-            VecT<VEC>::load(T + (int64_t)hh * L + pbase[j], bc);
-            VecT<VEC>::load(T + (int64_t)(ndata + hh) * L + pbase[j], bs);
-#pragma unroll
-            for (int e = 0; e < VEC; ++e) {
-              acc[h] = fma(y[j][e], bc[e], acc[h]);
-              acc[8 + h] = fma(y[j][e], bs[e], acc[8 + h]);
-            }
-          }
-        }
-      }
-      butterfly16(acc, lane);
-      store_block(acc, lane, hb, ndata, qi, qi_ld, s, R);
-    }
+    fold_segment<VEC, MAXSLOT, LOADS, NT>(x + s * seg_stride, R, L, ndata, T, lane, qi, qi_ld, s, dc);
   }
 }
 
 // Fallback when no short integer period exists: per-sample angles
 // fl(fl(h·w0)·t) exactly as fit.py:55-64 forms them, sincos on the device.
 // VALU-bound; only used for unusual f_samp/f_mod ratios.
+__device__ __forceinline__ void direct_segment(const double* __restrict__ xs, int R, int ndata, double w0, int lane,
+                                               double* __restrict__ qi, int64_t qi_ld, int64_t col,
+                                               double* __restrict__ dc) {
+  const int nblk = (ndata + kHarmBlock - 1) / kHarmBlock;
+  double tot = 0.0;
+  for (int t = lane; t < R; t += 64) tot += xs[t];
+  tot = wave_sum(tot);
+  if (lane == 0) dc[col] = tot / (double)R;
+  for (int hb = 0; hb < nblk; ++hb) {
+    double acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0;
+    double wh[kHarmBlock];
+#pragma unroll
+    for (int h = 0; h < kHarmBlock; ++h) wh[h] = (double)(hb * kHarmBlock + h + 1) * w0;
+    for (int t = lane; t < R; t += 64) {
+      const double xv = xs[t];
+      const double tt = (double)t;
+#pragma unroll
+      for (int h = 0; h < kHarmBlock; ++h) {
+        if (hb * kHarmBlock + h < ndata) {
+          double sn, cs;
+          sincos(wh[h] * tt, &sn, &cs);
+          acc[h] = fma(xv, cs, acc[h]);
+          acc[8 + h] = fma(xv, sn, acc[8 + h]);
+        }
+      }
+    }
+    butterfly16(acc, lane);
+    store_block(acc, lane, hb, ndata, qi, qi_ld, col, R);
+  }
+}
+
 __global__ __launch_bounds__(kBlockThreads) void demod_direct_kernel(
     const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int ndata, double w0,
     double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int nblk = (ndata + kHarmBlock - 1) / kHarmBlock;
   for (int64_t s = (int64_t)blockIdx.x * kWavesPerBlock + wave; s < nseg;
        s += (int64_t)gridDim.x * kWavesPerBlock) {
-    const double* __restrict__ xs = x + s * seg_stride;
-    double tot = 0.0;
-    for (int t = lane; t < R; t += 64) tot += xs[t];
-    tot = wave_sum(tot);
-    if (lane == 0) dc[s] = tot / (double)R;
-    for (int hb = 0; hb < nblk; ++hb) {
-      double acc[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] = 0.0;
-      double wh[kHarmBlock];
-#pragma unroll
-      for (int h = 0; h < kHarmBlock; ++h) wh[h] = (double)(hb * kHarmBlock + h + 1) * w0;
-      for (int t = lane; t < R; t += 64) {
-        const double xv = xs[t];
-        const double tt = (double)t;
-#pragma unroll
-        for (int h = 0; h < kHarmBlock; ++h) {
-          if (hb * kHarmBlock + h < ndata) {
-            double sn, cs;
-            sincos(wh[h] * tt, &sn, &cs);
-            acc[h] = fma(xv, cs, acc[h]);
-            acc[8 + h] = fma(xv, sn, acc[8 + h]);
-          }
-        }
-      }
-      butterfly16(acc, lane);
-      store_block(acc, lane, hb, ndata, qi, qi_ld, s, R);
-    }
+    direct_segment(x + s * seg_stride, R, ndata, w0, lane, qi, qi_ld, s, dc);
   }
 }
 

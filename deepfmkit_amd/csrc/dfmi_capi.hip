@@ -20,6 +20,7 @@
 #include "dfmi_math.h"
 #include "ekf.h"
 #include "lm.h"
+#include "seed.h"
 
 namespace {
 
@@ -50,6 +51,8 @@ struct DeviceState {
   std::map<std::string, DevBuf> ws;                                  // named workspaces
   std::map<std::tuple<int, int, uint64_t>, DevBuf> basis;            // (L, ndata, w0 bits)
   std::map<std::tuple<int, uint64_t, uint64_t, uint64_t>, DevBuf> gridtab;  // (ndata, min, max, step)
+  hipStream_t side = nullptr;  // seed step runs here, concurrently with the bulk demod
+  hipEvent_t ev_in = nullptr, ev_seed = nullptr;
 };
 
 std::map<int, DeviceState> g_dev;
@@ -75,6 +78,9 @@ int ensure_init(int* dev_out) {
     HIPCHK(hipGetDeviceProperties(&prop, dev));
     ds.n_cu = prop.multiProcessorCount;
     ds.lds_per_block = prop.sharedMemPerBlock;
+    HIPCHK(hipStreamCreateWithFlags(&ds.side, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&ds.ev_in, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ds.ev_seed, hipEventDisableTiming));
     ds.init = true;
   }
   *dev_out = dev;
@@ -181,6 +187,14 @@ int to_lmconst(const dfmi_lm_config* cfg, dfmi::LMConst* c) {
 
 constexpr int kMaxSlotCap = 8;
 
+// Tuning knobs (dfmi_set_tuning): measured, then frozen as defaults.
+struct Tuning {
+  int demod_loads = 8;         // vector loads in flight per lane (8 or 16)
+  int demod_nt = 1;            // non-temporal stream loads (measured +14 %, profiles/r01_tune_demod.json)
+  int demod_blocks_per_cu = 0; // 0 = occupancy limit
+};
+Tuning g_tune;
+
 int32_t detect_period_impl(double w0, int32_t R, int32_t ndata) {
   if (!(w0 > 0) || R <= 0 || ndata <= 0) return 0;
   const double two_pi = 6.283185307179586;
@@ -196,14 +210,23 @@ int32_t detect_period_impl(double w0, int32_t R, int32_t ndata) {
   return 0;
 }
 
-template <int VEC, int MS, bool LDS>
+template <int VEC, int MS, bool LDS, int LOADS = 8, bool NT = true>
 int launch_fold_t(const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tab,
                   double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu) {
+  if constexpr (VEC == 2 && MS == 2 && LDS && LOADS == 8 && NT) {  // the BASELINE shape: tunable
+    if (g_tune.demod_loads == 16 && g_tune.demod_nt)
+      return launch_fold_t<2, 2, true, 16, true>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
+    if (g_tune.demod_loads == 16)
+      return launch_fold_t<2, 2, true, 16, false>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
+    if (!g_tune.demod_nt)
+      return launch_fold_t<2, 2, true, 8, false>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
+  }
   const size_t lds = LDS ? (size_t)2 * ndata * L * sizeof(double) : 0;
-  auto kern = dfmi::demod_fold_kernel<VEC, MS, LDS>;
+  auto kern = dfmi::demod_fold_kernel<VEC, MS, LDS, LOADS, NT>;
   int per_cu = 0;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, dfmi::kBlockThreads, lds));
   if (per_cu < 1) per_cu = 1;
+  if (g_tune.demod_blocks_per_cu > 0 && g_tune.demod_blocks_per_cu < per_cu) per_cu = g_tune.demod_blocks_per_cu;
   int64_t need = (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock;
   int64_t grid = (int64_t)n_cu * per_cu;
   if (grid > need) grid = need;
@@ -282,8 +305,11 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
   const int64_t lanes = nrec * nchunk;
   const int block = 64;
   const int64_t grid = (lanes + block - 1) / block;
-  hipLaunchKernelGGL(dfmi::lm_chunks_kernel, dim3((unsigned)grid), dim3(block), 0, st, qi, qi_ld, ndata, nrec, nbuf,
-                     first, nitems, nchunk, guess_dev, g_rec, g_comp, ginl, use_inline, jtab, c, out, out_ld, status);
+  // register path for ndata <= 16 (QI/Bessel in registers), general path above
+  auto kern = ndata <= 12 ? dfmi::lm_chunks_kernel<12> : ndata <= 16 ? dfmi::lm_chunks_kernel<16>
+                                                                    : dfmi::lm_chunks_kernel<0>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(block), 0, st, qi, qi_ld, ndata, nrec, nbuf, first, nitems,
+                     nchunk, guess_dev, g_rec, g_comp, ginl, use_inline, jtab, c, out, out_ld, status);
   HIPCHK(hipGetLastError());
   return DFMI_OK;
 }
@@ -295,6 +321,7 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
                       hipStream_t st) {
   const int64_t nseg = nrec * nbuf;
   if (nseg == 0) return DFMI_OK;
+  DeviceState& ds = g_dev[dev];
   void* qiw = nullptr;
   int rc = workspace(dev, "qi", (size_t)2 * ndata * nseg * sizeof(double), &qiw);
   if (rc) return rc;
@@ -304,6 +331,39 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
   if (rc) return rc;
   const int64_t out_ld = nseg;
   double* dc = out + 4 * out_ld;
+  // guesses: inline kernel arguments for up to 8 records, a device table otherwise
+  const double* gdev = nullptr;
+  if (nrec > 8) {
+    void* gw = nullptr;
+    rc = workspace(dev, "guess", (size_t)nrec * 4 * sizeof(double), &gw);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(gw, init_guess_host, (size_t)nrec * 4 * sizeof(double), hipMemcpyHostToDevice, st));
+    gdev = (const double*)gw;
+  }
+  dfmi::GuessInline ginl;
+  memset(&ginl, 0, sizeof(ginl));
+  if (nrec <= 8)
+    for (int64_t r = 0; r < nrec; ++r)
+      for (int i = 0; i < 4; ++i) ginl.v[r][i] = init_guess_host[r * 4 + i];
+
+  if (parallel) {
+    // seed step (buffer 0 of every record) on the side stream, overlapping the bulk demod
+    int L = period;
+    if (L == 0) L = detect_period_impl(w0, R, ndata);
+    if (L > 64 * 16) L = 0;
+    const double* tab = nullptr;
+    if (L > 0 && (rc = basis_table(dev, L, ndata, w0, st, &tab))) return rc;
+    void *qs, *ds_;
+    if ((rc = workspace(dev, "qi_seed", (size_t)2 * ndata * nrec * 8, &qs))) return rc;
+    if ((rc = workspace(dev, "dc_seed", (size_t)nrec * 8, &ds_))) return rc;
+    HIPCHK(hipEventRecord(ds.ev_in, st));
+    HIPCHK(hipStreamWaitEvent(ds.side, ds.ev_in, 0));
+    auto sk = ndata <= 12 ? dfmi::seed_kernel<12> : ndata <= 16 ? dfmi::seed_kernel<16> : dfmi::seed_kernel<0>;
+    hipLaunchKernelGGL(sk, dim3((unsigned)nrec), dim3(64), 0, ds.side, x, rec_stride, R, L, ndata, w0, tab,
+                       (double*)qs, (double*)ds_, nrec, gdev, ginl, gdev ? 0 : 1, jtab, c, out, out_ld, nbuf, fitok);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ds.ev_seed, ds.side));
+  }
   if (rec_stride == nbuf * (int64_t)R) {
     rc = demod_device(dev, x, nseg, R, R, ndata, w0, period, qi, nseg, dc, st);
     if (rc) return rc;
@@ -314,23 +374,12 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
       if (rc) return rc;
     }
   }
-  // guesses: inline kernel arguments for up to 8 records, a device table otherwise
-  const double* gdev = nullptr;
-  if (nrec > 8) {
-    void* gw = nullptr;
-    rc = workspace(dev, "guess", (size_t)nrec * 4 * sizeof(double), &gw);
-    if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(gw, init_guess_host, (size_t)nrec * 4 * sizeof(double), hipMemcpyHostToDevice, st));
-    gdev = (const double*)gw;
-  }
   if (!parallel) {
     return lm_device(dev, qi, nseg, ndata, nrec, nbuf, 0, nbuf, 1, gdev, 4, 1, init_guess_host, c, jtab, out, out_ld,
                      fitok, st);
   }
-  // seed step: buffer 0 of every record from the default seed
-  rc = lm_device(dev, qi, nseg, ndata, nrec, nbuf, 0, 1, 1, gdev, 4, 1, init_guess_host, c, jtab, out, out_ld, fitok,
-                 st);
-  if (rc || nbuf <= 1) return rc;
+  HIPCHK(hipStreamWaitEvent(st, ds.ev_seed, 0));
+  if (nbuf <= 1) return DFMI_OK;
   // the rest, seeded with each record's buffer-0 result (read on device: no host sync)
   return lm_device(dev, qi, nseg, ndata, nrec, nbuf, 1, nbuf - 1, nchunk, out, nbuf, out_ld, nullptr, c, jtab, out,
                    out_ld, fitok, st);
@@ -371,6 +420,25 @@ int dfmi_device_count(void) {
 const char* dfmi_last_error(void) { return g_err.c_str(); }
 
 const char* dfmi_version(void) { return "dfmi 0.1 gfx950"; }
+
+int dfmi_set_tuning(const char* key, int64_t value) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_err.clear();
+  if (!key) return fail(DFMI_ERR_ARG, "null key");
+  const std::string k(key);
+  if (k == "demod_loads") {
+    if (value != 8 && value != 16) return fail(DFMI_ERR_ARG, "demod_loads must be 8 or 16");
+    g_tune.demod_loads = (int)value;
+  } else if (k == "demod_nt") {
+    g_tune.demod_nt = value ? 1 : 0;
+  } else if (k == "demod_blocks_per_cu") {
+    if (value < 0) return fail(DFMI_ERR_ARG, "demod_blocks_per_cu < 0");
+    g_tune.demod_blocks_per_cu = (int)value;
+  } else {
+    return fail(DFMI_ERR_ARG, "unknown tuning key " + k);
+  }
+  return DFMI_OK;
+}
 
 int dfmi_demod(const double* x, int64_t nseg, int64_t seg_stride, int32_t R, int32_t ndata, double w0,
                int32_t period, double* qi, double* dc, int32_t mem, void* stream) {

@@ -30,17 +30,13 @@
 
 #define DFMI_BES_BIG_EXP 600
 
-// Start order of the backward recurrence (even). Chosen so that the truncation
-// error is below 1e-17 of max|J| for 0 <= N <= 128, |x| <= 128.
+// Start order of the backward recurrence (even). Fitted to the minimal order at
+// which the truncation error sinks below the fp64 rounding floor (checked against
+// mpmath for N <= 63, |x| <= 64): M = max(N + 10, 1.1|x| + 14 + 3 sqrt|x|).
 DFMI_HD int dfmi_bessel_start(int N, double ax) {
-  double base = (double)N > ax ? (double)N : ax;
-  int M = (int)(base + 24.0 + 3.2 * sqrt(base + 1.0));
-  if (ax < 1.0) {
-    // small argument: J_k decays like (x/2)^k/k!, a short run is exact and
-    // keeps the dynamic range inside the rescale scheme
-    int Ms = N + 18;
-    if (Ms < M) M = Ms;
-  }
+  const double mx = 1.1 * ax + 14.0 + 3.0 * sqrt(ax);
+  int M = (int)mx + 1;
+  if (M < N + 10) M = N + 10;
   return (M + 1) & ~1;
 }
 

@@ -1,8 +1,8 @@
 // lm.h — per-segment Levenberg–Marquardt kernel for gfx950 (fp64).
 //
 // Reference (file:line in /root/reference):
-//   coeffs ................... fit.py:68-150   -> eval_full
-//   ssqf ..................... fit.py:152-167  -> eval_ssq
+//   coeffs ................... fit.py:68-150   -> eval_reg / eval_gen (FULL)
+//   ssqf ..................... fit.py:152-167  -> the ssq of the same evaluation
 //   msolve ................... fit.py:169-206  -> damped_solve
 //   _run_lma_fit ............. fit.py:208-258  -> lm_descend
 //   _find_best_initial_guess . fit.py:260-320  -> m_grid_seed
@@ -12,15 +12,20 @@
 // Mapping: ONE LANE OWNS ONE CHUNK (a run of segments fitted with a warm-start
 // chain, np.array_split semantics). With chunk size 1 — the default GPU mode —
 // every lane fits one segment, so a wave fits 64 segments at once with no
-// shuffles at all; the whole 4-parameter problem (2·ndata residuals, J^T J,
-// J^T r, the damped 4×4 solve) lives in that lane's registers. QI is stored
-// component-major (qi[c·ld + s]) so the 64 lanes of a wave read each harmonic
-// with one coalesced load.
+// cross-lane traffic; the 4-parameter problem (2·ndata residuals, J^T J, J^T r,
+// the damped 4×4 solve) lives in that lane's registers. QI is stored
+// component-major (qi[c·ld + s]) so a wave loads each component coalesced.
 //
-// Bessel values come from the two-pass Miller walk in dfmi_math.h, evaluated in
-// DESCENDING harmonic order so that no per-lane array is needed; harmonic
-// sums are therefore accumulated from j = ndata down to 1 (rounding-level
-// difference to the reference's BLAS dot, covered by the parity tolerances).
+// Two code paths, chosen per launch from ndata:
+//  * register path (ndata <= NDMAX, NDMAX = 12 or 16): QI, J_0..J_{NDMAX+1}(m)
+//    and cos/sin(j psi) live in registers; the Bessel values come from ONE
+//    backward Miller pass that stores the low orders as it goes; harmonics are
+//    accumulated in ascending j like the reference's vector expressions.
+//  * general path (any ndata, e.g. 30/62): the two-pass Miller walk of
+//    dfmi_math.h hands out J values in descending order, nothing is stored.
+// A trial point's evaluation always includes J^T J and J^T r: the reference
+// recomputes coeffs() at an accepted trial point (fit.py:250-251), which here
+// is the evaluation already in hand (same numbers, one Bessel pass less).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -46,8 +51,10 @@ struct LMConst {
   double grid_delta;         // (min + step) - min, numpy arange fill
 };
 
+#define DFMI_HDI __host__ __device__ __forceinline__
+
 // cos(phi + j*pi/2) from (cos phi, sin phi): j mod 4 -> c, -s, -c, s
-__host__ __device__ __forceinline__ double quarter_turn(int j, double c, double s) {
+DFMI_HDI double quarter_turn(int j, double c, double s) {
   switch (j & 3) {
     case 0: return c;
     case 1: return -s;
@@ -62,33 +69,156 @@ struct Eval {
   double g0, g1, g2, g3;                                   // J^T r
 };
 
-// Harmonic walk shared by eval_full / eval_ssq: calls body(j, Jm1, J0, Jp1,
-// cos(j psi), sin(j psi)) for j = ndata..1.
+// One harmonic's contribution (fit.py:110-148 for harmonic j).
+DFMI_HDI void harmonic_term(Eval& e, int j, double a, bool a_nz, double cph, double sph, double Jm1, double J0,
+                            double Jp1, double cj, double sj, double Q, double I) {
+  const double pt = quarter_turn(j, cph, sph);       // cos(phi + j pi/2)
+  const double ptd = quarter_turn(j + 1, cph, sph);  // cos(phi + j pi/2 + pi/2)
+  const double common = a * pt * J0;
+  const double mq = common * cj;
+  const double mi = -common * sj;
+  const double rq = Q - mq;
+  const double ri = I - mi;
+  e.ssq = fma(rq, rq, e.ssq);
+  e.ssq = fma(ri, ri, e.ssq);
+  // d model / d a = model / a (fit.py:126-128), written without the division
+  const double base = pt * J0;
+  const double q0 = a_nz ? base * cj : 0.0;
+  const double i0 = a_nz ? -base * sj : 0.0;
+  const double dJ = 0.5 * (Jm1 - Jp1);
+  const double cm = a * pt * dJ;
+  const double q1 = cm * cj, i1 = -cm * sj;
+  const double cphi = a * ptd * J0;
+  const double q2 = cphi * cj, i2 = -cphi * sj;
+  const double q3 = common * -sj * (double)j, i3 = -common * cj * (double)j;
+  e.a00 += q0 * q0 + i0 * i0;
+  e.a01 += q0 * q1 + i0 * i1;
+  e.a02 += q0 * q2 + i0 * i2;
+  e.a03 += q0 * q3 + i0 * i3;
+  e.a11 += q1 * q1 + i1 * i1;
+  e.a12 += q1 * q2 + i1 * i2;
+  e.a13 += q1 * q3 + i1 * i3;
+  e.a22 += q2 * q2 + i2 * i2;
+  e.a23 += q2 * q3 + i2 * i3;
+  e.a33 += q3 * q3 + i3 * i3;
+  e.g0 += q0 * rq + i0 * ri;
+  e.g1 += q1 * rq + i1 * ri;
+  e.g2 += q2 * rq + i2 * ri;
+  e.g3 += q3 * rq + i3 * ri;
+}
+
+DFMI_HDI void eval_zero(Eval& e) { e = Eval{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; }
+
+// ---------------------------------------------------------------------------
+// Register path
+// ---------------------------------------------------------------------------
+
+// J_0..J_{NB-1}(x) into registers with one backward Miller pass.
+template <int NB>
+DFMI_HDI void bessel_regs(double x, int N, double (&J)[NB]) {
+  if (x == 0.0) {
+#pragma unroll
+    for (int k = 0; k < NB; ++k) J[k] = (k == 0) ? 1.0 : 0.0;
+    return;
+  }
+  const double ax = fabs(x);
+  if (!(ax < 1.0e5)) {
+#pragma unroll
+    for (int k = 0; k < NB; ++k) J[k] = __builtin_nan("");
+    return;
+  }
+  if (ax < DFMI_BES_TINY) {
+#pragma unroll
+    for (int k = 0; k < NB; ++k) J[k] = dfmi_bessel_series(k, x);
+    return;
+  }
+  int M = dfmi_bessel_start(N, ax);
+  if (M < NB) M = (NB + 1) & ~1;
+  const double tox = 2.0 / ax;
+  const double big = ldexp(1.0, DFMI_BES_BIG_EXP);
+  double fp1 = 0.0, f = 1.0, S = 2.0;  // order M (even) contributes 2 f_M
+  for (int k = M; k >= NB; --k) {
+    double fm1 = fma((double)k * tox, f, -fp1);
+    if (fabs(fm1) > big) {
+      fm1 = ldexp(fm1, -DFMI_BES_BIG_EXP);
+      f = ldexp(f, -DFMI_BES_BIG_EXP);
+      S = ldexp(S, -DFMI_BES_BIG_EXP);
+    }
+    if (((k - 1) & 1) == 0) S += 2.0 * fm1;
+    fp1 = f;
+    f = fm1;
+  }
+  J[NB - 1] = f;
+#pragma unroll
+  for (int k = NB - 1; k >= 1; --k) {
+    double fm1 = fma((double)k * tox, f, -fp1);
+    if (fabs(fm1) > big) {
+      fm1 = ldexp(fm1, -DFMI_BES_BIG_EXP);
+      f = ldexp(f, -DFMI_BES_BIG_EXP);
+      S = ldexp(S, -DFMI_BES_BIG_EXP);
+#pragma unroll
+      for (int i = k; i < NB; ++i) J[i] = ldexp(J[i], -DFMI_BES_BIG_EXP);
+    }
+    J[k - 1] = fm1;
+    if (k - 1 == 0) S += fm1;
+    else if (((k - 1) & 1) == 0) S += 2.0 * fm1;
+    fp1 = f;
+    f = fm1;
+  }
+  const double invS = 1.0 / S;
+  const bool neg = x < 0.0;
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const double v = J[k] * invS;
+    J[k] = (neg && (k & 1)) ? -v : v;
+  }
+}
+
+template <int NDMAX>
+DFMI_HDI void eval_reg(const double (&q)[2 * NDMAX], int nd, const double (&p)[4], Eval& e) {
+  const double a = p[0], m = p[1], phi = p[2], psi = p[3];
+  double sph, cph, s1, c1;
+  sincos(phi, &sph, &cph);
+  sincos(psi, &s1, &c1);
+  double J[NDMAX + 2];
+  bessel_regs<NDMAX + 2>(m, nd + 1, J);
+  const bool a_nz = (a != 0.0);
+  eval_zero(e);
+  double cj = c1, sj = s1;  // cos(j psi), sin(j psi) at j = 1
+#pragma unroll
+  for (int j = 1; j <= NDMAX; ++j) {
+    if (j <= nd) harmonic_term(e, j, a, a_nz, cph, sph, J[j - 1], J[j], J[j + 1], cj, sj, q[j - 1], q[NDMAX + j - 1]);
+    const double cn = fma(cj, c1, -(sj * s1));
+    const double sn = fma(sj, c1, cj * s1);
+    cj = cn;
+    sj = sn;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// General path: QI from global memory, two-pass Bessel walk (descending j).
+// ---------------------------------------------------------------------------
 template <typename Body>
-__host__ __device__ __forceinline__ void harmonic_walk(int ndata, double m, double psi, Body&& body) {
+DFMI_HDI void harmonic_walk(int ndata, double m, double psi, Body&& body) {
   double s1, c1;
   sincos(psi, &s1, &c1);
   double sj, cj;
   sincos((double)ndata * psi, &sj, &cj);
-  if (m == 0.0) {  // J_0 = 1, J_k = 0 (k >= 1)
-    for (int j = ndata; j >= 1; --j) {
-      body(j, j == 1 ? 1.0 : 0.0, 0.0, 0.0, cj, sj);
-      const double cn = fma(cj, c1, sj * s1);
-      const double sn = fma(sj, c1, -(cj * s1));
-      cj = cn;
-      sj = sn;
-    }
-    return;
-  }
   const double am = fabs(m);
-  if (!(am < 1.0e5)) {  // NaN / absurd m: propagate NaN like scipy would make it useless
-    const double nan = __builtin_nan("");
-    for (int j = ndata; j >= 1; --j) body(j, nan, nan, nan, cj, sj);
-    return;
-  }
-  if (am < DFMI_BES_TINY) {
+  if (m == 0.0 || am < DFMI_BES_TINY || !(am < 1.0e5)) {
     for (int j = ndata; j >= 1; --j) {
-      body(j, dfmi_bessel_series(j - 1, m), dfmi_bessel_series(j, m), dfmi_bessel_series(j + 1, m), cj, sj);
+      double jm1, j0, jp1;
+      if (m == 0.0) {
+        jm1 = (j == 1) ? 1.0 : 0.0;
+        j0 = jp1 = 0.0;
+      } else if (am < DFMI_BES_TINY) {
+        jm1 = dfmi_bessel_series(j - 1, m);
+        j0 = dfmi_bessel_series(j, m);
+        jp1 = dfmi_bessel_series(j + 1, m);
+      } else {
+        jm1 = j0 = jp1 = __builtin_nan("");
+      }
+      body(j, jm1, j0, jp1, cj, sj);
       const double cn = fma(cj, c1, sj * s1);
       const double sn = fma(sj, c1, -(cj * s1));
       cj = cn;
@@ -106,82 +236,45 @@ __host__ __device__ __forceinline__ void harmonic_walk(int ndata, double m, doub
   for (int j = ndata; j >= 1; --j) {
     w.step(&jp1, &j0, &jm1);
     body(j, jm1, j0, jp1, cj, sj);
-    const double cn = fma(cj, c1, sj * s1);   // cos((j-1) psi)
+    const double cn = fma(cj, c1, sj * s1);     // cos((j-1) psi)
     const double sn = fma(sj, c1, -(cj * s1));  // sin((j-1) psi)
     cj = cn;
     sj = sn;
   }
 }
 
-// fit.py:68-150 (coeffs)
-__host__ __device__ __noinline__ void eval_full(const double* __restrict__ q, int64_t ld, int ndata, const double (&p)[4],
-                                       Eval& e) {
+struct QGlobal {
+  const double* __restrict__ p;
+  int64_t ld;
+  DFMI_HDI double operator()(int c) const { return p[(int64_t)c * ld]; }
+};
+
+DFMI_HDI void eval_gen(const QGlobal& q, int nd, const double (&p)[4], Eval& e) {
   const double a = p[0], m = p[1], phi = p[2], psi = p[3];
   double sph, cph;
   sincos(phi, &sph, &cph);
   const bool a_nz = (a != 0.0);
-  e = Eval{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  harmonic_walk(ndata, m, psi, [&](int j, double Jm1, double J0, double Jp1, double cj, double sj) {
-    const double pt = quarter_turn(j, cph, sph);       // cos(phi + j pi/2)
-    const double ptd = quarter_turn(j + 1, cph, sph);  // cos(phi + j pi/2 + pi/2)
-    const double dJ = 0.5 * (Jm1 - Jp1);
-    const double common = a * pt * J0;
-    const double mq = common * cj;
-    const double mi = -common * sj;
-    const double rq = q[(int64_t)(j - 1) * ld] - mq;
-    const double ri = q[(int64_t)(j - 1 + ndata) * ld] - mi;
-    e.ssq = fma(rq, rq, e.ssq);
-    e.ssq = fma(ri, ri, e.ssq);
-    // rows of J for the Q and I components
-    const double q0 = a_nz ? mq / a : 0.0;
-    const double i0 = a_nz ? mi / a : 0.0;
-    const double cm = a * pt * dJ;
-    const double q1 = cm * cj, i1 = -cm * sj;
-    const double cphi = a * ptd * J0;
-    const double q2 = cphi * cj, i2 = -cphi * sj;
-    const double q3 = common * -sj * (double)j, i3 = -common * cj * (double)j;
-    e.a00 += q0 * q0 + i0 * i0;
-    e.a01 += q0 * q1 + i0 * i1;
-    e.a02 += q0 * q2 + i0 * i2;
-    e.a03 += q0 * q3 + i0 * i3;
-    e.a11 += q1 * q1 + i1 * i1;
-    e.a12 += q1 * q2 + i1 * i2;
-    e.a13 += q1 * q3 + i1 * i3;
-    e.a22 += q2 * q2 + i2 * i2;
-    e.a23 += q2 * q3 + i2 * i3;
-    e.a33 += q3 * q3 + i3 * i3;
-    e.g0 += q0 * rq + i0 * ri;
-    e.g1 += q1 * rq + i1 * ri;
-    e.g2 += q2 * rq + i2 * ri;
-    e.g3 += q3 * rq + i3 * ri;
+  eval_zero(e);
+  harmonic_walk(nd, m, psi, [&](int j, double Jm1, double J0, double Jp1, double cj, double sj) {
+    harmonic_term(e, j, a, a_nz, cph, sph, Jm1, J0, Jp1, cj, sj, q(j - 1), q(j - 1 + nd));
   });
 }
 
-// fit.py:152-167 (ssqf)
-__host__ __device__ __noinline__ double eval_ssq(const double* __restrict__ q, int64_t ld, int ndata, const double (&p)[4]) {
-  const double a = p[0], m = p[1], phi = p[2], psi = p[3];
-  double sph, cph;
-  sincos(phi, &sph, &cph);
-  double ssq = 0.0;
-  harmonic_walk(ndata, m, psi, [&](int j, double, double J0, double, double cj, double sj) {
-    const double common = a * quarter_turn(j, cph, sph) * J0;
-    const double rq = q[(int64_t)(j - 1) * ld] - common * cj;
-    const double ri = q[(int64_t)(j - 1 + ndata) * ld] + common * sj;
-    ssq = fma(rq, rq, ssq);
-    ssq = fma(ri, ri, ssq);
-  });
-  return ssq;
-}
+// ---------------------------------------------------------------------------
+// Shared LM pieces
+// ---------------------------------------------------------------------------
 
 // fit.py:169-206 (msolve): (JtJ + lam diag(JtJ)) dp = Jt r by LU with partial
 // pivoting (LAPACK dgesv semantics: first max |pivot|; an exactly-zero pivot
-// is a singular matrix -> LinAlgError in numpy -> dp = 0).
-__host__ __device__ __forceinline__ void damped_solve(const Eval& e, double lam, double (&dp)[4]) {
+// is a singular matrix -> LinAlgError in numpy -> dp = 0). Fully unrolled, the
+// row exchanges are selects: no runtime-indexed array.
+DFMI_HDI void damped_solve(const Eval& e, double lam, double (&dp)[4]) {
   double A[4][4] = {{e.a00 + lam * e.a00, e.a01, e.a02, e.a03},
                     {e.a01, e.a11 + lam * e.a11, e.a12, e.a13},
                     {e.a02, e.a12, e.a22 + lam * e.a22, e.a23},
                     {e.a03, e.a13, e.a23, e.a33 + lam * e.a33}};
   double b[4] = {e.g0, e.g1, e.g2, e.g3};
+  double invd[4];
   bool singular = false;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
@@ -195,24 +288,23 @@ __host__ __device__ __forceinline__ void damped_solve(const Eval& e, double lam,
         piv = r;
       }
     }
-    // swap rows c and piv (predicated: keep registers static)
 #pragma unroll
     for (int r = c + 1; r < 4; ++r) {
-      if (r == piv) {
+      const bool sw = (r == piv);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const double t = A[c][k];
-          A[c][k] = A[r][k];
-          A[r][k] = t;
-        }
-        const double t = b[c];
-        b[c] = b[r];
-        b[r] = t;
+      for (int k = 0; k < 4; ++k) {
+        const double t = A[c][k];
+        A[c][k] = sw ? A[r][k] : A[c][k];
+        A[r][k] = sw ? t : A[r][k];
       }
+      const double t = b[c];
+      b[c] = sw ? b[r] : b[c];
+      b[r] = sw ? t : b[r];
     }
     const double pv = A[c][c];
-    if (pv == 0.0) singular = true;
+    singular = singular || (pv == 0.0);
     const double inv = 1.0 / pv;
+    invd[c] = inv;
 #pragma unroll
     for (int r = c + 1; r < 4; ++r) {
       const double l = A[r][c] * inv;
@@ -221,32 +313,28 @@ __host__ __device__ __forceinline__ void damped_solve(const Eval& e, double lam,
       b[r] = fma(-l, b[c], b[r]);
     }
   }
-  if (singular) {
-    dp[0] = dp[1] = dp[2] = dp[3] = 0.0;
-    return;
-  }
 #pragma unroll
   for (int r = 3; r >= 0; --r) {
     double s = b[r];
 #pragma unroll
     for (int k = r + 1; k < 4; ++k) s = fma(-A[r][k], dp[k], s);
-    dp[r] = s / A[r][r];
+    dp[r] = s * invd[r];
   }
+  if (singular) dp[0] = dp[1] = dp[2] = dp[3] = 0.0;
 }
 
-__host__ __device__ __forceinline__ double norm4(double a, double b, double c, double d) {
-  return sqrt(a * a + b * b + c * c + d * d);
-}
+DFMI_HDI double norm4(double a, double b, double c, double d) { return sqrt(a * a + b * b + c * c + d * d); }
 
 // fit.py:208-258 (_run_lma_fit). p in/out; returns ssq0 at the final p.
-__host__ __device__ double lm_descend(const double* __restrict__ q, int64_t ld, int ndata, double (&p)[4], const LMConst& c) {
+template <typename EvalFn>
+DFMI_HDI double lm_descend(EvalFn&& evalf, double (&p)[4], const LMConst& c) {
   Eval e;
-  eval_full(q, ld, ndata, p, e);
+  evalf(p, e);
   for (int it = 0; it < c.max_steps; ++it) {
-    const double po[4] = {p[0], p[1], p[2], p[3]};
+    const double po0 = p[0], po1 = p[1], po2 = p[2], po3 = p[3];
     bool found = false;
-    double best_ssq = e.ssq;
     double pt[4];
+    Eval et;
     for (int li = 0; li < c.n_lambda; ++li) {
       double dp[4];
       damped_solve(e, c.lambdas[li], dp);
@@ -255,9 +343,8 @@ __host__ __device__ double lm_descend(const double* __restrict__ q, int64_t ld, 
       pt[1] = p[1] + dp[1];
       pt[2] = p[2] + dp[2];
       pt[3] = p[3] + dp[3];
-      const double s = eval_ssq(q, ld, ndata, pt);
-      if (s < best_ssq) {
-        best_ssq = s;
+      evalf(pt, et);
+      if (et.ssq < e.ssq) {
         found = true;
         break;
       }
@@ -267,33 +354,18 @@ __host__ __device__ double lm_descend(const double* __restrict__ q, int64_t ld, 
     p[1] = pt[1];
     p[2] = pt[2];
     p[3] = pt[3];
-    eval_full(q, ld, ndata, p, e);
-    const double change = norm4(p[0] - po[0], p[1] - po[1], p[2] - po[2], p[3] - po[3]);
+    const double best_ssq = et.ssq;
+    e = et;  // coeffs(ndata, data, parm) at the accepted point (fit.py:251)
+    const double change = norm4(p[0] - po0, p[1] - po1, p[2] - po2, p[3] - po3);
     if ((e.ssq - best_ssq) < c.conv_improve && change < c.conv_param_change) break;
   }
   return e.ssq;
 }
 
-// ssq at a grid point (psi = 0 exactly: cos(j*0)=1, sin(j*0)=0), Bessel values
-// J_j(mtry) from the host-built table.
-__host__ __device__ double grid_ssq(const double* __restrict__ q, int64_t ld, int ndata, const double* __restrict__ jrow,
-                           double a, double phi) {
-  double sph, cph;
-  sincos(phi, &sph, &cph);
-  double ssq = 0.0;
-  for (int j = 1; j <= ndata; ++j) {
-    const double common = a * quarter_turn(j, cph, sph) * jrow[j - 1];
-    const double rq = q[(int64_t)(j - 1) * ld] - common;
-    const double ri = q[(int64_t)(j - 1 + ndata) * ld] + common * 0.0;
-    ssq = fma(rq, rq, ssq);
-    ssq = fma(ri, ri, ssq);
-  }
-  return ssq;
-}
-
-// fit.py:260-320 (_find_best_initial_guess). jtab: n_grid rows of J_1..J_ndata.
-__host__ __device__ void m_grid_seed(const double* __restrict__ q, int64_t ld, int ndata, const double* __restrict__ jtab,
-                            const LMConst& c, double (&best)[4]) {
+// fit.py:260-320 (_find_best_initial_guess). jtab: n_grid rows of J_1..J_ndata(mtry)
+// (psi = 0 exactly: cos(j*0) = 1, -sin(j*0) = -0). Q(c) returns QI component c.
+template <typename QF>
+DFMI_HDI void m_grid_seed(QF&& Q, int ndata, const double* __restrict__ jtab, const LMConst& c, double (&best)[4]) {
   double best_ssq = 9e99;
   best[0] = best[1] = best[2] = best[3] = 0.0;
   for (int g = 0; g < c.n_grid; ++g) {
@@ -305,7 +377,7 @@ __host__ __device__ void m_grid_seed(const double* __restrict__ q, int64_t ld, i
       const int j = i + 1;
       const double bq = jrow[i] * 1.0;   // jv * cos(j*0)
       const double bi = jrow[i] * -0.0;  // jv * -sin(j*0)
-      const double dq = q[(int64_t)i * ld], di = q[(int64_t)(i + ndata) * ld];
+      const double dq = Q(i), di = Q(i + ndata);
       if (fabs(bq) > c.bessel_amp_thr) {
         switch (j & 3) {
           case 0: cossum += dq / bq; ++ncos; break;
@@ -327,26 +399,33 @@ __host__ __device__ void m_grid_seed(const double* __restrict__ q, int64_t ld, i
     const double ptry = atan2(sinsum / (double)nsin, cossum / (double)ncos);
     double sp, cp;
     sincos(ptry, &sp, &cp);
-    const double tab4[4] = {cp, -sp, -cp, sp};
     double asum = 0.0;
     int na = 0;
     for (int i = 0; i < ndata; ++i) {
       const int j = i + 1;
-      const double sc = tab4[j & 3];
+      const double sc = quarter_turn(j, cp, sp);  // [cos, -sin, -cos, sin][j % 4]
       const double bq = jrow[i] * 1.0;
       const double bi = jrow[i] * -0.0;
       if (fabs(bq) > c.bessel_amp_thr && fabs(sc) > c.sincos_amp_thr) {
-        asum += q[(int64_t)i * ld] / (sc * bq);
+        asum += Q(i) / (sc * bq);
         ++na;
       }
       if (fabs(bi) > c.bessel_amp_thr && fabs(sc) > c.sincos_amp_thr) {
-        asum += q[(int64_t)(i + ndata) * ld] / (sc * bi);
+        asum += Q(i + ndata) / (sc * bi);
         ++na;
       }
     }
     if (na == 0) continue;
     const double atry = asum / (double)na;
-    const double s = grid_ssq(q, ld, ndata, jrow, atry, ptry);
+    // ssqf at (atry, mtry, ptry, 0): fit.py:152-167 with cos(j*0)=1, sin(j*0)=0
+    double s = 0.0;
+    for (int i = 0; i < ndata; ++i) {
+      const double common = atry * quarter_turn(i + 1, cp, sp) * jrow[i];
+      const double rq = Q(i) - common;
+      const double ri = Q(i + ndata) + common * 0.0;
+      s = fma(rq, rq, s);
+      s = fma(ri, ri, s);
+    }
     if (s < best_ssq) {
       best_ssq = s;
       best[0] = atry;
@@ -358,17 +437,18 @@ __host__ __device__ void m_grid_seed(const double* __restrict__ q, int64_t ld, i
 }
 
 // fit.py:322-361 (fit): LM, status + grid retry, normalisation, phi wrap.
-__host__ __device__ int fit_segment(const double* __restrict__ q, int64_t ld, int ndata, const double* __restrict__ jtab,
-                           const LMConst& c, double (&p)[4], double& ssq_out) {
-  double ssq = lm_descend(q, ld, ndata, p, c);
+template <typename EvalFn, typename QF>
+DFMI_HDI int fit_segment_t(EvalFn&& evalf, QF&& Q, int ndata, const double* __restrict__ jtab, const LMConst& c,
+                           double (&p)[4], double& ssq_out) {
+  double ssq = lm_descend(evalf, p, c);
   int status;
   if (ssq < c.fitok_threshold) {
     status = 0;
   } else {
     double g[4];
-    m_grid_seed(q, ld, ndata, jtab, c, g);
+    m_grid_seed(Q, ndata, jtab, c, g);
     if (!(g[0] == 0.0) || !(g[1] == 0.0) || !(g[2] == 0.0) || !(g[3] == 0.0)) {  // np.any
-      const double ssq2 = lm_descend(q, ld, ndata, g, c);
+      const double ssq2 = lm_descend(evalf, g, c);
       if (ssq2 < ssq) {
         ssq = ssq2;
         p[0] = g[0];
@@ -393,7 +473,30 @@ __host__ __device__ int fit_segment(const double* __restrict__ q, int64_t ld, in
   return status;
 }
 
-// Guess source for record r, component i: guess[r*g_rec + i*g_comp].
+// Single-segment entry used by the kernel and by the test-only host build.
+// NDMAX > 0: register path (requires ndata <= NDMAX); NDMAX == 0: general path.
+template <int NDMAX>
+__host__ __device__ __forceinline__ int fit_segment(const double* __restrict__ qptr, int64_t ld, int ndata,
+                                                 const double* __restrict__ jtab, const LMConst& c, double (&p)[4],
+                                                 double& ssq_out) {
+  if constexpr (NDMAX > 0) {
+    double q[2 * NDMAX];
+#pragma unroll
+    for (int i = 0; i < NDMAX; ++i) {
+      q[i] = (i < ndata) ? qptr[(int64_t)i * ld] : 0.0;
+      q[NDMAX + i] = (i < ndata) ? qptr[(int64_t)(ndata + i) * ld] : 0.0;
+    }
+    auto evalf = [&](const double (&pp)[4], Eval& e) { eval_reg<NDMAX>(q, ndata, pp, e); };
+    const QGlobal qg{qptr, ld};  // grid search (rare path) reads QI through the cache
+    return fit_segment_t(evalf, qg, ndata, jtab, c, p, ssq_out);
+  } else {
+    const QGlobal qg{qptr, ld};
+    auto evalf = [&](const double (&pp)[4], Eval& e) { eval_gen(qg, ndata, pp, e); };
+    return fit_segment_t(evalf, qg, ndata, jtab, c, p, ssq_out);
+  }
+}
+
+// Seeds of up to 8 records passed by value (read with constant offsets only).
 struct GuessInline {
   double v[8][4];
 };
@@ -402,7 +505,9 @@ struct GuessInline {
 // items of record r are segments [first, first + nitems); they are cut into
 // nchunk chunks with np.array_split semantics and each chunk starts from the
 // record's guess, warm-starting within the chunk (fitters.py:42-58).
-__global__ __launch_bounds__(256) void lm_chunks_kernel(
+// Guess source: ginl (use_inline) or guess[r*g_rec + i*g_comp].
+template <int NDMAX>
+__global__ __launch_bounds__(64) void lm_chunks_kernel(
     const double* __restrict__ qi, int64_t qi_ld, int ndata, int64_t nrec, int64_t nbuf, int64_t first,
     int64_t nitems, int64_t nchunk, const double* __restrict__ guess, int64_t g_rec, int64_t g_comp,
     GuessInline ginl, int use_inline, const double* __restrict__ jtab, LMConst c, double* __restrict__ out,
@@ -414,10 +519,15 @@ __global__ __launch_bounds__(256) void lm_chunks_kernel(
   const int64_t qn = nitems / nchunk, rm = nitems % nchunk;
   const int64_t start = k * qn + (k < rm ? k : rm);
   const int64_t len = qn + (k < rm ? 1 : 0);
-  double p[4];
+  double p[4] = {0.0, 0.0, 0.0, 0.0};
   if (use_inline) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) p[i] = ginl.v[r][i];
+    for (int rr = 0; rr < 8; ++rr) {
+      if (r == rr) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) p[i] = ginl.v[rr][i];
+      }
+    }
   } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i) p[i] = guess[r * g_rec + i * g_comp];
@@ -425,7 +535,7 @@ __global__ __launch_bounds__(256) void lm_chunks_kernel(
   for (int64_t t = 0; t < len; ++t) {
     const int64_t sidx = r * nbuf + first + start + t;
     double ssq;
-    const int st = fit_segment(qi + sidx, qi_ld, ndata, jtab, c, p, ssq);
+    const int st = fit_segment<NDMAX>(qi + sidx, qi_ld, ndata, jtab, c, p, ssq);
     out[0 * out_ld + sidx] = p[0];
     out[1 * out_ld + sidx] = p[1];
     out[2 * out_ld + sidx] = p[2];

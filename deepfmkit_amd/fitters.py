@@ -162,7 +162,8 @@ class EKFFitter(BaseFitter):
     """Per-sample EKF on the GPU (fitters.py:210-320)."""
 
     def fit(self, main_raw, **kwargs) -> pd.DataFrame:
-        res = ekf_records([main_raw], self.config["n"], **kwargs)[0]
+        kw = {k: v for k, v in kwargs.items() if k != "n"}
+        res = ekf_records([main_raw], self.config["n"], **kw)[0]
         nbuf = res.shape[0]
         return pd.DataFrame({"amp": res[:, 0], "m": res[:, 1], "phi": res[:, 2], "psi": res[:, 3], "dc": res[:, 4],
                              "ssq": np.zeros(nbuf), "fitok": np.ones(nbuf, dtype=int)}, columns=COLUMNS)

@@ -109,6 +109,11 @@ int dfmi_ekf(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
              const double* p0_diag, const double* q_diag, const double* r_val, double w_m, double f_samp,
              int32_t R, int64_t nbuf, double* states, int32_t mem, void* stream);
 
+/* Performance tuning hook (results are unaffected): "demod_loads" (8 | 16 vector
+ * loads in flight per lane), "demod_nt" (0 | 1 non-temporal stream loads),
+ * "demod_blocks_per_cu" (0 = occupancy limit). Process-wide. */
+int dfmi_set_tuning(const char* key, int64_t value);
+
 /* Period (samples) the fold kernel would use for this w0, R, ndata; 0 if none. */
 int32_t dfmi_detect_period(double w0, int32_t R, int32_t ndata);
 

@@ -87,3 +87,47 @@ def compare_fit(ours, ref, tol=1e-9, min_status_match=0.999, dc_rel=1e-13, ssq_r
     assert rep["dc_rel"] <= dc_rel, rep
     assert rep["ssq_bad"] == 0, rep
     return rep
+
+
+def resolution_tol(nd, qi, p, floor=1e-9, k=10.0):
+    """Per-parameter parity tolerance for one fit: max(floor, k * sqrt(eps * ssq * cov_ii)),
+    cov = (J^T J)^-1 at the reference solution p.
+
+    Rationale: the reference's LM accepts a step only if ssq_try < ssq0 in fp64
+    (fit.py:240), so it cannot resolve parameter changes whose effect on ssq is
+    below one ulp of ssq: |dp_i| ~ sqrt(eps * ssq * cov_ii). For the BASELINE
+    configs (40 dB) this is ~1e-11 and the 1e-9 floor governs; for noise-dominated
+    fits (ssq ~ 1) it is ~1e-8, and the reference's own answer is not determined
+    more finely than that."""
+    from oracle import nls_oracle as O
+    ssq, jtj, _ = O.model_and_jacobian(nd, np.asarray(qi, dtype=np.float64), np.asarray(p, dtype=np.float64))
+    try:
+        cov = np.abs(np.diag(np.linalg.inv(jtj.reshape(4, 4))))
+    except np.linalg.LinAlgError:
+        return np.full(4, np.inf)
+    return np.maximum(floor, k * np.sqrt(np.finfo(float).eps * max(ssq, 1e-300) * cov))
+
+
+def check_lm_group(npz, group, st, p, ssq):
+    """Parity of a batch of fit.fit results against the golden vectors of `group`."""
+    rs, rp, rq = npz[f"g{group}_status"], npz[f"g{group}_p"], npz[f"g{group}_ssq"]
+    qi = npz[f"g{group}_qi"]
+    nd = qi.shape[1] // 2
+    assert (st == rs).all(), np.where(st != rs)
+    # a == 0 (all-zero data) leaves m, phi, psi undetermined (ssq = 0 for any value)
+    degenerate = np.abs(rp[:, 0]) < 1e-100
+    assert np.all(np.abs(p[degenerate, 0]) < 1e-100)
+    d = np.abs(p - rp)
+    d[:, 2] = wrapped(p[:, 2] - rp[:, 2])
+    within = np.ones(len(rs), bool)
+    for i in np.where(~degenerate)[0]:
+        within[i] = np.all(d[i] <= resolution_tol(nd, qi[i], rp[i]))
+    good = ~degenerate & (rs <= 1)
+    assert within[good].all(), [(i, d[i]) for i in np.where(good & ~within)[0]]
+    noisy = ~degenerate & (rs == 2)
+    if noisy.any():  # noise-dominated fits: report, gate the bulk (SURVEY.md §8d)
+        assert within[noisy].mean() >= 0.9, within[noisy].mean()
+    rel = np.abs(ssq - rq) / np.maximum(rq, 1e-300)
+    ok = good
+    assert np.all((rel[ok] <= 1e-6) | (np.abs(ssq - rq)[ok] <= 1e-20))
+    return within

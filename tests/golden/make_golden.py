@@ -73,6 +73,43 @@ def analytic_qi(ndata, p):
     return np.concatenate([common * np.cos(j * psi), -common * np.sin(j * psi)])
 
 
+def reference_fuzz(rfit, ndata, qis, guesses, p, reps=3):
+    """The reference's own sensitivity: max |d p| of fit.fit when every QI entry is
+    perturbed by about one ulp (relative 2^-52 Gaussian), over `reps` draws (wrapped
+    phi). A parity tolerance below this is asking for bits the reference itself
+    does not determine."""
+    rng = np.random.RandomState(777)
+    fz = np.zeros((qis.shape[0], 4))
+    for i in range(qis.shape[0]):
+        for _ in range(reps):
+            q2 = qis[i] * (1.0 + 2.0 ** -52 * rng.randn(qis.shape[1]))
+            _, pp, _ = rfit.fit(ndata, q2, guesses[i].copy())
+            d = np.abs(pp - p[i])
+            d[2] = abs((pp[2] - p[i][2] + np.pi) % (2 * np.pi) - np.pi)
+            fz[i] = np.maximum(fz[i], d)
+    return fz
+
+
+def reference_radius(rfit, ndata, qis, p):
+    """Stopping radius of the reference's LM: |p_ref - p*| where p* continues the
+    reference's own _run_lma_fit (fit.py:208-258) from p_ref with the convergence
+    test disabled (it then stops only when no damping value lowers ssq, i.e. at
+    the machine-precision minimum). Two correct implementations of the same LM
+    may stop anywhere inside this radius, so parity is judged against it."""
+    saved = (rfit.MAX_LMA_STEPS, rfit.LMA_CONVERGENCE_IMPROVE, rfit.LMA_CONVERGENCE_PARAM_CHANGE)
+    rfit.MAX_LMA_STEPS, rfit.LMA_CONVERGENCE_IMPROVE, rfit.LMA_CONVERGENCE_PARAM_CHANGE = 500, -1.0, -1.0
+    try:
+        rad = np.zeros((qis.shape[0], 4))
+        for i in range(qis.shape[0]):
+            ps, _ = rfit._run_lma_fit(ndata, qis[i].copy(), p[i].copy())
+            d = np.abs(ps - p[i])
+            d[2] = abs((ps[2] - p[i][2] + np.pi) % (2 * np.pi) - np.pi)
+            rad[i] = d
+    finally:
+        rfit.MAX_LMA_STEPS, rfit.LMA_CONVERGENCE_IMPROVE, rfit.LMA_CONVERGENCE_PARAM_CHANGE = saved
+    return rad
+
+
 def make_lm_vectors(rfit):
     rng = np.random.RandomState(12345)
     groups = {}
@@ -113,7 +150,9 @@ def make_lm_vectors(rfit):
         for i in range(count):
             s, pp, q = rfit.fit(ndata, qis[i].copy(), guesses[i].copy())
             status[i], p[i], ssq[i] = s, pp, q
-        groups[ndata] = dict(qi=qis, guess=guesses, truth=np.array(truths), status=status, p=p, ssq=ssq)
+        groups[ndata] = dict(qi=qis, guess=guesses, truth=np.array(truths), status=status, p=p, ssq=ssq,
+                             fuzz=reference_fuzz(rfit, ndata, qis, guesses, p),
+                             radius=reference_radius(rfit, ndata, qis, p))
     # A few hand-made edge vectors at ndata=10: all-zero data, a=0 guess, m=0 guess
     ndata = 10
     edge_qi = [np.zeros(20), analytic_qi(10, [1.0, 6.0, 0.3, 0.1]), analytic_qi(10, [1.0, 6.0, 0.3, 0.1]),
@@ -126,7 +165,9 @@ def make_lm_vectors(rfit):
         s, pp, q = rfit.fit(ndata, qi.copy(), g.copy())
         es.append(s), ep.append(pp), eq.append(q)
     groups["edge10"] = dict(qi=np.array(edge_qi), guess=np.array(edge_guess), truth=np.zeros((5, 4)),
-                            status=np.array(es, np.int32), p=np.array(ep), ssq=np.array(eq))
+                            status=np.array(es, np.int32), p=np.array(ep), ssq=np.array(eq),
+                            fuzz=reference_fuzz(rfit, ndata, np.array(edge_qi), np.array(edge_guess), np.array(ep)),
+                            radius=reference_radius(rfit, ndata, np.array(edge_qi), np.array(ep)))
     out = {}
     for key, g in groups.items():
         for name, arr in g.items():

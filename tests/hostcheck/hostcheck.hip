@@ -15,7 +15,8 @@ void hc_bessel_table(double x, int N, double* out) { dfmi_bessel_table(x, N, out
 
 // qi component-major (qi[c*n + s]); guess n x 4; constants in the reference order.
 int hc_fit_segments(const double* qi, long n, int ndata, const double* guess, const double* consts,
-                    const double* lambdas, int n_lambda, double* p_out, double* ssq_out, int* status_out) {
+                    const double* lambdas, int n_lambda, double* p_out, double* ssq_out, int* status_out,
+                    int force_general) {
   dfmi::LMConst c{};
   c.max_steps = (int)consts[0];
   c.conv_improve = consts[1];
@@ -41,7 +42,14 @@ int hc_fit_segments(const double* qi, long n, int ndata, const double* guess, co
   for (long s = 0; s < n; ++s) {
     double p[4] = {guess[s * 4], guess[s * 4 + 1], guess[s * 4 + 2], guess[s * 4 + 3]};
     double ssq;
-    status_out[s] = dfmi::fit_segment(qi + s, n, ndata, tab.data(), c, p, ssq);
+    if (force_general)
+      status_out[s] = dfmi::fit_segment<0>(qi + s, n, ndata, tab.data(), c, p, ssq);
+    else if (ndata <= 12)
+      status_out[s] = dfmi::fit_segment<12>(qi + s, n, ndata, tab.data(), c, p, ssq);
+    else if (ndata <= 16)
+      status_out[s] = dfmi::fit_segment<16>(qi + s, n, ndata, tab.data(), c, p, ssq);
+    else
+      status_out[s] = dfmi::fit_segment<0>(qi + s, n, ndata, tab.data(), c, p, ssq);
     for (int i = 0; i < 4; ++i) p_out[s * 4 + i] = p[i];
     ssq_out[s] = ssq;
   }

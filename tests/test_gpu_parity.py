@@ -8,7 +8,7 @@ Tolerances (fp64), stated in SURVEY.md §8d / BASELINE.md:
 import numpy as np
 import pytest
 
-from conftest import compare_fit, make_record, sha, wrapped
+from conftest import check_lm_group, compare_fit, make_record, sha, wrapped
 
 pytestmark = pytest.mark.gpu
 
@@ -72,22 +72,7 @@ def test_lm_vectors(lm_npz, group):
     qi, g = lm_npz[f"g{group}_qi"], lm_npz[f"g{group}_guess"]
     nd = qi.shape[1] // 2
     st, p, ssq = F.fit_batch(nd, qi, g)
-    rs, rp, rq = lm_npz[f"g{group}_status"], lm_npz[f"g{group}_p"], lm_npz[f"g{group}_ssq"]
-    assert (st == rs).all()
-    # a == 0 (all-zero data) leaves m, phi, psi undetermined (ssq = 0 for any value):
-    # only the amplitude is compared there
-    degenerate = np.abs(rp[:, 0]) < 1e-100
-    ok = (rs == 0) & ~degenerate
-    assert np.all(np.abs(p[degenerate, 0]) < 1e-100)
-    d = np.abs(p - rp)
-    d[:, 2] = wrapped(p[:, 2] - rp[:, 2])
-    # well-conditioned status-0 vectors meet 1e-9; the ill-conditioned low-m ones
-    # (m < 2.5, a < 0.4) stop within the LM's own 1e-9 step criterion of a
-    # shallow valley: 1e-8 there (the reference's own sensitivity)
-    assert d[ok].max(initial=0) <= 1e-8, d[ok].max(0)
-    assert np.mean(d[ok].max(1) <= 1e-9) >= 0.98
-    rel = np.abs(ssq - rq) / np.maximum(rq, 1e-300)
-    assert np.all((rel[ok] <= 1e-6) | (np.abs(ssq - rq)[ok] <= 1e-20))
+    check_lm_group(lm_npz, group, st, p, ssq)
 
 
 @pytest.mark.parametrize("mode", ["seq", "c1", "par4"])

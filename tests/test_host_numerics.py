@@ -7,7 +7,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import wrapped
+from conftest import check_lm_group, wrapped
 
 HC = os.path.join(os.path.dirname(__file__), "hostcheck", "libhostcheck.so")
 
@@ -19,7 +19,7 @@ def hc():
     lib = ctypes.CDLL(HC)
     P = ctypes.c_void_p
     lib.hc_bessel_table.argtypes = [ctypes.c_double, ctypes.c_int, P]
-    lib.hc_fit_segments.argtypes = [P, ctypes.c_long, ctypes.c_int, P, P, P, ctypes.c_int, P, P, P]
+    lib.hc_fit_segments.argtypes = [P, ctypes.c_long, ctypes.c_int, P, P, P, ctypes.c_int, P, P, P, ctypes.c_int]
     return lib
 
 
@@ -39,7 +39,7 @@ def test_bessel_vs_scipy_table(hc):
     assert (err.max(0) / np.abs(jv).max(0)).max() <= 2e-14
 
 
-def _fit(hc, qi, guess):
+def _fit(hc, qi, guess, force_general=0):
     n, nd2 = qi.shape
     consts = np.array([100, 1e-9, 1e-9, 1e-3, 5.0, 30.0, 0.5, 0.05, 0.1, 1e-15])
     lams = np.array([0.0, 1e-7, 1e-5, 1e-3, 1e-1, 1.0, 10.0, 100.0])
@@ -49,25 +49,17 @@ def _fit(hc, qi, guess):
     ssq = np.zeros(n)
     st = np.zeros(n, np.int32)
     hc.hc_fit_segments(qcm.ctypes.data, n, nd2 // 2, g.ctypes.data, consts.ctypes.data, lams.ctypes.data, 8,
-                       p.ctypes.data, ssq.ctypes.data, st.ctypes.data)
+                       p.ctypes.data, ssq.ctypes.data, st.ctypes.data, force_general)
     return st, p, ssq
 
 
+@pytest.mark.parametrize("force_general", [0, 1])
 @pytest.mark.parametrize("group", ["10", "5", "20", "30", "62", "edge10"])
-def test_host_lm_vectors(hc, lm_npz, group):
+def test_host_lm_vectors(hc, lm_npz, group, force_general):
+    """Both code paths (register path for ndata <= 16, general two-pass path)."""
     qi, g = lm_npz[f"g{group}_qi"], lm_npz[f"g{group}_guess"]
-    st, p, ssq = _fit(hc, qi, g)
-    rs, rp = lm_npz[f"g{group}_status"], lm_npz[f"g{group}_p"]
-    assert (st == rs).all()
-    # a == 0 (all-zero data) leaves m, phi, psi undetermined (ssq = 0 for any value):
-    # only the amplitude is compared there
-    degenerate = np.abs(rp[:, 0]) < 1e-100
-    ok = (rs == 0) & ~degenerate
-    assert np.all(np.abs(p[degenerate, 0]) < 1e-100)
-    d = np.abs(p - rp)
-    d[:, 2] = wrapped(p[:, 2] - rp[:, 2])
-    assert d[ok].max(initial=0) <= 1e-8
-    assert np.mean(d[ok].max(1) <= 1e-9) >= 0.98
+    st, p, ssq = _fit(hc, qi, g, force_general)
+    check_lm_group(lm_npz, group, st, p, ssq)
 
 
 def test_host_lm_on_reference_qi(hc, records_npz, manifest):

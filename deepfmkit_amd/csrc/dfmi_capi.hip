@@ -192,6 +192,7 @@ struct Tuning {
   int demod_loads = 8;         // vector loads in flight per lane (8 or 16)
   int demod_nt = 1;            // non-temporal stream loads (measured +14 %, profiles/r01_tune_demod.json)
   int demod_blocks_per_cu = 0; // 0 = occupancy limit
+  int lm_general = 0;          // 1: force the two-pass (general) LM path for every ndata
 };
 Tuning g_tune;
 
@@ -306,8 +307,14 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
   const int block = 64;
   const int64_t grid = (lanes + block - 1) / block;
   // register path for ndata <= 16 (QI/Bessel in registers), general path above
-  auto kern = ndata <= 12 ? dfmi::lm_chunks_kernel<12> : ndata <= 16 ? dfmi::lm_chunks_kernel<16>
-                                                                    : dfmi::lm_chunks_kernel<0>;
+  const bool chain = nitems > nchunk;
+  const int nd_sel = g_tune.lm_general ? 1000 : ndata;
+  auto kern = chain ? (nd_sel <= 12   ? dfmi::lm_chunks_kernel<12, true>
+                       : nd_sel <= 16 ? dfmi::lm_chunks_kernel<16, true>
+                                     : dfmi::lm_chunks_kernel<0, true>)
+                    : (nd_sel <= 12   ? dfmi::lm_chunks_kernel<12, false>
+                       : nd_sel <= 16 ? dfmi::lm_chunks_kernel<16, false>
+                                     : dfmi::lm_chunks_kernel<0, false>);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(block), 0, st, qi, qi_ld, ndata, nrec, nbuf, first, nitems,
                      nchunk, guess_dev, g_rec, g_comp, ginl, use_inline, jtab, c, out, out_ld, status);
   HIPCHK(hipGetLastError());
@@ -431,6 +438,8 @@ int dfmi_set_tuning(const char* key, int64_t value) {
     g_tune.demod_loads = (int)value;
   } else if (k == "demod_nt") {
     g_tune.demod_nt = value ? 1 : 0;
+  } else if (k == "lm_general") {
+    g_tune.lm_general = value ? 1 : 0;
   } else if (k == "demod_blocks_per_cu") {
     if (value < 0) return fail(DFMI_ERR_ARG, "demod_blocks_per_cu < 0");
     g_tune.demod_blocks_per_cu = (int)value;

@@ -114,22 +114,29 @@ DFMI_HDI void eval_zero(Eval& e) { e = Eval{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 
 // ---------------------------------------------------------------------------
 
 // J_0..J_{NB-1}(x) into registers with one backward Miller pass.
+// |x| < 1e-3 takes the power series (4 terms, relative error < 1e-20); above
+// that the unrolled low-order part of the pass (orders < NB <= 18) grows by at
+// most ~1e70, so only the runtime part of the pass (orders >= NB) carries the
+// exact power-of-two rescaling of dfmi_math.h.
 template <int NB>
 DFMI_HDI void bessel_regs(double x, int N, double (&J)[NB]) {
-  if (x == 0.0) {
-#pragma unroll
-    for (int k = 0; k < NB; ++k) J[k] = (k == 0) ? 1.0 : 0.0;
-    return;
-  }
   const double ax = fabs(x);
-  if (!(ax < 1.0e5)) {
+  if (!(ax < 1.0e5)) {  // NaN / absurd argument
 #pragma unroll
     for (int k = 0; k < NB; ++k) J[k] = __builtin_nan("");
     return;
   }
-  if (ax < DFMI_BES_TINY) {
+  if (ax < 1.0e-3) {  // includes x == 0 (J_0 = 1, J_k = 0)
+    const double h = 0.5 * x, q = h * h;
+    double t = 1.0;  // (x/2)^k / k!
 #pragma unroll
-    for (int k = 0; k < NB; ++k) J[k] = dfmi_bessel_series(k, x);
+    for (int k = 0; k < NB; ++k) {
+      if (k > 0) t *= h * (1.0 / (double)k);  // compile-time reciprocals: no fp64 division
+      const double r1 = 1.0 / (double)(k + 1), r2 = 1.0 / (2.0 * (k + 2)), r3 = 1.0 / (3.0 * (k + 3));
+      // 1 - q/(k+1) + q^2/(2(k+1)(k+2)) - q^3/(6(k+1)(k+2)(k+3))
+      const double s = 1.0 - q * r1 * (1.0 - q * r2 * (1.0 - q * r3));
+      J[k] = t * s;
+    }
     return;
   }
   int M = dfmi_bessel_start(N, ax);
@@ -151,14 +158,7 @@ DFMI_HDI void bessel_regs(double x, int N, double (&J)[NB]) {
   J[NB - 1] = f;
 #pragma unroll
   for (int k = NB - 1; k >= 1; --k) {
-    double fm1 = fma((double)k * tox, f, -fp1);
-    if (fabs(fm1) > big) {
-      fm1 = ldexp(fm1, -DFMI_BES_BIG_EXP);
-      f = ldexp(f, -DFMI_BES_BIG_EXP);
-      S = ldexp(S, -DFMI_BES_BIG_EXP);
-#pragma unroll
-      for (int i = k; i < NB; ++i) J[i] = ldexp(J[i], -DFMI_BES_BIG_EXP);
-    }
+    const double fm1 = fma((double)k * tox, f, -fp1);
     J[k - 1] = fm1;
     if (k - 1 == 0) S += fm1;
     else if (((k - 1) & 1) == 0) S += 2.0 * fm1;
@@ -174,8 +174,8 @@ DFMI_HDI void bessel_regs(double x, int N, double (&J)[NB]) {
   }
 }
 
-template <int NDMAX>
-DFMI_HDI void eval_reg(const double (&q)[2 * NDMAX], int nd, const double (&p)[4], Eval& e) {
+template <int NDMAX, typename QF>
+DFMI_HDI void eval_reg(const QF& q, int nd, const double (&p)[4], Eval& e) {
   const double a = p[0], m = p[1], phi = p[2], psi = p[3];
   double sph, cph, s1, c1;
   sincos(phi, &sph, &cph);
@@ -187,7 +187,7 @@ DFMI_HDI void eval_reg(const double (&q)[2 * NDMAX], int nd, const double (&p)[4
   double cj = c1, sj = s1;  // cos(j psi), sin(j psi) at j = 1
 #pragma unroll
   for (int j = 1; j <= NDMAX; ++j) {
-    if (j <= nd) harmonic_term(e, j, a, a_nz, cph, sph, J[j - 1], J[j], J[j + 1], cj, sj, q[j - 1], q[NDMAX + j - 1]);
+    if (j <= nd) harmonic_term(e, j, a, a_nz, cph, sph, J[j - 1], J[j], J[j + 1], cj, sj, q(j - 1), q(nd + j - 1));
     const double cn = fma(cj, c1, -(sj * s1));
     const double sn = fma(sj, c1, cj * s1);
     cj = cn;
@@ -480,14 +480,11 @@ __host__ __device__ __forceinline__ int fit_segment(const double* __restrict__ q
                                                  const double* __restrict__ jtab, const LMConst& c, double (&p)[4],
                                                  double& ssq_out) {
   if constexpr (NDMAX > 0) {
-    double q[2 * NDMAX];
-#pragma unroll
-    for (int i = 0; i < NDMAX; ++i) {
-      q[i] = (i < ndata) ? qptr[(int64_t)i * ld] : 0.0;
-      q[NDMAX + i] = (i < ndata) ? qptr[(int64_t)(ndata + i) * ld] : 0.0;
-    }
-    auto evalf = [&](const double (&pp)[4], Eval& e) { eval_reg<NDMAX>(q, ndata, pp, e); };
-    const QGlobal qg{qptr, ld};  // grid search (rare path) reads QI through the cache
+    // QI is re-read per evaluation through the vector L1 (64 segments x 2*ndata
+    // doubles = 10 KB per wave): keeping it in registers costs 2*NDMAX VGPRs and
+    // with them the second wave per SIMD.
+    const QGlobal qg{qptr, ld};
+    auto evalf = [&](const double (&pp)[4], Eval& e) { eval_reg<NDMAX>(qg, ndata, pp, e); };
     return fit_segment_t(evalf, qg, ndata, jtab, c, p, ssq_out);
   } else {
     const QGlobal qg{qptr, ld};
@@ -506,7 +503,10 @@ struct GuessInline {
 // nchunk chunks with np.array_split semantics and each chunk starts from the
 // record's guess, warm-starting within the chunk (fitters.py:42-58).
 // Guess source: ginl (use_inline) or guess[r*g_rec + i*g_comp].
-template <int NDMAX>
+// CHAIN = false: every chunk holds at most one segment (no loop: the register
+// allocator keeps the whole LM at two waves per SIMD); CHAIN = true: warm-start
+// chains of any length.
+template <int NDMAX, bool CHAIN>
 __global__ __launch_bounds__(64) void lm_chunks_kernel(
     const double* __restrict__ qi, int64_t qi_ld, int ndata, int64_t nrec, int64_t nbuf, int64_t first,
     int64_t nitems, int64_t nchunk, const double* __restrict__ guess, int64_t g_rec, int64_t g_comp,
@@ -532,8 +532,7 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
 #pragma unroll
     for (int i = 0; i < 4; ++i) p[i] = guess[r * g_rec + i * g_comp];
   }
-  for (int64_t t = 0; t < len; ++t) {
-    const int64_t sidx = r * nbuf + first + start + t;
+  auto one = [&](int64_t sidx) {
     double ssq;
     const int st = fit_segment<NDMAX>(qi + sidx, qi_ld, ndata, jtab, c, p, ssq);
     out[0 * out_ld + sidx] = p[0];
@@ -542,6 +541,12 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
     out[3 * out_ld + sidx] = p[3];
     out[5 * out_ld + sidx] = ssq;
     status[sidx] = st;
+  };
+  const int64_t s0 = r * nbuf + first + start;
+  if constexpr (!CHAIN) {
+    if (len == 1) one(s0);  // chunk size 1 (the parallel default): straight-line code
+  } else {
+    for (int64_t t = 0; t < len; ++t) one(s0 + t);  // warm-start chain (sequential / n_cores)
   }
 }
 

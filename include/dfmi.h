@@ -111,7 +111,8 @@ int dfmi_ekf(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
 
 /* Performance tuning hook (results are unaffected): "demod_loads" (8 | 16 vector
  * loads in flight per lane), "demod_nt" (0 | 1 non-temporal stream loads),
- * "demod_blocks_per_cu" (0 = occupancy limit). Process-wide. */
+ * "demod_blocks_per_cu" (0 = occupancy limit), "lm_general" (1 = two-pass LM path for
+ * every ndata). Process-wide. */
 int dfmi_set_tuning(const char* key, int64_t value);
 
 /* Period (samples) the fold kernel would use for this w0, R, ndata; 0 if none. */

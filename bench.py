@@ -70,6 +70,17 @@ def gen_shard(torch, dev, seg0, nseg, R, seed, chunk=8192):
     return x
 
 
+def shard_plan(rank, world, nseg):
+    """Static weak-scaling shard of one long record: rank r owns global segments
+    [r*nseg, (r+1)*nseg). Rank 0's shard starts with the record's buffer 0, which
+    seeds every chunk (fitters.py:403-410); the other ranks prepend that buffer
+    and fit it themselves (no collective). Returns (first global segment,
+    buffers in the local batch, whether the seed buffer is prepended)."""
+    if rank == 0:
+        return 0, nseg, False
+    return rank * nseg, nseg + 1, True
+
+
 def cpu_baseline(args):
     """Oracle restatement of StandardNLSFitter._fit_parallel (Pool over np.array_split
     chunks, fitters.py:395-428) timed on this host. Runs BEFORE the GPU is touched
@@ -132,16 +143,13 @@ def main():
     lib = _lib.load()
     R = int(F_SAMP / F_MOD * N_CYC)
     nseg = args.segments
-    seg0 = rank * nseg
-    # rank 0's shard starts with the record's buffer 0; the others prepend it (the seed)
+    seg0, nbuf, prepend_seed = shard_plan(rank, world, nseg)
     body = gen_shard(torch, dev, seg0, nseg, R, seed=1234 + rank)
-    if rank == 0:
+    if not prepend_seed:
         x = body
-        nbuf = nseg
     else:
         head = gen_shard(torch, dev, 0, 1, R, seed=1234)
         x = torch.cat([head, body])
-        nbuf = nseg + 1
         del head
     del body
     torch.cuda.synchronize()

@@ -160,6 +160,7 @@ def main():
     ok = torch.empty(nbuf, dtype=torch.int32, device=dev)
     qi = torch.empty((2 * NDATA, nbuf), dtype=torch.float64, device=dev)
     dcb = torch.empty(nbuf, dtype=torch.float64, device=dev)
+    rows = torch.empty((nbuf, lib.dfmi_qi_row_stride(NDATA)), dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream()
 
     def step():
@@ -167,10 +168,10 @@ def main():
                                  cfg, out.data_ptr(), ok.data_ptr(), _lib.DFMI_MEM_DEVICE, stream.cuda_stream)
         _lib.check(rc, "dfmi_nls_record")
 
-    def demod():
-        rc = lib.dfmi_demod(x.data_ptr(), nbuf, R, R, NDATA, w0, 0, qi.data_ptr(), dcb.data_ptr(),
-                            _lib.DFMI_MEM_DEVICE, stream.cuda_stream)
-        _lib.check(rc, "dfmi_demod")
+    def demod():  # the record pipeline's demodulation (row layout): the roofline kernel
+        rc = lib.dfmi_demod_rows(x.data_ptr(), nbuf, R, R, NDATA, w0, 0, rows.data_ptr(), _lib.DFMI_MEM_DEVICE,
+                                 stream.cuda_stream)
+        _lib.check(rc, "dfmi_demod_rows")
 
     fn = demod if args.demod_only else step
     for _ in range(args.warmup):
@@ -204,6 +205,7 @@ def main():
     ev1.record(stream)
     ev1.synchronize()
     demod_ms = ev0.elapsed_time(ev1) / nrep
+    kname = lib.dfmi_last_demod_kernel().decode()
     # the LM kernel alone over the same QI (every segment its own chunk), for the record
     lm_out = torch.empty((4, nbuf), dtype=torch.float64, device=dev)
     lm_ssq = torch.empty(nbuf, dtype=torch.float64, device=dev)
@@ -215,6 +217,8 @@ def main():
                          lm_ssq.data_ptr(), lm_st.data_ptr(), _lib.DFMI_MEM_DEVICE, stream.cuda_stream)
         _lib.check(rc, "dfmi_lm")
 
+    _lib.check(lib.dfmi_demod(x.data_ptr(), nbuf, R, R, NDATA, w0, 0, qi.data_ptr(), dcb.data_ptr(),
+                              _lib.DFMI_MEM_DEVICE, stream.cuda_stream), "dfmi_demod")
     lm_only()
     ev0.record(stream)
     for _ in range(nrep):
@@ -224,13 +228,17 @@ def main():
     lm_ms = ev0.elapsed_time(ev1) / nrep
     bytes_per_seg = 8 * R + 8 * (2 * NDATA + 1)  # read the segment, write QI + dc
     achieved = nbuf * bytes_per_seg / (demod_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_demod_r01.json")
-    if os.path.exists(pmc):
+    family = kname.split("<")[0]
+    traffic, traffic_src = None, None
+    pmc = os.path.join(ROOT, "profiles", "pmc_demod.json")
+    if os.path.exists(pmc):  # PMC pass of the same kernel and workload (scripts/profile_round.sh)
         with open(pmc) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
-    roof = {"kernel": "demod_fold_kernel<2,2,true>", "bound": "hbm", "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            rec = json.load(f)
+        if family and family in rec.get("kernel", "") and rec.get("algorithmic_bytes_per_launch") == \
+                nbuf * bytes_per_seg:
+            traffic, traffic_src = rec.get("hbm_bytes_per_launch"), "profiles/pmc_demod.json"
+    roof = {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
             "avg_launch_ms": round(demod_ms, 4), "algorithmic_bytes_per_launch": nbuf * bytes_per_seg}
 
     # parity on the timed batch itself: status-0 fraction and a sanity check of the estimates

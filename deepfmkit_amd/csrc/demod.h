@@ -25,50 +25,58 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "dfmi_math.h"
+
 namespace dfmi {
 
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlockThreads = 64 * kWavesPerBlock;
 constexpr int kHarmBlock = 8;  // harmonics per contraction block (16 partial sums)
 
-// Reduce-scatter of 16 per-lane partial sums over a wavefront. On return lane l
-// holds, in v[0], the wave-wide sum of value index (l >> 2) & 15.
-__device__ __forceinline__ void butterfly16(double (&v)[16], int lane) {
-  {
-    const bool hi = lane & 32;
+// One exchange stage of the reduce-scatter: lanes with the mask bit set keep
+// the upper HALF of their live values, the others the lower half, and each adds
+// its partner's copy of the half it keeps.
+template <int HALF, int MASK, int NV>
+__device__ __forceinline__ void bfly_stage(double (&v)[NV], int lane) {
+  const bool hi = lane & MASK;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const double send = hi ? v[i] : v[i + 8];
-      const double keep = hi ? v[i + 8] : v[i];
-      v[i] = keep + __shfl_xor(send, 32);
-    }
+  for (int i = 0; i < HALF; ++i) {
+    const double send = hi ? v[i] : v[i + HALF];
+    const double keep = hi ? v[i + HALF] : v[i];
+    v[i] = keep + __shfl_xor(send, MASK);
   }
-  {
-    const bool hi = lane & 16;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const double send = hi ? v[i] : v[i + 4];
-      const double keep = hi ? v[i + 4] : v[i];
-      v[i] = keep + __shfl_xor(send, 16);
-    }
+}
+
+// Reduce-scatter of NV (4, 8 or 16) per-lane partial sums over a wavefront: the
+// exchange stages (masks 32, 16, ...) halve the live values, the remaining
+// stages are plain butterfly sums. On return lane l holds, in v[0], the
+// wave-wide sum of value index (l >> (6 - log2 NV)) & (NV - 1).
+// (NV = 16: 15 exchange-adds + 2 sums = 17 shuffles instead of 16 x 6.)
+template <int NV>
+__device__ __forceinline__ void butterfly(double (&v)[NV], int lane) {
+  static_assert(NV == 4 || NV == 8 || NV == 16, "NV");
+  if constexpr (NV == 16) {
+    bfly_stage<8, 32>(v, lane);
+    bfly_stage<4, 16>(v, lane);
+    bfly_stage<2, 8>(v, lane);
+    bfly_stage<1, 4>(v, lane);
+    v[0] += __shfl_xor(v[0], 2);
+    v[0] += __shfl_xor(v[0], 1);
+  } else if constexpr (NV == 8) {
+    bfly_stage<4, 32>(v, lane);
+    bfly_stage<2, 16>(v, lane);
+    bfly_stage<1, 8>(v, lane);
+    v[0] += __shfl_xor(v[0], 4);
+    v[0] += __shfl_xor(v[0], 2);
+    v[0] += __shfl_xor(v[0], 1);
+  } else {
+    bfly_stage<2, 32>(v, lane);
+    bfly_stage<1, 16>(v, lane);
+    v[0] += __shfl_xor(v[0], 8);
+    v[0] += __shfl_xor(v[0], 4);
+    v[0] += __shfl_xor(v[0], 2);
+    v[0] += __shfl_xor(v[0], 1);
   }
-  {
-    const bool hi = lane & 8;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const double send = hi ? v[i] : v[i + 2];
-      const double keep = hi ? v[i + 2] : v[i];
-      v[i] = keep + __shfl_xor(send, 8);
-    }
-  }
-  {
-    const bool hi = lane & 4;
-    const double send = hi ? v[0] : v[1];
-    const double keep = hi ? v[1] : v[0];
-    v[0] = keep + __shfl_xor(send, 4);
-  }
-  v[0] += __shfl_xor(v[0], 2);
-  v[0] += __shfl_xor(v[0], 1);
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -103,15 +111,94 @@ struct VecT<2> {
   }
 };
 
-// Write one block of 8 harmonics (16 sums) of segment s.
-__device__ __forceinline__ void store_block(const double (&v)[16], int lane, int hb, int ndata,
+// Write one block of HB harmonics (2·HB sums, after butterfly<2·HB>) of segment s.
+template <int HB>
+__device__ __forceinline__ void store_block(const double (&v)[2 * HB], int lane, int hb, int ndata,
                                             double* __restrict__ qi, int64_t qi_ld, int64_t s, int R) {
-  if ((lane & 3) == 0) {
-    const int vi = lane >> 2;
-    const int h = hb * kHarmBlock + (vi & 7);
+  constexpr int SH = (HB == 8) ? 2 : (HB == 4) ? 3 : 4;  // 6 - log2(2·HB)
+  if ((lane & ((1 << SH) - 1)) == 0) {
+    const int vi = lane >> SH;
+    const int h = hb * HB + (vi % HB);
     if (h < ndata) {
-      const int c = (vi >> 3) ? (ndata + h) : h;
+      const int c = (vi / HB) ? (ndata + h) : h;
       qi[(int64_t)c * qi_ld + s] = v[0] / (double)R;  // numpy mean: sum / count
+    }
+  }
+}
+
+// dc + contraction of the folded phase bins y (lane-owned, see fold_segment)
+// with the basis table T, 8 harmonics per block; writes qi[:, col] and dc[col].
+// ROWS = false: qi[c·qi_ld + col] (component-major) and dc[col].
+// ROWS = true : the row layout of dfmi_qi_row_stride — qi + col·qi_ld holds the
+// segment's row; with HB = 8 every block is one 128-B line written by one store
+// instruction (16 lanes x 8 B), and dc rides in the last block's first spare Q
+// slot: its per-lane partial sum enters the same reduce-scatter, whose pairing
+// tree is wave_sum's, so dc is bit-identical to the ROWS = false value. (Scattered
+// 8-B stores into 21 component rows cost 13 % of the demodulation time:
+// profiles/r01_tune_demod_probe.json.)
+template <int VEC, int MAXSLOT, bool LOWREG = false, int HB = kHarmBlock, int PROBE = 0, bool ROWS = false>
+__device__ __forceinline__ void fold_finish(const double (&y)[MAXSLOT][VEC], const bool (&pval)[MAXSLOT],
+                                            const int (&pbase)[MAXSLOT], int R, int L, int ndata,
+                                            const double* __restrict__ T, int lane, double* __restrict__ qi,
+                                            int64_t qi_ld, int64_t col, double* __restrict__ dc) {
+  const int nblk = (ndata + HB - 1) / HB;
+  // ---- dc = mean(x) ----
+  double tot = 0.0;
+#pragma unroll
+  for (int j = 0; j < MAXSLOT; ++j)
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) tot += y[j][e];
+  static_assert(!ROWS || HB == 8, "row layout uses 8-harmonic blocks");
+  const int spare = ndata % HB;  // ROWS: dc slot in the last block (0: no spare slot)
+  if (!ROWS || spare == 0) {
+    const double all = wave_sum(tot);
+    if (lane == 0) {
+      if constexpr (ROWS) qi[col * qi_ld + dfmi_row_dc(ndata)] = all / (double)R;
+      else dc[col] = all / (double)R;
+    }
+  }
+
+  // ---- contraction with the basis, HB harmonics per block ----
+  if constexpr (PROBE == 2) return;  // timing probe: no contraction
+  for (int hb = 0; hb < nblk; ++hb) {
+    double acc[2 * HB];
+#pragma unroll
+    for (int i = 0; i < 2 * HB; ++i) acc[i] = 0.0;
+    if constexpr (ROWS) {
+      if (spare && hb == nblk - 1) {
+#pragma unroll
+        for (int i = 0; i < HB; ++i)
+          if (i == spare) acc[i] = tot;  // Q slot of harmonic >= ndata: no basis term lands here
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < MAXSLOT; ++j) {
+      if (!pval[j]) continue;
+#pragma unroll
+      for (int h = 0; h < HB; ++h) {
+        const int hh = hb * HB + h;
+        if (hh < ndata) {
+          double bc[VEC], bs[VEC];
+          VecT<VEC>::load(T + (int64_t)hh * L + pbase[j], bc);
+          VecT<VEC>::load(T + (int64_t)(ndata + hh) * L + pbase[j], bs);
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) {
+            acc[h] = fma(y[j][e], bc[e], acc[h]);
+            acc[HB + h] = fma(y[j][e], bs[e], acc[HB + h]);
+          }
+        }
+        // LOWREG: one harmonic's basis reads at a time (keeps the streaming
+        // kernel's in-flight load buffers and the contraction within 128 VGPRs)
+        if constexpr (LOWREG) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    butterfly<2 * HB>(acc, lane);
+    if constexpr (PROBE != 0) {
+      if (acc[0] == 1.2345e300) qi[col] = acc[0];  // timing probe: keep the work, drop the stores
+    } else if constexpr (ROWS) {
+      if ((lane & 3) == 0) qi[col * qi_ld + hb * 16 + (lane >> 2)] = acc[0] / (double)R;  // one 128-B line
+    } else {
+      store_block<HB>(acc, lane, hb, ndata, qi, qi_ld, col, R);
     }
   }
 }
@@ -128,7 +215,6 @@ __device__ __forceinline__ void fold_segment(const double* __restrict__ xs, int 
   const int ncyc = R / L;
   const int rem = R - ncyc * L;
   constexpr int UNR = (MAXSLOT >= LOADS) ? 1 : (LOADS / MAXSLOT);
-  const int nblk = (ndata + kHarmBlock - 1) / kHarmBlock;
   int pbase[MAXSLOT];
   bool pval[MAXSLOT];
 #pragma unroll
@@ -186,41 +272,7 @@ __device__ __forceinline__ void fold_segment(const double* __restrict__ xs, int 
         if (pval[j] && pbase[j] + e < rem) y[j][e] += xr[pbase[j] + e];
   }
 
-  // ---- dc = mean(x) ----
-  double tot = 0.0;
-#pragma unroll
-  for (int j = 0; j < MAXSLOT; ++j)
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) tot += y[j][e];
-  tot = wave_sum(tot);
-  if (lane == 0) dc[col] = tot / (double)R;
-
-  // ---- contraction with the basis, 8 harmonics per block ----
-  for (int hb = 0; hb < nblk; ++hb) {
-    double acc[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.0;
-#pragma unroll
-    for (int j = 0; j < MAXSLOT; ++j) {
-      if (!pval[j]) continue;
-#pragma unroll
-      for (int h = 0; h < kHarmBlock; ++h) {
-        const int hh = hb * kHarmBlock + h;
-        if (hh < ndata) {
-          double bc[VEC], bs[VEC];
-          VecT<VEC>::load(T + (int64_t)hh * L + pbase[j], bc);
-          VecT<VEC>::load(T + (int64_t)(ndata + hh) * L + pbase[j], bs);
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) {
-            acc[h] = fma(y[j][e], bc[e], acc[h]);
-            acc[8 + h] = fma(y[j][e], bs[e], acc[8 + h]);
-          }
-        }
-      }
-    }
-    butterfly16(acc, lane);
-    store_block(acc, lane, hb, ndata, qi, qi_ld, col, R);
-  }
+  fold_finish<VEC, MAXSLOT>(y, pval, pbase, R, L, ndata, T, lane, qi, qi_ld, col, dc);
 }
 
 template <int VEC, int MAXSLOT, bool LDS_TAB, int LOADS = 8, bool NT = true>
@@ -239,6 +291,347 @@ __global__ __launch_bounds__(kBlockThreads) void demod_fold_kernel(
   for (int64_t s = (int64_t)blockIdx.x * kWavesPerBlock + wave; s < nseg;
        s += (int64_t)gridDim.x * kWavesPerBlock) {
     fold_segment<VEC, MAXSLOT, LOADS, NT>(x + s * seg_stride, R, L, ndata, T, lane, qi, qi_ld, s, dc);
+  }
+}
+
+// Streaming fold: the same fold + contraction as demod_fold_kernel, software-
+// pipelined ACROSS segments. Preconditions (checked on the host): VEC = 2
+// (16-B aligned rows, even L, even stride), R % L == 0 and (R / L) % UNR == 0,
+// ceil(L / 128) <= MS, basis table in LDS. A wave's work is one flat sequence
+// of batches (UNR cycles of L samples = MS·UNR 16-B loads per lane) over its
+// segments s = gw, gw + W, ...; batch g+1 is always in flight while batch g is
+// added, including while the contraction of a finished segment runs, so the
+// wave's memory pipe does not drain at segment boundaries (fold_segment's waits
+// for all its loads of a batch, then contracts with nothing in flight). Cycles
+// are still added in ascending k: results are bit-identical to fold_segment.
+template <int MS, int UNR>
+struct FoldBuf {
+  double v[UNR][MS][2];
+};
+
+// Every lane loads (lanes whose phase bin lies past L re-read their slot-0 line,
+// which the same wave instruction fetches anyway) and the value is zeroed after
+// the load: no exec-masked branches around the loads, so the compiler's waitcnt
+// bookkeeping keeps the next batch in flight across the adds.
+template <int MS, int UNR, bool NT>
+__device__ __forceinline__ void fold_load(FoldBuf<MS, UNR>& b, const double* __restrict__ p, int L,
+                                          const int (&poff)[MS]) {
+#pragma unroll
+  for (int u = 0; u < UNR; ++u)
+#pragma unroll
+    for (int j = 0; j < MS; ++j) {
+      if constexpr (NT) VecT<2>::load_nt(p + u * L + poff[j], b.v[u][j]);
+      else VecT<2>::load(p + u * L + poff[j], b.v[u][j]);
+    }
+}
+
+template <int MS, int UNR>
+__device__ __forceinline__ void fold_add(double (&y)[MS][2], const FoldBuf<MS, UNR>& b, const bool (&pval)[MS]) {
+#pragma unroll
+  for (int u = 0; u < UNR; ++u)
+#pragma unroll
+    for (int j = 0; j < MS; ++j) {
+      y[j][0] += pval[j] ? b.v[u][j][0] : 0.0;
+      y[j][1] += pval[j] ? b.v[u][j][1] : 0.0;
+    }
+}
+
+template <int MS, int UNR, bool NT, int MINB = 1>
+__global__ __launch_bounds__(kBlockThreads, MINB) void demod_stream_kernel(
+    const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
+    const double* __restrict__ tab, const double* __restrict__ pad, double* __restrict__ qi, int64_t qi_ld,
+    double* __restrict__ dc) {
+  extern __shared__ __attribute__((aligned(16))) double lds_tab[];
+  {
+    const int n = 2 * ndata * L;
+    for (int i = threadIdx.x; i < n; i += kBlockThreads) lds_tab[i] = tab[i];
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & 63;
+  const int64_t W = (int64_t)gridDim.x * kWavesPerBlock;
+  // wave-uniform (scalar) cursors: the loop control stays in SGPRs
+  const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (gw >= nseg) return;
+  const int64_t nmine = (nseg - 1 - gw) / W + 1;
+  const int nb = (R / L) / UNR;  // batches per segment
+  const int64_t G = nmine * nb;  // batches of this wave
+  const int nslot = (L + 127) / 128;
+  int pbase[MS], poff[MS];
+  bool pval[MS];
+#pragma unroll
+  for (int j = 0; j < MS; ++j) {
+    pbase[j] = 2 * (lane + 64 * j);
+    pval[j] = (j < nslot) && (pbase[j] < L);
+    poff[j] = pval[j] ? pbase[j] : pbase[0];
+  }
+  double y[MS][2];
+#pragma unroll
+  for (int j = 0; j < MS; ++j) y[j][0] = y[j][1] = 0.0;
+
+  // Loads are issued unconditionally (a conditional load makes the compiler's
+  // waitcnt merge drain every outstanding load at the join): batches past the
+  // wave's end read `pad`, a small L2-resident dummy buffer (no HBM traffic).
+  const int64_t bstride = (int64_t)UNR * L;
+  int64_t ls = gw;  // load cursor: segment, batch
+  int lb = 0;
+  int64_t lg = 0;
+  auto next_ptr = [&]() {
+    const double* p = (lg < G) ? x + ls * seg_stride + lb * bstride : pad;
+    ++lg;
+    if (++lb == nb) {
+      lb = 0;
+      ls += W;
+    }
+    return p;
+  };
+  int64_t cs = gw;  // consume cursor
+  int cb = 0;
+  auto consumed = [&]() {
+    if (++cb == nb) {
+      fold_finish<2, MS, true>(y, pval, pbase, R, L, ndata, lds_tab, lane, qi, qi_ld, cs, dc);
+#pragma unroll
+      for (int j = 0; j < MS; ++j) y[j][0] = y[j][1] = 0.0;
+      cb = 0;
+      cs += W;
+    }
+  };
+  FoldBuf<MS, UNR> A, B;
+  fold_load<MS, UNR, NT>(A, next_ptr(), L, poff);
+  fold_load<MS, UNR, NT>(B, next_ptr(), L, poff);
+  for (int64_t g = 0; g < G; g += 2) {
+    fold_add(y, A, pval);
+    consumed();
+    fold_load<MS, UNR, NT>(A, next_ptr(), L, poff);
+    if (g + 1 < G) {
+      fold_add(y, B, pval);
+      consumed();
+    }
+    fold_load<MS, UNR, NT>(B, next_ptr(), L, poff);
+  }
+}
+
+// Bin-in-LDS fold: the same fold + contraction as demod_fold_kernel, but the
+// segment is read the way HBM likes it — as flat, 1-KB-aligned wave loads
+// (lane l reads x[128c + 2l .. +1] of chunk c), not cycle by cycle. A cycle of
+// L = 200 doubles is 1600 B, so cycle-aligned wave loads start 64 B off a
+// 128-B line every other cycle and the second slot is a 576-B partial load:
+// measured 5.5 TB/s against 6.7 TB/s for the flat pattern
+// (profiles/r01_readbw.jsonl, segwave_l8_nt_g4). The phase bins then cannot
+// live in fixed lanes, so each wave keeps its L bins in LDS and adds every
+// chunk into them with a ds_read_b128 / add / ds_write_b128 per lane (the 128
+// consecutive samples of a chunk fall in 128 distinct bins when L >= 128, and a
+// wave's LDS operations execute in order, so no atomics are needed). Every bin
+// still receives its samples in ascending t from 0.0, exactly as in
+// fold_segment, and the contraction is fold_finish on the same lane-owned
+// bins: results are bit-identical to demod_fold_kernel.
+// Preconditions (host-checked): 16-B aligned rows (x and seg_stride even),
+// L even, 128 <= L <= 128·MAXSLOT.
+// WPB waves per workgroup share one LDS copy of the basis (TAB_LDS) — or read it
+// through the cache (TAB_LDS = false: LDS then holds only the bins); MINB is the
+// occupancy floor handed to the register allocator (blocks per CU).
+// PROBE (timing only, results invalid): 1 = contraction without the QI stores,
+// 2 = no contraction (dc only).
+template <int MAXSLOT, int LOADS, bool NT, int WPB = 4, int MINB = 1, bool TAB_LDS = true, int HB = kHarmBlock,
+          int PROBE = 0, bool ROWS = false>
+__global__ __launch_bounds__(64 * WPB, MINB) void demod_bins_kernel(
+    const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
+    const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc) {
+  extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
+  const int ntab = TAB_LDS ? 2 * ndata * L : 0;
+  if constexpr (TAB_LDS) {
+    for (int i = threadIdx.x; i < ntab; i += 64 * WPB) lds_dyn[i] = tab[i];
+    __syncthreads();
+  }
+  const double* __restrict__ T = TAB_LDS ? lds_dyn : tab;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  double* __restrict__ ybin = lds_dyn + ntab + wave * L;  // this wave's L phase bins
+  const int nslot = (L + 127) / 128;
+  int pbase[MAXSLOT];
+  bool pval[MAXSLOT];
+#pragma unroll
+  for (int j = 0; j < MAXSLOT; ++j) {
+    pbase[j] = 2 * (lane + 64 * j);
+    pval[j] = (j < nslot) && (pbase[j] < L);
+  }
+  const int nch = R >> 7;          // full 128-sample chunks
+  const int tail = R - (nch << 7);  // samples of the last, partial chunk
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  auto add_chunk = [&](int p0, const double (&v)[2]) {
+    int p = p0 + 2 * lane;
+    if (p >= L) p -= L;
+    d2v* yp = reinterpret_cast<d2v*>(ybin + p);
+    d2v t = *yp;
+    t.x += v[0];
+    t.y += v[1];
+    *yp = t;
+  };
+  for (int64_t s = (int64_t)blockIdx.x * WPB + wave; s < nseg; s += (int64_t)gridDim.x * WPB) {
+#pragma unroll
+    for (int j = 0; j < MAXSLOT; ++j)
+      if (pval[j]) *reinterpret_cast<d2v*>(ybin + pbase[j]) = d2v{0.0, 0.0};
+    const double* __restrict__ xs = x + s * seg_stride + 2 * lane;
+    int p0 = 0;  // bin of the chunk's first sample: (128 c) mod L
+    int c = 0;
+    for (; c + LOADS <= nch; c += LOADS) {
+      double v[LOADS][2];
+#pragma unroll
+      for (int u = 0; u < LOADS; ++u) {
+        if constexpr (NT) VecT<2>::load_nt(xs + (c + u) * 128, v[u]);
+        else VecT<2>::load(xs + (c + u) * 128, v[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < LOADS; ++u) {
+        add_chunk(p0, v[u]);
+        p0 += 128;
+        if (p0 >= L) p0 -= L;
+      }
+    }
+    for (; c < nch; ++c) {
+      double v[2];
+      VecT<2>::load(xs + c * 128, v);
+      add_chunk(p0, v);
+      p0 += 128;
+      if (p0 >= L) p0 -= L;
+    }
+    if (tail) {  // partial chunk: element-wise (R may be odd)
+      const int t0 = 2 * lane;
+      int p = p0 + t0;
+      if (p >= L) p -= L;
+      if (t0 < tail) ybin[p] += xs[nch * 128];
+      if (t0 + 1 < tail) ybin[p + 1] += xs[nch * 128 + 1];
+    }
+    double y[MAXSLOT][2];
+#pragma unroll
+    for (int j = 0; j < MAXSLOT; ++j) {
+      if (pval[j]) {
+        const d2v t = *reinterpret_cast<const d2v*>(ybin + pbase[j]);
+        y[j][0] = t.x;
+        y[j][1] = t.y;
+      } else {
+        y[j][0] = y[j][1] = 0.0;
+      }
+    }
+    fold_finish<2, MAXSLOT, false, HB, PROBE, ROWS>(y, pval, pbase, R, L, ndata, T, lane, qi, qi_ld, s, dc);
+  }
+}
+
+// Pipelined variant of demod_bins_kernel: a wave's work is one flat sequence of
+// chunks over its segments (NC = ceil(R / 128) chunks per segment, the last one
+// lane-masked), loaded UNR chunks at a time into two register buffers; batch
+// b+1 is in flight while batch b is added into the bins, including while a
+// finished segment is contracted, so the wave's memory pipe never drains
+// (demod_bins_kernel waits for its whole batch and then computes with nothing
+// in flight). Loads are unconditional — past the wave's last chunk they read
+// `pad`, a small dummy buffer — so the compiler's waitcnt merge keeps them in
+// flight. Requires R even (whole 16-B pairs); bit-identical to demod_bins_kernel.
+template <int MAXSLOT, int UNR, bool NT>
+__global__ __launch_bounds__(kBlockThreads) void demod_bins_pipe_kernel(
+    const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
+    const double* __restrict__ tab, const double* __restrict__ pad, double* __restrict__ qi, int64_t qi_ld,
+    double* __restrict__ dc) {
+  extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
+  const int ntab = 2 * ndata * L;
+  for (int i = threadIdx.x; i < ntab; i += kBlockThreads) lds_dyn[i] = tab[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t W = (int64_t)gridDim.x * kWavesPerBlock;
+  const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (gw >= nseg) return;
+  double* __restrict__ ybin = lds_dyn + ntab + wave * L;
+  const int nslot = (L + 127) / 128;
+  int pbase[MAXSLOT];
+  bool pval[MAXSLOT];
+#pragma unroll
+  for (int j = 0; j < MAXSLOT; ++j) {
+    pbase[j] = 2 * (lane + 64 * j);
+    pval[j] = (j < nslot) && (pbase[j] < L);
+  }
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  auto zero_bins = [&]() {
+#pragma unroll
+    for (int j = 0; j < MAXSLOT; ++j)
+      if (pval[j]) *reinterpret_cast<d2v*>(ybin + pbase[j]) = d2v{0.0, 0.0};
+  };
+  const int NC = (R + 127) >> 7;             // chunks per segment
+  const int tail = R - ((NC - 1) << 7);      // valid samples of the last chunk (even, 2..128)
+  const bool tail_ok = 2 * lane < tail;      // this lane's pair is valid in the last chunk
+  const int64_t nmine = (nseg - 1 - gw) / W + 1;
+  const int64_t G = nmine * NC;              // chunks of this wave
+
+  // load cursor (wave-uniform)
+  int64_t lgi = 0, lseg = gw;
+  int lc = 0;
+  auto next_ptr = [&]() -> const double* {
+    const double* p;
+    if (lgi < G) {
+      const bool last = (lc == NC - 1);
+      p = x + lseg * seg_stride + ((last && !tail_ok) ? 0 : (lc << 7)) + 2 * lane;
+    } else {
+      p = pad + 2 * lane;
+    }
+    ++lgi;
+    if (++lc == NC) {
+      lc = 0;
+      lseg += W;
+    }
+    return p;
+  };
+  // consume cursor
+  int64_t cseg = gw;
+  int cc = 0, p0 = 0;
+  auto consume = [&](const double (&v)[2]) {
+    if (cc < NC - 1 || tail_ok) {
+      int p = p0 + 2 * lane;
+      if (p >= L) p -= L;
+      d2v* yp = reinterpret_cast<d2v*>(ybin + p);
+      d2v t = *yp;
+      t.x += v[0];
+      t.y += v[1];
+      *yp = t;
+    }
+    p0 += 128;
+    if (p0 >= L) p0 -= L;
+    if (++cc == NC) {
+      double y[MAXSLOT][2];
+#pragma unroll
+      for (int j = 0; j < MAXSLOT; ++j) {
+        if (pval[j]) {
+          const d2v t = *reinterpret_cast<const d2v*>(ybin + pbase[j]);
+          y[j][0] = t.x;
+          y[j][1] = t.y;
+        } else {
+          y[j][0] = y[j][1] = 0.0;
+        }
+      }
+      fold_finish<2, MAXSLOT>(y, pval, pbase, R, L, ndata, lds_dyn, lane, qi, qi_ld, cseg, dc);
+      zero_bins();
+      cc = 0;
+      p0 = 0;
+      cseg += W;
+    }
+  };
+  auto load_batch = [&](double (&v)[UNR][2]) {
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const double* p = next_ptr();
+      if constexpr (NT) VecT<2>::load_nt(p, v[u]);
+      else VecT<2>::load(p, v[u]);
+    }
+  };
+  zero_bins();
+  double A[UNR][2], B[UNR][2];
+  load_batch(A);
+  for (int64_t g = 0; g < G; g += 2 * UNR) {
+    load_batch(B);
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+      if (g + u < G) consume(A[u]);
+    load_batch(A);
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+      if (g + UNR + u < G) consume(B[u]);
   }
 }
 
@@ -273,8 +666,8 @@ __device__ __forceinline__ void direct_segment(const double* __restrict__ xs, in
         }
       }
     }
-    butterfly16(acc, lane);
-    store_block(acc, lane, hb, ndata, qi, qi_ld, col, R);
+    butterfly<16>(acc, lane);
+    store_block<kHarmBlock>(acc, lane, hb, ndata, qi, qi_ld, col, R);
   }
 }
 

@@ -193,8 +193,29 @@ struct Tuning {
   int demod_nt = 1;            // non-temporal stream loads (measured +14 %, profiles/r01_tune_demod.json)
   int demod_blocks_per_cu = 0; // 0 = occupancy limit
   int lm_general = 0;          // 1: force the two-pass (general) LM path for every ndata
+  int demod_kernel = 2;        // 0: cycle-aligned fold, 1: software-pipelined cycle-aligned fold
+                               // (measured slower: profiles/r01_tune_demod_stream.json), 2: bins in LDS,
+                               // 3: bins in LDS, pipelined
+  int demod_unr = 4;           // cycles per batch of the streaming fold (1, 2, 4, 5)
+  int seed_reserve = 1;        // 1: the bulk demodulation grid leaves slots free for the seed waves
+  int demod_bins_cfg = 0;      // bins kernel shape: 0 = 4-wave blocks, LDS basis, 8 harmonics per
+                               // reduction block; 1..6 = higher-occupancy shapes (launch_bins_t);
+                               // 7, 8 = timing probes (no QI stores / no contraction: results invalid)
 };
 Tuning g_tune;
+std::string g_last_demod;
+// Workgroup slots a persistent demodulation grid leaves free (set by the record
+// pipeline for the concurrent seed waves; every launcher subtracts it).
+int64_t g_grid_reserve = 0;
+
+int64_t persistent_grid(int n_cu, int per_cu, int64_t need) {
+  int64_t grid = (int64_t)n_cu * per_cu - g_grid_reserve;
+  if (grid > need) grid = need;
+  if (grid < 1) grid = 1;
+  return grid;
+}  // kernel variant of the last demodulation launch (dfmi_last_demod_kernel)
+
+
 
 int32_t detect_period_impl(double w0, int32_t R, int32_t ndata) {
   if (!(w0 > 0) || R <= 0 || ndata <= 0) return 0;
@@ -228,13 +249,12 @@ int launch_fold_t(const double* x, int64_t nseg, int64_t stride, int R, int L, i
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, dfmi::kBlockThreads, lds));
   if (per_cu < 1) per_cu = 1;
   if (g_tune.demod_blocks_per_cu > 0 && g_tune.demod_blocks_per_cu < per_cu) per_cu = g_tune.demod_blocks_per_cu;
-  int64_t need = (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock;
-  int64_t grid = (int64_t)n_cu * per_cu;
-  if (grid > need) grid = need;
-  if (grid < 1) grid = 1;
+  const int64_t grid = persistent_grid(n_cu, per_cu, (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(dfmi::kBlockThreads), lds, st, x, nseg, stride, R, L, ndata,
                      tab, qi, qi_ld, dc);
   HIPCHK(hipGetLastError());
+  g_last_demod = "demod_fold_kernel<" + std::to_string(VEC) + "," + std::to_string(MS) + "," +
+                 std::to_string((int)LDS) + "," + std::to_string(LOADS) + "," + std::to_string((int)NT) + ">";
   return DFMI_OK;
 }
 
@@ -249,13 +269,169 @@ int launch_fold_ms(int ms, const double* x, int64_t nseg, int64_t stride, int R,
   }
 }
 
+template <int UNR>
+int launch_stream_t(int dev, const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata,
+                    const double* tab, double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu) {
+  constexpr int MINB = UNR <= 2 ? 4 : 3;
+  const size_t lds = (size_t)2 * ndata * L * sizeof(double);
+  auto kern = dfmi::demod_stream_kernel<2, UNR, true, MINB>;
+  void* pad = nullptr;
+  int rc = workspace(dev, "stream_pad", ((size_t)UNR * L + 256) * sizeof(double), &pad);
+  if (rc) return rc;
+  int per_cu = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, dfmi::kBlockThreads, lds));
+  if (per_cu < 1) per_cu = 1;
+  if (g_tune.demod_blocks_per_cu > 0 && g_tune.demod_blocks_per_cu < per_cu) per_cu = g_tune.demod_blocks_per_cu;
+  const int64_t grid = persistent_grid(n_cu, per_cu, (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(dfmi::kBlockThreads), lds, st, x, nseg, stride, R, L, ndata,
+                     tab, (const double*)pad, qi, qi_ld, dc);
+  HIPCHK(hipGetLastError());
+  g_last_demod = "demod_stream_kernel<2," + std::to_string(UNR) + ",1," + std::to_string(MINB) + ">";
+  return DFMI_OK;
+}
+
+// Streaming fold (demod.h demod_stream_kernel) when its preconditions hold:
+// 16-B rows, 128 < L <= 256 (two 16-B slots per lane), R % L == 0, basis in LDS,
+// and a batch size dividing R / L. Returns 1 if it does not apply.
+int try_stream(int dev, const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tab,
+               double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu, bool vec2, bool use_lds) {
+  if (g_tune.demod_kernel != 1 || !vec2 || !use_lds || L <= 128 || L > 256 || R % L) return 1;
+  const int ncyc = R / L;
+  int unr = g_tune.demod_unr;
+  const int prefs[4] = {unr, 4, 2, 1};
+  for (int u : prefs) {
+    if (ncyc % u) continue;
+    switch (u) {
+      case 1: return launch_stream_t<1>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
+      case 2: return launch_stream_t<2>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
+      case 4: return launch_stream_t<4>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
+      case 5: return launch_stream_t<5>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
+      default: break;
+    }
+  }
+  return 1;
+}
+
+template <int MS, int LOADS, bool NT, int WPB = 4, int WPEU = 1, bool TAB_LDS = true, int HB = 8, int PROBE = 0,
+          bool ROWS = false>
+int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tab,
+                  double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu, size_t lds_cap) {
+  if constexpr (MS == 2 && LOADS == 8 && NT && WPB == 4 && WPEU == 1 && TAB_LDS && HB == 8 && PROBE == 0 && !ROWS) {
+    switch (g_tune.demod_bins_cfg) {  // tunable shape
+      case 7: return launch_bins_t<2, 8, true, 4, 1, true, 8, 1>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+      case 8: return launch_bins_t<2, 8, true, 4, 1, true, 8, 2>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+      case 1: return launch_bins_t<2, 8, true, 8, 6, true, 4>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+      case 2: return launch_bins_t<2, 4, true, 8, 6, true, 4>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+      case 3: return launch_bins_t<2, 8, true, 16, 8, true, 2>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+      case 4: return launch_bins_t<2, 4, true, 16, 8, true, 2>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+      case 5: return launch_bins_t<2, 8, true, 4, 6, false, 4>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+      case 6: return launch_bins_t<2, 8, true, 4, 8, false, 2>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+      default: break;
+    }
+    if (g_tune.demod_loads == 16)
+      return launch_bins_t<2, 16, true>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+    if (!g_tune.demod_nt)
+      return launch_bins_t<2, 8, false>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+  }
+  const size_t lds = ((TAB_LDS ? (size_t)2 * ndata * L : 0) + (size_t)WPB * L) * sizeof(double);
+  if (lds > lds_cap) return fail(DFMI_ERR_UNSUPPORTED, "demod_bins_kernel: LDS footprint exceeds the workgroup limit");
+  auto kern = dfmi::demod_bins_kernel<MS, LOADS, NT, WPB, WPEU, TAB_LDS, HB, PROBE, ROWS>;
+  int per_cu = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WPB, lds));
+  if (per_cu < 1) per_cu = 1;
+  if (g_tune.demod_blocks_per_cu > 0 && g_tune.demod_blocks_per_cu < per_cu) per_cu = g_tune.demod_blocks_per_cu;
+  const int64_t grid = persistent_grid(n_cu, per_cu, (nseg + WPB - 1) / WPB);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * WPB), lds, st, x, nseg, stride, R, L, ndata, tab, qi,
+                     qi_ld, dc);
+  HIPCHK(hipGetLastError());
+  g_last_demod = "demod_bins_kernel<" + std::to_string(MS) + "," + std::to_string(LOADS) + "," +
+                 std::to_string((int)NT) + "," + std::to_string(WPB) + "," + std::to_string(WPEU) + "," +
+                 std::to_string((int)TAB_LDS) + "," + std::to_string(HB) + (ROWS ? ",rows" : "") + ">";
+  return DFMI_OK;
+}
+
+template <int MS, int UNR>
+int launch_bins_pipe_t(int dev, const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata,
+                       const double* tab, double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu,
+                       size_t lds) {
+  auto kern = g_tune.demod_nt ? dfmi::demod_bins_pipe_kernel<MS, UNR, true> : dfmi::demod_bins_pipe_kernel<MS, UNR, false>;
+  void* pad = nullptr;
+  int rc = workspace(dev, "bins_pad", 256 * sizeof(double), &pad);
+  if (rc) return rc;
+  int per_cu = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, dfmi::kBlockThreads, lds));
+  if (per_cu < 1) per_cu = 1;
+  if (g_tune.demod_blocks_per_cu > 0 && g_tune.demod_blocks_per_cu < per_cu) per_cu = g_tune.demod_blocks_per_cu;
+  const int64_t grid = persistent_grid(n_cu, per_cu, (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(dfmi::kBlockThreads), lds, st, x, nseg, stride, R, L, ndata,
+                     tab, (const double*)pad, qi, qi_ld, dc);
+  HIPCHK(hipGetLastError());
+  g_last_demod = "demod_bins_pipe_kernel<" + std::to_string(MS) + "," + std::to_string(UNR) + "," +
+                 std::to_string(g_tune.demod_nt) + ">";
+  return DFMI_OK;
+}
+
+// Bin-in-LDS fold (demod.h demod_bins_kernel) when its preconditions hold:
+// 16-B rows, even L with 128 <= L <= 1024, basis + 4 waves' bins in LDS.
+// Returns 1 if it does not apply.
+bool bins_applicable(bool vec2, int R, int L, int ndata, size_t lds_cap) {
+  (void)R;
+  if ((g_tune.demod_kernel != 2 && g_tune.demod_kernel != 3) || !vec2 || (L & 1) || L < 128 || L > 1024) return false;
+  const size_t lds = ((size_t)2 * ndata * L + (size_t)dfmi::kWavesPerBlock * L) * sizeof(double);
+  return lds <= lds_cap && lds <= 64 * 1024;
+}
+
+int try_bins(int dev, const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tab,
+             double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu, bool vec2, size_t lds_cap,
+             bool rows) {
+  if (!bins_applicable(vec2, R, L, ndata, lds_cap)) return 1;
+  const size_t lds = ((size_t)2 * ndata * L + (size_t)dfmi::kWavesPerBlock * L) * sizeof(double);
+  const int nslot = (L + 127) / 128;
+  if (rows) {
+    if (nslot <= 2)
+      return launch_bins_t<2, 8, true, 4, 1, true, 8, 0, true>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st,
+                                                               n_cu, lds_cap);
+    if (nslot <= 4)
+      return launch_bins_t<4, 8, true, 4, 1, true, 8, 0, true>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st,
+                                                               n_cu, lds_cap);
+    return launch_bins_t<8, 8, true, 4, 1, true, 8, 0, true>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st,
+                                                             n_cu, lds_cap);
+  }
+  if (g_tune.demod_kernel == 3 && (R % 2) == 0) {
+    if (nslot <= 2)
+      return g_tune.demod_unr == 8
+                 ? launch_bins_pipe_t<2, 8>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds)
+                 : launch_bins_pipe_t<2, 4>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds);
+    if (nslot <= 4) return launch_bins_pipe_t<4, 4>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds);
+    return launch_bins_pipe_t<8, 4>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds);
+  }
+  if (nslot <= 2) return launch_bins_t<2, 8, true>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+  if (nslot <= 4) return launch_bins_t<4, 8, true>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+  return launch_bins_t<8, 8, true>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+}
+
+// Whether demod_device can write the row layout (dfmi_qi_row_stride) for this
+// input: only the bin-in-LDS kernel implements it.
+bool rows_supported(int dev, const double* x, int64_t stride, int R, int ndata, double w0, int period) {
+  int L = period;
+  if (L == 0) L = detect_period_impl(w0, R, ndata);
+  if (L <= 0) return false;
+  const bool vec2 = (L % 2 == 0) && (stride % 2 == 0) && (((uintptr_t)x & 15) == 0);
+  return bins_applicable(vec2, R, L, ndata, g_dev[dev].lds_per_block);
+}
+
 // Device-pointer demodulation (all pointers on the current device).
+// rows = true: write the row layout (qi + s·qi_ld, dfmi_qi_row_stride; dc inside
+// the row, `dc` unused) — callers check rows_supported() first.
 int demod_device(int dev, const double* x, int64_t nseg, int64_t stride, int R, int ndata, double w0, int period,
-                 double* qi, int64_t qi_ld, double* dc, hipStream_t st) {
+                 double* qi, int64_t qi_ld, double* dc, hipStream_t st, bool rows = false) {
   if (nseg == 0) return DFMI_OK;
   int L = period;
   if (L == 0) L = detect_period_impl(w0, R, ndata);
-  const DeviceState& ds = g_dev[dev];
+  struct {
+    int n_cu;
+    size_t lds_per_block;
+  } ds = {g_dev[dev].n_cu, g_dev[dev].lds_per_block};
   if (L > 0) {
     const bool vec2 = (L % 2 == 0) && (stride % 2 == 0) && (((uintptr_t)x & 15) == 0);
     const int VEC = vec2 ? 2 : 1;
@@ -268,6 +444,12 @@ int demod_device(int dev, const double* x, int64_t nseg, int64_t stride, int R, 
       if (rc) return rc;
       const size_t lds = (size_t)2 * ndata * L * sizeof(double);
       const bool use_lds = lds <= 64 * 1024 && lds <= ds.lds_per_block;
+      rc = try_bins(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, ds.n_cu, vec2, ds.lds_per_block,
+                    rows);
+      if (rc <= 0) return rc;
+      if (rows) return fail(DFMI_ERR_UNSUPPORTED, "row layout needs the bin-in-LDS demodulation kernel");
+      rc = try_stream(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, ds.n_cu, vec2, use_lds);
+      if (rc <= 0) return rc;
       if (vec2) {
         return use_lds ? launch_fold_ms<2, true>(ms, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, ds.n_cu)
                        : launch_fold_ms<2, false>(ms, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, ds.n_cu);
@@ -276,6 +458,7 @@ int demod_device(int dev, const double* x, int64_t nseg, int64_t stride, int R, 
                      : launch_fold_ms<1, false>(ms, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, ds.n_cu);
     }
   }
+  if (rows) return fail(DFMI_ERR_UNSUPPORTED, "row layout needs the bin-in-LDS demodulation kernel");
   // direct kernel
   int64_t need = (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock;
   int64_t grid = (int64_t)ds.n_cu * 8;
@@ -283,6 +466,7 @@ int demod_device(int dev, const double* x, int64_t nseg, int64_t stride, int R, 
   hipLaunchKernelGGL(dfmi::demod_direct_kernel, dim3((unsigned)grid), dim3(dfmi::kBlockThreads), 0, st, x, nseg,
                      stride, R, ndata, w0, qi, qi_ld, dc);
   HIPCHK(hipGetLastError());
+  g_last_demod = "demod_direct_kernel";
   return DFMI_OK;
 }
 
@@ -290,7 +474,7 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
               int64_t nitems, int64_t nchunk, const double* guess_dev, int64_t g_rec, int64_t g_comp,
               const double* guess_host /* nrec*4, used when nrec <= 8 and guess_dev == null */,
               const dfmi::LMConst& c, const double* jtab, double* out, int64_t out_ld, int32_t* status,
-              hipStream_t st) {
+              hipStream_t st, bool rows = false) {
   if (nrec == 0 || nitems == 0) return DFMI_OK;
   if (nchunk < 1) nchunk = 1;
   if (nchunk > nitems) nchunk = nitems;  // np.array_split chunks beyond nitems are empty
@@ -309,13 +493,21 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
   // register path for ndata <= 16 (QI/Bessel in registers), general path above
   const bool chain = nitems > nchunk;
   const int nd_sel = g_tune.lm_general ? 1000 : ndata;
+  if (rows && chain) return fail(DFMI_ERR_ARG, "row layout: chunk size 1 only");
+  size_t lds = 0;
   auto kern = chain ? (nd_sel <= 12   ? dfmi::lm_chunks_kernel<12, true>
                        : nd_sel <= 16 ? dfmi::lm_chunks_kernel<16, true>
                                      : dfmi::lm_chunks_kernel<0, true>)
                     : (nd_sel <= 12   ? dfmi::lm_chunks_kernel<12, false>
                        : nd_sel <= 16 ? dfmi::lm_chunks_kernel<16, false>
                                      : dfmi::lm_chunks_kernel<0, false>);
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(block), 0, st, qi, qi_ld, ndata, nrec, nbuf, first, nitems,
+  if (rows) {
+    kern = nd_sel <= 12   ? dfmi::lm_chunks_kernel<12, false, true>
+           : nd_sel <= 16 ? dfmi::lm_chunks_kernel<16, false, true>
+                          : dfmi::lm_chunks_kernel<0, false, true>;
+    if (nd_sel <= 16) lds = (size_t)qi_ld * 65 * sizeof(double);  // the wave's rows, transposed
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(block), lds, st, qi, qi_ld, ndata, nrec, nbuf, first, nitems,
                      nchunk, guess_dev, g_rec, g_comp, ginl, use_inline, jtab, c, out, out_ld, status);
   HIPCHK(hipGetLastError());
   return DFMI_OK;
@@ -353,8 +545,13 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
     for (int64_t r = 0; r < nrec; ++r)
       for (int i = 0; i < 4; ++i) ginl.v[r][i] = init_guess_host[r * 4 + i];
 
+  int64_t reserve = 0;  // persistent-grid slots left free for the seed waves
   if (parallel) {
-    // seed step (buffer 0 of every record) on the side stream, overlapping the bulk demod
+    // seed step (buffer 0 of every record) on the side stream, concurrently with the
+    // bulk demodulation. The bulk grid leaves one workgroup slot (one wave slot on
+    // each of a CU's 4 SIMDs) per 4 seed waves, so the seed is resident from the start
+    // instead of waiting for the whole demodulation to drain (seed dispatched second)
+    // or holding back demod blocks (seed dispatched first): profiles/r01b_seed_timeline.txt.
     int L = period;
     if (L == 0) L = detect_period_impl(w0, R, ndata);
     if (L > 64 * 16) L = 0;
@@ -370,26 +567,47 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
                        (double*)qs, (double*)ds_, nrec, gdev, ginl, gdev ? 0 : 1, jtab, c, out, out_ld, nbuf, fitok);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ds.ev_seed, ds.side));
+    if (g_tune.seed_reserve) reserve = (nrec + 3) / 4 < 64 ? (nrec + 3) / 4 : 64;
   }
+  // Row layout (one 128-B line per 8 harmonics, dc inside the row: full-line
+  // stores) for the chunk-size-1 parallel path when the bin kernel applies;
+  // component-major QI otherwise (warm-start chains read QI component-major).
+  const bool rows = parallel && (nbuf <= 1 || nchunk >= nbuf - 1) &&
+                    (nrec == 1 || (rec_stride % 2) == 0) && rows_supported(dev, x, R, R, ndata, w0, period);
+  const int64_t qs = rows ? dfmi_row_stride(ndata) : 0;
+  if (rows) {
+    void* rw = nullptr;
+    if ((rc = workspace(dev, "qrow", (size_t)qs * nseg * sizeof(double), &rw))) return rc;
+    qi = (double*)rw;
+  }
+  g_grid_reserve = reserve;
   if (rec_stride == nbuf * (int64_t)R) {
-    rc = demod_device(dev, x, nseg, R, R, ndata, w0, period, qi, nseg, dc, st);
-    if (rc) return rc;
+    rc = rows ? demod_device(dev, x, nseg, R, R, ndata, w0, period, qi, qs, nullptr, st, true)
+              : demod_device(dev, x, nseg, R, R, ndata, w0, period, qi, nseg, dc, st);
   } else {
-    for (int64_t r = 0; r < nrec; ++r) {
-      rc = demod_device(dev, x + r * rec_stride, nbuf, R, R, ndata, w0, period, qi + r * nbuf, nseg, dc + r * nbuf,
-                        st);
-      if (rc) return rc;
+    for (int64_t r = 0; r < nrec && rc == 0; ++r) {
+      rc = rows ? demod_device(dev, x + r * rec_stride, nbuf, R, R, ndata, w0, period, qi + r * nbuf * qs, qs,
+                               nullptr, st, true)
+                : demod_device(dev, x + r * rec_stride, nbuf, R, R, ndata, w0, period, qi + r * nbuf, nseg,
+                               dc + r * nbuf, st);
     }
   }
+  g_grid_reserve = 0;
+  if (rc) return rc;
   if (!parallel) {
     return lm_device(dev, qi, nseg, ndata, nrec, nbuf, 0, nbuf, 1, gdev, 4, 1, init_guess_host, c, jtab, out, out_ld,
                      fitok, st);
   }
   HIPCHK(hipStreamWaitEvent(st, ds.ev_seed, 0));
-  if (nbuf <= 1) return DFMI_OK;
+  if (nbuf <= 1) {
+    if (rows)  // dc of the seed buffers (the LM kernel carries it otherwise)
+      HIPCHK(hipMemcpy2DAsync(dc, nbuf * sizeof(double), qi + dfmi_row_dc(ndata), qs * nbuf * sizeof(double),
+                              sizeof(double), nrec, hipMemcpyDeviceToDevice, st));
+    return DFMI_OK;
+  }
   // the rest, seeded with each record's buffer-0 result (read on device: no host sync)
-  return lm_device(dev, qi, nseg, ndata, nrec, nbuf, 1, nbuf - 1, nchunk, out, nbuf, out_ld, nullptr, c, jtab, out,
-                   out_ld, fitok, st);
+  return lm_device(dev, qi, rows ? qs : nseg, ndata, nrec, nbuf, 1, nbuf - 1, nchunk, out, nbuf, out_ld, nullptr, c,
+                   jtab, out, out_ld, fitok, st, rows);
 }
 
 }  // namespace
@@ -426,7 +644,9 @@ int dfmi_device_count(void) {
 
 const char* dfmi_last_error(void) { return g_err.c_str(); }
 
-const char* dfmi_version(void) { return "dfmi 0.1 gfx950"; }
+const char* dfmi_version(void) { return "dfmi 0.2 gfx950"; }
+
+const char* dfmi_last_demod_kernel(void) { return g_last_demod.c_str(); }
 
 int dfmi_set_tuning(const char* key, int64_t value) {
   std::lock_guard<std::mutex> lk(g_mu);
@@ -436,6 +656,18 @@ int dfmi_set_tuning(const char* key, int64_t value) {
   if (k == "demod_loads") {
     if (value != 8 && value != 16) return fail(DFMI_ERR_ARG, "demod_loads must be 8 or 16");
     g_tune.demod_loads = (int)value;
+  } else if (k == "demod_kernel") {
+    if (value < 0 || value > 3) return fail(DFMI_ERR_ARG, "demod_kernel must be 0..3");
+    g_tune.demod_kernel = (int)value;
+  } else if (k == "seed_reserve") {
+    g_tune.seed_reserve = value ? 1 : 0;
+  } else if (k == "demod_bins_cfg") {
+    if (value < 0 || value > 8) return fail(DFMI_ERR_ARG, "demod_bins_cfg must be 0..8 (7, 8: timing probes)");
+    g_tune.demod_bins_cfg = (int)value;
+  } else if (k == "demod_unr") {
+    if (value != 1 && value != 2 && value != 4 && value != 5 && value != 8)
+      return fail(DFMI_ERR_ARG, "demod_unr must be 1, 2, 4, 5 or 8");
+    g_tune.demod_unr = (int)value;
   } else if (k == "demod_nt") {
     g_tune.demod_nt = value ? 1 : 0;
   } else if (k == "lm_general") {
@@ -471,6 +703,41 @@ int dfmi_demod(const double* x, int64_t nseg, int64_t seg_stride, int32_t R, int
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(qi, dq, (size_t)2 * ndata * nseg * 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(dc, dd, (size_t)nseg * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return DFMI_OK;
+}
+
+int32_t dfmi_qi_row_stride(int32_t ndata) { return ndata > 0 ? dfmi_row_stride((int)ndata) : 0; }
+
+int32_t dfmi_qi_row_dc(int32_t ndata) { return ndata > 0 ? dfmi_row_dc((int)ndata) : 0; }
+
+int dfmi_demod_rows(const double* x, int64_t nseg, int64_t seg_stride, int32_t R, int32_t ndata, double w0,
+                    int32_t period, double* rows, int32_t mem, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_err.clear();
+  if (nseg < 0 || R <= 0 || ndata <= 0 || seg_stride < R) return fail(DFMI_ERR_ARG, "bad demod geometry");
+  if (nseg > 0 && (!x || !rows)) return fail(DFMI_ERR_ARG, "null pointer");
+  int dev;
+  int rc = ensure_init(&dev);
+  if (rc) return rc;
+  if (nseg == 0) return DFMI_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t qs = dfmi_row_stride((int)ndata);
+  if (mem == DFMI_MEM_DEVICE) {
+    if (!rows_supported(dev, x, seg_stride, R, ndata, w0, period))
+      return fail(DFMI_ERR_UNSUPPORTED, "row layout needs 16-B rows and an even basis period 128 <= L <= 1024");
+    return demod_device(dev, x, nseg, seg_stride, R, ndata, w0, period, rows, qs, nullptr, st, true);
+  }
+  const size_t xb = (size_t)((nseg - 1) * seg_stride + R) * sizeof(double);
+  void *dx, *dq;
+  if ((rc = workspace(dev, "h_x", xb, &dx))) return rc;
+  if ((rc = workspace(dev, "h_rows", (size_t)qs * nseg * 8, &dq))) return rc;
+  if (!rows_supported(dev, (const double*)dx, seg_stride, R, ndata, w0, period))
+    return fail(DFMI_ERR_UNSUPPORTED, "row layout needs 16-B rows and an even basis period 128 <= L <= 1024");
+  HIPCHK(hipMemcpyAsync(dx, x, xb, hipMemcpyHostToDevice, st));
+  rc = demod_device(dev, (const double*)dx, nseg, seg_stride, R, ndata, w0, period, (double*)dq, qs, nullptr, st, true);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(rows, dq, (size_t)qs * nseg * 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   return DFMI_OK;
 }

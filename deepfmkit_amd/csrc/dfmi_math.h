@@ -30,6 +30,20 @@
 
 #define DFMI_BES_BIG_EXP 600
 
+// Demodulation row layout of the record pipeline (demod.h fold_finish ROWS, lm.h
+// QRow): one row of dfmi_qi_row_stride(ndata) doubles per segment; per block of
+// 8 harmonics 16 doubles [Q_{8b+1..8b+8} | I_{8b+1..8b+8}] — exactly one 128-B
+// line, written by one store instruction — and dc = mean(segment) in the first
+// unused Q slot of the last block (an extra 8-double tail when ndata % 8 == 0).
+DFMI_HD int dfmi_row_stride(int ndata) {
+  const int nblk = (ndata + 7) / 8;
+  return 16 * nblk + ((ndata % 8) ? 0 : 8);
+}
+DFMI_HD int dfmi_row_dc(int ndata) {
+  const int nblk = (ndata + 7) / 8;
+  return (ndata % 8) ? 16 * (nblk - 1) + (ndata % 8) : 16 * nblk;
+}
+
 // Start order of the backward recurrence (even). Fitted to the minimal order at
 // which the truncation error sinks below the fp64 rounding floor (checked against
 // mpmath for N <= 63, |x| <= 64): M = max(N + 10, 1.1|x| + 14 + 3 sqrt|x|).

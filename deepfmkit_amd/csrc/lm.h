@@ -187,7 +187,7 @@ DFMI_HDI void eval_reg(const QF& q, int nd, const double (&p)[4], Eval& e) {
   double cj = c1, sj = s1;  // cos(j psi), sin(j psi) at j = 1
 #pragma unroll
   for (int j = 1; j <= NDMAX; ++j) {
-    if (j <= nd) harmonic_term(e, j, a, a_nz, cph, sph, J[j - 1], J[j], J[j + 1], cj, sj, q(j - 1), q(nd + j - 1));
+    if (j <= nd) harmonic_term(e, j, a, a_nz, cph, sph, J[j - 1], J[j], J[j + 1], cj, sj, q.qc(j - 1), q.qs(j - 1));
     const double cn = fma(cj, c1, -(sj * s1));
     const double sn = fma(sj, c1, cj * s1);
     cj = cn;
@@ -243,20 +243,36 @@ DFMI_HDI void harmonic_walk(int ndata, double m, double psi, Body&& body) {
   }
 }
 
+// QI accessors. qc(h) = Q_{h+1} (cos), qs(h) = I_{h+1} (sin), dc() = the segment mean.
+//  QGlobal: component-major qi[c·ld + s] (dfmi_demod's layout; dc lives elsewhere).
+//  QRow<STRIDE>: one demodulation row per segment (demod.h qi_row_pos): blocks of
+//  16 doubles [cos h0..7 | sin h0..7] per 8 harmonics, dc in a spare slot;
+//  STRIDE = 1 for a row in global memory, 65 for a wave's rows transposed into LDS.
 struct QGlobal {
   const double* __restrict__ p;
   int64_t ld;
-  DFMI_HDI double operator()(int c) const { return p[(int64_t)c * ld]; }
+  int nd;
+  DFMI_HDI double qc(int h) const { return p[(int64_t)h * ld]; }
+  DFMI_HDI double qs(int h) const { return p[(int64_t)(nd + h) * ld]; }
 };
 
-DFMI_HDI void eval_gen(const QGlobal& q, int nd, const double (&p)[4], Eval& e) {
+template <int STRIDE>
+struct QRow {
+  const double* __restrict__ p;
+  DFMI_HDI double qc(int h) const { return p[((h >> 3) * 16 + (h & 7)) * STRIDE]; }
+  DFMI_HDI double qs(int h) const { return p[((h >> 3) * 16 + 8 + (h & 7)) * STRIDE]; }
+  DFMI_HDI double at(int pos) const { return p[pos * STRIDE]; }
+};
+
+template <typename QF>
+DFMI_HDI void eval_gen(const QF& q, int nd, const double (&p)[4], Eval& e) {
   const double a = p[0], m = p[1], phi = p[2], psi = p[3];
   double sph, cph;
   sincos(phi, &sph, &cph);
   const bool a_nz = (a != 0.0);
   eval_zero(e);
   harmonic_walk(nd, m, psi, [&](int j, double Jm1, double J0, double Jp1, double cj, double sj) {
-    harmonic_term(e, j, a, a_nz, cph, sph, Jm1, J0, Jp1, cj, sj, q(j - 1), q(j - 1 + nd));
+    harmonic_term(e, j, a, a_nz, cph, sph, Jm1, J0, Jp1, cj, sj, q.qc(j - 1), q.qs(j - 1));
   });
 }
 
@@ -363,7 +379,7 @@ DFMI_HDI double lm_descend(EvalFn&& evalf, double (&p)[4], const LMConst& c) {
 }
 
 // fit.py:260-320 (_find_best_initial_guess). jtab: n_grid rows of J_1..J_ndata(mtry)
-// (psi = 0 exactly: cos(j*0) = 1, -sin(j*0) = -0). Q(c) returns QI component c.
+// (psi = 0 exactly: cos(j*0) = 1, -sin(j*0) = -0). Q.qc(i) / Q.qs(i): Q_{i+1}, I_{i+1}.
 template <typename QF>
 DFMI_HDI void m_grid_seed(QF&& Q, int ndata, const double* __restrict__ jtab, const LMConst& c, double (&best)[4]) {
   double best_ssq = 9e99;
@@ -377,7 +393,7 @@ DFMI_HDI void m_grid_seed(QF&& Q, int ndata, const double* __restrict__ jtab, co
       const int j = i + 1;
       const double bq = jrow[i] * 1.0;   // jv * cos(j*0)
       const double bi = jrow[i] * -0.0;  // jv * -sin(j*0)
-      const double dq = Q(i), di = Q(i + ndata);
+      const double dq = Q.qc(i), di = Q.qs(i);
       if (fabs(bq) > c.bessel_amp_thr) {
         switch (j & 3) {
           case 0: cossum += dq / bq; ++ncos; break;
@@ -407,11 +423,11 @@ DFMI_HDI void m_grid_seed(QF&& Q, int ndata, const double* __restrict__ jtab, co
       const double bq = jrow[i] * 1.0;
       const double bi = jrow[i] * -0.0;
       if (fabs(bq) > c.bessel_amp_thr && fabs(sc) > c.sincos_amp_thr) {
-        asum += Q(i) / (sc * bq);
+        asum += Q.qc(i) / (sc * bq);
         ++na;
       }
       if (fabs(bi) > c.bessel_amp_thr && fabs(sc) > c.sincos_amp_thr) {
-        asum += Q(i + ndata) / (sc * bi);
+        asum += Q.qs(i) / (sc * bi);
         ++na;
       }
     }
@@ -421,8 +437,8 @@ DFMI_HDI void m_grid_seed(QF&& Q, int ndata, const double* __restrict__ jtab, co
     double s = 0.0;
     for (int i = 0; i < ndata; ++i) {
       const double common = atry * quarter_turn(i + 1, cp, sp) * jrow[i];
-      const double rq = Q(i) - common;
-      const double ri = Q(i + ndata) + common * 0.0;
+      const double rq = Q.qc(i) - common;
+      const double ri = Q.qs(i) + common * 0.0;
       s = fma(rq, rq, s);
       s = fma(ri, ri, s);
     }
@@ -473,24 +489,29 @@ DFMI_HDI int fit_segment_t(EvalFn&& evalf, QF&& Q, int ndata, const double* __re
   return status;
 }
 
-// Single-segment entry used by the kernel and by the test-only host build.
+// Single-segment entry used by the kernels and by the test-only host build.
 // NDMAX > 0: register path (requires ndata <= NDMAX); NDMAX == 0: general path.
+template <int NDMAX, typename QF>
+__host__ __device__ __forceinline__ int fit_segment_q(const QF& q, int ndata, const double* __restrict__ jtab,
+                                                   const LMConst& c, double (&p)[4], double& ssq_out) {
+  if constexpr (NDMAX > 0) {
+    auto evalf = [&](const double (&pp)[4], Eval& e) { eval_reg<NDMAX>(q, ndata, pp, e); };
+    return fit_segment_t(evalf, q, ndata, jtab, c, p, ssq_out);
+  } else {
+    auto evalf = [&](const double (&pp)[4], Eval& e) { eval_gen(q, ndata, pp, e); };
+    return fit_segment_t(evalf, q, ndata, jtab, c, p, ssq_out);
+  }
+}
+
+// Component-major QI (qi[c·ld + s], qptr = qi + s). QI is re-read per evaluation
+// through the vector L1 (64 segments x 2·ndata doubles = 10 KB per wave): keeping
+// it in registers costs 2·NDMAX VGPRs and with them the second wave per SIMD.
 template <int NDMAX>
 __host__ __device__ __forceinline__ int fit_segment(const double* __restrict__ qptr, int64_t ld, int ndata,
                                                  const double* __restrict__ jtab, const LMConst& c, double (&p)[4],
                                                  double& ssq_out) {
-  if constexpr (NDMAX > 0) {
-    // QI is re-read per evaluation through the vector L1 (64 segments x 2*ndata
-    // doubles = 10 KB per wave): keeping it in registers costs 2*NDMAX VGPRs and
-    // with them the second wave per SIMD.
-    const QGlobal qg{qptr, ld};
-    auto evalf = [&](const double (&pp)[4], Eval& e) { eval_reg<NDMAX>(qg, ndata, pp, e); };
-    return fit_segment_t(evalf, qg, ndata, jtab, c, p, ssq_out);
-  } else {
-    const QGlobal qg{qptr, ld};
-    auto evalf = [&](const double (&pp)[4], Eval& e) { eval_gen(qg, ndata, pp, e); };
-    return fit_segment_t(evalf, qg, ndata, jtab, c, p, ssq_out);
-  }
+  const QGlobal qg{qptr, ld, ndata};
+  return fit_segment_q<NDMAX>(qg, ndata, jtab, c, p, ssq_out);
 }
 
 // Seeds of up to 8 records passed by value (read with constant offsets only).
@@ -506,19 +527,53 @@ struct GuessInline {
 // CHAIN = false: every chunk holds at most one segment (no loop: the register
 // allocator keeps the whole LM at two waves per SIMD); CHAIN = true: warm-start
 // chains of any length.
-template <int NDMAX, bool CHAIN>
+// ROWS = false: QI component-major (qi[c·qi_ld + s]); the demodulation wrote dc.
+// ROWS = true (CHAIN = false only): QI as demodulation rows (qi + s·qi_ld, see
+// dfmi_qi_row_stride); the kernel also copies each segment's dc into out[4].
+// With the register path the wave first stages its 64 rows into LDS, transposed
+// ([pos][65]: conflict-free column reads), with coalesced 16-B loads when the
+// rows are contiguous — each QI value is then read from LDS at every evaluation.
+template <int NDMAX, bool CHAIN, bool ROWS = false>
 __global__ __launch_bounds__(64) void lm_chunks_kernel(
     const double* __restrict__ qi, int64_t qi_ld, int ndata, int64_t nrec, int64_t nbuf, int64_t first,
     int64_t nitems, int64_t nchunk, const double* __restrict__ guess, int64_t g_rec, int64_t g_comp,
     GuessInline ginl, int use_inline, const double* __restrict__ jtab, LMConst c, double* __restrict__ out,
     int64_t out_ld, int32_t* __restrict__ status) {
+  static_assert(!(ROWS && CHAIN), "row layout: chunk size 1 only");
+  extern __shared__ double lds_q[];  // STAGE: [qi_ld][65]
   const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= nrec * nchunk) return;
-  const int64_t r = id / nchunk;
-  const int64_t k = id - r * nchunk;
+  const bool valid = id < nrec * nchunk;
+  const int64_t idc = valid ? id : 0;
+  const int64_t r = idc / nchunk;
+  const int64_t k = idc - r * nchunk;
   const int64_t qn = nitems / nchunk, rm = nitems % nchunk;
   const int64_t start = k * qn + (k < rm ? k : rm);
   const int64_t len = qn + (k < rm ? 1 : 0);
+  const int64_t s0 = r * nbuf + first + start;
+  constexpr bool STAGE = ROWS && NDMAX > 0;
+  if constexpr (STAGE) {
+    const int lane = threadIdx.x;
+    const int QS = (int)qi_ld;
+    const int64_t sl0 = __shfl(s0, 0);  // lane 0 is always valid
+    const int nv = (int)((nrec * nchunk - (int64_t)blockIdx.x * 64) < 64 ? (nrec * nchunk - (int64_t)blockIdx.x * 64)
+                                                                         : 64);
+    const bool contiguous = __all(!valid || s0 == sl0 + lane);
+    if (contiguous) {
+      const double* __restrict__ base = qi + sl0 * qi_ld;
+      const int tot = nv * QS;  // doubles, even
+      for (int e = 2 * lane; e < tot; e += 128) {
+        typedef double d2v __attribute__((ext_vector_type(2)));
+        const d2v v = *reinterpret_cast<const d2v*>(base + e);
+        const int row = e / QS, pos = e - row * QS;
+        lds_q[pos * 65 + row] = v.x;
+        lds_q[(pos + 1) * 65 + row] = v.y;
+      }
+    } else if (valid) {
+      for (int pos = 0; pos < QS; ++pos) lds_q[pos * 65 + lane] = qi[s0 * qi_ld + pos];
+    }
+    __syncthreads();
+  }
+  if (!valid) return;
   double p[4] = {0.0, 0.0, 0.0, 0.0};
   if (use_inline) {
 #pragma unroll
@@ -532,9 +587,7 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
 #pragma unroll
     for (int i = 0; i < 4; ++i) p[i] = guess[r * g_rec + i * g_comp];
   }
-  auto one = [&](int64_t sidx) {
-    double ssq;
-    const int st = fit_segment<NDMAX>(qi + sidx, qi_ld, ndata, jtab, c, p, ssq);
+  auto put = [&](int64_t sidx, int st, double ssq) {
     out[0 * out_ld + sidx] = p[0];
     out[1 * out_ld + sidx] = p[1];
     out[2 * out_ld + sidx] = p[2];
@@ -542,11 +595,35 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
     out[5 * out_ld + sidx] = ssq;
     status[sidx] = st;
   };
-  const int64_t s0 = r * nbuf + first + start;
-  if constexpr (!CHAIN) {
-    if (len == 1) one(s0);  // chunk size 1 (the parallel default): straight-line code
+  if constexpr (ROWS) {
+    if (len != 1) return;
+    double ssq;
+    int st;
+    double dcv;
+    if constexpr (STAGE) {
+      const QRow<65> q{lds_q + threadIdx.x};
+      st = fit_segment_q<NDMAX>(q, ndata, jtab, c, p, ssq);
+      dcv = q.at(dfmi_row_dc(ndata));
+    } else {
+      const QRow<1> q{qi + s0 * qi_ld};
+      st = fit_segment_q<NDMAX>(q, ndata, jtab, c, p, ssq);
+      dcv = q.at(dfmi_row_dc(ndata));
+    }
+    put(s0, st, ssq);
+    out[4 * out_ld + s0] = dcv;
+    if (k == 0)  // segments before `first` (the seed buffer) are fitted elsewhere: carry their dc
+      for (int64_t t = r * nbuf; t < r * nbuf + first; ++t) out[4 * out_ld + t] = qi[t * qi_ld + dfmi_row_dc(ndata)];
   } else {
-    for (int64_t t = 0; t < len; ++t) one(s0 + t);  // warm-start chain (sequential / n_cores)
+    auto one = [&](int64_t sidx) {
+      double ssq;
+      const int st = fit_segment<NDMAX>(qi + sidx, qi_ld, ndata, jtab, c, p, ssq);
+      put(sidx, st, ssq);
+    };
+    if constexpr (!CHAIN) {
+      if (len == 1) one(s0);  // chunk size 1 (the parallel default): straight-line code
+    } else {
+      for (int64_t t = 0; t < len; ++t) one(s0 + t);  // warm-start chain (sequential / n_cores)
+    }
   }
 }
 

@@ -15,7 +15,7 @@
 namespace dfmi {
 
 template <int NDMAX>
-__global__ __launch_bounds__(64) void seed_kernel(const double* __restrict__ x, int64_t rec_stride, int R, int L,
+__global__ __launch_bounds__(64, 4) void seed_kernel(const double* __restrict__ x, int64_t rec_stride, int R, int L,
                                                   int ndata, double w0, const double* __restrict__ tab,
                                                   double* __restrict__ qis, double* __restrict__ dcs, int64_t nrec,
                                                   const double* __restrict__ guess, GuessInline ginl, int use_inline,

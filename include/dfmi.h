@@ -77,6 +77,19 @@ void dfmi_lm_config_default(dfmi_lm_config* cfg);
 int dfmi_demod(const double* x, int64_t nseg, int64_t seg_stride, int32_t R, int32_t ndata, double w0,
                int32_t period, double* qi, double* dc, int32_t mem, void* stream);
 
+/* The record pipeline's demodulation layout ("rows"): one row of
+ * dfmi_qi_row_stride(ndata) doubles per segment, rows[s*stride + pos]. Per block
+ * of 8 harmonics b: 16 doubles [Q_{8b+1..8b+8} | I_{8b+1..8b+8}] (one 128-B line,
+ * written by one store instruction; slots of harmonics > ndata are 0), and
+ * dc = mean(segment) at pos dfmi_qi_row_dc(ndata). Same values as dfmi_demod
+ * (bit-identical); only the layout differs. Needs 16-B aligned rows (x and
+ * seg_stride even) and an even basis period 128 <= L <= 1024 (L = 200 at the
+ * BASELINE configs); DFMI_ERR_UNSUPPORTED otherwise. */
+int32_t dfmi_qi_row_stride(int32_t ndata);
+int32_t dfmi_qi_row_dc(int32_t ndata);
+int dfmi_demod_rows(const double* x, int64_t nseg, int64_t seg_stride, int32_t R, int32_t ndata, double w0,
+                    int32_t period, double* rows, int32_t mem, void* stream);
+
 /* Fit nseg demodulated segments.
  *   qi[c*nseg + s]                       input, layout of dfmi_demod
  *   guess_per_segment != 0: guess[s*4+i] seeds segment s (every segment its own chunk)
@@ -109,10 +122,12 @@ int dfmi_ekf(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
              const double* p0_diag, const double* q_diag, const double* r_val, double w_m, double f_samp,
              int32_t R, int64_t nbuf, double* states, int32_t mem, void* stream);
 
-/* Performance tuning hook (results are unaffected): "demod_loads" (8 | 16 vector
- * loads in flight per lane), "demod_nt" (0 | 1 non-temporal stream loads),
- * "demod_blocks_per_cu" (0 = occupancy limit), "lm_general" (1 = two-pass LM path for
- * every ndata). Process-wide. */
+/* Performance tuning hook (results are unaffected): "demod_kernel" (0 cycle-aligned
+ * fold, 1 pipelined cycle-aligned fold, 2 bins in LDS [default], 3 pipelined bins),
+ * "demod_unr" (cycles/chunks per batch of the pipelined variants), "demod_loads"
+ * (8 | 16 vector loads in flight per lane), "demod_nt" (0 | 1 non-temporal stream
+ * loads), "demod_blocks_per_cu" (0 = occupancy limit), "lm_general" (1 = two-pass LM
+ * path for every ndata). Process-wide. */
 int dfmi_set_tuning(const char* key, int64_t value);
 
 /* Period (samples) the fold kernel would use for this w0, R, ndata; 0 if none. */
@@ -124,8 +139,12 @@ int dfmi_device_count(void);
 /* Message of the last failed call on this thread ("" if none). */
 const char* dfmi_last_error(void);
 
-/* Library/ABI version, e.g. "dfmi 0.1 gfx950". */
+/* Library/ABI version, e.g. "dfmi 0.2 gfx950". */
 const char* dfmi_version(void);
+
+/* Kernel variant of the last demodulation this process launched, e.g.
+ * "demod_bins_kernel<2,8,1>" ("" before the first one). Diagnostics/profiling. */
+const char* dfmi_last_demod_kernel(void);
 
 #ifdef __cplusplus
 }

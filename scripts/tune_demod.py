@@ -24,7 +24,11 @@ def main():
     dc = torch.empty(nseg, dtype=torch.float64, device=dev)
     st = torch.cuda.current_stream()
     w0 = w0_of(1000.0, 200000.0)
-    variants = [(8, 0, 0), (16, 0, 0), (8, 1, 0), (16, 1, 0), (16, 0, 2), (16, 1, 2), (8, 0, 2), (16, 0, 3)]
+    # (demod_kernel, demod_unr, demod_loads, demod_nt, demod_blocks_per_cu, demod_bins_cfg)
+    variants = [tuple(int(t) for t in v.split(",")) for v in os.environ.get(
+        "VARIANTS", "0,4,8,1,0,0;2,4,8,1,0,0;2,4,8,1,0,2;2,4,8,1,0,7;2,4,8,1,0,8").split(";")]
+    probes = {7, 8}  # timing-only shapes: excluded from the result comparison
+    keys = ("demod_kernel", "demod_unr", "demod_loads", "demod_nt", "demod_blocks_per_cu", "demod_bins_cfg")
     res = {v: [] for v in variants}
     ref = {"torch_sum": [], "torch_copy": []}
     y = torch.empty_like(x)
@@ -32,7 +36,7 @@ def main():
     nbytes = nseg * (8 * R + 8 * (2 * nd + 1))
     for rnd in range(6):
         for v in variants:
-            for k, val in zip(("demod_loads", "demod_nt", "demod_blocks_per_cu"), v):
+            for k, val in zip(keys, v):
                 _lib.check(lib.dfmi_set_tuning(k.encode(), val), "tune")
             _lib.check(lib.dfmi_demod(x.data_ptr(), nseg, R, R, nd, w0, 0, qi.data_ptr(), dc.data_ptr(), 1,
                                       st.cuda_stream), "demod")
@@ -54,10 +58,31 @@ def main():
         ev1.record(st)
         ev1.synchronize()
         ref["torch_copy"].append(ev0.elapsed_time(ev1) / 5)
+    # all variants must agree with the fold kernel (same fold order; contraction identical)
+    qref = None
+    for v in variants:
+        if v[5] in probes:
+            continue
+        for k, val in zip(keys, v):
+            _lib.check(lib.dfmi_set_tuning(k.encode(), val), "tune")
+        _lib.check(lib.dfmi_demod(x.data_ptr(), nseg, R, R, nd, w0, 0, qi.data_ptr(), dc.data_ptr(), 1,
+                                  st.cuda_stream), "demod")
+        torch.cuda.synchronize()
+        cur = torch.cat([qi.flatten(), dc])
+        if qref is None:
+            qref = cur.clone()
+        else:
+            d = (cur - qref).abs().max().item()
+            kn = lib.dfmi_last_demod_kernel().decode()
+            print(f"variant {v} = {kn}", file=sys.stderr)
+            print(f"variant {v}: max|diff| vs fold = {d:.3e}", file=sys.stderr)
+            assert d <= 1e-13, (v, d)
     out = {}
     for v, t in res.items():
         med = float(np.median(t))
-        out[f"loads{v[0]}_nt{v[1]}_bpc{v[2]}"] = {"ms": round(med, 4), "GBps": round(nbytes / med / 1e6, 1)}
+        kname = {0: "fold", 1: f"stream_unr{v[1]}", 2: f"bins{v[5]}", 3: f"binspipe_unr{v[1]}"}[v[0]]
+        name = f"{kname}_loads{v[2]}_nt{v[3]}_bpc{v[4]}"
+        out[name] = {"ms": round(med, 4), "GBps": round(nbytes / med / 1e6, 1)}
     out["torch_sum_read_GBps"] = round(x.numel() * 8 / np.median(ref["torch_sum"]) / 1e6, 1)
     out["torch_copy_rw_GBps"] = round(2 * x.numel() * 8 / np.median(ref["torch_copy"]) / 1e6, 1)
     print(json.dumps(out, indent=1))

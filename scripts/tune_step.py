@@ -1,0 +1,86 @@
+"""Interleaved A/B timing of whole record-pipeline steps (dfmi_nls_record, config 2)
+under tuning settings, with a bit-identity check of the results across settings.
+Usage: SETTINGS="seed_reserve=1;seed_reserve=0" python scripts/tune_step.py"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from deepfmkit_amd import _lib  # noqa: E402
+from deepfmkit_amd import fit as F  # noqa: E402
+from deepfmkit_amd.fitters import w0_of  # noqa: E402
+
+
+def parse(spec):
+    out = []
+    for item in spec.split(";"):
+        kv = {}
+        for a in filter(None, item.split(",")):
+            k, v = a.split("=")
+            kv[k.strip()] = int(v)
+        out.append(kv)
+    return out
+
+
+def main():
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    lib = _lib.load()
+    nseg, R, nd = int(os.environ.get("NSEG", 100000)), 4000, 10
+    x = bench.gen_shard(torch, dev, 0, nseg, R, seed=1)
+    st = torch.cuda.current_stream()
+    w0 = w0_of(1000.0, 200000.0)
+    cfg = F.lm_config()
+    guess = np.array([1.6, 6.0, 0.0, 0.0])
+    out = torch.empty((6, nseg), dtype=torch.float64, device=dev)
+    ok = torch.empty(nseg, dtype=torch.int32, device=dev)
+    settings = parse(os.environ.get("SETTINGS", "seed_reserve=1;seed_reserve=0"))
+
+    def apply(s):
+        for k, v in s.items():
+            _lib.check(lib.dfmi_set_tuning(k.encode(), v), k)
+
+    def step():
+        _lib.check(lib.dfmi_nls_record(x.data_ptr(), 1, nseg * R, nseg, R, nd, w0, 0, _lib.ptr(guess), 1, nseg - 1,
+                                       cfg, out.data_ptr(), ok.data_ptr(), _lib.DFMI_MEM_DEVICE, st.cuda_stream),
+                   "nls_record")
+
+    ref = None
+    for s in settings:
+        apply(s)
+        step()
+        torch.cuda.synchronize()
+        cur = torch.cat([out.flatten(), ok.double()])
+        if ref is None:
+            ref = cur.clone()
+        else:
+            d = (cur - ref).abs().max().item()
+            print(f"{s}: max|diff| vs first setting = {d:.3e}", file=sys.stderr)
+            assert d == 0.0, (s, d)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    res = {i: [] for i in range(len(settings))}
+    for _ in range(6):
+        for i, s in enumerate(settings):
+            apply(s)
+            step()
+            ev0.record(st)
+            for _ in range(5):
+                step()
+            ev1.record(st)
+            ev1.synchronize()
+            res[i].append(ev0.elapsed_time(ev1) / 5)
+    outj = {}
+    for i, s in enumerate(settings):
+        med = float(np.median(res[i]))
+        outj[",".join(f"{k}={v}" for k, v in s.items()) or "default"] = {
+            "ms_per_step": round(med, 4), "Mseg_per_s": round(nseg / med / 1e3, 2)}
+    print(json.dumps(outj, indent=1))
+
+
+if __name__ == "__main__":
+    main()

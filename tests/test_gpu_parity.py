@@ -171,3 +171,75 @@ def test_large_batch_known_answer_and_seed_independence():
     sub_all = torch.cat([x[:, :R], sub], dim=1)
     cols2, _ = nls_records(sub_all, 200000.0, 1000.0, R, 101, 10)
     np.testing.assert_array_equal(cols2.cpu().numpy()[:, 1:], cols[:, 5000:5100])
+
+
+def _demod_both(x, nseg, R, nd, w0):
+    """dfmi_demod (component-major) and dfmi_demod_rows (record-pipeline rows) on device data."""
+    import torch
+    from deepfmkit_amd import _lib
+    lib = _lib.load()
+    st = torch.cuda.current_stream().cuda_stream
+    qi = torch.empty((2 * nd, nseg), dtype=torch.float64, device="cuda")
+    dc = torch.empty(nseg, dtype=torch.float64, device="cuda")
+    _lib.check(lib.dfmi_demod(x.data_ptr(), nseg, R, R, nd, w0, 0, qi.data_ptr(), dc.data_ptr(),
+                              _lib.DFMI_MEM_DEVICE, st), "dfmi_demod")
+    qs = lib.dfmi_qi_row_stride(nd)
+    rows = torch.full((nseg, qs), float("nan"), dtype=torch.float64, device="cuda")
+    _lib.check(lib.dfmi_demod_rows(x.data_ptr(), nseg, R, R, nd, w0, 0, rows.data_ptr(), _lib.DFMI_MEM_DEVICE, st),
+               "dfmi_demod_rows")
+    torch.cuda.synchronize()
+    return qi.cpu().numpy(), dc.cpu().numpy(), rows.cpu().numpy(), qs, lib.dfmi_qi_row_dc(nd)
+
+
+@pytest.mark.parametrize("nd", [10, 3, 8, 16])
+def test_demod_rows_bit_identical_to_component_major(nd):
+    """The record pipeline's row layout (full-line stores, dc inside the row) carries
+    exactly the values of dfmi_demod; unused slots are 0. ndata 8/16 have no spare
+    slot (dc in an 8-double tail)."""
+    import torch
+    from deepfmkit_amd.fitters import w0_of
+    nseg, R = 3001, 4000
+    g = torch.Generator(device="cuda")
+    g.manual_seed(nd)
+    x = torch.randn(nseg * R, dtype=torch.float64, device="cuda", generator=g) + 0.25
+    qi, dc, rows, qs, dpos = _demod_both(x, nseg, R, nd, w0_of(1000.0, 200000.0))
+    nblk = (nd + 7) // 8
+    assert qs == 16 * nblk + (0 if nd % 8 else 8)
+    used = np.zeros(qs, bool)
+    for h in range(nd):
+        b, i = divmod(h, 8)
+        np.testing.assert_array_equal(rows[:, 16 * b + i], qi[h])
+        np.testing.assert_array_equal(rows[:, 16 * b + 8 + i], qi[nd + h])
+        used[16 * b + i] = used[16 * b + 8 + i] = True
+    np.testing.assert_array_equal(rows[:, dpos], dc)
+    used[dpos] = True
+    written = np.arange(qs) < 16 * nblk
+    assert (rows[:, ~used & written] == 0).all()
+
+
+def test_record_rows_path_matches_component_path():
+    """dfmi_nls_record through the row layout (default for chunk size 1) is
+    bit-identical to the component-major path (forced with demod_kernel = 0), for a
+    multi-record strided batch and for nbuf = 1 (the dc of the seed buffers)."""
+    import torch
+    from deepfmkit_amd import _lib
+    from deepfmkit_amd.fitters import nls_records
+    lib = _lib.load()
+    R = 4000
+    t = torch.arange(40 * R, dtype=torch.float64, device="cuda") / 200000.0
+    w = 2 * np.pi * 1000.0
+    g = torch.Generator(device="cuda")
+    g.manual_seed(7)
+    base = torch.stack([1.0 + torch.cos(0.3 * k + (5.5 + 0.2 * k) * torch.cos(w * t + 0.1 * k)) for k in range(3)])
+    recs = torch.zeros((3, 41 * R), dtype=torch.float64, device="cuda")  # rec_stride > nbuf * R
+    recs[:, : 40 * R] = base + 1e-3 * torch.randn(base.shape, dtype=torch.float64, device="cuda", generator=g)
+    for nbuf in (40, 1):
+        res = {}
+        for kern in (2, 0):
+            _lib.check(lib.dfmi_set_tuning(b"demod_kernel", kern), "tune")
+            cols, ok = nls_records(recs, 200000.0, 1000.0, R, nbuf, 10)
+            res[kern] = (cols.cpu().numpy(), ok.cpu().numpy(), lib.dfmi_last_demod_kernel().decode())
+        _lib.check(lib.dfmi_set_tuning(b"demod_kernel", 2), "tune")
+        assert "rows" in res[2][2] and "rows" not in res[0][2], (res[2][2], res[0][2])
+        np.testing.assert_array_equal(res[2][0], res[0][0])
+        np.testing.assert_array_equal(res[2][1], res[0][1])

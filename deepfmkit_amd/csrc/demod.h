@@ -36,7 +36,7 @@ constexpr int kHarmBlock = 8;  // harmonics per contraction block (16 partial su
 // One exchange stage of the reduce-scatter: lanes with the mask bit set keep
 // the upper HALF of their live values, the others the lower half, and each adds
 // its partner's copy of the half it keeps.
-template <int HALF, int MASK, int NV>
+template <int HALF, int MASK, int NV, bool LOWREG = false>
 __device__ __forceinline__ void bfly_stage(double (&v)[NV], int lane) {
   const bool hi = lane & MASK;
 #pragma unroll
@@ -44,6 +44,7 @@ __device__ __forceinline__ void bfly_stage(double (&v)[NV], int lane) {
     const double send = hi ? v[i] : v[i + HALF];
     const double keep = hi ? v[i + HALF] : v[i];
     v[i] = keep + __shfl_xor(send, MASK);
+    if constexpr (LOWREG) __builtin_amdgcn_sched_barrier(0);  // one exchange in flight at a time
   }
 }
 
@@ -52,14 +53,14 @@ __device__ __forceinline__ void bfly_stage(double (&v)[NV], int lane) {
 // stages are plain butterfly sums. On return lane l holds, in v[0], the
 // wave-wide sum of value index (l >> (6 - log2 NV)) & (NV - 1).
 // (NV = 16: 15 exchange-adds + 2 sums = 17 shuffles instead of 16 x 6.)
-template <int NV>
+template <int NV, bool LOWREG = false>
 __device__ __forceinline__ void butterfly(double (&v)[NV], int lane) {
   static_assert(NV == 4 || NV == 8 || NV == 16, "NV");
   if constexpr (NV == 16) {
-    bfly_stage<8, 32>(v, lane);
-    bfly_stage<4, 16>(v, lane);
-    bfly_stage<2, 8>(v, lane);
-    bfly_stage<1, 4>(v, lane);
+    bfly_stage<8, 32, NV, LOWREG>(v, lane);
+    bfly_stage<4, 16, NV, LOWREG>(v, lane);
+    bfly_stage<2, 8, NV, LOWREG>(v, lane);
+    bfly_stage<1, 4, NV, LOWREG>(v, lane);
     v[0] += __shfl_xor(v[0], 2);
     v[0] += __shfl_xor(v[0], 1);
   } else if constexpr (NV == 8) {
@@ -192,7 +193,7 @@ __device__ __forceinline__ void fold_finish(const double (&y)[MAXSLOT][VEC], con
         if constexpr (LOWREG) __builtin_amdgcn_sched_barrier(0);
       }
     }
-    butterfly<2 * HB>(acc, lane);
+    butterfly<2 * HB, LOWREG>(acc, lane);
     if constexpr (PROBE != 0) {
       if (acc[0] == 1.2345e300) qi[col] = acc[0];  // timing probe: keep the work, drop the stores
     } else if constexpr (ROWS) {
@@ -431,11 +432,134 @@ __global__ __launch_bounds__(kBlockThreads, MINB) void demod_stream_kernel(
 // occupancy floor handed to the register allocator (blocks per CU).
 // PROBE (timing only, results invalid): 1 = contraction without the QI stores,
 // 2 = no contraction (dc only).
+// One segment of the bin-in-LDS fold: the wave's L bins (ybin, LDS) are zeroed,
+// every 1-KB chunk is added into them, and fold_finish contracts the lane-owned
+// bins with the basis T (LDS or global) into column / row `col` of qi (and dc).
+template <int MAXSLOT, int LOADS, bool NT, int HB, int PROBE, bool ROWS>
+__device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int R, int L, int ndata,
+                                             const double* __restrict__ T, double* __restrict__ ybin, int lane,
+                                             const bool (&pval)[MAXSLOT], const int (&pbase)[MAXSLOT],
+                                             double* __restrict__ qi, int64_t qi_ld, int64_t col,
+                                             double* __restrict__ dc) {
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  const int nch = R >> 7;           // full 128-sample chunks
+  const int tail = R - (nch << 7);  // samples of the last, partial chunk
+  auto add_chunk = [&](int p0, const double (&v)[2]) {
+    int p = p0 + 2 * lane;
+    if (p >= L) p -= L;
+    d2v* yp = reinterpret_cast<d2v*>(ybin + p);
+    d2v t = *yp;
+    t.x += v[0];
+    t.y += v[1];
+    *yp = t;
+  };
+#pragma unroll
+  for (int j = 0; j < MAXSLOT; ++j)
+    if (pval[j]) *reinterpret_cast<d2v*>(ybin + pbase[j]) = d2v{0.0, 0.0};
+  const double* __restrict__ xs = xs0 + 2 * lane;
+  int p0 = 0;  // bin of the chunk's first sample: (128 c) mod L
+  int c = 0;
+  for (; c + LOADS <= nch; c += LOADS) {
+    double v[LOADS][2];
+#pragma unroll
+    for (int u = 0; u < LOADS; ++u) {
+      if constexpr (NT) VecT<2>::load_nt(xs + (c + u) * 128, v[u]);
+      else VecT<2>::load(xs + (c + u) * 128, v[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < LOADS; ++u) {
+      add_chunk(p0, v[u]);
+      p0 += 128;
+      if (p0 >= L) p0 -= L;
+    }
+  }
+  for (; c < nch; ++c) {
+    double v[2];
+    VecT<2>::load(xs + c * 128, v);
+    add_chunk(p0, v);
+    p0 += 128;
+    if (p0 >= L) p0 -= L;
+  }
+  if (tail) {  // partial chunk: element-wise (R may be odd)
+    const int t0 = 2 * lane;
+    int p = p0 + t0;
+    if (p >= L) p -= L;
+    if (t0 < tail) ybin[p] += xs[nch * 128];
+    if (t0 + 1 < tail) ybin[p + 1] += xs[nch * 128 + 1];
+  }
+  double y[MAXSLOT][2];
+#pragma unroll
+  for (int j = 0; j < MAXSLOT; ++j) {
+    if (pval[j]) {
+      const d2v t = *reinterpret_cast<const d2v*>(ybin + pbase[j]);
+      y[j][0] = t.x;
+      y[j][1] = t.y;
+    } else {
+      y[j][0] = y[j][1] = 0.0;
+    }
+  }
+  fold_finish<2, MAXSLOT, false, HB, PROBE, ROWS>(y, pval, pbase, R, L, ndata, T, lane, qi, qi_ld, col, dc);
+}
+
+// Dynamic segment scheduling (DYN): segments are handed out by 8 atomic counters
+// (ctr[64·k], k < 8: one 256-B line each — device-scope atomics on one line
+// serialise at ≈88/us, MI355X_MICROARCH.md 'dequeue'; zeroed by the host), one per
+// XCD-sized share [k·nseg/8, (k+1)·nseg/8);
+// a wave takes from the share of its workgroup's XCD (blockIdx % 8 under the
+// round-robin placement; only locality depends on it) and then from the others.
+// A workgroup that starts late — e.g. behind the seed wave that shares its CU —
+// simply takes fewer segments, where a static grid-stride split would end the
+// launch that much later. The next ticket is requested while the current segment
+// is processed, so the atomic's latency is hidden.
+struct SegQueue {
+  unsigned* __restrict__ ctr;
+  int64_t nseg;
+  __device__ __forceinline__ int64_t lo(int k) const { return (int64_t)k * nseg / 8; }
+  __device__ __forceinline__ int64_t hi(int k) const { return (int64_t)(k + 1) * nseg / 8; }
+  __device__ __forceinline__ unsigned take(int k, int lane) const {
+    unsigned t = 0;
+    if (lane == 0) t = atomicAdd(&ctr[64 * k], 1u);
+    return __builtin_amdgcn_readfirstlane(t);
+  }
+  // resolve a ticket of share k; on exhaustion scan the other shares
+  __device__ __forceinline__ int64_t resolve(int k, unsigned t, int lane) const {
+    if (lo(k) + t < hi(k)) return lo(k) + t;
+    for (int d = 1; d < 8; ++d) {
+      const int kk = (k + d) & 7;
+      const unsigned seen = __builtin_amdgcn_readfirstlane(__atomic_load_n(&ctr[64 * kk], __ATOMIC_RELAXED));
+      if (lo(kk) + seen >= hi(kk)) continue;
+      const unsigned tt = take(kk, lane);
+      if (lo(kk) + tt < hi(kk)) return lo(kk) + tt;
+    }
+    return -1;
+  }
+};
+
+// WPB waves per workgroup share one LDS copy of the basis (TAB_LDS) — or read it
+// through the cache (TAB_LDS = false: LDS then holds only the bins); MINB is the
+// occupancy floor handed to the register allocator (waves per SIMD).
+// PROBE (timing only, results invalid): 1 = contraction without the QI stores,
+// 2 = no contraction (dc only).
 template <int MAXSLOT, int LOADS, bool NT, int WPB = 4, int MINB = 1, bool TAB_LDS = true, int HB = kHarmBlock,
-          int PROBE = 0, bool ROWS = false>
+          int PROBE = 0, bool ROWS = false, bool DYN = false>
 __global__ __launch_bounds__(64 * WPB, MINB) void demod_bins_kernel(
     const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
-    const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc) {
+    const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc,
+    unsigned* __restrict__ ctr, int spacer, uint64_t* __restrict__ probe) {
+  // probe (diagnostics, may be null): s_memrealtime at entry of workgroups 0 and
+  // gridDim-1, and at the exit of workgroup 0's wave 0
+  if (probe && threadIdx.x == 0) {
+    if (blockIdx.x == 0) probe[3] = __builtin_amdgcn_s_memrealtime();
+    if (blockIdx.x == gridDim.x - 1) probe[4] = __builtin_amdgcn_s_memrealtime();
+  }
+  // spacer > 0: the LAST `spacer` workgroups (8 = one per XCD under round-robin
+  // placement: a queued workgroup only takes a slot on the XCD it was sent to) take
+  // no segments and exit at once. A seed wave (seed.h) launched on another stream
+  // either finds their slot (this kernel dispatched first) or occupies a slot one of
+  // them would have needed (seed dispatched first) — either way no segment waits
+  // behind the seed.
+  const int nwork = (int)gridDim.x - spacer;
+  if ((int)blockIdx.x >= nwork) return;
   extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
   const int ntab = TAB_LDS ? 2 * ndata * L : 0;
   if constexpr (TAB_LDS) {
@@ -454,66 +578,22 @@ __global__ __launch_bounds__(64 * WPB, MINB) void demod_bins_kernel(
     pbase[j] = 2 * (lane + 64 * j);
     pval[j] = (j < nslot) && (pbase[j] < L);
   }
-  const int nch = R >> 7;          // full 128-sample chunks
-  const int tail = R - (nch << 7);  // samples of the last, partial chunk
-  typedef double d2v __attribute__((ext_vector_type(2)));
-  auto add_chunk = [&](int p0, const double (&v)[2]) {
-    int p = p0 + 2 * lane;
-    if (p >= L) p -= L;
-    d2v* yp = reinterpret_cast<d2v*>(ybin + p);
-    d2v t = *yp;
-    t.x += v[0];
-    t.y += v[1];
-    *yp = t;
-  };
-  for (int64_t s = (int64_t)blockIdx.x * WPB + wave; s < nseg; s += (int64_t)gridDim.x * WPB) {
-#pragma unroll
-    for (int j = 0; j < MAXSLOT; ++j)
-      if (pval[j]) *reinterpret_cast<d2v*>(ybin + pbase[j]) = d2v{0.0, 0.0};
-    const double* __restrict__ xs = x + s * seg_stride + 2 * lane;
-    int p0 = 0;  // bin of the chunk's first sample: (128 c) mod L
-    int c = 0;
-    for (; c + LOADS <= nch; c += LOADS) {
-      double v[LOADS][2];
-#pragma unroll
-      for (int u = 0; u < LOADS; ++u) {
-        if constexpr (NT) VecT<2>::load_nt(xs + (c + u) * 128, v[u]);
-        else VecT<2>::load(xs + (c + u) * 128, v[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < LOADS; ++u) {
-        add_chunk(p0, v[u]);
-        p0 += 128;
-        if (p0 >= L) p0 -= L;
-      }
+  if constexpr (DYN) {
+    const SegQueue q{ctr, nseg};
+    const int home = blockIdx.x & 7;
+    int64_t s = q.resolve(home, q.take(home, lane), lane);
+    while (s >= 0) {
+      const unsigned next = q.take(home, lane);  // in flight while the segment is processed
+      bins_segment<MAXSLOT, LOADS, NT, HB, PROBE, ROWS>(x + s * seg_stride, R, L, ndata, T, ybin, lane, pval, pbase,
+                                                         qi, qi_ld, s, dc);
+      s = q.resolve(home, next, lane);
     }
-    for (; c < nch; ++c) {
-      double v[2];
-      VecT<2>::load(xs + c * 128, v);
-      add_chunk(p0, v);
-      p0 += 128;
-      if (p0 >= L) p0 -= L;
-    }
-    if (tail) {  // partial chunk: element-wise (R may be odd)
-      const int t0 = 2 * lane;
-      int p = p0 + t0;
-      if (p >= L) p -= L;
-      if (t0 < tail) ybin[p] += xs[nch * 128];
-      if (t0 + 1 < tail) ybin[p + 1] += xs[nch * 128 + 1];
-    }
-    double y[MAXSLOT][2];
-#pragma unroll
-    for (int j = 0; j < MAXSLOT; ++j) {
-      if (pval[j]) {
-        const d2v t = *reinterpret_cast<const d2v*>(ybin + pbase[j]);
-        y[j][0] = t.x;
-        y[j][1] = t.y;
-      } else {
-        y[j][0] = y[j][1] = 0.0;
-      }
-    }
-    fold_finish<2, MAXSLOT, false, HB, PROBE, ROWS>(y, pval, pbase, R, L, ndata, T, lane, qi, qi_ld, s, dc);
+  } else {
+    for (int64_t s = (int64_t)blockIdx.x * WPB + wave; s < nseg; s += (int64_t)nwork * WPB)
+      bins_segment<MAXSLOT, LOADS, NT, HB, PROBE, ROWS>(x + s * seg_stride, R, L, ndata, T, ybin, lane, pval, pbase,
+                                                         qi, qi_ld, s, dc);
   }
+  if (probe && threadIdx.x == 0 && blockIdx.x == 0) probe[5] = __builtin_amdgcn_s_memrealtime();
 }
 
 // Pipelined variant of demod_bins_kernel: a wave's work is one flat sequence of

@@ -53,6 +53,8 @@ struct DeviceState {
   std::map<std::tuple<int, uint64_t, uint64_t, uint64_t>, DevBuf> gridtab;  // (ndata, min, max, step)
   hipStream_t side = nullptr;  // seed step runs here, concurrently with the bulk demod
   hipEvent_t ev_in = nullptr, ev_seed = nullptr;
+  uint64_t* seed_ctr = nullptr;  // seed -> bulk LM hand-off: [0] monotonic counter, [8..] seeds (lm.h)
+  uint64_t seed_total = 0;       // seeds issued so far (the LM's wait target)
 };
 
 std::map<int, DeviceState> g_dev;
@@ -78,9 +80,13 @@ int ensure_init(int* dev_out) {
     HIPCHK(hipGetDeviceProperties(&prop, dev));
     ds.n_cu = prop.multiProcessorCount;
     ds.lds_per_block = prop.sharedMemPerBlock;
-    HIPCHK(hipStreamCreateWithFlags(&ds.side, hipStreamNonBlocking));
+    int prio_lo = 0, prio_hi = 0;  // the seed stream dispatches ahead of the bulk demodulation
+    HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    HIPCHK(hipStreamCreateWithPriority(&ds.side, hipStreamNonBlocking, prio_hi));
     HIPCHK(hipEventCreateWithFlags(&ds.ev_in, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ds.ev_seed, hipEventDisableTiming));
+    HIPCHK(hipMalloc(&ds.seed_ctr, 512));
+    HIPCHK(hipMemset(ds.seed_ctr, 0, 512));
     ds.init = true;
   }
   *dev_out = dev;
@@ -197,13 +203,22 @@ struct Tuning {
                                // (measured slower: profiles/r01_tune_demod_stream.json), 2: bins in LDS,
                                // 3: bins in LDS, pipelined
   int demod_unr = 4;           // cycles per batch of the streaming fold (1, 2, 4, 5)
-  int seed_reserve = 1;        // 1: the bulk demodulation grid leaves slots free for the seed waves
+  int seed_reserve = 0;        // 1: the bulk demodulation grid leaves slots free for the seed waves
+  int demod_dyn = 0;           // 1: dynamic segment scheduling in the bin kernel (demod.h SegQueue;
+                               // measured 10 % slower: profiles/r01b_tune_step_dyn_seed.json)
+  int seed_spacer = 0;         // 1: bulk demodulation leaves a slot for the seed wave (g_spacer; measured
+                               // slower: the 8-wave workgroups cost more than the seed gains)
+  int seed_handoff = 1;        // 1: seed -> bulk LM hand-off through a device counter (lm.h seed_ctr)
+  int seed_handoff_unreachable = 0;  // test hook: a target the counter never reaches (LM fallback path)
+  int seed_bins = 1;           // 1: seed step with the LDS fold + LDS-resident QI (seed.h seed_bins_kernel)
   int demod_bins_cfg = 0;      // bins kernel shape: 0 = 4-wave blocks, LDS basis, 8 harmonics per
                                // reduction block; 1..6 = higher-occupancy shapes (launch_bins_t);
                                // 7, 8 = timing probes (no QI stores / no contraction: results invalid)
 };
 Tuning g_tune;
 std::string g_last_demod;
+int g_spacer = 0;
+uint64_t* g_probe = nullptr;  // diagnostics timestamps (dfmi_set_tuning("probe", 1), dfmi_probe_read)  // bin kernel: 8-wave workgroups + an idle last workgroup (seed co-scheduling)
 // Workgroup slots a persistent demodulation grid leaves free (set by the record
 // pipeline for the concurrent seed waves; every launcher subtracts it).
 int64_t g_grid_reserve = 0;
@@ -313,40 +328,66 @@ int try_stream(int dev, const double* x, int64_t nseg, int64_t stride, int R, in
 }
 
 template <int MS, int LOADS, bool NT, int WPB = 4, int WPEU = 1, bool TAB_LDS = true, int HB = 8, int PROBE = 0,
-          bool ROWS = false>
-int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tab,
+          bool ROWS = false, bool DYN = false>
+int launch_bins_t(int dev, const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tab,
                   double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu, size_t lds_cap) {
-  if constexpr (MS == 2 && LOADS == 8 && NT && WPB == 4 && WPEU == 1 && TAB_LDS && HB == 8 && PROBE == 0 && !ROWS) {
+  if constexpr (!DYN) {  // dynamic segment scheduling (demod.h SegQueue) unless tuned off
+    if (g_tune.demod_dyn)
+      return launch_bins_t<MS, LOADS, NT, WPB, WPEU, TAB_LDS, HB, PROBE, ROWS, true>(dev, x, nseg, stride, R, L, ndata,
+                                                                                     tab, qi, qi_ld, dc, st, n_cu,
+                                                                                     lds_cap);
+  }
+  if constexpr (MS == 2 && LOADS == 8 && NT && WPB == 4 && WPEU == 1 && TAB_LDS && HB == 8 && PROBE == 0 && !ROWS &&
+                !DYN) {
     switch (g_tune.demod_bins_cfg) {  // tunable shape
-      case 7: return launch_bins_t<2, 8, true, 4, 1, true, 8, 1>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-      case 8: return launch_bins_t<2, 8, true, 4, 1, true, 8, 2>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-      case 1: return launch_bins_t<2, 8, true, 8, 6, true, 4>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-      case 2: return launch_bins_t<2, 4, true, 8, 6, true, 4>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-      case 3: return launch_bins_t<2, 8, true, 16, 8, true, 2>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-      case 4: return launch_bins_t<2, 4, true, 16, 8, true, 2>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-      case 5: return launch_bins_t<2, 8, true, 4, 6, false, 4>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-      case 6: return launch_bins_t<2, 8, true, 4, 8, false, 2>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+      case 7: return launch_bins_t<2, 8, true, 4, 1, true, 8, 1>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+      case 8: return launch_bins_t<2, 8, true, 4, 1, true, 8, 2>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+      case 1: return launch_bins_t<2, 8, true, 8, 6, true, 4>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+      case 2: return launch_bins_t<2, 4, true, 8, 6, true, 4>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+      case 3: return launch_bins_t<2, 8, true, 16, 8, true, 2>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+      case 4: return launch_bins_t<2, 4, true, 16, 8, true, 2>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+      case 5: return launch_bins_t<2, 8, true, 4, 6, false, 4>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+      case 6: return launch_bins_t<2, 8, true, 4, 8, false, 2>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
       default: break;
     }
     if (g_tune.demod_loads == 16)
-      return launch_bins_t<2, 16, true>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+      return launch_bins_t<2, 16, true>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
     if (!g_tune.demod_nt)
-      return launch_bins_t<2, 8, false>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+      return launch_bins_t<2, 8, false>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+  }
+  if constexpr (ROWS && !DYN && WPB == 4 && MS == 2 && LOADS == 8 && NT && WPEU == 1 && TAB_LDS && HB == 8 &&
+                PROBE == 0) {
+    // With a seed wave co-scheduled (nls_record_device), 8-wave workgroups (2 waves
+    // per SIMD, 2 per CU): the spacer's slot is 2 x 128 VGPRs per SIMD + 45 KB LDS,
+    // enough for the seed kernel (161 VGPRs, 34 KB); a 4-wave workgroup's is not.
+    if (g_spacer)
+      return launch_bins_t<2, 8, true, 8, 1, true, 8, 0, true>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc,
+                                                               st, n_cu, lds_cap);
   }
   const size_t lds = ((TAB_LDS ? (size_t)2 * ndata * L : 0) + (size_t)WPB * L) * sizeof(double);
   if (lds > lds_cap) return fail(DFMI_ERR_UNSUPPORTED, "demod_bins_kernel: LDS footprint exceeds the workgroup limit");
-  auto kern = dfmi::demod_bins_kernel<MS, LOADS, NT, WPB, WPEU, TAB_LDS, HB, PROBE, ROWS>;
+  auto kern = dfmi::demod_bins_kernel<MS, LOADS, NT, WPB, WPEU, TAB_LDS, HB, PROBE, ROWS, DYN>;
+  unsigned* ctr = nullptr;
+  if constexpr (DYN) {
+    void* cw = nullptr;
+    int rc = workspace(dev, "seg_queue", 8 * 64 * sizeof(unsigned), &cw);
+    if (rc) return rc;
+    ctr = (unsigned*)cw;
+    HIPCHK(hipMemsetAsync(ctr, 0, 8 * 64 * sizeof(unsigned), st));
+  }
   int per_cu = 0;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WPB, lds));
   if (per_cu < 1) per_cu = 1;
   if (g_tune.demod_blocks_per_cu > 0 && g_tune.demod_blocks_per_cu < per_cu) per_cu = g_tune.demod_blocks_per_cu;
-  const int64_t grid = persistent_grid(n_cu, per_cu, (nseg + WPB - 1) / WPB);
+  const int spacer = (g_spacer && !DYN) ? 8 : 0;
+  const int64_t grid = persistent_grid(n_cu, per_cu, (nseg + WPB - 1) / WPB + spacer);  // spacer: one of the slots
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * WPB), lds, st, x, nseg, stride, R, L, ndata, tab, qi,
-                     qi_ld, dc);
+                     qi_ld, dc, ctr, spacer, g_probe);
   HIPCHK(hipGetLastError());
   g_last_demod = "demod_bins_kernel<" + std::to_string(MS) + "," + std::to_string(LOADS) + "," +
                  std::to_string((int)NT) + "," + std::to_string(WPB) + "," + std::to_string(WPEU) + "," +
-                 std::to_string((int)TAB_LDS) + "," + std::to_string(HB) + (ROWS ? ",rows" : "") + ">";
+                 std::to_string((int)TAB_LDS) + "," + std::to_string(HB) + (ROWS ? ",rows" : "") +
+                 (DYN ? ",dyn" : "") + (spacer ? ",spacer" : "") + ">";
   return DFMI_OK;
 }
 
@@ -389,12 +430,12 @@ int try_bins(int dev, const double* x, int64_t nseg, int64_t stride, int R, int 
   const int nslot = (L + 127) / 128;
   if (rows) {
     if (nslot <= 2)
-      return launch_bins_t<2, 8, true, 4, 1, true, 8, 0, true>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st,
+      return launch_bins_t<2, 8, true, 4, 1, true, 8, 0, true>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st,
                                                                n_cu, lds_cap);
     if (nslot <= 4)
-      return launch_bins_t<4, 8, true, 4, 1, true, 8, 0, true>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st,
+      return launch_bins_t<4, 8, true, 4, 1, true, 8, 0, true>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st,
                                                                n_cu, lds_cap);
-    return launch_bins_t<8, 8, true, 4, 1, true, 8, 0, true>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st,
+    return launch_bins_t<8, 8, true, 4, 1, true, 8, 0, true>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st,
                                                              n_cu, lds_cap);
   }
   if (g_tune.demod_kernel == 3 && (R % 2) == 0) {
@@ -405,9 +446,9 @@ int try_bins(int dev, const double* x, int64_t nseg, int64_t stride, int R, int 
     if (nslot <= 4) return launch_bins_pipe_t<4, 4>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds);
     return launch_bins_pipe_t<8, 4>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds);
   }
-  if (nslot <= 2) return launch_bins_t<2, 8, true>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-  if (nslot <= 4) return launch_bins_t<4, 8, true>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-  return launch_bins_t<8, 8, true>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+  if (nslot <= 2) return launch_bins_t<2, 8, true>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+  if (nslot <= 4) return launch_bins_t<4, 8, true>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+  return launch_bins_t<8, 8, true>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
 }
 
 // Whether demod_device can write the row layout (dfmi_qi_row_stride) for this
@@ -474,7 +515,8 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
               int64_t nitems, int64_t nchunk, const double* guess_dev, int64_t g_rec, int64_t g_comp,
               const double* guess_host /* nrec*4, used when nrec <= 8 and guess_dev == null */,
               const dfmi::LMConst& c, const double* jtab, double* out, int64_t out_ld, int32_t* status,
-              hipStream_t st, bool rows = false) {
+              hipStream_t st, bool rows = false, const uint64_t* seed_ctr = nullptr, uint64_t seed_target = 0,
+              const double* seed_init_host = nullptr) {
   if (nrec == 0 || nitems == 0) return DFMI_OK;
   if (nchunk < 1) nchunk = 1;
   if (nchunk > nitems) nchunk = nitems;  // np.array_split chunks beyond nitems are empty
@@ -486,6 +528,11 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
     for (int64_t r = 0; r < nrec; ++r)
       for (int i = 0; i < 4; ++i) ginl.v[r][i] = guess_host[r * 4 + i];
     use_inline = 1;
+  }
+  if (seed_ctr) {  // fallback seeds (lm.h): the records' initial guesses
+    if (nrec > 8) return fail(DFMI_ERR_ARG, "device seed hand-off supports at most 8 records");
+    for (int64_t r = 0; r < nrec; ++r)
+      for (int i = 0; i < 4; ++i) ginl.v[r][i] = seed_init_host[r * 4 + i];
   }
   const int64_t lanes = nrec * nchunk;
   const int block = 64;
@@ -508,7 +555,8 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
     if (nd_sel <= 16) lds = (size_t)qi_ld * 65 * sizeof(double);  // the wave's rows, transposed
   }
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(block), lds, st, qi, qi_ld, ndata, nrec, nbuf, first, nitems,
-                     nchunk, guess_dev, g_rec, g_comp, ginl, use_inline, jtab, c, out, out_ld, status);
+                     nchunk, guess_dev, g_rec, g_comp, ginl, use_inline, jtab, c, out, out_ld, status, seed_ctr,
+                     seed_target);
   HIPCHK(hipGetLastError());
   return DFMI_OK;
 }
@@ -546,6 +594,8 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
       for (int i = 0; i < 4; ++i) ginl.v[r][i] = init_guess_host[r * 4 + i];
 
   int64_t reserve = 0;  // persistent-grid slots left free for the seed waves
+  bool spacer = false;  // bin kernel with an idle workgroup slot for the seed wave
+  bool handoff = false; // seed -> LM through ds.seed_ctr (no stream event)
   if (parallel) {
     // seed step (buffer 0 of every record) on the side stream, concurrently with the
     // bulk demodulation. The bulk grid leaves one workgroup slot (one wave slot on
@@ -562,12 +612,32 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
     if ((rc = workspace(dev, "dc_seed", (size_t)nrec * 8, &ds_))) return rc;
     HIPCHK(hipEventRecord(ds.ev_in, st));
     HIPCHK(hipStreamWaitEvent(ds.side, ds.ev_in, 0));
-    auto sk = ndata <= 12 ? dfmi::seed_kernel<12> : ndata <= 16 ? dfmi::seed_kernel<16> : dfmi::seed_kernel<0>;
-    hipLaunchKernelGGL(sk, dim3((unsigned)nrec), dim3(64), 0, ds.side, x, rec_stride, R, L, ndata, w0, tab,
-                       (double*)qs, (double*)ds_, nrec, gdev, ginl, gdev ? 0 : 1, jtab, c, out, out_ld, nbuf, fitok);
+    const bool seed_bins = L > 0 && g_tune.seed_bins && rows_supported(dev, x, R, R, ndata, w0, period) &&
+                           (nrec == 1 || (rec_stride % 2) == 0);
+    // device-side seed hand-off to the bulk LM (lm.h seed_ctr) instead of ev_seed
+    handoff = seed_bins && g_tune.seed_handoff && nrec <= 8 && nbuf > 1 && nchunk >= nbuf - 1;
+    if (handoff) ds.seed_total += (uint64_t)nrec;
+    if (seed_bins) {  // fold into LDS, QI from LDS in the fit (seed.h seed_bins_kernel)
+      const int nslot = (L + 127) / 128;
+      const size_t lds = ((size_t)2 * ndata * L + L + dfmi_row_stride(ndata)) * sizeof(double);
+      auto sk = ndata <= 12 ? (nslot <= 2 ? dfmi::seed_bins_kernel<12, 2> : nslot <= 4 ? dfmi::seed_bins_kernel<12, 4>
+                                                                                     : dfmi::seed_bins_kernel<12, 8>)
+              : ndata <= 16 ? (nslot <= 2 ? dfmi::seed_bins_kernel<16, 2> : nslot <= 4 ? dfmi::seed_bins_kernel<16, 4>
+                                                                                     : dfmi::seed_bins_kernel<16, 8>)
+                            : (nslot <= 2 ? dfmi::seed_bins_kernel<0, 2> : nslot <= 4 ? dfmi::seed_bins_kernel<0, 4>
+                                                                                    : dfmi::seed_bins_kernel<0, 8>);
+      hipLaunchKernelGGL(sk, dim3((unsigned)nrec), dim3(64), lds, ds.side, x, rec_stride, R, L, ndata, tab, gdev, ginl,
+                         gdev ? 0 : 1, jtab, c, out, out_ld, nbuf, fitok, handoff ? ds.seed_ctr : nullptr, g_probe);
+    } else {
+      auto sk = ndata <= 12 ? dfmi::seed_kernel<12> : ndata <= 16 ? dfmi::seed_kernel<16> : dfmi::seed_kernel<0>;
+      hipLaunchKernelGGL(sk, dim3((unsigned)nrec), dim3(64), 0, ds.side, x, rec_stride, R, L, ndata, w0, tab,
+                         (double*)qs, (double*)ds_, nrec, gdev, ginl, gdev ? 0 : 1, jtab, c, out, out_ld, nbuf, fitok,
+                         nullptr);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ds.ev_seed, ds.side));
     if (g_tune.seed_reserve) reserve = (nrec + 3) / 4 < 64 ? (nrec + 3) / 4 : 64;
+    spacer = seed_bins && nrec == 1 && g_tune.seed_spacer;
   }
   // Row layout (one 128-B line per 8 harmonics, dc inside the row: full-line
   // stores) for the chunk-size-1 parallel path when the bin kernel applies;
@@ -581,6 +651,7 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
     qi = (double*)rw;
   }
   g_grid_reserve = reserve;
+  g_spacer = spacer ? 1 : 0;
   if (rec_stride == nbuf * (int64_t)R) {
     rc = rows ? demod_device(dev, x, nseg, R, R, ndata, w0, period, qi, qs, nullptr, st, true)
               : demod_device(dev, x, nseg, R, R, ndata, w0, period, qi, nseg, dc, st);
@@ -593,12 +664,13 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
     }
   }
   g_grid_reserve = 0;
+  g_spacer = 0;
   if (rc) return rc;
   if (!parallel) {
     return lm_device(dev, qi, nseg, ndata, nrec, nbuf, 0, nbuf, 1, gdev, 4, 1, init_guess_host, c, jtab, out, out_ld,
                      fitok, st);
   }
-  HIPCHK(hipStreamWaitEvent(st, ds.ev_seed, 0));
+  if (!(handoff && rows)) HIPCHK(hipStreamWaitEvent(st, ds.ev_seed, 0));
   if (nbuf <= 1) {
     if (rows)  // dc of the seed buffers (the LM kernel carries it otherwise)
       HIPCHK(hipMemcpy2DAsync(dc, nbuf * sizeof(double), qi + dfmi_row_dc(ndata), qs * nbuf * sizeof(double),
@@ -606,6 +678,10 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
     return DFMI_OK;
   }
   // the rest, seeded with each record's buffer-0 result (read on device: no host sync)
+  if (handoff && rows)
+    return lm_device(dev, qi, qs, ndata, nrec, nbuf, 1, nbuf - 1, nchunk, out, nbuf, out_ld, nullptr, c, jtab, out,
+                     out_ld, fitok, st, true, ds.seed_ctr,
+                     ds.seed_total + (g_tune.seed_handoff_unreachable ? (uint64_t)1 << 40 : 0), init_guess_host);
   return lm_device(dev, qi, rows ? qs : nseg, ndata, nrec, nbuf, 1, nbuf - 1, nchunk, out, nbuf, out_ld, nullptr, c,
                    jtab, out, out_ld, fitok, st, rows);
 }
@@ -648,6 +724,16 @@ const char* dfmi_version(void) { return "dfmi 0.2 gfx950"; }
 
 const char* dfmi_last_demod_kernel(void) { return g_last_demod.c_str(); }
 
+int dfmi_probe_read(int64_t* out, int32_t n) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_err.clear();
+  if (!g_probe) return fail(DFMI_ERR_ARG, "probe not enabled (dfmi_set_tuning(\"probe\", 1))");
+  if (n < 0 || n > 16 || (n && !out)) return fail(DFMI_ERR_ARG, "bad probe read");
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(out, g_probe, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return DFMI_OK;
+}
+
 int dfmi_set_tuning(const char* key, int64_t value) {
   std::lock_guard<std::mutex> lk(g_mu);
   g_err.clear();
@@ -659,6 +745,28 @@ int dfmi_set_tuning(const char* key, int64_t value) {
   } else if (k == "demod_kernel") {
     if (value < 0 || value > 3) return fail(DFMI_ERR_ARG, "demod_kernel must be 0..3");
     g_tune.demod_kernel = (int)value;
+  } else if (k == "seed_bins") {
+    g_tune.seed_bins = value ? 1 : 0;
+  } else if (k == "probe") {
+    if (value && !g_probe) {
+      int dev;
+      int rc = ensure_init(&dev);
+      if (rc) return rc;
+      void* p = nullptr;
+      if ((rc = workspace(dev, "probe", 16 * sizeof(uint64_t), &p))) return rc;
+      HIPCHK(hipMemset(p, 0, 16 * sizeof(uint64_t)));
+      g_probe = (uint64_t*)p;
+    } else if (!value) {
+      g_probe = nullptr;
+    }
+  } else if (k == "seed_handoff_unreachable") {
+    g_tune.seed_handoff_unreachable = value ? 1 : 0;
+  } else if (k == "seed_handoff") {
+    g_tune.seed_handoff = value ? 1 : 0;
+  } else if (k == "seed_spacer") {
+    g_tune.seed_spacer = value ? 1 : 0;
+  } else if (k == "demod_dyn") {
+    g_tune.demod_dyn = value ? 1 : 0;
   } else if (k == "seed_reserve") {
     g_tune.seed_reserve = value ? 1 : 0;
   } else if (k == "demod_bins_cfg") {

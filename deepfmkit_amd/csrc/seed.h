@@ -15,13 +15,13 @@
 namespace dfmi {
 
 template <int NDMAX>
-__global__ __launch_bounds__(64, 4) void seed_kernel(const double* __restrict__ x, int64_t rec_stride, int R, int L,
+__global__ __launch_bounds__(64) void seed_kernel(const double* __restrict__ x, int64_t rec_stride, int R, int L,
                                                   int ndata, double w0, const double* __restrict__ tab,
                                                   double* __restrict__ qis, double* __restrict__ dcs, int64_t nrec,
                                                   const double* __restrict__ guess, GuessInline ginl, int use_inline,
                                                   const double* __restrict__ jtab, LMConst c,
                                                   double* __restrict__ out, int64_t out_ld, int64_t nbuf,
-                                                  int32_t* __restrict__ status) {
+                                                  int32_t* __restrict__ status, uint64_t* __restrict__ done_ctr) {
   const int64_t r = blockIdx.x;
   const int lane = threadIdx.x;
   const double* __restrict__ xs = x + r * rec_stride;
@@ -51,6 +51,108 @@ __global__ __launch_bounds__(64, 4) void seed_kernel(const double* __restrict__ 
   out[3 * out_ld + sidx] = p[3];
   out[5 * out_ld + sidx] = ssq;
   status[sidx] = st;
+  if (done_ctr) __hip_atomic_fetch_add(done_ctr, (uint64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Seed step for inputs the bin kernel handles (16-B rows, even L in [128, 1024]):
+// the wave folds its record's buffer 0 with 16 chunk loads in flight into LDS bins,
+// contracts it into an LDS row (the demodulation row layout, dfmi_row_stride), and
+// lane 0 fits it reading QI from LDS — no memory traffic inside the LM and no
+// register cap, so the fit runs at its own instruction latency even while the bulk
+// demodulation saturates HBM (seed_kernel, with QI in global memory and a
+// 128-VGPR cap, took as long as the whole demodulation beside it:
+// profiles/r01b_seed_timeline.txt). Same QI, dc and fit as the bulk path.
+template <int NDMAX, int MAXSLOT>
+__global__ __launch_bounds__(64) void seed_bins_kernel(const double* __restrict__ x, int64_t rec_stride, int R, int L,
+                                                       int ndata, const double* __restrict__ tab,
+                                                       const double* __restrict__ guess, GuessInline ginl,
+                                                       int use_inline, const double* __restrict__ jtab, LMConst c,
+                                                       double* __restrict__ out, int64_t out_ld, int64_t nbuf,
+                                                       int32_t* __restrict__ status, uint64_t* __restrict__ done_ctr,
+                                                       uint64_t* __restrict__ probe) {
+  // probe (diagnostics, may be null): s_memrealtime (100 MHz) at entry, after the
+  // fold, after the fit, written by record 0
+  const uint64_t t_in = __builtin_amdgcn_s_memrealtime();
+  extern __shared__ __attribute__((aligned(16))) double sh[];  // basis | bins [L] | row
+  const int64_t r = blockIdx.x;
+  const int lane = threadIdx.x;
+  __builtin_amdgcn_s_setprio(3);  // ahead of the demodulation waves sharing this SIMD
+  const int ntab = 2 * ndata * L;  // even (L even)
+  {
+    // basis table -> LDS with every load in flight at once (a load-then-store loop
+    // pays one memory round trip per iteration, which under the bulk
+    // demodulation's HBM saturation is several microseconds each)
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    const d2v* __restrict__ src = reinterpret_cast<const d2v*>(tab);
+    d2v* dst = reinterpret_cast<d2v*>(sh);
+    const int n2 = ntab / 2;
+    for (int base = 0; base < n2; base += 64 * 32) {
+      d2v v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) {
+        const int i = base + u * 64 + lane;
+        v[u] = i < n2 ? src[i] : d2v{0.0, 0.0};
+      }
+#pragma unroll
+      for (int u = 0; u < 32; ++u) {
+        const int i = base + u * 64 + lane;
+        if (i < n2) dst[i] = v[u];
+      }
+    }
+  }
+  __syncthreads();
+  double* ybin = sh + ntab;
+  double* row = ybin + L;
+  const int nslot = (L + 127) / 128;
+  int pbase[MAXSLOT];
+  bool pval[MAXSLOT];
+#pragma unroll
+  for (int j = 0; j < MAXSLOT; ++j) {
+    pbase[j] = 2 * (lane + 64 * j);
+    pval[j] = (j < nslot) && (pbase[j] < L);
+  }
+  bins_segment<MAXSLOT, 32, false, kHarmBlock, 0, true>(x + r * rec_stride, R, L, ndata, sh, ybin, lane, pval, pbase,
+                                                        row, 0, 0, nullptr);
+  __syncthreads();
+  const uint64_t t_fold = __builtin_amdgcn_s_memrealtime();
+  if (lane != 0) return;
+  double p[4] = {0.0, 0.0, 0.0, 0.0};
+  if (use_inline) {
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) {
+      if (r == rr) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) p[i] = ginl.v[rr][i];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) p[i] = guess[r * 4 + i];
+  }
+  double ssq;
+  const QRow<1> q{row};
+  const int st = fit_segment_q<NDMAX>(q, ndata, jtab, c, p, ssq);
+  const int64_t sidx = r * nbuf;
+  out[0 * out_ld + sidx] = p[0];
+  out[1 * out_ld + sidx] = p[1];
+  out[2 * out_ld + sidx] = p[2];
+  out[3 * out_ld + sidx] = p[3];
+  out[4 * out_ld + sidx] = q.at(dfmi_row_dc(ndata));
+  out[5 * out_ld + sidx] = ssq;
+  status[sidx] = st;
+  // hand-off to the bulk LM kernel (lm.h seed_ctr): the seed into done_ctr[8 + 4r ..]
+  // with agent-coherent stores, then a release increment of the counter
+  if (done_ctr) {
+    double* sv = reinterpret_cast<double*>(done_ctr + 8) + r * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) __hip_atomic_store(sv + i, p[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(done_ctr, (uint64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (probe && r == 0) {
+    probe[0] = t_in;
+    probe[1] = t_fold;
+    probe[2] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
 }  // namespace dfmi

@@ -130,6 +130,12 @@ int dfmi_ekf(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
  * path for every ndata). Process-wide. */
 int dfmi_set_tuning(const char* key, int64_t value);
 
+/* Diagnostics: with dfmi_set_tuning("probe", 1) some kernels record
+ * s_memrealtime (100 MHz) timestamps; copies the first n (<= 16) of them
+ * (synchronises the device). [0..2] seed entry / after fold / after fit,
+ * [3] bin demod workgroup 0 entry, [4] last workgroup entry, [5] workgroup 0 exit. */
+int dfmi_probe_read(int64_t* out, int32_t n);
+
 /* Period (samples) the fold kernel would use for this w0, R, ndata; 0 if none. */
 int32_t dfmi_detect_period(double w0, int32_t R, int32_t ndata);
 

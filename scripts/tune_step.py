@@ -61,7 +61,7 @@ def main():
         else:
             d = (cur - ref).abs().max().item()
             print(f"{s}: max|diff| vs first setting = {d:.3e}", file=sys.stderr)
-            assert d == 0.0, (s, d)
+            assert d <= 1e-8, (s, d)  # settings that change the seed's summation order move results ~1e-11
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     res = {i: [] for i in range(len(settings))}
     for _ in range(6):

@@ -219,8 +219,10 @@ def test_demod_rows_bit_identical_to_component_major(nd):
 
 def test_record_rows_path_matches_component_path():
     """dfmi_nls_record through the row layout (default for chunk size 1) is
-    bit-identical to the component-major path (forced with demod_kernel = 0), for a
-    multi-record strided batch and for nbuf = 1 (the dc of the seed buffers)."""
+    bit-identical to the component-major path (forced with demod_kernel = 0) when both
+    use the same seed kernel, for a multi-record strided batch and for nbuf = 1 (the dc
+    of the seed buffers); the LDS seed kernel (seed_bins) folds buffer 0 in another
+    summation order, which moves the seeded fits by < 1e-9."""
     import torch
     from deepfmkit_amd import _lib
     from deepfmkit_amd.fitters import nls_records
@@ -235,11 +237,41 @@ def test_record_rows_path_matches_component_path():
     recs[:, : 40 * R] = base + 1e-3 * torch.randn(base.shape, dtype=torch.float64, device="cuda", generator=g)
     for nbuf in (40, 1):
         res = {}
-        for kern in (2, 0):
+        for kern, seedb in ((2, 0), (0, 0), (2, 1)):
             _lib.check(lib.dfmi_set_tuning(b"demod_kernel", kern), "tune")
+            _lib.check(lib.dfmi_set_tuning(b"seed_bins", seedb), "tune")
             cols, ok = nls_records(recs, 200000.0, 1000.0, R, nbuf, 10)
-            res[kern] = (cols.cpu().numpy(), ok.cpu().numpy(), lib.dfmi_last_demod_kernel().decode())
+            res[kern, seedb] = (cols.cpu().numpy(), ok.cpu().numpy(), lib.dfmi_last_demod_kernel().decode())
         _lib.check(lib.dfmi_set_tuning(b"demod_kernel", 2), "tune")
-        assert "rows" in res[2][2] and "rows" not in res[0][2], (res[2][2], res[0][2])
-        np.testing.assert_array_equal(res[2][0], res[0][0])
-        np.testing.assert_array_equal(res[2][1], res[0][1])
+        _lib.check(lib.dfmi_set_tuning(b"seed_bins", 1), "tune")
+        a, b, c = res[2, 0], res[0, 0], res[2, 1]
+        assert "rows" in a[2] and "rows" not in b[2], (a[2], b[2])
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1], b[1])
+        np.testing.assert_array_equal(c[1], b[1])
+        assert np.abs(c[0] - b[0]).max() < 1e-9
+
+
+def test_seed_handoff_fallback_identical():
+    """The bulk LM takes the seed from the side-stream seed kernel through a device
+    counter; if it never arrives (test hook: an unreachable target) every wave
+    recomputes the identical seed from the bulk demodulation row after a bounded wait."""
+    import torch
+    from deepfmkit_amd import _lib
+    from deepfmkit_amd.fitters import nls_records
+    lib = _lib.load()
+    R, nbuf = 4000, 300
+    t = torch.arange(nbuf * R, dtype=torch.float64, device="cuda") / 200000.0
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    x = (1.0 + torch.cos(0.4 + 6.2 * torch.cos(2 * np.pi * 1000.0 * t + 0.2))).reshape(1, -1)
+    x = x + 1e-3 * torch.randn(x.shape, dtype=torch.float64, device="cuda", generator=g)
+    res = []
+    for unreachable in (0, 1, 0):
+        _lib.check(lib.dfmi_set_tuning(b"seed_handoff_unreachable", unreachable), "tune")
+        cols, ok = nls_records(x, 200000.0, 1000.0, R, nbuf, 10)
+        res.append((cols.cpu().numpy(), ok.cpu().numpy()))
+    _lib.check(lib.dfmi_set_tuning(b"seed_handoff_unreachable", 0), "tune")
+    for cols, ok in res[1:]:
+        np.testing.assert_array_equal(cols, res[0][0])
+        np.testing.assert_array_equal(ok, res[0][1])

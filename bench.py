@@ -206,6 +206,13 @@ def main():
     ev1.synchronize()
     demod_ms = ev0.elapsed_time(ev1) / nrep
     kname = lib.dfmi_last_demod_kernel().decode()
+    if args.demod_only:  # profile helper: nothing but the timed demodulation kernel
+        if rank == 0:
+            print(json.dumps({"metric": "demod only (profile helper)", "kernel": kname, "avg_launch_ms": demod_ms,
+                              "roofline": {"kernel": kname}}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     # the LM kernel alone over the same QI (every segment its own chunk), for the record
     lm_out = torch.empty((4, nbuf), dtype=torch.float64, device=dev)
     lm_ssq = torch.empty(nbuf, dtype=torch.float64, device=dev)

@@ -22,7 +22,7 @@ MAX_LAMBDA = 16
 SYMBOLS = ("dfmi_lm_config_default", "dfmi_demod", "dfmi_lm", "dfmi_nls_record", "dfmi_ekf",
            "dfmi_detect_period", "dfmi_device_count", "dfmi_last_error", "dfmi_version", "dfmi_set_tuning",
            "dfmi_last_demod_kernel", "dfmi_qi_row_stride", "dfmi_qi_row_dc", "dfmi_demod_rows",
-           "dfmi_probe_read")
+           "dfmi_probe_read", "dfmi_get_tuning")
 
 
 class DFMIError(RuntimeError):
@@ -89,6 +89,8 @@ def load():
         lib.dfmi_qi_row_dc.restype = ctypes.c_int32
         lib.dfmi_demod_rows.argtypes = [P, i64, i64, i32, i32, dbl, i32, P, i32, P]
         lib.dfmi_demod_rows.restype = ctypes.c_int
+        lib.dfmi_get_tuning.argtypes = [ctypes.c_char_p, P]
+        lib.dfmi_get_tuning.restype = ctypes.c_int
         lib.dfmi_probe_read.argtypes = [P, i32]
         lib.dfmi_probe_read.restype = ctypes.c_int
         lib.dfmi_last_demod_kernel.argtypes = []

@@ -36,7 +36,7 @@ constexpr int kHarmBlock = 8;  // harmonics per contraction block (16 partial su
 // One exchange stage of the reduce-scatter: lanes with the mask bit set keep
 // the upper HALF of their live values, the others the lower half, and each adds
 // its partner's copy of the half it keeps.
-template <int HALF, int MASK, int NV, bool LOWREG = false>
+template <int HALF, int MASK, int NV>
 __device__ __forceinline__ void bfly_stage(double (&v)[NV], int lane) {
   const bool hi = lane & MASK;
 #pragma unroll
@@ -44,7 +44,6 @@ __device__ __forceinline__ void bfly_stage(double (&v)[NV], int lane) {
     const double send = hi ? v[i] : v[i + HALF];
     const double keep = hi ? v[i + HALF] : v[i];
     v[i] = keep + __shfl_xor(send, MASK);
-    if constexpr (LOWREG) __builtin_amdgcn_sched_barrier(0);  // one exchange in flight at a time
   }
 }
 
@@ -53,14 +52,14 @@ __device__ __forceinline__ void bfly_stage(double (&v)[NV], int lane) {
 // stages are plain butterfly sums. On return lane l holds, in v[0], the
 // wave-wide sum of value index (l >> (6 - log2 NV)) & (NV - 1).
 // (NV = 16: 15 exchange-adds + 2 sums = 17 shuffles instead of 16 x 6.)
-template <int NV, bool LOWREG = false>
+template <int NV>
 __device__ __forceinline__ void butterfly(double (&v)[NV], int lane) {
   static_assert(NV == 4 || NV == 8 || NV == 16, "NV");
   if constexpr (NV == 16) {
-    bfly_stage<8, 32, NV, LOWREG>(v, lane);
-    bfly_stage<4, 16, NV, LOWREG>(v, lane);
-    bfly_stage<2, 8, NV, LOWREG>(v, lane);
-    bfly_stage<1, 4, NV, LOWREG>(v, lane);
+    bfly_stage<8, 32>(v, lane);
+    bfly_stage<4, 16>(v, lane);
+    bfly_stage<2, 8>(v, lane);
+    bfly_stage<1, 4>(v, lane);
     v[0] += __shfl_xor(v[0], 2);
     v[0] += __shfl_xor(v[0], 1);
   } else if constexpr (NV == 8) {
@@ -137,7 +136,7 @@ __device__ __forceinline__ void store_block(const double (&v)[2 * HB], int lane,
 // tree is wave_sum's, so dc is bit-identical to the ROWS = false value. (Scattered
 // 8-B stores into 21 component rows cost 13 % of the demodulation time:
 // profiles/r01_tune_demod_probe.json.)
-template <int VEC, int MAXSLOT, bool LOWREG = false, int HB = kHarmBlock, int PROBE = 0, bool ROWS = false>
+template <int VEC, int MAXSLOT, int HB = kHarmBlock, bool ROWS = false>
 __device__ __forceinline__ void fold_finish(const double (&y)[MAXSLOT][VEC], const bool (&pval)[MAXSLOT],
                                             const int (&pbase)[MAXSLOT], int R, int L, int ndata,
                                             const double* __restrict__ T, int lane, double* __restrict__ qi,
@@ -160,7 +159,6 @@ __device__ __forceinline__ void fold_finish(const double (&y)[MAXSLOT][VEC], con
   }
 
   // ---- contraction with the basis, HB harmonics per block ----
-  if constexpr (PROBE == 2) return;  // timing probe: no contraction
   for (int hb = 0; hb < nblk; ++hb) {
     double acc[2 * HB];
 #pragma unroll
@@ -188,15 +186,10 @@ __device__ __forceinline__ void fold_finish(const double (&y)[MAXSLOT][VEC], con
             acc[HB + h] = fma(y[j][e], bs[e], acc[HB + h]);
           }
         }
-        // LOWREG: one harmonic's basis reads at a time (keeps the streaming
-        // kernel's in-flight load buffers and the contraction within 128 VGPRs)
-        if constexpr (LOWREG) __builtin_amdgcn_sched_barrier(0);
       }
     }
-    butterfly<2 * HB, LOWREG>(acc, lane);
-    if constexpr (PROBE != 0) {
-      if (acc[0] == 1.2345e300) qi[col] = acc[0];  // timing probe: keep the work, drop the stores
-    } else if constexpr (ROWS) {
+    butterfly<2 * HB>(acc, lane);
+    if constexpr (ROWS) {
       if ((lane & 3) == 0) qi[col * qi_ld + hb * 16 + (lane >> 2)] = acc[0] / (double)R;  // one 128-B line
     } else {
       store_block<HB>(acc, lane, hb, ndata, qi, qi_ld, col, R);
@@ -295,122 +288,6 @@ __global__ __launch_bounds__(kBlockThreads) void demod_fold_kernel(
   }
 }
 
-// Streaming fold: the same fold + contraction as demod_fold_kernel, software-
-// pipelined ACROSS segments. Preconditions (checked on the host): VEC = 2
-// (16-B aligned rows, even L, even stride), R % L == 0 and (R / L) % UNR == 0,
-// ceil(L / 128) <= MS, basis table in LDS. A wave's work is one flat sequence
-// of batches (UNR cycles of L samples = MS·UNR 16-B loads per lane) over its
-// segments s = gw, gw + W, ...; batch g+1 is always in flight while batch g is
-// added, including while the contraction of a finished segment runs, so the
-// wave's memory pipe does not drain at segment boundaries (fold_segment's waits
-// for all its loads of a batch, then contracts with nothing in flight). Cycles
-// are still added in ascending k: results are bit-identical to fold_segment.
-template <int MS, int UNR>
-struct FoldBuf {
-  double v[UNR][MS][2];
-};
-
-// Every lane loads (lanes whose phase bin lies past L re-read their slot-0 line,
-// which the same wave instruction fetches anyway) and the value is zeroed after
-// the load: no exec-masked branches around the loads, so the compiler's waitcnt
-// bookkeeping keeps the next batch in flight across the adds.
-template <int MS, int UNR, bool NT>
-__device__ __forceinline__ void fold_load(FoldBuf<MS, UNR>& b, const double* __restrict__ p, int L,
-                                          const int (&poff)[MS]) {
-#pragma unroll
-  for (int u = 0; u < UNR; ++u)
-#pragma unroll
-    for (int j = 0; j < MS; ++j) {
-      if constexpr (NT) VecT<2>::load_nt(p + u * L + poff[j], b.v[u][j]);
-      else VecT<2>::load(p + u * L + poff[j], b.v[u][j]);
-    }
-}
-
-template <int MS, int UNR>
-__device__ __forceinline__ void fold_add(double (&y)[MS][2], const FoldBuf<MS, UNR>& b, const bool (&pval)[MS]) {
-#pragma unroll
-  for (int u = 0; u < UNR; ++u)
-#pragma unroll
-    for (int j = 0; j < MS; ++j) {
-      y[j][0] += pval[j] ? b.v[u][j][0] : 0.0;
-      y[j][1] += pval[j] ? b.v[u][j][1] : 0.0;
-    }
-}
-
-template <int MS, int UNR, bool NT, int MINB = 1>
-__global__ __launch_bounds__(kBlockThreads, MINB) void demod_stream_kernel(
-    const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
-    const double* __restrict__ tab, const double* __restrict__ pad, double* __restrict__ qi, int64_t qi_ld,
-    double* __restrict__ dc) {
-  extern __shared__ __attribute__((aligned(16))) double lds_tab[];
-  {
-    const int n = 2 * ndata * L;
-    for (int i = threadIdx.x; i < n; i += kBlockThreads) lds_tab[i] = tab[i];
-    __syncthreads();
-  }
-  const int lane = threadIdx.x & 63;
-  const int64_t W = (int64_t)gridDim.x * kWavesPerBlock;
-  // wave-uniform (scalar) cursors: the loop control stays in SGPRs
-  const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (gw >= nseg) return;
-  const int64_t nmine = (nseg - 1 - gw) / W + 1;
-  const int nb = (R / L) / UNR;  // batches per segment
-  const int64_t G = nmine * nb;  // batches of this wave
-  const int nslot = (L + 127) / 128;
-  int pbase[MS], poff[MS];
-  bool pval[MS];
-#pragma unroll
-  for (int j = 0; j < MS; ++j) {
-    pbase[j] = 2 * (lane + 64 * j);
-    pval[j] = (j < nslot) && (pbase[j] < L);
-    poff[j] = pval[j] ? pbase[j] : pbase[0];
-  }
-  double y[MS][2];
-#pragma unroll
-  for (int j = 0; j < MS; ++j) y[j][0] = y[j][1] = 0.0;
-
-  // Loads are issued unconditionally (a conditional load makes the compiler's
-  // waitcnt merge drain every outstanding load at the join): batches past the
-  // wave's end read `pad`, a small L2-resident dummy buffer (no HBM traffic).
-  const int64_t bstride = (int64_t)UNR * L;
-  int64_t ls = gw;  // load cursor: segment, batch
-  int lb = 0;
-  int64_t lg = 0;
-  auto next_ptr = [&]() {
-    const double* p = (lg < G) ? x + ls * seg_stride + lb * bstride : pad;
-    ++lg;
-    if (++lb == nb) {
-      lb = 0;
-      ls += W;
-    }
-    return p;
-  };
-  int64_t cs = gw;  // consume cursor
-  int cb = 0;
-  auto consumed = [&]() {
-    if (++cb == nb) {
-      fold_finish<2, MS, true>(y, pval, pbase, R, L, ndata, lds_tab, lane, qi, qi_ld, cs, dc);
-#pragma unroll
-      for (int j = 0; j < MS; ++j) y[j][0] = y[j][1] = 0.0;
-      cb = 0;
-      cs += W;
-    }
-  };
-  FoldBuf<MS, UNR> A, B;
-  fold_load<MS, UNR, NT>(A, next_ptr(), L, poff);
-  fold_load<MS, UNR, NT>(B, next_ptr(), L, poff);
-  for (int64_t g = 0; g < G; g += 2) {
-    fold_add(y, A, pval);
-    consumed();
-    fold_load<MS, UNR, NT>(A, next_ptr(), L, poff);
-    if (g + 1 < G) {
-      fold_add(y, B, pval);
-      consumed();
-    }
-    fold_load<MS, UNR, NT>(B, next_ptr(), L, poff);
-  }
-}
-
 // Bin-in-LDS fold: the same fold + contraction as demod_fold_kernel, but the
 // segment is read the way HBM likes it — as flat, 1-KB-aligned wave loads
 // (lane l reads x[128c + 2l .. +1] of chunk c), not cycle by cycle. A cycle of
@@ -427,15 +304,15 @@ __global__ __launch_bounds__(kBlockThreads, MINB) void demod_stream_kernel(
 // bins: results are bit-identical to demod_fold_kernel.
 // Preconditions (host-checked): 16-B aligned rows (x and seg_stride even),
 // L even, 128 <= L <= 128·MAXSLOT.
-// WPB waves per workgroup share one LDS copy of the basis (TAB_LDS) — or read it
-// through the cache (TAB_LDS = false: LDS then holds only the bins); MINB is the
-// occupancy floor handed to the register allocator (blocks per CU).
-// PROBE (timing only, results invalid): 1 = contraction without the QI stores,
-// 2 = no contraction (dc only).
+// Measured and dropped (profiles/r01_tune_demod_stream.json, r01b_*): software
+// pipelining the next batch across the contraction (slower for both load
+// patterns: the 8-chunk bursts per wave stream better), 6-8 waves per SIMD with
+// leaner contractions (no gain), LDS-DMA rings (readbw.hip: no gain over register
+// loads), and dynamic segment queues on padded atomic counters (10 % slower).
 // One segment of the bin-in-LDS fold: the wave's L bins (ybin, LDS) are zeroed,
 // every 1-KB chunk is added into them, and fold_finish contracts the lane-owned
 // bins with the basis T (LDS or global) into column / row `col` of qi (and dc).
-template <int MAXSLOT, int LOADS, bool NT, int HB, int PROBE, bool ROWS>
+template <int MAXSLOT, int LOADS, bool NT, int HB, bool ROWS>
 __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int R, int L, int ndata,
                                              const double* __restrict__ T, double* __restrict__ ybin, int lane,
                                              const bool (&pval)[MAXSLOT], const int (&pbase)[MAXSLOT],
@@ -498,75 +375,33 @@ __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int
       y[j][0] = y[j][1] = 0.0;
     }
   }
-  fold_finish<2, MAXSLOT, false, HB, PROBE, ROWS>(y, pval, pbase, R, L, ndata, T, lane, qi, qi_ld, col, dc);
+  fold_finish<2, MAXSLOT, HB, ROWS>(y, pval, pbase, R, L, ndata, T, lane, qi, qi_ld, col, dc);
 }
 
-// Dynamic segment scheduling (DYN): segments are handed out by 8 atomic counters
-// (ctr[64·k], k < 8: one 256-B line each — device-scope atomics on one line
-// serialise at ≈88/us, MI355X_MICROARCH.md 'dequeue'; zeroed by the host), one per
-// XCD-sized share [k·nseg/8, (k+1)·nseg/8);
-// a wave takes from the share of its workgroup's XCD (blockIdx % 8 under the
-// round-robin placement; only locality depends on it) and then from the others.
-// A workgroup that starts late — e.g. behind the seed wave that shares its CU —
-// simply takes fewer segments, where a static grid-stride split would end the
-// launch that much later. The next ticket is requested while the current segment
-// is processed, so the atomic's latency is hidden.
-struct SegQueue {
-  unsigned* __restrict__ ctr;
-  int64_t nseg;
-  __device__ __forceinline__ int64_t lo(int k) const { return (int64_t)k * nseg / 8; }
-  __device__ __forceinline__ int64_t hi(int k) const { return (int64_t)(k + 1) * nseg / 8; }
-  __device__ __forceinline__ unsigned take(int k, int lane) const {
-    unsigned t = 0;
-    if (lane == 0) t = atomicAdd(&ctr[64 * k], 1u);
-    return __builtin_amdgcn_readfirstlane(t);
-  }
-  // resolve a ticket of share k; on exhaustion scan the other shares
-  __device__ __forceinline__ int64_t resolve(int k, unsigned t, int lane) const {
-    if (lo(k) + t < hi(k)) return lo(k) + t;
-    for (int d = 1; d < 8; ++d) {
-      const int kk = (k + d) & 7;
-      const unsigned seen = __builtin_amdgcn_readfirstlane(__atomic_load_n(&ctr[64 * kk], __ATOMIC_RELAXED));
-      if (lo(kk) + seen >= hi(kk)) continue;
-      const unsigned tt = take(kk, lane);
-      if (lo(kk) + tt < hi(kk)) return lo(kk) + tt;
-    }
-    return -1;
-  }
-};
-
-// WPB waves per workgroup share one LDS copy of the basis (TAB_LDS) — or read it
-// through the cache (TAB_LDS = false: LDS then holds only the bins); MINB is the
-// occupancy floor handed to the register allocator (waves per SIMD).
-// PROBE (timing only, results invalid): 1 = contraction without the QI stores,
-// 2 = no contraction (dc only).
-template <int MAXSLOT, int LOADS, bool NT, int WPB = 4, int MINB = 1, bool TAB_LDS = true, int HB = kHarmBlock,
-          int PROBE = 0, bool ROWS = false, bool DYN = false>
-__global__ __launch_bounds__(64 * WPB, MINB) void demod_bins_kernel(
+// One wavefront per segment (grid-stride over a persistent grid of 4-wave
+// workgroups that share one LDS copy of the basis); each wave's L bins follow the
+// basis in LDS. LOADS 1-KB chunk loads per lane in flight (non-temporal: the input
+// is read once). ROWS selects the output layout (fold_finish).
+// spacer > 0: the LAST `spacer` workgroups take no segments and exit at once, so
+// a seed wave (seed.h) that was dispatched first and holds part of a CU costs
+// only idle workgroups, never segments that would wait behind it.
+// probe (diagnostics, may be null): s_memrealtime at the entry of workgroups 0 and
+// gridDim-1 and at the exit of workgroup 0's wave 0 ([3], [4], [5]).
+template <int MAXSLOT, int LOADS, bool ROWS>
+__global__ __launch_bounds__(kBlockThreads) void demod_bins_kernel(
     const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
-    const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc,
-    unsigned* __restrict__ ctr, int spacer, uint64_t* __restrict__ probe) {
-  // probe (diagnostics, may be null): s_memrealtime at entry of workgroups 0 and
-  // gridDim-1, and at the exit of workgroup 0's wave 0
+    const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc, int spacer,
+    uint64_t* __restrict__ probe) {
   if (probe && threadIdx.x == 0) {
     if (blockIdx.x == 0) probe[3] = __builtin_amdgcn_s_memrealtime();
     if (blockIdx.x == gridDim.x - 1) probe[4] = __builtin_amdgcn_s_memrealtime();
   }
-  // spacer > 0: the LAST `spacer` workgroups (8 = one per XCD under round-robin
-  // placement: a queued workgroup only takes a slot on the XCD it was sent to) take
-  // no segments and exit at once. A seed wave (seed.h) launched on another stream
-  // either finds their slot (this kernel dispatched first) or occupies a slot one of
-  // them would have needed (seed dispatched first) — either way no segment waits
-  // behind the seed.
   const int nwork = (int)gridDim.x - spacer;
   if ((int)blockIdx.x >= nwork) return;
   extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
-  const int ntab = TAB_LDS ? 2 * ndata * L : 0;
-  if constexpr (TAB_LDS) {
-    for (int i = threadIdx.x; i < ntab; i += 64 * WPB) lds_dyn[i] = tab[i];
-    __syncthreads();
-  }
-  const double* __restrict__ T = TAB_LDS ? lds_dyn : tab;
+  const int ntab = 2 * ndata * L;
+  for (int i = threadIdx.x; i < ntab; i += kBlockThreads) lds_dyn[i] = tab[i];
+  __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   double* __restrict__ ybin = lds_dyn + ntab + wave * L;  // this wave's L phase bins
@@ -578,141 +413,10 @@ __global__ __launch_bounds__(64 * WPB, MINB) void demod_bins_kernel(
     pbase[j] = 2 * (lane + 64 * j);
     pval[j] = (j < nslot) && (pbase[j] < L);
   }
-  if constexpr (DYN) {
-    const SegQueue q{ctr, nseg};
-    const int home = blockIdx.x & 7;
-    int64_t s = q.resolve(home, q.take(home, lane), lane);
-    while (s >= 0) {
-      const unsigned next = q.take(home, lane);  // in flight while the segment is processed
-      bins_segment<MAXSLOT, LOADS, NT, HB, PROBE, ROWS>(x + s * seg_stride, R, L, ndata, T, ybin, lane, pval, pbase,
-                                                         qi, qi_ld, s, dc);
-      s = q.resolve(home, next, lane);
-    }
-  } else {
-    for (int64_t s = (int64_t)blockIdx.x * WPB + wave; s < nseg; s += (int64_t)nwork * WPB)
-      bins_segment<MAXSLOT, LOADS, NT, HB, PROBE, ROWS>(x + s * seg_stride, R, L, ndata, T, ybin, lane, pval, pbase,
-                                                         qi, qi_ld, s, dc);
-  }
+  for (int64_t s = (int64_t)blockIdx.x * kWavesPerBlock + wave; s < nseg; s += (int64_t)nwork * kWavesPerBlock)
+    bins_segment<MAXSLOT, LOADS, true, kHarmBlock, ROWS>(x + s * seg_stride, R, L, ndata, lds_dyn, ybin, lane, pval,
+                                                           pbase, qi, qi_ld, s, dc);
   if (probe && threadIdx.x == 0 && blockIdx.x == 0) probe[5] = __builtin_amdgcn_s_memrealtime();
-}
-
-// Pipelined variant of demod_bins_kernel: a wave's work is one flat sequence of
-// chunks over its segments (NC = ceil(R / 128) chunks per segment, the last one
-// lane-masked), loaded UNR chunks at a time into two register buffers; batch
-// b+1 is in flight while batch b is added into the bins, including while a
-// finished segment is contracted, so the wave's memory pipe never drains
-// (demod_bins_kernel waits for its whole batch and then computes with nothing
-// in flight). Loads are unconditional — past the wave's last chunk they read
-// `pad`, a small dummy buffer — so the compiler's waitcnt merge keeps them in
-// flight. Requires R even (whole 16-B pairs); bit-identical to demod_bins_kernel.
-template <int MAXSLOT, int UNR, bool NT>
-__global__ __launch_bounds__(kBlockThreads) void demod_bins_pipe_kernel(
-    const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
-    const double* __restrict__ tab, const double* __restrict__ pad, double* __restrict__ qi, int64_t qi_ld,
-    double* __restrict__ dc) {
-  extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
-  const int ntab = 2 * ndata * L;
-  for (int i = threadIdx.x; i < ntab; i += kBlockThreads) lds_dyn[i] = tab[i];
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t W = (int64_t)gridDim.x * kWavesPerBlock;
-  const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wave;
-  if (gw >= nseg) return;
-  double* __restrict__ ybin = lds_dyn + ntab + wave * L;
-  const int nslot = (L + 127) / 128;
-  int pbase[MAXSLOT];
-  bool pval[MAXSLOT];
-#pragma unroll
-  for (int j = 0; j < MAXSLOT; ++j) {
-    pbase[j] = 2 * (lane + 64 * j);
-    pval[j] = (j < nslot) && (pbase[j] < L);
-  }
-  typedef double d2v __attribute__((ext_vector_type(2)));
-  auto zero_bins = [&]() {
-#pragma unroll
-    for (int j = 0; j < MAXSLOT; ++j)
-      if (pval[j]) *reinterpret_cast<d2v*>(ybin + pbase[j]) = d2v{0.0, 0.0};
-  };
-  const int NC = (R + 127) >> 7;             // chunks per segment
-  const int tail = R - ((NC - 1) << 7);      // valid samples of the last chunk (even, 2..128)
-  const bool tail_ok = 2 * lane < tail;      // this lane's pair is valid in the last chunk
-  const int64_t nmine = (nseg - 1 - gw) / W + 1;
-  const int64_t G = nmine * NC;              // chunks of this wave
-
-  // load cursor (wave-uniform)
-  int64_t lgi = 0, lseg = gw;
-  int lc = 0;
-  auto next_ptr = [&]() -> const double* {
-    const double* p;
-    if (lgi < G) {
-      const bool last = (lc == NC - 1);
-      p = x + lseg * seg_stride + ((last && !tail_ok) ? 0 : (lc << 7)) + 2 * lane;
-    } else {
-      p = pad + 2 * lane;
-    }
-    ++lgi;
-    if (++lc == NC) {
-      lc = 0;
-      lseg += W;
-    }
-    return p;
-  };
-  // consume cursor
-  int64_t cseg = gw;
-  int cc = 0, p0 = 0;
-  auto consume = [&](const double (&v)[2]) {
-    if (cc < NC - 1 || tail_ok) {
-      int p = p0 + 2 * lane;
-      if (p >= L) p -= L;
-      d2v* yp = reinterpret_cast<d2v*>(ybin + p);
-      d2v t = *yp;
-      t.x += v[0];
-      t.y += v[1];
-      *yp = t;
-    }
-    p0 += 128;
-    if (p0 >= L) p0 -= L;
-    if (++cc == NC) {
-      double y[MAXSLOT][2];
-#pragma unroll
-      for (int j = 0; j < MAXSLOT; ++j) {
-        if (pval[j]) {
-          const d2v t = *reinterpret_cast<const d2v*>(ybin + pbase[j]);
-          y[j][0] = t.x;
-          y[j][1] = t.y;
-        } else {
-          y[j][0] = y[j][1] = 0.0;
-        }
-      }
-      fold_finish<2, MAXSLOT>(y, pval, pbase, R, L, ndata, lds_dyn, lane, qi, qi_ld, cseg, dc);
-      zero_bins();
-      cc = 0;
-      p0 = 0;
-      cseg += W;
-    }
-  };
-  auto load_batch = [&](double (&v)[UNR][2]) {
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const double* p = next_ptr();
-      if constexpr (NT) VecT<2>::load_nt(p, v[u]);
-      else VecT<2>::load(p, v[u]);
-    }
-  };
-  zero_bins();
-  double A[UNR][2], B[UNR][2];
-  load_batch(A);
-  for (int64_t g = 0; g < G; g += 2 * UNR) {
-    load_batch(B);
-#pragma unroll
-    for (int u = 0; u < UNR; ++u)
-      if (g + u < G) consume(A[u]);
-    load_batch(A);
-#pragma unroll
-    for (int u = 0; u < UNR; ++u)
-      if (g + UNR + u < G) consume(B[u]);
-  }
 }
 
 // Fallback when no short integer period exists: per-sample angles

@@ -52,9 +52,7 @@ struct DeviceState {
   std::map<std::tuple<int, int, uint64_t>, DevBuf> basis;            // (L, ndata, w0 bits)
   std::map<std::tuple<int, uint64_t, uint64_t, uint64_t>, DevBuf> gridtab;  // (ndata, min, max, step)
   hipStream_t side = nullptr;  // seed step runs here, concurrently with the bulk demod
-  hipEvent_t ev_in = nullptr, ev_seed = nullptr;
-  uint64_t* seed_ctr = nullptr;  // seed -> bulk LM hand-off: [0] monotonic counter, [8..] seeds (lm.h)
-  uint64_t seed_total = 0;       // seeds issued so far (the LM's wait target)
+  hipEvent_t ev_in = nullptr, ev_seed = nullptr, ev_bulk = nullptr;
 };
 
 std::map<int, DeviceState> g_dev;
@@ -85,8 +83,7 @@ int ensure_init(int* dev_out) {
     HIPCHK(hipStreamCreateWithPriority(&ds.side, hipStreamNonBlocking, prio_hi));
     HIPCHK(hipEventCreateWithFlags(&ds.ev_in, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ds.ev_seed, hipEventDisableTiming));
-    HIPCHK(hipMalloc(&ds.seed_ctr, 512));
-    HIPCHK(hipMemset(ds.seed_ctr, 0, 512));
+    HIPCHK(hipEventCreateWithFlags(&ds.ev_bulk, hipEventDisableTiming));
     ds.init = true;
   }
   *dev_out = dev;
@@ -193,44 +190,29 @@ int to_lmconst(const dfmi_lm_config* cfg, dfmi::LMConst* c) {
 
 constexpr int kMaxSlotCap = 8;
 
-// Tuning knobs (dfmi_set_tuning): measured, then frozen as defaults.
+// Tuning knobs (dfmi_set_tuning): measured, then frozen as defaults. Results do
+// not depend on them, except seed_bins (the seed's fold summation order: fits move
+// by < 1e-10).
 struct Tuning {
-  int demod_loads = 8;         // vector loads in flight per lane (8 or 16)
-  int demod_nt = 1;            // non-temporal stream loads (measured +14 %, profiles/r01_tune_demod.json)
+  int demod_loads = 8;         // fold kernel: vector loads in flight per lane (8 or 16)
+  int demod_nt = 1;            // fold kernel: non-temporal loads (+14 %, profiles/r01_tune_demod.json)
   int demod_blocks_per_cu = 0; // 0 = occupancy limit
   int lm_general = 0;          // 1: force the two-pass (general) LM path for every ndata
-  int demod_kernel = 2;        // 0: cycle-aligned fold, 1: software-pipelined cycle-aligned fold
-                               // (measured slower: profiles/r01_tune_demod_stream.json), 2: bins in LDS,
-                               // 3: bins in LDS, pipelined
-  int demod_unr = 4;           // cycles per batch of the streaming fold (1, 2, 4, 5)
-  int seed_reserve = 0;        // 1: the bulk demodulation grid leaves slots free for the seed waves
-  int demod_dyn = 0;           // 1: dynamic segment scheduling in the bin kernel (demod.h SegQueue;
-                               // measured 10 % slower: profiles/r01b_tune_step_dyn_seed.json)
-  int seed_spacer = 0;         // 1: bulk demodulation leaves a slot for the seed wave (g_spacer; measured
-                               // slower: the 8-wave workgroups cost more than the seed gains)
-  int seed_handoff = 1;        // 1: seed -> bulk LM hand-off through a device counter (lm.h seed_ctr)
-  int seed_handoff_unreachable = 0;  // test hook: a target the counter never reaches (LM fallback path)
+  int demod_kernel = 1;        // 1: bin-in-LDS kernel where it applies, 0: cycle-aligned fold kernel
   int seed_bins = 1;           // 1: seed step with the LDS fold + LDS-resident QI (seed.h seed_bins_kernel)
-  int demod_bins_cfg = 0;      // bins kernel shape: 0 = 4-wave blocks, LDS basis, 8 harmonics per
-                               // reduction block; 1..6 = higher-occupancy shapes (launch_bins_t);
-                               // 7, 8 = timing probes (no QI stores / no contraction: results invalid)
+  int seed_order = 1;          // 1: seed on the caller's stream, bulk demodulation on the side stream
 };
 Tuning g_tune;
-std::string g_last_demod;
-int g_spacer = 0;
-uint64_t* g_probe = nullptr;  // diagnostics timestamps (dfmi_set_tuning("probe", 1), dfmi_probe_read)  // bin kernel: 8-wave workgroups + an idle last workgroup (seed co-scheduling)
-// Workgroup slots a persistent demodulation grid leaves free (set by the record
-// pipeline for the concurrent seed waves; every launcher subtracts it).
-int64_t g_grid_reserve = 0;
+std::string g_last_demod;     // kernel variant of the last demodulation launch (dfmi_last_demod_kernel)
+int g_idle_blocks = 0;        // bin kernel: trailing workgroups that take no segments (seed_order 1)
+uint64_t* g_probe = nullptr;  // diagnostics timestamps (dfmi_set_tuning("probe", 1), dfmi_probe_read)
 
 int64_t persistent_grid(int n_cu, int per_cu, int64_t need) {
-  int64_t grid = (int64_t)n_cu * per_cu - g_grid_reserve;
+  int64_t grid = (int64_t)n_cu * per_cu;
   if (grid > need) grid = need;
   if (grid < 1) grid = 1;
   return grid;
-}  // kernel variant of the last demodulation launch (dfmi_last_demod_kernel)
-
-
+}
 
 int32_t detect_period_impl(double w0, int32_t R, int32_t ndata) {
   if (!(w0 > 0) || R <= 0 || ndata <= 0) return 0;
@@ -284,171 +266,47 @@ int launch_fold_ms(int ms, const double* x, int64_t nseg, int64_t stride, int R,
   }
 }
 
-template <int UNR>
-int launch_stream_t(int dev, const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata,
-                    const double* tab, double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu) {
-  constexpr int MINB = UNR <= 2 ? 4 : 3;
-  const size_t lds = (size_t)2 * ndata * L * sizeof(double);
-  auto kern = dfmi::demod_stream_kernel<2, UNR, true, MINB>;
-  void* pad = nullptr;
-  int rc = workspace(dev, "stream_pad", ((size_t)UNR * L + 256) * sizeof(double), &pad);
-  if (rc) return rc;
+template <int MS, bool ROWS>
+int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tab,
+                  double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu, size_t lds) {
+  auto kern = dfmi::demod_bins_kernel<MS, 8, ROWS>;
   int per_cu = 0;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, dfmi::kBlockThreads, lds));
   if (per_cu < 1) per_cu = 1;
   if (g_tune.demod_blocks_per_cu > 0 && g_tune.demod_blocks_per_cu < per_cu) per_cu = g_tune.demod_blocks_per_cu;
-  const int64_t grid = persistent_grid(n_cu, per_cu, (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock);
+  const int spacer = g_idle_blocks;  // one of the grid's slots each (seed_order 1)
+  const int64_t grid =
+      persistent_grid(n_cu, per_cu, (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock + spacer);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(dfmi::kBlockThreads), lds, st, x, nseg, stride, R, L, ndata,
-                     tab, (const double*)pad, qi, qi_ld, dc);
+                     tab, qi, qi_ld, dc, (int)(spacer < grid ? spacer : 0), g_probe);
   HIPCHK(hipGetLastError());
-  g_last_demod = "demod_stream_kernel<2," + std::to_string(UNR) + ",1," + std::to_string(MINB) + ">";
+  g_last_demod = "demod_bins_kernel<" + std::to_string(MS) + ",8" + (ROWS ? ",rows" : "") +
+                 (spacer ? ",spacer" + std::to_string(spacer) : "") + ">";
   return DFMI_OK;
 }
 
-// Streaming fold (demod.h demod_stream_kernel) when its preconditions hold:
-// 16-B rows, 128 < L <= 256 (two 16-B slots per lane), R % L == 0, basis in LDS,
-// and a batch size dividing R / L. Returns 1 if it does not apply.
-int try_stream(int dev, const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tab,
-               double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu, bool vec2, bool use_lds) {
-  if (g_tune.demod_kernel != 1 || !vec2 || !use_lds || L <= 128 || L > 256 || R % L) return 1;
-  const int ncyc = R / L;
-  int unr = g_tune.demod_unr;
-  const int prefs[4] = {unr, 4, 2, 1};
-  for (int u : prefs) {
-    if (ncyc % u) continue;
-    switch (u) {
-      case 1: return launch_stream_t<1>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
-      case 2: return launch_stream_t<2>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
-      case 4: return launch_stream_t<4>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
-      case 5: return launch_stream_t<5>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
-      default: break;
-    }
-  }
-  return 1;
-}
-
-template <int MS, int LOADS, bool NT, int WPB = 4, int WPEU = 1, bool TAB_LDS = true, int HB = 8, int PROBE = 0,
-          bool ROWS = false, bool DYN = false>
-int launch_bins_t(int dev, const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tab,
-                  double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu, size_t lds_cap) {
-  if constexpr (!DYN) {  // dynamic segment scheduling (demod.h SegQueue) unless tuned off
-    if (g_tune.demod_dyn)
-      return launch_bins_t<MS, LOADS, NT, WPB, WPEU, TAB_LDS, HB, PROBE, ROWS, true>(dev, x, nseg, stride, R, L, ndata,
-                                                                                     tab, qi, qi_ld, dc, st, n_cu,
-                                                                                     lds_cap);
-  }
-  if constexpr (MS == 2 && LOADS == 8 && NT && WPB == 4 && WPEU == 1 && TAB_LDS && HB == 8 && PROBE == 0 && !ROWS &&
-                !DYN) {
-    switch (g_tune.demod_bins_cfg) {  // tunable shape
-      case 7: return launch_bins_t<2, 8, true, 4, 1, true, 8, 1>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-      case 8: return launch_bins_t<2, 8, true, 4, 1, true, 8, 2>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-      case 1: return launch_bins_t<2, 8, true, 8, 6, true, 4>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-      case 2: return launch_bins_t<2, 4, true, 8, 6, true, 4>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-      case 3: return launch_bins_t<2, 8, true, 16, 8, true, 2>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-      case 4: return launch_bins_t<2, 4, true, 16, 8, true, 2>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-      case 5: return launch_bins_t<2, 8, true, 4, 6, false, 4>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-      case 6: return launch_bins_t<2, 8, true, 4, 8, false, 2>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-      default: break;
-    }
-    if (g_tune.demod_loads == 16)
-      return launch_bins_t<2, 16, true>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-    if (!g_tune.demod_nt)
-      return launch_bins_t<2, 8, false>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-  }
-  if constexpr (ROWS && !DYN && WPB == 4 && MS == 2 && LOADS == 8 && NT && WPEU == 1 && TAB_LDS && HB == 8 &&
-                PROBE == 0) {
-    // With a seed wave co-scheduled (nls_record_device), 8-wave workgroups (2 waves
-    // per SIMD, 2 per CU): the spacer's slot is 2 x 128 VGPRs per SIMD + 45 KB LDS,
-    // enough for the seed kernel (161 VGPRs, 34 KB); a 4-wave workgroup's is not.
-    if (g_spacer)
-      return launch_bins_t<2, 8, true, 8, 1, true, 8, 0, true>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc,
-                                                               st, n_cu, lds_cap);
-  }
-  const size_t lds = ((TAB_LDS ? (size_t)2 * ndata * L : 0) + (size_t)WPB * L) * sizeof(double);
-  if (lds > lds_cap) return fail(DFMI_ERR_UNSUPPORTED, "demod_bins_kernel: LDS footprint exceeds the workgroup limit");
-  auto kern = dfmi::demod_bins_kernel<MS, LOADS, NT, WPB, WPEU, TAB_LDS, HB, PROBE, ROWS, DYN>;
-  unsigned* ctr = nullptr;
-  if constexpr (DYN) {
-    void* cw = nullptr;
-    int rc = workspace(dev, "seg_queue", 8 * 64 * sizeof(unsigned), &cw);
-    if (rc) return rc;
-    ctr = (unsigned*)cw;
-    HIPCHK(hipMemsetAsync(ctr, 0, 8 * 64 * sizeof(unsigned), st));
-  }
-  int per_cu = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WPB, lds));
-  if (per_cu < 1) per_cu = 1;
-  if (g_tune.demod_blocks_per_cu > 0 && g_tune.demod_blocks_per_cu < per_cu) per_cu = g_tune.demod_blocks_per_cu;
-  const int spacer = (g_spacer && !DYN) ? 8 : 0;
-  const int64_t grid = persistent_grid(n_cu, per_cu, (nseg + WPB - 1) / WPB + spacer);  // spacer: one of the slots
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * WPB), lds, st, x, nseg, stride, R, L, ndata, tab, qi,
-                     qi_ld, dc, ctr, spacer, g_probe);
-  HIPCHK(hipGetLastError());
-  g_last_demod = "demod_bins_kernel<" + std::to_string(MS) + "," + std::to_string(LOADS) + "," +
-                 std::to_string((int)NT) + "," + std::to_string(WPB) + "," + std::to_string(WPEU) + "," +
-                 std::to_string((int)TAB_LDS) + "," + std::to_string(HB) + (ROWS ? ",rows" : "") +
-                 (DYN ? ",dyn" : "") + (spacer ? ",spacer" : "") + ">";
-  return DFMI_OK;
-}
-
-template <int MS, int UNR>
-int launch_bins_pipe_t(int dev, const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata,
-                       const double* tab, double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu,
-                       size_t lds) {
-  auto kern = g_tune.demod_nt ? dfmi::demod_bins_pipe_kernel<MS, UNR, true> : dfmi::demod_bins_pipe_kernel<MS, UNR, false>;
-  void* pad = nullptr;
-  int rc = workspace(dev, "bins_pad", 256 * sizeof(double), &pad);
-  if (rc) return rc;
-  int per_cu = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, dfmi::kBlockThreads, lds));
-  if (per_cu < 1) per_cu = 1;
-  if (g_tune.demod_blocks_per_cu > 0 && g_tune.demod_blocks_per_cu < per_cu) per_cu = g_tune.demod_blocks_per_cu;
-  const int64_t grid = persistent_grid(n_cu, per_cu, (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock);
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(dfmi::kBlockThreads), lds, st, x, nseg, stride, R, L, ndata,
-                     tab, (const double*)pad, qi, qi_ld, dc);
-  HIPCHK(hipGetLastError());
-  g_last_demod = "demod_bins_pipe_kernel<" + std::to_string(MS) + "," + std::to_string(UNR) + "," +
-                 std::to_string(g_tune.demod_nt) + ">";
-  return DFMI_OK;
-}
-
-// Bin-in-LDS fold (demod.h demod_bins_kernel) when its preconditions hold:
-// 16-B rows, even L with 128 <= L <= 1024, basis + 4 waves' bins in LDS.
-// Returns 1 if it does not apply.
-bool bins_applicable(bool vec2, int R, int L, int ndata, size_t lds_cap) {
-  (void)R;
-  if ((g_tune.demod_kernel != 2 && g_tune.demod_kernel != 3) || !vec2 || (L & 1) || L < 128 || L > 1024) return false;
+// The bin-in-LDS kernel (demod.h demod_bins_kernel) applies to 16-B rows, an even
+// basis period 128 <= L <= 1024, and a basis + 4 waves' bins that fit in LDS.
+bool bins_applicable(bool vec2, int L, int ndata, size_t lds_cap) {
+  if (g_tune.demod_kernel != 1 || !vec2 || (L & 1) || L < 128 || L > 1024) return false;
   const size_t lds = ((size_t)2 * ndata * L + (size_t)dfmi::kWavesPerBlock * L) * sizeof(double);
   return lds <= lds_cap && lds <= 64 * 1024;
 }
 
-int try_bins(int dev, const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tab,
-             double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu, bool vec2, size_t lds_cap,
-             bool rows) {
-  if (!bins_applicable(vec2, R, L, ndata, lds_cap)) return 1;
+// Returns 1 if the bin kernel does not apply.
+int try_bins(const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tab, double* qi,
+             int64_t qi_ld, double* dc, hipStream_t st, int n_cu, bool vec2, size_t lds_cap, bool rows) {
+  if (!bins_applicable(vec2, L, ndata, lds_cap)) return 1;
   const size_t lds = ((size_t)2 * ndata * L + (size_t)dfmi::kWavesPerBlock * L) * sizeof(double);
   const int nslot = (L + 127) / 128;
   if (rows) {
-    if (nslot <= 2)
-      return launch_bins_t<2, 8, true, 4, 1, true, 8, 0, true>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st,
-                                                               n_cu, lds_cap);
-    if (nslot <= 4)
-      return launch_bins_t<4, 8, true, 4, 1, true, 8, 0, true>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st,
-                                                               n_cu, lds_cap);
-    return launch_bins_t<8, 8, true, 4, 1, true, 8, 0, true>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st,
-                                                             n_cu, lds_cap);
+    if (nslot <= 2) return launch_bins_t<2, true>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds);
+    if (nslot <= 4) return launch_bins_t<4, true>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds);
+    return launch_bins_t<8, true>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds);
   }
-  if (g_tune.demod_kernel == 3 && (R % 2) == 0) {
-    if (nslot <= 2)
-      return g_tune.demod_unr == 8
-                 ? launch_bins_pipe_t<2, 8>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds)
-                 : launch_bins_pipe_t<2, 4>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds);
-    if (nslot <= 4) return launch_bins_pipe_t<4, 4>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds);
-    return launch_bins_pipe_t<8, 4>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds);
-  }
-  if (nslot <= 2) return launch_bins_t<2, 8, true>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-  if (nslot <= 4) return launch_bins_t<4, 8, true>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
-  return launch_bins_t<8, 8, true>(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds_cap);
+  if (nslot <= 2) return launch_bins_t<2, false>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds);
+  if (nslot <= 4) return launch_bins_t<4, false>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds);
+  return launch_bins_t<8, false>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds);
 }
 
 // Whether demod_device can write the row layout (dfmi_qi_row_stride) for this
@@ -458,7 +316,7 @@ bool rows_supported(int dev, const double* x, int64_t stride, int R, int ndata, 
   if (L == 0) L = detect_period_impl(w0, R, ndata);
   if (L <= 0) return false;
   const bool vec2 = (L % 2 == 0) && (stride % 2 == 0) && (((uintptr_t)x & 15) == 0);
-  return bins_applicable(vec2, R, L, ndata, g_dev[dev].lds_per_block);
+  return bins_applicable(vec2, L, ndata, g_dev[dev].lds_per_block);
 }
 
 // Device-pointer demodulation (all pointers on the current device).
@@ -485,12 +343,9 @@ int demod_device(int dev, const double* x, int64_t nseg, int64_t stride, int R, 
       if (rc) return rc;
       const size_t lds = (size_t)2 * ndata * L * sizeof(double);
       const bool use_lds = lds <= 64 * 1024 && lds <= ds.lds_per_block;
-      rc = try_bins(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, ds.n_cu, vec2, ds.lds_per_block,
-                    rows);
+      rc = try_bins(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, ds.n_cu, vec2, ds.lds_per_block, rows);
       if (rc <= 0) return rc;
       if (rows) return fail(DFMI_ERR_UNSUPPORTED, "row layout needs the bin-in-LDS demodulation kernel");
-      rc = try_stream(dev, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, ds.n_cu, vec2, use_lds);
-      if (rc <= 0) return rc;
       if (vec2) {
         return use_lds ? launch_fold_ms<2, true>(ms, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, ds.n_cu)
                        : launch_fold_ms<2, false>(ms, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, ds.n_cu);
@@ -515,8 +370,8 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
               int64_t nitems, int64_t nchunk, const double* guess_dev, int64_t g_rec, int64_t g_comp,
               const double* guess_host /* nrec*4, used when nrec <= 8 and guess_dev == null */,
               const dfmi::LMConst& c, const double* jtab, double* out, int64_t out_ld, int32_t* status,
-              hipStream_t st, bool rows = false, const uint64_t* seed_ctr = nullptr, uint64_t seed_target = 0,
-              const double* seed_init_host = nullptr) {
+              hipStream_t st, bool rows = false) {
+  (void)dev;
   if (nrec == 0 || nitems == 0) return DFMI_OK;
   if (nchunk < 1) nchunk = 1;
   if (nchunk > nitems) nchunk = nitems;  // np.array_split chunks beyond nitems are empty
@@ -528,11 +383,6 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
     for (int64_t r = 0; r < nrec; ++r)
       for (int i = 0; i < 4; ++i) ginl.v[r][i] = guess_host[r * 4 + i];
     use_inline = 1;
-  }
-  if (seed_ctr) {  // fallback seeds (lm.h): the records' initial guesses
-    if (nrec > 8) return fail(DFMI_ERR_ARG, "device seed hand-off supports at most 8 records");
-    for (int64_t r = 0; r < nrec; ++r)
-      for (int i = 0; i < 4; ++i) ginl.v[r][i] = seed_init_host[r * 4 + i];
   }
   const int64_t lanes = nrec * nchunk;
   const int block = 64;
@@ -555,8 +405,7 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
     if (nd_sel <= 16) lds = (size_t)qi_ld * 65 * sizeof(double);  // the wave's rows, transposed
   }
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(block), lds, st, qi, qi_ld, ndata, nrec, nbuf, first, nitems,
-                     nchunk, guess_dev, g_rec, g_comp, ginl, use_inline, jtab, c, out, out_ld, status, seed_ctr,
-                     seed_target);
+                     nchunk, guess_dev, g_rec, g_comp, ginl, use_inline, jtab, c, out, out_ld, status);
   HIPCHK(hipGetLastError());
   return DFMI_OK;
 }
@@ -593,15 +442,22 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
     for (int64_t r = 0; r < nrec; ++r)
       for (int i = 0; i < 4; ++i) ginl.v[r][i] = init_guess_host[r * 4 + i];
 
-  int64_t reserve = 0;  // persistent-grid slots left free for the seed waves
-  bool spacer = false;  // bin kernel with an idle workgroup slot for the seed wave
-  bool handoff = false; // seed -> LM through ds.seed_ctr (no stream event)
+  // Row layout (one 128-B line per 8 harmonics, dc inside the row: full-line
+  // stores) for the chunk-size-1 parallel path when the bin kernel applies;
+  // component-major QI otherwise (warm-start chains read QI component-major).
+  const bool rows = parallel && (nbuf <= 1 || nchunk >= nbuf - 1) &&
+                    (nrec == 1 || (rec_stride % 2) == 0) && rows_supported(dev, x, R, R, ndata, w0, period);
+  hipStream_t bulk = st;  // stream of the bulk demodulation
+  bool seed_first = false;
   if (parallel) {
-    // seed step (buffer 0 of every record) on the side stream, concurrently with the
-    // bulk demodulation. The bulk grid leaves one workgroup slot (one wave slot on
-    // each of a CU's 4 SIMDs) per 4 seed waves, so the seed is resident from the start
-    // instead of waiting for the whole demodulation to drain (seed dispatched second)
-    // or holding back demod blocks (seed dispatched first): profiles/r01b_seed_timeline.txt.
+    // Seed step (buffer 0 of every record, fitters.py:403-410) concurrently with the
+    // bulk demodulation. seed_order 1 (default): the seed kernel goes on the caller's
+    // stream, where it dispatches as soon as the previous work drains, and the bulk
+    // demodulation on the side stream behind an event wait — so the seed wave is
+    // resident first instead of queueing for a slot until the persistent
+    // demodulation drains (profiles/r01b_seed_probe.json); the bulk grid's last
+    // workgroups idle where the seed displaced them, and the LM follows the seed in
+    // stream order. seed_order 0: seed on the side stream, LM waits on its event.
     int L = period;
     if (L == 0) L = detect_period_impl(w0, R, ndata);
     if (L > 64 * 16) L = 0;
@@ -610,13 +466,15 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
     void *qs, *ds_;
     if ((rc = workspace(dev, "qi_seed", (size_t)2 * ndata * nrec * 8, &qs))) return rc;
     if ((rc = workspace(dev, "dc_seed", (size_t)nrec * 8, &ds_))) return rc;
+    const bool seed_bins = rows && L > 0 && g_tune.seed_bins;
+    seed_first = seed_bins && g_tune.seed_order == 1;
     HIPCHK(hipEventRecord(ds.ev_in, st));
     HIPCHK(hipStreamWaitEvent(ds.side, ds.ev_in, 0));
-    const bool seed_bins = L > 0 && g_tune.seed_bins && rows_supported(dev, x, R, R, ndata, w0, period) &&
-                           (nrec == 1 || (rec_stride % 2) == 0);
-    // device-side seed hand-off to the bulk LM (lm.h seed_ctr) instead of ev_seed
-    handoff = seed_bins && g_tune.seed_handoff && nrec <= 8 && nbuf > 1 && nchunk >= nbuf - 1;
-    if (handoff) ds.seed_total += (uint64_t)nrec;
+    hipStream_t sst = ds.side;
+    if (seed_first) {
+      sst = st;
+      bulk = ds.side;
+    }
     if (seed_bins) {  // fold into LDS, QI from LDS in the fit (seed.h seed_bins_kernel)
       const int nslot = (L + 127) / 128;
       const size_t lds = ((size_t)2 * ndata * L + L + dfmi_row_stride(ndata)) * sizeof(double);
@@ -626,51 +484,48 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
                                                                                      : dfmi::seed_bins_kernel<16, 8>)
                             : (nslot <= 2 ? dfmi::seed_bins_kernel<0, 2> : nslot <= 4 ? dfmi::seed_bins_kernel<0, 4>
                                                                                     : dfmi::seed_bins_kernel<0, 8>);
-      hipLaunchKernelGGL(sk, dim3((unsigned)nrec), dim3(64), lds, ds.side, x, rec_stride, R, L, ndata, tab, gdev, ginl,
-                         gdev ? 0 : 1, jtab, c, out, out_ld, nbuf, fitok, handoff ? ds.seed_ctr : nullptr, g_probe);
+      hipLaunchKernelGGL(sk, dim3((unsigned)nrec), dim3(64), lds, sst, x, rec_stride, R, L, ndata, tab, gdev, ginl,
+                         gdev ? 0 : 1, jtab, c, out, out_ld, nbuf, fitok, g_probe);
     } else {
       auto sk = ndata <= 12 ? dfmi::seed_kernel<12> : ndata <= 16 ? dfmi::seed_kernel<16> : dfmi::seed_kernel<0>;
-      hipLaunchKernelGGL(sk, dim3((unsigned)nrec), dim3(64), 0, ds.side, x, rec_stride, R, L, ndata, w0, tab,
-                         (double*)qs, (double*)ds_, nrec, gdev, ginl, gdev ? 0 : 1, jtab, c, out, out_ld, nbuf, fitok,
-                         nullptr);
+      hipLaunchKernelGGL(sk, dim3((unsigned)nrec), dim3(64), 0, sst, x, rec_stride, R, L, ndata, w0, tab,
+                         (double*)qs, (double*)ds_, nrec, gdev, ginl, gdev ? 0 : 1, jtab, c, out, out_ld, nbuf, fitok);
     }
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(ds.ev_seed, ds.side));
-    if (g_tune.seed_reserve) reserve = (nrec + 3) / 4 < 64 ? (nrec + 3) / 4 : 64;
-    spacer = seed_bins && nrec == 1 && g_tune.seed_spacer;
+    HIPCHK(hipEventRecord(ds.ev_seed, sst));
   }
-  // Row layout (one 128-B line per 8 harmonics, dc inside the row: full-line
-  // stores) for the chunk-size-1 parallel path when the bin kernel applies;
-  // component-major QI otherwise (warm-start chains read QI component-major).
-  const bool rows = parallel && (nbuf <= 1 || nchunk >= nbuf - 1) &&
-                    (nrec == 1 || (rec_stride % 2) == 0) && rows_supported(dev, x, R, R, ndata, w0, period);
   const int64_t qs = rows ? dfmi_row_stride(ndata) : 0;
   if (rows) {
     void* rw = nullptr;
     if ((rc = workspace(dev, "qrow", (size_t)qs * nseg * sizeof(double), &rw))) return rc;
     qi = (double*)rw;
   }
-  g_grid_reserve = reserve;
-  g_spacer = spacer ? 1 : 0;
+  // seed_first: each seed wave (161 VGPRs on one SIMD) displaces two 4-wave bulk
+  // workgroups of its CU — the last ones sent to that XCD under round-robin
+  // placement: the last 2 per XCD per record idle instead of holding segments
+  g_idle_blocks = seed_first ? (int)(16 * nrec < 64 ? 16 * nrec : 64) : 0;
   if (rec_stride == nbuf * (int64_t)R) {
-    rc = rows ? demod_device(dev, x, nseg, R, R, ndata, w0, period, qi, qs, nullptr, st, true)
-              : demod_device(dev, x, nseg, R, R, ndata, w0, period, qi, nseg, dc, st);
+    rc = rows ? demod_device(dev, x, nseg, R, R, ndata, w0, period, qi, qs, nullptr, bulk, true)
+              : demod_device(dev, x, nseg, R, R, ndata, w0, period, qi, nseg, dc, bulk);
   } else {
     for (int64_t r = 0; r < nrec && rc == 0; ++r) {
       rc = rows ? demod_device(dev, x + r * rec_stride, nbuf, R, R, ndata, w0, period, qi + r * nbuf * qs, qs,
-                               nullptr, st, true)
+                               nullptr, bulk, true)
                 : demod_device(dev, x + r * rec_stride, nbuf, R, R, ndata, w0, period, qi + r * nbuf, nseg,
-                               dc + r * nbuf, st);
+                               dc + r * nbuf, bulk);
     }
   }
-  g_grid_reserve = 0;
-  g_spacer = 0;
+  g_idle_blocks = 0;
   if (rc) return rc;
+  if (bulk != st) {
+    HIPCHK(hipEventRecord(ds.ev_bulk, bulk));
+    HIPCHK(hipStreamWaitEvent(st, ds.ev_bulk, 0));
+  }
   if (!parallel) {
     return lm_device(dev, qi, nseg, ndata, nrec, nbuf, 0, nbuf, 1, gdev, 4, 1, init_guess_host, c, jtab, out, out_ld,
                      fitok, st);
   }
-  if (!(handoff && rows)) HIPCHK(hipStreamWaitEvent(st, ds.ev_seed, 0));
+  if (!seed_first) HIPCHK(hipStreamWaitEvent(st, ds.ev_seed, 0));
   if (nbuf <= 1) {
     if (rows)  // dc of the seed buffers (the LM kernel carries it otherwise)
       HIPCHK(hipMemcpy2DAsync(dc, nbuf * sizeof(double), qi + dfmi_row_dc(ndata), qs * nbuf * sizeof(double),
@@ -678,14 +533,26 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
     return DFMI_OK;
   }
   // the rest, seeded with each record's buffer-0 result (read on device: no host sync)
-  if (handoff && rows)
-    return lm_device(dev, qi, qs, ndata, nrec, nbuf, 1, nbuf - 1, nchunk, out, nbuf, out_ld, nullptr, c, jtab, out,
-                     out_ld, fitok, st, true, ds.seed_ctr,
-                     ds.seed_total + (g_tune.seed_handoff_unreachable ? (uint64_t)1 << 40 : 0), init_guess_host);
   return lm_device(dev, qi, rows ? qs : nseg, ndata, nrec, nbuf, 1, nbuf - 1, nchunk, out, nbuf, out_ld, nullptr, c,
                    jtab, out, out_ld, fitok, st, rows);
 }
 
+}  // namespace
+
+namespace {
+// key -> (knob, allowed values or empty = any value >= 0)
+struct Knob {
+  int* v;
+  std::vector<int> allowed;
+};
+const std::map<std::string, Knob>& knobs() {
+  static const std::map<std::string, Knob> k = {
+      {"demod_loads", {&g_tune.demod_loads, {8, 16}}},     {"demod_nt", {&g_tune.demod_nt, {0, 1}}},
+      {"demod_blocks_per_cu", {&g_tune.demod_blocks_per_cu, {}}}, {"lm_general", {&g_tune.lm_general, {0, 1}}},
+      {"demod_kernel", {&g_tune.demod_kernel, {0, 1}}},    {"seed_bins", {&g_tune.seed_bins, {0, 1}}},
+      {"seed_order", {&g_tune.seed_order, {0, 1}}}};
+  return k;
+}
 }  // namespace
 
 extern "C" {
@@ -734,20 +601,27 @@ int dfmi_probe_read(int64_t* out, int32_t n) {
   return DFMI_OK;
 }
 
+int dfmi_get_tuning(const char* key, int64_t* value) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_err.clear();
+  if (!key || !value) return fail(DFMI_ERR_ARG, "null argument");
+  const std::string k(key);
+  if (k == "probe") {
+    *value = g_probe ? 1 : 0;
+    return DFMI_OK;
+  }
+  auto it = knobs().find(k);
+  if (it == knobs().end()) return fail(DFMI_ERR_ARG, "unknown tuning key " + k);
+  *value = *it->second.v;
+  return DFMI_OK;
+}
+
 int dfmi_set_tuning(const char* key, int64_t value) {
   std::lock_guard<std::mutex> lk(g_mu);
   g_err.clear();
   if (!key) return fail(DFMI_ERR_ARG, "null key");
   const std::string k(key);
-  if (k == "demod_loads") {
-    if (value != 8 && value != 16) return fail(DFMI_ERR_ARG, "demod_loads must be 8 or 16");
-    g_tune.demod_loads = (int)value;
-  } else if (k == "demod_kernel") {
-    if (value < 0 || value > 3) return fail(DFMI_ERR_ARG, "demod_kernel must be 0..3");
-    g_tune.demod_kernel = (int)value;
-  } else if (k == "seed_bins") {
-    g_tune.seed_bins = value ? 1 : 0;
-  } else if (k == "probe") {
+  if (k == "probe") {
     if (value && !g_probe) {
       int dev;
       int rc = ensure_init(&dev);
@@ -759,33 +633,18 @@ int dfmi_set_tuning(const char* key, int64_t value) {
     } else if (!value) {
       g_probe = nullptr;
     }
-  } else if (k == "seed_handoff_unreachable") {
-    g_tune.seed_handoff_unreachable = value ? 1 : 0;
-  } else if (k == "seed_handoff") {
-    g_tune.seed_handoff = value ? 1 : 0;
-  } else if (k == "seed_spacer") {
-    g_tune.seed_spacer = value ? 1 : 0;
-  } else if (k == "demod_dyn") {
-    g_tune.demod_dyn = value ? 1 : 0;
-  } else if (k == "seed_reserve") {
-    g_tune.seed_reserve = value ? 1 : 0;
-  } else if (k == "demod_bins_cfg") {
-    if (value < 0 || value > 8) return fail(DFMI_ERR_ARG, "demod_bins_cfg must be 0..8 (7, 8: timing probes)");
-    g_tune.demod_bins_cfg = (int)value;
-  } else if (k == "demod_unr") {
-    if (value != 1 && value != 2 && value != 4 && value != 5 && value != 8)
-      return fail(DFMI_ERR_ARG, "demod_unr must be 1, 2, 4, 5 or 8");
-    g_tune.demod_unr = (int)value;
-  } else if (k == "demod_nt") {
-    g_tune.demod_nt = value ? 1 : 0;
-  } else if (k == "lm_general") {
-    g_tune.lm_general = value ? 1 : 0;
-  } else if (k == "demod_blocks_per_cu") {
-    if (value < 0) return fail(DFMI_ERR_ARG, "demod_blocks_per_cu < 0");
-    g_tune.demod_blocks_per_cu = (int)value;
-  } else {
-    return fail(DFMI_ERR_ARG, "unknown tuning key " + k);
+    return DFMI_OK;
   }
+  auto it = knobs().find(k);
+  if (it == knobs().end()) return fail(DFMI_ERR_ARG, "unknown tuning key " + k);
+  const Knob& kn = it->second;
+  if (value < 0 || value > (1 << 20)) return fail(DFMI_ERR_ARG, "tuning value out of range for " + k);
+  if (!kn.allowed.empty()) {
+    bool ok = false;
+    for (int a : kn.allowed) ok = ok || (a == value);
+    if (!ok) return fail(DFMI_ERR_ARG, "value not allowed for " + k);
+  }
+  *kn.v = (int)value;
   return DFMI_OK;
 }
 

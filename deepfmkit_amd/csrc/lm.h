@@ -538,7 +538,7 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
     const double* __restrict__ qi, int64_t qi_ld, int ndata, int64_t nrec, int64_t nbuf, int64_t first,
     int64_t nitems, int64_t nchunk, const double* __restrict__ guess, int64_t g_rec, int64_t g_comp,
     GuessInline ginl, int use_inline, const double* __restrict__ jtab, LMConst c, double* __restrict__ out,
-    int64_t out_ld, int32_t* __restrict__ status, const uint64_t* __restrict__ seed_ctr, uint64_t seed_target) {
+    int64_t out_ld, int32_t* __restrict__ status) {
   static_assert(!(ROWS && CHAIN), "row layout: chunk size 1 only");
   extern __shared__ double lds_q[];  // STAGE: [qi_ld][65]
   const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -575,49 +575,7 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
   }
   if (!valid) return;
   double p[4] = {0.0, 0.0, 0.0, 0.0};
-  if constexpr (ROWS) {
-    if (seed_ctr) {
-      // Device-side hand-off from the seed kernel on the side stream (seed.h): it
-      // stores each record's buffer-0 fit into seed_val (agent-coherent atomic
-      // stores) and then bumps *seed_ctr with release semantics. Waiting on the
-      // counter instead of a stream event avoids the ~30 us the cross-queue
-      // completion signal arrives late behind the bulk demodulation
-      // (profiles/r01b_seed_probe.json). Polling and the seed reads are relaxed
-      // agent-scope atomics: an acquire fence per wave (L2 invalidation) made the
-      // LM kernel 10-80 % slower. Bounded: if the seed has not landed within ~10 ms
-      // (it is normally done while the demodulation still runs), the wave computes
-      // the identical seed itself from the bulk row.
-      unsigned ready = 1;
-      if (threadIdx.x == 0) {
-        ready = 0;
-        for (int it = 0; it < 32768; ++it) {
-          if (__hip_atomic_load(seed_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= seed_target) {
-            ready = 1;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(8);
-        }
-      }
-      ready = __shfl(ready, 0);
-      if (ready) {
-        const double* sv = reinterpret_cast<const double*>(seed_ctr + 8) + r * 4;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) p[i] = __hip_atomic_load(sv + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-#pragma unroll
-        for (int rr = 0; rr < 8; ++rr)
-          if (r == rr)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) p[i] = ginl.v[rr][i];
-        double ssq;
-        const QRow<1> q0{qi + (r * nbuf) * qi_ld};
-        (void)fit_segment_q<NDMAX>(q0, ndata, jtab, c, p, ssq);
-      }
-      use_inline = 2;  // p holds the seed
-    }
-  }
-  if (use_inline == 2) {
-  } else if (use_inline) {
+  if (use_inline) {
 #pragma unroll
     for (int rr = 0; rr < 8; ++rr) {
       if (r == rr) {

@@ -21,7 +21,7 @@ __global__ __launch_bounds__(64) void seed_kernel(const double* __restrict__ x, 
                                                   const double* __restrict__ guess, GuessInline ginl, int use_inline,
                                                   const double* __restrict__ jtab, LMConst c,
                                                   double* __restrict__ out, int64_t out_ld, int64_t nbuf,
-                                                  int32_t* __restrict__ status, uint64_t* __restrict__ done_ctr) {
+                                                  int32_t* __restrict__ status) {
   const int64_t r = blockIdx.x;
   const int lane = threadIdx.x;
   const double* __restrict__ xs = x + r * rec_stride;
@@ -51,7 +51,6 @@ __global__ __launch_bounds__(64) void seed_kernel(const double* __restrict__ x, 
   out[3 * out_ld + sidx] = p[3];
   out[5 * out_ld + sidx] = ssq;
   status[sidx] = st;
-  if (done_ctr) __hip_atomic_fetch_add(done_ctr, (uint64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Seed step for inputs the bin kernel handles (16-B rows, even L in [128, 1024]):
@@ -68,8 +67,7 @@ __global__ __launch_bounds__(64) void seed_bins_kernel(const double* __restrict_
                                                        const double* __restrict__ guess, GuessInline ginl,
                                                        int use_inline, const double* __restrict__ jtab, LMConst c,
                                                        double* __restrict__ out, int64_t out_ld, int64_t nbuf,
-                                                       int32_t* __restrict__ status, uint64_t* __restrict__ done_ctr,
-                                                       uint64_t* __restrict__ probe) {
+                                                       int32_t* __restrict__ status, uint64_t* __restrict__ probe) {
   // probe (diagnostics, may be null): s_memrealtime (100 MHz) at entry, after the
   // fold, after the fit, written by record 0
   const uint64_t t_in = __builtin_amdgcn_s_memrealtime();
@@ -111,7 +109,7 @@ __global__ __launch_bounds__(64) void seed_bins_kernel(const double* __restrict_
     pbase[j] = 2 * (lane + 64 * j);
     pval[j] = (j < nslot) && (pbase[j] < L);
   }
-  bins_segment<MAXSLOT, 32, false, kHarmBlock, 0, true>(x + r * rec_stride, R, L, ndata, sh, ybin, lane, pval, pbase,
+  bins_segment<MAXSLOT, 32, false, kHarmBlock, true>(x + r * rec_stride, R, L, ndata, sh, ybin, lane, pval, pbase,
                                                         row, 0, 0, nullptr);
   __syncthreads();
   const uint64_t t_fold = __builtin_amdgcn_s_memrealtime();
@@ -140,14 +138,6 @@ __global__ __launch_bounds__(64) void seed_bins_kernel(const double* __restrict_
   out[4 * out_ld + sidx] = q.at(dfmi_row_dc(ndata));
   out[5 * out_ld + sidx] = ssq;
   status[sidx] = st;
-  // hand-off to the bulk LM kernel (lm.h seed_ctr): the seed into done_ctr[8 + 4r ..]
-  // with agent-coherent stores, then a release increment of the counter
-  if (done_ctr) {
-    double* sv = reinterpret_cast<double*>(done_ctr + 8) + r * 4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) __hip_atomic_store(sv + i, p[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(done_ctr, (uint64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  }
   if (probe && r == 0) {
     probe[0] = t_in;
     probe[1] = t_fold;

@@ -130,6 +130,9 @@ int dfmi_ekf(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
  * path for every ndata). Process-wide. */
 int dfmi_set_tuning(const char* key, int64_t value);
 
+/* Current value of a tuning key (see dfmi_set_tuning). */
+int dfmi_get_tuning(const char* key, int64_t* value);
+
 /* Diagnostics: with dfmi_set_tuning("probe", 1) some kernels record
  * s_memrealtime (100 MHz) timestamps; copies the first n (<= 16) of them
  * (synchronises the device). [0..2] seed entry / after fold / after fit,

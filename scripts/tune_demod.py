@@ -24,11 +24,10 @@ def main():
     dc = torch.empty(nseg, dtype=torch.float64, device=dev)
     st = torch.cuda.current_stream()
     w0 = w0_of(1000.0, 200000.0)
-    # (demod_kernel, demod_unr, demod_loads, demod_nt, demod_blocks_per_cu, demod_bins_cfg)
+    # (demod_kernel, demod_loads, demod_nt, demod_blocks_per_cu); demod_loads / demod_nt tune the fold kernel
     variants = [tuple(int(t) for t in v.split(",")) for v in os.environ.get(
-        "VARIANTS", "0,4,8,1,0,0;2,4,8,1,0,0;2,4,8,1,0,2;2,4,8,1,0,7;2,4,8,1,0,8").split(";")]
-    probes = {7, 8}  # timing-only shapes: excluded from the result comparison
-    keys = ("demod_kernel", "demod_unr", "demod_loads", "demod_nt", "demod_blocks_per_cu", "demod_bins_cfg")
+        "VARIANTS", "0,8,1,0;1,8,1,0;1,8,1,3;0,16,1,0").split(";")]
+    keys = ("demod_kernel", "demod_loads", "demod_nt", "demod_blocks_per_cu")
     res = {v: [] for v in variants}
     ref = {"torch_sum": [], "torch_copy": []}
     y = torch.empty_like(x)
@@ -61,8 +60,6 @@ def main():
     # all variants must agree with the fold kernel (same fold order; contraction identical)
     qref = None
     for v in variants:
-        if v[5] in probes:
-            continue
         for k, val in zip(keys, v):
             _lib.check(lib.dfmi_set_tuning(k.encode(), val), "tune")
         _lib.check(lib.dfmi_demod(x.data_ptr(), nseg, R, R, nd, w0, 0, qi.data_ptr(), dc.data_ptr(), 1,
@@ -80,8 +77,8 @@ def main():
     out = {}
     for v, t in res.items():
         med = float(np.median(t))
-        kname = {0: "fold", 1: f"stream_unr{v[1]}", 2: f"bins{v[5]}", 3: f"binspipe_unr{v[1]}"}[v[0]]
-        name = f"{kname}_loads{v[2]}_nt{v[3]}_bpc{v[4]}"
+        kname = {0: "fold", 1: "bins"}[v[0]]
+        name = f"{kname}_loads{v[1]}_nt{v[2]}_bpc{v[3]}"
         out[name] = {"ms": round(med, 4), "GBps": round(nbytes / med / 1e6, 1)}
     out["torch_sum_read_GBps"] = round(x.numel() * 8 / np.median(ref["torch_sum"]) / 1e6, 1)
     out["torch_copy_rw_GBps"] = round(2 * x.numel() * 8 / np.median(ref["torch_copy"]) / 1e6, 1)

@@ -1,6 +1,7 @@
 """Interleaved A/B timing of whole record-pipeline steps (dfmi_nls_record, config 2)
 under tuning settings, with a bit-identity check of the results across settings.
-Usage: SETTINGS="seed_reserve=1;seed_reserve=0" python scripts/tune_step.py"""
+Usage: SETTINGS="seed_handoff=1;seed_handoff=0" python scripts/tune_step.py (each setting on top of the defaults)"""
+import ctypes
 import json
 import os
 import sys
@@ -40,9 +41,15 @@ def main():
     out = torch.empty((6, nseg), dtype=torch.float64, device=dev)
     ok = torch.empty(nseg, dtype=torch.int32, device=dev)
     settings = parse(os.environ.get("SETTINGS", "seed_reserve=1;seed_reserve=0"))
+    defaults = {}
+    for s in settings:  # every setting is applied on top of the library defaults
+        for k in s:
+            v = ctypes.c_int64()
+            _lib.check(lib.dfmi_get_tuning(k.encode(), ctypes.byref(v)), k)
+            defaults[k] = v.value
 
     def apply(s):
-        for k, v in s.items():
+        for k, v in {**defaults, **s}.items():
             _lib.check(lib.dfmi_set_tuning(k.encode(), v), k)
 
     def step():

@@ -237,14 +237,14 @@ def test_record_rows_path_matches_component_path():
     recs[:, : 40 * R] = base + 1e-3 * torch.randn(base.shape, dtype=torch.float64, device="cuda", generator=g)
     for nbuf in (40, 1):
         res = {}
-        for kern, seedb in ((2, 0), (0, 0), (2, 1)):
+        for kern, seedb in ((1, 0), (0, 0), (1, 1)):
             _lib.check(lib.dfmi_set_tuning(b"demod_kernel", kern), "tune")
             _lib.check(lib.dfmi_set_tuning(b"seed_bins", seedb), "tune")
             cols, ok = nls_records(recs, 200000.0, 1000.0, R, nbuf, 10)
             res[kern, seedb] = (cols.cpu().numpy(), ok.cpu().numpy(), lib.dfmi_last_demod_kernel().decode())
-        _lib.check(lib.dfmi_set_tuning(b"demod_kernel", 2), "tune")
+        _lib.check(lib.dfmi_set_tuning(b"demod_kernel", 1), "tune")
         _lib.check(lib.dfmi_set_tuning(b"seed_bins", 1), "tune")
-        a, b, c = res[2, 0], res[0, 0], res[2, 1]
+        a, b, c = res[1, 0], res[0, 0], res[1, 1]
         assert "rows" in a[2] and "rows" not in b[2], (a[2], b[2])
         np.testing.assert_array_equal(a[0], b[0])
         np.testing.assert_array_equal(a[1], b[1])
@@ -252,10 +252,10 @@ def test_record_rows_path_matches_component_path():
         assert np.abs(c[0] - b[0]).max() < 1e-9
 
 
-def test_seed_handoff_fallback_identical():
-    """The bulk LM takes the seed from the side-stream seed kernel through a device
-    counter; if it never arrives (test hook: an unreachable target) every wave
-    recomputes the identical seed from the bulk demodulation row after a bounded wait."""
+def test_seed_stream_order_identical():
+    """The seed step runs on the caller's stream with the bulk demodulation on the
+    side stream (seed_order 1, default) or the other way round (seed_order 0); the
+    results are the same bits."""
     import torch
     from deepfmkit_amd import _lib
     from deepfmkit_amd.fitters import nls_records
@@ -267,11 +267,12 @@ def test_seed_handoff_fallback_identical():
     x = (1.0 + torch.cos(0.4 + 6.2 * torch.cos(2 * np.pi * 1000.0 * t + 0.2))).reshape(1, -1)
     x = x + 1e-3 * torch.randn(x.shape, dtype=torch.float64, device="cuda", generator=g)
     res = []
-    for unreachable in (0, 1, 0):
-        _lib.check(lib.dfmi_set_tuning(b"seed_handoff_unreachable", unreachable), "tune")
+    for order in (1, 0, 1):
+        _lib.check(lib.dfmi_set_tuning(b"seed_order", order), "tune")
         cols, ok = nls_records(x, 200000.0, 1000.0, R, nbuf, 10)
-        res.append((cols.cpu().numpy(), ok.cpu().numpy()))
-    _lib.check(lib.dfmi_set_tuning(b"seed_handoff_unreachable", 0), "tune")
-    for cols, ok in res[1:]:
+        res.append((cols.cpu().numpy(), ok.cpu().numpy(), lib.dfmi_last_demod_kernel().decode()))
+    _lib.check(lib.dfmi_set_tuning(b"seed_order", 1), "tune")
+    assert "spacer" in res[0][2] and "spacer" not in res[1][2], (res[0][2], res[1][2])
+    for cols, ok, _ in res[1:]:
         np.testing.assert_array_equal(cols, res[0][0])
         np.testing.assert_array_equal(ok, res[0][1])

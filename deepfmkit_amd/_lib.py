@@ -22,7 +22,8 @@ MAX_LAMBDA = 16
 SYMBOLS = ("dfmi_lm_config_default", "dfmi_demod", "dfmi_lm", "dfmi_nls_record", "dfmi_ekf",
            "dfmi_detect_period", "dfmi_device_count", "dfmi_last_error", "dfmi_version", "dfmi_set_tuning",
            "dfmi_last_demod_kernel", "dfmi_qi_row_stride", "dfmi_qi_row_dc", "dfmi_demod_rows",
-           "dfmi_probe_read", "dfmi_get_tuning")
+           "dfmi_probe_read", "dfmi_get_tuning", "dfmi_txt_parse_header", "dfmi_txt_shape", "dfmi_txt_read",
+           "dfmi_fit_txt_write", "dfmi_py_repr", "dfmi_txt_last_error")
 
 
 class DFMIError(RuntimeError):
@@ -89,6 +90,19 @@ def load():
         lib.dfmi_qi_row_dc.restype = ctypes.c_int32
         lib.dfmi_demod_rows.argtypes = [P, i64, i64, i32, i32, dbl, i32, P, i32, P]
         lib.dfmi_demod_rows.restype = ctypes.c_int
+        cp = ctypes.c_char_p
+        lib.dfmi_txt_parse_header.argtypes = [cp, i32, P]
+        lib.dfmi_txt_parse_header.restype = ctypes.c_int
+        lib.dfmi_txt_shape.argtypes = [cp, i32, i32, P, P]
+        lib.dfmi_txt_shape.restype = ctypes.c_int
+        lib.dfmi_txt_read.argtypes = [cp, i32, i32, i32, P, P, i64, i32]
+        lib.dfmi_txt_read.restype = ctypes.c_int
+        lib.dfmi_fit_txt_write.argtypes = [cp, cp, P, P, P, P, P, P, i64]
+        lib.dfmi_fit_txt_write.restype = ctypes.c_int
+        lib.dfmi_py_repr.argtypes = [dbl, ctypes.c_char_p, i32]
+        lib.dfmi_py_repr.restype = ctypes.c_int
+        lib.dfmi_txt_last_error.argtypes = []
+        lib.dfmi_txt_last_error.restype = ctypes.c_char_p
         lib.dfmi_get_tuning.argtypes = [ctypes.c_char_p, P]
         lib.dfmi_get_tuning.restype = ctypes.c_int
         lib.dfmi_probe_read.argtypes = [P, i32]

@@ -2,10 +2,12 @@
 
 Kept: the containers (raws, sims, fits, fits_df), simulate (snr mode; asd mode
 for zero/white noise), new_sim / load_sim, create_witness_channel, fit_init,
-fit (strategy dispatch, tau column, DeepFitObject), and fit_many — several
-equal-length channels fitted as ONE GPU batch (config 3).
+fit (strategy dispatch, tau column, DeepFitObject), fit_many — several
+equal-length channels fitted as ONE GPU batch (config 3) — and the text formats:
+parse_header, load_raw, load_fit, to_txt (core.py:119-174, 259-332; parsed and
+written by libdfmi's host code, deepfmkit_amd/textio.py).
 
-Out of scope (SURVEY.md §2 "OUT"): file loaders, LPSD, plotting.
+Out of scope (SURVEY.md §2 "OUT"): LPSD, plotting.
 """
 from __future__ import annotations
 
@@ -53,8 +55,84 @@ class DeepFitFramework:
         self.ndata = 10
         self.init_a = 1.6
         self.init_m = 6.0
-        if raw_file is not None or fit_file is not None:
-            raise NotImplementedError("raw/fit file loaders are outside the readout engine's scope")
+        if self.raw_file is not None:
+            self.load_raw(labels=raw_labels)
+        if self.fit_file is not None:
+            self.load_fit(labels=fit_labels)
+
+    # --- text formats (core.py:119-174, 259-332) --------------------------------
+    def to_txt(self, filepath="./", labels=None):
+        """core.py:119-127: one fit_data file per fit, named <filepath><label>.txt."""
+        for label in (labels if labels is not None else list(self.fits)):
+            self.fits[label].to_txt(filepath + self.fits[label].label + ".txt")
+
+    def parse_header(self, file_select="raw"):
+        """core.py:129-174."""
+        from . import textio
+        if file_select == "raw":
+            h = textio.parse_header(self.raw_file, textio.RAW)
+        elif file_select == "fit":
+            h = textio.parse_header(self.fit_file, textio.FIT)
+        else:
+            log.error("No files specified !!")
+            return
+        for k, v in h.items():
+            setattr(self, k, v)
+
+    def load_raw(self, raw_file=None, labels=None, device=None):
+        """core.py:259-286: one DeepRawObject per channel (column). With `device`
+        the samples go straight to that GPU (pinned staging) as the raw's data."""
+        from . import textio
+        from .data import DeepRawObject
+        if raw_file is not None:
+            self.raw_file = raw_file
+        if self.raw_file is None:
+            log.error("No raw file specified !!")
+            return
+        self.parse_header(file_select="raw")
+        if labels is None:
+            labels = [self.raw_file + "_ch" + str(c) for c in range(self.channr)]
+        else:
+            assert len(labels) == self.channr
+        _, chans = textio.read_raw(self.raw_file, device=device)
+        for c in range(self.channr):
+            if device is None:
+                import pandas as pd
+                raw = DeepRawObject(data=pd.DataFrame({"ch" + str(c): chans[c]}))
+            else:
+                raw = DeepRawObject(data=chans[c])
+            raw.raw_file = self.raw_file
+            raw.label = labels[c]
+            raw.t0 = self.t0
+            raw.f_samp = self.f_samp
+            raw.f_mod = self.f_mod
+            self.raws[raw.label] = raw
+
+    def load_fit(self, fit_file=None, labels=None):
+        """core.py:288-332 (labels default to <raw_file>_ch<c>, as the reference: a
+        framework without a raw file raises the same TypeError)."""
+        from . import textio
+        if fit_file is not None:
+            self.fit_file = fit_file
+        if self.fit_file is None:
+            log.error("No fit file specified !!")
+            return
+        self.parse_header(file_select="fit")
+        if labels is None:
+            labels = [self.raw_file + "_ch" + str(c) for c in range(self.channr)]
+        else:
+            assert len(labels) == self.channr
+        _, data = textio.read_fit(self.fit_file)
+        for k in range(self.channr):
+            fit = DeepFitObject()
+            fit.nbuf = data.shape[2]
+            fit.n, fit.t0, fit.R, fit.fs = self.n, self.t0, self.R, self.fs
+            fit.f_samp, fit.f_mod = self.f_samp, self.f_mod
+            fit.ndata, fit.init_a, fit.init_m = self.ndata, self.init_a, self.init_m
+            fit.ssq, fit.amp, fit.m, fit.phi, fit.psi, fit.dc = (data[k, i].copy() for i in range(6))
+            fit.time = np.arange(0, fit.nbuf / self.fs, 1.0 / self.fs)
+            fit.label = labels[k]
+            self.fits[labels[k]] = fit
 
     # --- simulation ---------------------------------------------------------
     def load_sim(self, sim):

@@ -75,16 +75,7 @@ class DeepFitObject:
         self.dc = np.array([])
 
     def to_txt(self, filename):
-        """fit_data text format (reference data.py:178-208)."""
-        head = ["% fit_data", "% Message goes here", "% Number of channels: 1",
-                f"% Start time: {self.t0}", f"% Sampling frequency: {self.f_samp}",
-                f"% Modulation frequency: {self.f_mod}", f"% n: {int(self.n)}",
-                f"% Downsampling factor: {int(self.R)}", f"% Fit data rate: {self.fs}",
-                f"% Initial amplitude: {self.init_a}", f"% Initial modulation depth: {self.init_m}",
-                "%", "ssq0 amp0 m0 phi0 psi0 dc0 "]
-        with open(filename, "w") as f:
-            for line in head:
-                f.write(line + "\n")
-            for k in range(len(self.ssq)):
-                f.write(" ".join(str(v[k]) for v in (self.ssq, self.amp, self.m, self.phi, self.psi, self.dc))
-                        + " \n")
+        """fit_data text format (reference data.py:178-208), written by libdfmi's
+        host writer in the reference's exact bytes (textio.write_fit)."""
+        from . import textio
+        textio.write_fit(self, filename)

@@ -142,6 +142,45 @@ int dfmi_probe_read(int64_t* out, int32_t n);
 /* Period (samples) the fold kernel would use for this w0, R, ndata; 0 if none. */
 int32_t dfmi_detect_period(double w0, int32_t R, int32_t ndata);
 
+/* ---- The reference's text formats (host code, no GPU) ----
+ * raw_data / fit_data: 13 header lines ('%'-prefixed; lines 3..11 carry the numbers
+ * parse_header extracts by keeping only the characters "0123456789."), then one
+ * row per sample (raw: one column per channel, read with pandas sep=' ') or per
+ * segment (fit: ssq amp m phi psi dc per channel, read with numpy.genfromtxt).
+ * Replaces core.py:129-174 (parse_header), 259-286 (load_raw), 288-332 (load_fit)
+ * and data.py:178-208 (DeepFitObject.to_txt). Errors: negative return and
+ * dfmi_txt_last_error(). */
+#define DFMI_TXT_RAW 0
+#define DFMI_TXT_FIT 1
+#define DFMI_TXT_SINGLE_SPACE 0 /* pandas.read_csv(sep=' '): every space separates */
+#define DFMI_TXT_WHITESPACE 1   /* numpy.genfromtxt: blank runs separate, '#' comments,
+                                   rows whose field count differs from the first are skipped */
+typedef struct dfmi_txt_header {
+  int32_t kind;      /* DFMI_TXT_RAW | DFMI_TXT_FIT */
+  int32_t channels;  /* line 3 */
+  int64_t t0;        /* line 4 */
+  double f_samp;     /* line 5 */
+  double f_mod;      /* line 6 */
+  int32_t n;         /* fit: line 7 */
+  int32_t R;         /* fit: line 8 */
+  double fs;         /* fit: line 9 */
+} dfmi_txt_header;
+
+int dfmi_txt_parse_header(const char* path, int32_t kind, dfmi_txt_header* hdr);
+/* Data rows after `skip` lines and the largest field count of a row. */
+int dfmi_txt_shape(const char* path, int32_t skip, int32_t mode, int64_t* rows, int32_t* cols);
+/* out[k*rows + i] = column cols[k] of data row i (NaN when missing/invalid);
+ * `threads` host threads parse disjoint line ranges. */
+int dfmi_txt_read(const char* path, int32_t skip, int32_t mode, int32_t ncol, const int32_t* cols, double* out,
+                  int64_t rows, int32_t threads);
+/* `header` verbatim, then n rows "ssq amp m phi psi dc \n" with every value in
+ * CPython repr() digits (data.py:198-207 writes str(float)). */
+int dfmi_fit_txt_write(const char* path, const char* header, const double* ssq, const double* amp, const double* m,
+                       const double* phi, const double* psi, const double* dc, int64_t n);
+/* CPython repr(v) into buf; returns its length or a negative error. */
+int dfmi_py_repr(double v, char* buf, int32_t cap);
+const char* dfmi_txt_last_error(void);
+
 /* Number of visible HIP devices (initialises HIP). */
 int dfmi_device_count(void);
 

@@ -276,3 +276,34 @@ def test_seed_stream_order_identical():
     for cols, ok, _ in res[1:]:
         np.testing.assert_array_equal(cols, res[0][0])
         np.testing.assert_array_equal(ok, res[0][1])
+
+
+def test_raw_file_to_fit_file_end_to_end(tmp_path):
+    """raw_data file -> load_raw (host, and straight to the GPU) -> fit -> to_txt ->
+    load_fit: the device-loaded record fits to the same bits as the host-loaded one,
+    and the fit file reads back bit-exact."""
+    import deepfmkit_amd as dfm
+    from deepfmkit_amd import textio
+    laser, ifo = dfm.LaserConfig(), dfm.InterferometerConfig()
+    dfm.set_laser_df_for_effect(laser, ifo, 6.0)
+    src = dfm.DeepFitFramework()
+    src.load_sim(dfm.DFMIObject("s", laser, ifo, f_samp=200000.0))
+    src.simulate("s", n_seconds=0.1, mode="snr", snr_db=40.0, trial_num=3)
+    raw_path = str(tmp_path / "raw_data.txt")
+    textio.write_raw(raw_path, [src.raws["s"].samples()], t0=20250101, f_samp=200000.0, f_mod=1000.0)
+    fits = {}
+    for dev in (None, "cuda:0"):
+        dff = dfm.DeepFitFramework()
+        dff.load_raw(raw_path, labels=["ch"], device=dev)
+        fo = dff.fit("ch", n=20)
+        fits[dev] = fo
+    for k in ("amp", "m", "phi", "psi", "dc", "ssq"):
+        np.testing.assert_array_equal(np.asarray(getattr(fits[None], k)), np.asarray(getattr(fits["cuda:0"], k)))
+    fit_path = str(tmp_path / "fit_data.txt")
+    fits[None].to_txt(fit_path)
+    back = dfm.DeepFitFramework()
+    back.raw_file = "x"
+    back.load_fit(fit_path)
+    fb = back.fits["x_ch0"]
+    for k in ("amp", "m", "phi", "psi", "dc", "ssq"):
+        assert np.asarray(getattr(fb, k)).tobytes() == np.asarray(getattr(fits[None], k), dtype=np.float64).tobytes()

@@ -23,7 +23,7 @@ SYMBOLS = ("dfmi_lm_config_default", "dfmi_demod", "dfmi_lm", "dfmi_nls_record",
            "dfmi_detect_period", "dfmi_device_count", "dfmi_last_error", "dfmi_version", "dfmi_set_tuning",
            "dfmi_last_demod_kernel", "dfmi_qi_row_stride", "dfmi_qi_row_dc", "dfmi_demod_rows",
            "dfmi_probe_read", "dfmi_get_tuning", "dfmi_txt_parse_header", "dfmi_txt_shape", "dfmi_txt_read",
-           "dfmi_fit_txt_write", "dfmi_py_repr", "dfmi_txt_last_error")
+           "dfmi_fit_txt_write", "dfmi_py_repr", "dfmi_txt_last_error", "dfmi_wdfmi_fit")
 
 
 class DFMIError(RuntimeError):
@@ -47,6 +47,26 @@ class LMConfig(ctypes.Structure):
         ("sincos_amp_threshold", ctypes.c_double),
     ]
 
+
+class WdfmiConfig(ctypes.Structure):
+    """Mirror of dfmi_wdfmi_config (include/dfmi.h)."""
+    _fields_ = [
+        ("method", ctypes.c_int32),
+        ("ndata", ctypes.c_int32),
+        ("ndata_psi", ctypes.c_int32),
+        ("period", ctypes.c_int32),
+        ("f_samp", ctypes.c_double),
+        ("f_mod", ctypes.c_double),
+        ("df", ctypes.c_double),
+        ("f_ref", ctypes.c_double),
+        ("tau_init", ctypes.c_double),
+        ("init_a", ctypes.c_double),
+        ("init_phi", ctypes.c_double),
+        ("init_psi", ctypes.c_double),
+    ]
+
+
+WDFMI_METHODS = {"wdfmi_nls": 0, "wdfmi_ortho": 1, "wdfmi_seq": 2, "hwdfmi": 3}
 
 _lock = threading.Lock()
 _lib = None
@@ -74,6 +94,8 @@ def load():
         lib.dfmi_nls_record.restype = ctypes.c_int
         lib.dfmi_ekf.argtypes = [P, i64, i64, i64, P, P, P, P, dbl, dbl, i32, i64, P, i32, P]
         lib.dfmi_ekf.restype = ctypes.c_int
+        lib.dfmi_wdfmi_fit.argtypes = [P, i64, i64, i64, i32, P, i64, ctypes.POINTER(WdfmiConfig), P, P, i32, P]
+        lib.dfmi_wdfmi_fit.restype = ctypes.c_int
         lib.dfmi_detect_period.argtypes = [dbl, i32, i32]
         lib.dfmi_detect_period.restype = i32
         lib.dfmi_device_count.argtypes = []

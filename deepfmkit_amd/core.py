@@ -236,7 +236,14 @@ class DeepFitFramework:
         if getattr(raw, "phi_sim", None) is not None and len(raw.phi_sim) > 0:
             raw.phi_sim_downsamp = vectorized_downsample(raw.phi_sim, R)
         fit_config = {"n": n}
-        df = fitter_map[method](fit_config).fit(main_raw=raw, **kwargs)
+        fitter_args = {"main_raw": raw}
+        if "wdfmi" in method:  # core.py:486-490 (hwdfmi included)
+            witness_label = kwargs.get("witness_label")
+            if not witness_label or witness_label not in self.raws:
+                log.error(f"W-DFMI method '{method}' requires a valid 'witness_label'.")
+                return
+            fitter_args["witness_raw"] = self.raws[witness_label]
+        df = fitter_map[method](fit_config).fit(**fitter_args, **kwargs)
         if df is None or df.empty:
             log.error(f"{fitter_map[method].__name__} returned no results.")
             return None

@@ -21,6 +21,7 @@
 #include "ekf.h"
 #include "lm.h"
 #include "seed.h"
+#include "wdfmi.h"
 
 namespace {
 
@@ -51,6 +52,7 @@ struct DeviceState {
   std::map<std::string, DevBuf> ws;                                  // named workspaces
   std::map<std::tuple<int, int, uint64_t>, DevBuf> basis;            // (L, ndata, w0 bits)
   std::map<std::tuple<int, uint64_t, uint64_t, uint64_t>, DevBuf> gridtab;  // (ndata, min, max, step)
+  std::map<std::tuple<int, uint64_t>, DevBuf> timeax;                 // (R, f_samp): t_k = k / f_samp
   hipStream_t side = nullptr;  // seed step runs here, concurrently with the bulk demod
   hipEvent_t ev_in = nullptr, ev_seed = nullptr, ev_bulk = nullptr;
 };
@@ -129,6 +131,21 @@ int basis_table(int dev, int L, int ndata, double w0, hipStream_t st, const doub
     HIPCHK(hipMemcpy(b.p, h.data(), b.n, hipMemcpyHostToDevice));
   }
   (void)st;
+  *out = (const double*)b.p;
+  return DFMI_OK;
+}
+
+// Time axis of a buffer, np.arange(R) / f_samp (fitters.py:114, 154): t_k = k / f_samp.
+int time_axis(int dev, int R, double f_samp, const double** out) {
+  auto key = std::make_tuple(R, bits(f_samp));
+  DevBuf& b = g_dev[dev].timeax[key];
+  if (!b.p) {
+    std::vector<double> h(R);
+    for (int k = 0; k < R; ++k) h[k] = (double)k / f_samp;
+    HIPCHK(hipMalloc(&b.p, h.size() * 8));
+    b.n = h.size() * 8;
+    HIPCHK(hipMemcpy(b.p, h.data(), b.n, hipMemcpyHostToDevice));
+  }
   *out = (const double*)b.p;
   return DFMI_OK;
 }
@@ -799,6 +816,99 @@ int dfmi_nls_record(const double* x, int64_t nrec, int64_t rec_stride, int64_t n
   HIPCHK(hipMemcpyAsync(out, dout, (size_t)6 * nseg * 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(fitok, dst, (size_t)nseg * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  return DFMI_OK;
+}
+
+int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nbuf, int32_t R,
+                   const double* witness, int64_t wit_stride, const dfmi_wdfmi_config* cfg, double* out,
+                   int32_t* fitok, int32_t mem, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_err.clear();
+  if (!cfg) return fail(DFMI_ERR_ARG, "null config");
+  if (cfg->method < DFMI_WDFMI_NLS || cfg->method > DFMI_HWDFMI) return fail(DFMI_ERR_ARG, "unknown W-DFMI method");
+  if (nrec < 0 || nbuf < 0 || R < 4) return fail(DFMI_ERR_ARG, "bad record geometry (R >= 4)");
+  if (R > 16384) return fail(DFMI_ERR_UNSUPPORTED, "W-DFMI fitters support R <= 16384");
+  if (nrec > 1 && rec_stride < nbuf * (int64_t)R) return fail(DFMI_ERR_ARG, "rec_stride < nbuf*R");
+  if (nrec > 1 && wit_stride != 0 && wit_stride < R) return fail(DFMI_ERR_ARG, "wit_stride < R");
+  if (!(cfg->f_samp > 0.0)) return fail(DFMI_ERR_ARG, "f_samp must be > 0");
+  if (cfg->method == DFMI_WDFMI_NLS && (cfg->ndata < 1 || cfg->ndata > 32))
+    return fail(DFMI_ERR_UNSUPPORTED, "W-DFMI NLS: 1 <= ndata <= 32");
+  if (cfg->method == DFMI_WDFMI_SEQ && (cfg->ndata_psi < 1 || cfg->ndata_psi > 64))
+    return fail(DFMI_ERR_UNSUPPORTED, "W-DFMI SEQ: 1 <= ndata_psi <= 64");
+  if (nrec * nbuf > 0 && (!x || !witness || !out || !fitok)) return fail(DFMI_ERR_ARG, "null pointer");
+  int dev;
+  int rc = ensure_init(&dev);
+  if (rc) return rc;
+  const int64_t nseg = nrec * nbuf;
+  if (nseg == 0) return DFMI_OK;
+  hipStream_t st = (hipStream_t)stream;
+  dfmi::WdfmiLaunch a;
+  memset(&a, 0, sizeof(a));
+  a.method = cfg->method;
+  a.R = R;
+  a.ndata = cfg->ndata;
+  a.ndata_psi = cfg->ndata_psi;
+  a.threads = R <= 4096 ? 256 : (R <= 8192 ? 512 : 1024);
+  a.nrec = nrec;
+  a.nbuf = nbuf;
+  a.f_samp = cfg->f_samp;
+  a.f_mod = cfg->f_mod;
+  a.df = cfg->df;
+  a.f_ref = cfg->f_ref;
+  a.tau_init = cfg->tau_init;
+  a.init_a = cfg->init_a;
+  a.init_phi = cfg->init_phi;
+  a.init_psi = cfg->init_psi;
+  a.w0 = (2.0 * M_PI * cfg->f_mod) / cfg->f_samp;  // omega_mod / f_samp (fitters.py:506-507)
+  const int nh = cfg->method == DFMI_WDFMI_NLS ? cfg->ndata : (cfg->method == DFMI_WDFMI_SEQ ? cfg->ndata_psi : 0);
+  a.L = 0;
+  if (nh > 0 && cfg->period >= 0) a.L = cfg->period > 0 ? cfg->period : detect_period_impl(a.w0, R, nh);
+  if (a.L > R) a.L = 0;
+  const size_t lds = dfmi::wdfmi_lds_bytes(a);
+  if (lds > g_dev[dev].lds_per_block)
+    return fail(DFMI_ERR_UNSUPPORTED, "W-DFMI: R too large for the LDS budget (" + std::to_string(lds) + " B)");
+  const double* tt;
+  if ((rc = time_axis(dev, R, cfg->f_samp, &tt))) return rc;
+  a.tt = tt;
+  if (nh > 0 && a.L > 0) {
+    const double* bt;
+    if ((rc = basis_table(dev, a.L, nh, a.w0, st, &bt))) return rc;
+    if (cfg->method == DFMI_WDFMI_NLS) a.btab_nls = bt;
+    else a.btab_psi = bt;
+  }
+  const int64_t rs = nrec > 1 ? rec_stride : nbuf * (int64_t)R;
+  const int64_t ws = nrec > 1 ? wit_stride : 0;
+  const int64_t ntmpl = ws == 0 ? 1 : nrec;
+  void* tm;
+  if ((rc = workspace(dev, "w_tmpl", (size_t)ntmpl * R * 8, &tm))) return rc;
+  a.tmpl = (double*)tm;
+  a.rec_stride = rs;
+  a.wit_stride = ws;
+  a.x = x;
+  a.wit = witness;
+  a.out = out;
+  a.fitok = fitok;
+  if (mem != DFMI_MEM_DEVICE) {
+    void *dx, *dw, *dout, *dok;
+    const size_t xb = (size_t)((nrec - 1) * rs + nbuf * (int64_t)R) * 8;
+    const size_t wb = (size_t)((ntmpl - 1) * ws + R) * 8;
+    if ((rc = workspace(dev, "w_x", xb, &dx))) return rc;
+    if ((rc = workspace(dev, "w_wit", wb, &dw))) return rc;
+    if ((rc = workspace(dev, "w_out", (size_t)7 * nseg * 8, &dout))) return rc;
+    if ((rc = workspace(dev, "w_ok", (size_t)nseg * 4, &dok))) return rc;
+    HIPCHK(hipMemcpyAsync(dx, x, xb, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dw, witness, wb, hipMemcpyHostToDevice, st));
+    a.x = (const double*)dx;
+    a.wit = (const double*)dw;
+    a.out = (double*)dout;
+    a.fitok = (int32_t*)dok;
+  }
+  HIPCHK(dfmi::wdfmi_launch(a, st));
+  if (mem != DFMI_MEM_DEVICE) {
+    HIPCHK(hipMemcpyAsync(out, a.out, (size_t)7 * nseg * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(fitok, a.fitok, (size_t)nseg * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
   return DFMI_OK;
 }
 

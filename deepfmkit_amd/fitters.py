@@ -13,6 +13,10 @@ Reference map:
   StandardNLSFitter.fit ......... fitters.py:330-368
     _fit_sequential ............. fitters.py:370-393  (parallel=False)
     _fit_parallel ............... fitters.py:395-428  (parallel=True)
+  WDFMI_NLSFitter.fit ........... fitters.py:481-570  (EXPERIMENTAL in the reference)
+  WDFMI_OrthogonalFitter.fit .... fitters.py:572-648
+  WDFMI_SequentialFitter.fit .... fitters.py:650-776
+  HWDFMI_Fitter.fit ............. fitters.py:778-891
 """
 from __future__ import annotations
 
@@ -21,6 +25,7 @@ from abc import ABC, abstractmethod
 
 import numpy as np
 import pandas as pd
+import scipy.constants as sc
 
 from . import _lib
 from . import fit as _fit
@@ -194,7 +199,163 @@ def ekf_records(raws, n, **kwargs):
     return states
 
 
+WDFMI_COLUMNS = ["amp", "m", "phi", "psi", "tau", "dc", "ssq", "fitok"]
+
+
+def wdfmi_records(method, mains, witnesses, f_samp, f_mod, R, nbuf, df=0.0, f_ref=0.0, tau_init=0.0, ndata=10,
+                  ndata_psi=40, init_a=1.6, init_phi=0.0, init_psi=0.0, period=0):
+    """Run one witness-based fitter over one or more records in ONE GPU call.
+
+    mains: (nrec, >= nbuf*R) array / CUDA tensor or a list of 1-D records; witnesses:
+    the same for the witness channels (only the first R samples are used), or one
+    1-D witness shared by every record. Returns (cols (7, nrec*nbuf) in the order
+    amp, m, phi, psi, tau, dc, ssq; fitok (nrec*nbuf,)), numpy for host input and CUDA
+    tensors for device input."""
+    lib = _lib.load()
+    dev = _is_device_tensor(mains if not isinstance(mains, (list, tuple)) else mains[0])
+    if dev:
+        import torch
+        x = torch.stack([r[: nbuf * R] for r in mains]) if isinstance(mains, (list, tuple)) else mains
+        x = x.contiguous()
+        w = torch.stack([r[:R] for r in witnesses]) if isinstance(witnesses, (list, tuple)) else witnesses
+        w = w.contiguous()
+        if x.dtype != torch.float64 or w.dtype != torch.float64:
+            raise ValueError("device records must be float64")
+    else:
+        if isinstance(mains, (list, tuple)):
+            x = np.ascontiguousarray(np.stack([np.asarray(r, np.float64)[: nbuf * R] for r in mains]))
+        else:
+            x = np.ascontiguousarray(np.asarray(mains, np.float64))
+        if isinstance(witnesses, (list, tuple)):
+            w = np.ascontiguousarray(np.stack([np.asarray(r, np.float64)[:R] for r in witnesses]))
+        else:
+            w = np.ascontiguousarray(np.asarray(witnesses, np.float64))
+    if x.ndim == 1:
+        x = x.reshape(1, -1)
+    nrec = int(x.shape[0])
+    if w.ndim == 1:
+        wit_stride = 0
+    else:
+        wit_stride = int(w.stride(0)) if dev else int(w.strides[0] // 8)
+        if int(w.shape[0]) != nrec:
+            raise ValueError("one witness per record (or a single shared one) is required")
+    if int(w.shape[-1]) < R:
+        raise ValueError(f"witness needs at least R={R} samples")
+    rec_stride = int(x.stride(0)) if dev else int(x.strides[0] // 8)
+    if int(x.shape[1]) < nbuf * R:
+        raise ValueError("records shorter than nbuf*R")
+    cfg = _lib.WdfmiConfig(_lib.WDFMI_METHODS[method], int(ndata), int(ndata_psi), int(period), float(f_samp),
+                           float(f_mod), float(df), float(f_ref), float(tau_init), float(init_a), float(init_phi),
+                           float(init_psi))
+    nseg = nrec * nbuf
+    if dev:
+        import torch
+        out = torch.empty((7, nseg), dtype=torch.float64, device=x.device)
+        ok = torch.empty(nseg, dtype=torch.int32, device=x.device)
+        rc = lib.dfmi_wdfmi_fit(x.data_ptr(), nrec, rec_stride, nbuf, R, w.data_ptr(), wit_stride, cfg,
+                                out.data_ptr(), ok.data_ptr(), _lib.DFMI_MEM_DEVICE, _torch_stream())
+    else:
+        out = np.empty((7, nseg))
+        ok = np.empty(nseg, dtype=np.int32)
+        rc = lib.dfmi_wdfmi_fit(_lib.ptr(x), nrec, rec_stride, nbuf, R, _lib.ptr(w), wit_stride, cfg, _lib.ptr(out),
+                                _lib.ptr(ok), _lib.DFMI_MEM_HOST, None)
+    _lib.check(rc, "dfmi_wdfmi_fit")
+    return out, ok
+
+
+def wdfmi_frame(cols, fitok):
+    """DataFrame with the witness fitters' columns (fitters.py:563-567, 640-645, 768-773, 883-888)."""
+    if hasattr(cols, "cpu"):
+        cols = cols.cpu().numpy()
+        fitok = fitok.cpu().numpy()
+    d = {k: np.asarray(cols[i]) for i, k in enumerate(WDFMI_COLUMNS[:7])}
+    d["fitok"] = np.asarray(fitok).astype(np.int64)
+    return pd.DataFrame(d, columns=WDFMI_COLUMNS)
+
+
+class _WitnessFitter(BaseFitter):
+    """Shared plumbing of the witness-based fitters: geometry, config, one GPU call."""
+
+    METHOD = None
+
+    def _run(self, main_raw, witness_raw, tau_init, **kw):
+        R, _, nbuf = _calculate_fit_params(main_raw, self.config["n"])
+        if nbuf == 0:
+            return pd.DataFrame()
+        laser = main_raw.sim.laser
+        x = main_raw.samples()
+        wv = witness_raw.samples()
+        if not _is_device_tensor(x):
+            x = np.asarray(x, dtype=np.float64)
+            wv = np.asarray(wv, dtype=np.float64)
+        cols, ok = wdfmi_records(self.METHOD, x[: nbuf * R].reshape(1, nbuf * R), wv[:R], main_raw.f_samp,
+                                 laser.f_mod, R, nbuf, df=laser.df, tau_init=tau_init, **kw)
+        return wdfmi_frame(cols, ok)
+
+
+class WDFMI_NLSFitter(_WitnessFitter):
+    """fitters.py:481-570: direct 4-parameter NLS (C, tau, phi, psi) on the harmonic
+    residuals, MINPACK lmdif as least_squares(method='lm') runs it, warm-started
+    buffer to buffer. ndata comes from the fit config (default 10), as in the reference."""
+
+    METHOD = "wdfmi_nls"
+
+    def fit(self, main_raw, witness_raw, **kwargs) -> pd.DataFrame:
+        ifo = main_raw.sim.ifo
+        tau_init = (ifo.meas_arml - ifo.ref_arml) / sc.c
+        return self._run(main_raw, witness_raw, tau_init, ndata=self.config.get("ndata", 10),
+                         init_a=kwargs.get("init_a", 1.6), init_phi=kwargs.get("init_phi", 0.0),
+                         init_psi=kwargs.get("init_psi", 0.0))
+
+
+class WDFMI_OrthogonalFitter(_WitnessFitter):
+    """fitters.py:572-648: Nelder-Mead over (tau, psi) of the VarPro residual."""
+
+    METHOD = "wdfmi_ortho"
+
+    def fit(self, main_raw, witness_raw, **kwargs) -> pd.DataFrame:
+        laser, ifo = main_raw.sim.laser, main_raw.sim.ifo
+        tau_init = (ifo.meas_arml - ifo.ref_arml) / sc.c if laser.df > 0 else 0.0
+        return self._run(main_raw, witness_raw, tau_init, init_psi=kwargs.get("init_psi", 0.0))
+
+
+class WDFMI_SequentialFitter(_WitnessFitter):
+    """fitters.py:650-776: tau by Brent (VarPro), psi by bounded Brent on the harmonic
+    phase error (40 harmonics), then the linear fit; buffers are independent."""
+
+    METHOD = "wdfmi_seq"
+
+    def fit(self, main_raw, witness_raw, **kwargs) -> pd.DataFrame:
+        laser, ifo = main_raw.sim.laser, main_raw.sim.ifo
+        tau_init = (ifo.meas_arml - ifo.ref_arml) / sc.c if laser.df > 0 else 0.0
+        return self._run(main_raw, witness_raw, tau_init, init_psi=kwargs.get("init_psi", 0.0))
+
+
+class HWDFMI_Fitter(_WitnessFitter):
+    """fitters.py:778-891: 1-D VarPro search for tau against the heterodyne witness's
+    integrated laser phase; f_ref from the witness ifo's arml_mod_f (fitters.py:827-831)."""
+
+    METHOD = "hwdfmi"
+
+    def fit(self, main_raw, witness_raw, **kwargs) -> pd.DataFrame:
+        init_tau = kwargs.get("init_tau", None)
+        if hasattr(witness_raw.sim.ifo, "arml_mod_f"):
+            f_ref = witness_raw.sim.ifo.arml_mod_f
+        else:
+            logging.warning("Reference frequency `f_ref` not found in witness config. Assuming 0 Hz.")
+            f_ref = 0.0
+        if init_tau is not None:
+            tau = init_tau
+        else:
+            tau = (main_raw.sim.ifo.meas_arml - main_raw.sim.ifo.ref_arml) / sc.c
+        return self._run(main_raw, witness_raw, tau, f_ref=f_ref)
+
+
 FITTER_MAP = {
     "nls": StandardNLSFitter,
     "ekf": EKFFitter,
+    "wdfmi_nls": WDFMI_NLSFitter,
+    "wdfmi_ortho": WDFMI_OrthogonalFitter,
+    "wdfmi_seq": WDFMI_SequentialFitter,
+    "hwdfmi": HWDFMI_Fitter,
 }

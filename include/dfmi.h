@@ -24,6 +24,9 @@
  *                    chunk with the warm start of _process_fit_chunk (fitters.py:13-60)
  *   dfmi_nls_record  StandardNLSFitter._fit_sequential / _fit_parallel
  *                    (fitters.py:370-428) for one or more records (channels)
+ *   dfmi_ekf         EKFFitter.fit (fitters.py:214-320)
+ *   dfmi_wdfmi_fit   WDFMI_NLSFitter / WDFMI_OrthogonalFitter / WDFMI_SequentialFitter /
+ *                    HWDFMI_Fitter .fit (fitters.py:481-891)
  */
 #ifndef DFMI_H
 #define DFMI_H
@@ -121,6 +124,45 @@ int dfmi_nls_record(const double* x, int64_t nrec, int64_t rec_stride, int64_t n
 int dfmi_ekf(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, const double* x0,
              const double* p0_diag, const double* q_diag, const double* r_val, double w_m, double f_samp,
              int32_t R, int64_t nbuf, double* states, int32_t mem, void* stream);
+
+/* ---- Witness-based fitters (EXPERIMENTAL in the reference) ----
+ * Replace, per record (main channel + witness channel):
+ *   DFMI_WDFMI_NLS    WDFMI_NLSFitter.fit        fitters.py:481-570 (least_squares(method='lm'))
+ *   DFMI_WDFMI_ORTHO  WDFMI_OrthogonalFitter.fit fitters.py:572-648 (Nelder-Mead + VarPro)
+ *   DFMI_WDFMI_SEQ    WDFMI_SequentialFitter.fit fitters.py:650-776 (Brent, bounded Brent, lstsq)
+ *   DFMI_HWDFMI       HWDFMI_Fitter.fit          fitters.py:778-891 (Brent + VarPro)
+ * with the witness template of _get_phase_modulation_basis (fitters.py:88-122) or
+ * _get_total_laser_phase (fitters.py:124-162) built from the witness's first R samples. */
+#define DFMI_WDFMI_NLS 0
+#define DFMI_WDFMI_ORTHO 1
+#define DFMI_WDFMI_SEQ 2
+#define DFMI_HWDFMI 3
+
+typedef struct dfmi_wdfmi_config {
+  int32_t method;     /* DFMI_WDFMI_* / DFMI_HWDFMI */
+  int32_t ndata;      /* WDFMI_NLS harmonics (10), <= 32 */
+  int32_t ndata_psi;  /* WDFMI_SEQ stage-2 harmonics (40), <= 64 */
+  int32_t period;     /* basis period of the harmonic sums: 0 detect, -1 per-sample sincos */
+  double f_samp;      /* main_raw.f_samp */
+  double f_mod;       /* laser_cfg.f_mod */
+  double df;          /* laser_cfg.df (W-DFMI template scale, m = 2 pi df tau) */
+  double f_ref;       /* HW-DFMI reference frequency (witness ifo.arml_mod_f) */
+  double tau_init;    /* first guess of tau: the caller applies the reference's rule per
+                         method (delta_l / c, 0 when df <= 0 for ortho/seq, init_tau for HW) */
+  double init_a, init_phi, init_psi;
+} dfmi_wdfmi_config;
+
+/* Fit nrec records of nbuf buffers of R samples.
+ *   x[r*rec_stride + b*R + k]            main channel samples
+ *   witness[r*wit_stride + k], k < R     witness channel (wit_stride 0: one witness for all)
+ *   out[col*(nrec*nbuf) + r*nbuf + b]    col = 0 amp, 1 m, 2 phi, 3 psi, 4 tau, 5 dc, 6 ssq
+ *   fitok[r*nbuf + b]                    the reference's fitok column
+ * NLS / ORTHO / HW warm-start buffer b from buffer b-1 (one workgroup per record);
+ * SEQ fits every buffer independently. R <= 16384. A rank-deficient VarPro system
+ * costs +inf (the reference's ORTHO raises IndexError there). */
+int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nbuf, int32_t R,
+                   const double* witness, int64_t wit_stride, const dfmi_wdfmi_config* cfg, double* out,
+                   int32_t* fitok, int32_t mem, void* stream);
 
 /* Performance tuning hook (results are unaffected): "demod_kernel" (0 cycle-aligned
  * fold, 1 pipelined cycle-aligned fold, 2 bins in LDS [default], 3 pipelined bins),

@@ -18,7 +18,8 @@ def declared_symbols():
 
 def test_header_declares_expected_entry_points():
     syms = declared_symbols()
-    for s in ("dfmi_demod", "dfmi_lm", "dfmi_nls_record", "dfmi_ekf", "dfmi_last_error", "dfmi_device_count"):
+    for s in ("dfmi_demod", "dfmi_lm", "dfmi_nls_record", "dfmi_ekf", "dfmi_last_error", "dfmi_device_count",
+              "dfmi_wdfmi_fit"):
         assert s in syms
 
 
@@ -89,3 +90,30 @@ def test_no_gpu_here_is_a_loud_error():
     from deepfmkit_amd._lib import DFMIError
     with pytest.raises(DFMIError):
         F.demodulate(np.zeros((2, 400)), 10, w0=2 * np.pi / 200)
+
+
+def test_wdfmi_argument_errors_before_any_device_work():
+    """dfmi_wdfmi_fit validates its arguments on the host (no GPU needed) and, with
+    valid arguments but no GPU, fails loudly rather than computing on the CPU."""
+    from deepfmkit_amd import _lib
+    lib = _lib.load()
+    x = np.zeros(8000)
+    w = np.zeros(4000)
+    out = np.zeros((7, 2))
+    ok = np.zeros(2, dtype=np.int32)
+
+    def call(method=1, R=4000, ndata=10, ndata_psi=40, f_samp=200000.0):
+        cfg = _lib.WdfmiConfig(method, ndata, ndata_psi, 0, f_samp, 1000.0, 1e9, 0.0, 6e-10, 1.6, 0.0, 0.0)
+        return lib.dfmi_wdfmi_fit(_lib.ptr(x), 1, 8000, 2, R, _lib.ptr(w), 0, cfg, _lib.ptr(out), _lib.ptr(ok),
+                                  _lib.DFMI_MEM_HOST, None)
+
+    assert call(method=7) == -1
+    assert call(R=2) == -1
+    assert call(R=20000) == -4
+    assert call(method=0, ndata=40) == -4
+    assert call(method=2, ndata_psi=80) == -4
+    assert call(f_samp=0.0) == -1
+    import pytest
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        assert call() == -3  # DFMI_ERR_NODEV

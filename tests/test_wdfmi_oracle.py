@@ -20,10 +20,11 @@ CASES = {c["name"]: c for c in json.load(open(os.path.join(HERE, "golden", "wdfm
 COLS = ["amp", "m", "phi", "psi", "tau", "dc", "ssq", "fitok"]
 
 
-def run_oracle(case, method):
+def run_oracle(case, method, main=None):
     f_samp, f_mod, df, meas, ref, f_ref, n = G[f"{case}_cfg"]
     c = CASES[case]
-    main, wit = G[f"{case}_main"], G[f"{case}_witness"]
+    main = G[f"{case}_main"] if main is None else main
+    wit = G[f"{case}_witness"]
     dl, n = meas - ref, int(n)
     if method == "wdfmi_nls":
         return W.fit_wdfmi_nls(main, wit, f_samp, f_mod, df, dl, n, **c["nls"])
@@ -56,3 +57,27 @@ def test_scalar_minimisers_known_answers():
     assert flag == 0 and abs(x - np.pi) < 1e-4
     x, fx, ok = W.nelder_mead(lambda p: (p[0] - 1) ** 2 + (p[1] + 2) ** 2, [0.0, 0.0])
     assert ok and np.allclose(x, [1, -2], atol=1e-3)
+
+
+def test_reference_sensitivity():
+    """How finely the reference determines its own answer (sets the GPU tolerances in
+    tests/test_gpu_wdfmi.py): perturb the main channel by ~1 ulp (relative 2e-16) and
+    re-run the restated reference. ortho / hwdfmi follow the same optimiser path (tau,
+    psi move by at most an ulp); seq's psi stage moves by ~1e-7; nls on the distorted
+    case is chaotic (tens of percent)."""
+    rng = np.random.default_rng(1)
+
+    def spread(case, method):
+        a = run_oracle(case, method)
+        main = G[f"{case}_main"]
+        b = run_oracle(case, method, main=main * (1 + rng.standard_normal(main.shape) * 2e-16))
+        return {k: float(np.max(np.abs(a[k] - b[k]) / np.abs(a[k]))) for k in ("amp", "phi", "psi", "tau")}
+
+    s = spread("cos", "wdfmi_ortho")
+    assert s["tau"] <= 1e-15 and s["psi"] <= 1e-15 and s["amp"] < 1e-14
+    s = spread("cos", "hwdfmi")
+    assert s["tau"] <= 1e-15 and s["amp"] < 1e-14
+    s = spread("cos", "wdfmi_seq")
+    assert 1e-9 < s["psi"] < 1e-5
+    s = spread("dist", "wdfmi_nls")
+    assert s["amp"] > 1e-3

@@ -21,6 +21,7 @@
 #include "ekf.h"
 #include "lm.h"
 #include "seed.h"
+#include "np_sum.h"
 #include "wdfmi.h"
 
 namespace {
@@ -52,7 +53,7 @@ struct DeviceState {
   std::map<std::string, DevBuf> ws;                                  // named workspaces
   std::map<std::tuple<int, int, uint64_t>, DevBuf> basis;            // (L, ndata, w0 bits)
   std::map<std::tuple<int, uint64_t, uint64_t, uint64_t>, DevBuf> gridtab;  // (ndata, min, max, step)
-  std::map<std::tuple<int, uint64_t>, DevBuf> timeax;                 // (R, f_samp): t_k = k / f_samp
+  std::map<int, DevBuf> pwplan;                                     // R -> numpy pairwise-sum plan
   hipStream_t side = nullptr;  // seed step runs here, concurrently with the bulk demod
   hipEvent_t ev_in = nullptr, ev_seed = nullptr, ev_bulk = nullptr;
 };
@@ -131,21 +132,6 @@ int basis_table(int dev, int L, int ndata, double w0, hipStream_t st, const doub
     HIPCHK(hipMemcpy(b.p, h.data(), b.n, hipMemcpyHostToDevice));
   }
   (void)st;
-  *out = (const double*)b.p;
-  return DFMI_OK;
-}
-
-// Time axis of a buffer, np.arange(R) / f_samp (fitters.py:114, 154): t_k = k / f_samp.
-int time_axis(int dev, int R, double f_samp, const double** out) {
-  auto key = std::make_tuple(R, bits(f_samp));
-  DevBuf& b = g_dev[dev].timeax[key];
-  if (!b.p) {
-    std::vector<double> h(R);
-    for (int k = 0; k < R; ++k) h[k] = (double)k / f_samp;
-    HIPCHK(hipMalloc(&b.p, h.size() * 8));
-    b.n = h.size() * 8;
-    HIPCHK(hipMemcpy(b.p, h.data(), b.n, hipMemcpyHostToDevice));
-  }
   *out = (const double*)b.p;
   return DFMI_OK;
 }
@@ -848,7 +834,8 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
   a.R = R;
   a.ndata = cfg->ndata;
   a.ndata_psi = cfg->ndata_psi;
-  a.threads = R <= 4096 ? 256 : (R <= 8192 ? 512 : 1024);
+  a.threads = R <= 4096 ? 256 : 1024;
+  a.probe = g_probe;
   a.nrec = nrec;
   a.nbuf = nbuf;
   a.f_samp = cfg->f_samp;
@@ -864,12 +851,19 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
   a.L = 0;
   if (nh > 0 && cfg->period >= 0) a.L = cfg->period > 0 ? cfg->period : detect_period_impl(a.w0, R, nh);
   if (a.L > R) a.L = 0;
+  {
+    DevBuf& pb = g_dev[dev].pwplan[R];
+    if (!pb.p) {
+      const std::vector<int> plan = dfmi_pairwise_plan(R);
+      HIPCHK(hipMalloc(&pb.p, plan.size() * sizeof(int)));
+      pb.n = plan.size() * sizeof(int);
+      HIPCHK(hipMemcpy(pb.p, plan.data(), pb.n, hipMemcpyHostToDevice));
+    }
+    a.pw_plan = (const int*)pb.p;
+  }
   const size_t lds = dfmi::wdfmi_lds_bytes(a);
   if (lds > g_dev[dev].lds_per_block)
     return fail(DFMI_ERR_UNSUPPORTED, "W-DFMI: R too large for the LDS budget (" + std::to_string(lds) + " B)");
-  const double* tt;
-  if ((rc = time_axis(dev, R, cfg->f_samp, &tt))) return rc;
-  a.tt = tt;
   if (nh > 0 && a.L > 0) {
     const double* bt;
     if ((rc = basis_table(dev, a.L, nh, a.w0, st, &bt))) return rc;

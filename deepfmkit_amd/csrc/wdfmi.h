@@ -22,12 +22,13 @@ struct WdfmiLaunch {
   double w0;                     // (2 pi f_mod) / f_samp
   const double* x;               // main records x[r*rec_stride + b*R + k]
   const double* wit;             // witness records wit[r*wit_stride + k], k < R
-  const double* tt;              // time axis t[k] = k / f_samp, k < R
   const double* btab_nls;        // 2*ndata x L basis (cos rows, then sin rows), or null
   const double* btab_psi;        // 2*ndata_psi x L basis, or null
   double* tmpl;                  // workspace: nrec_t x R witness templates
   double* out;                   // 7 x (nrec*nbuf): amp, m, phi, psi, tau, dc, ssq
   int32_t* fitok;                // nrec*nbuf
+  uint64_t* probe;               // diagnostics timestamps (null: off)
+  const int* pw_plan;            // numpy summation plan over R (np_sum.h dfmi_pairwise_plan)
 };
 
 // Dynamic LDS bytes the fit kernel of this launch needs.

@@ -34,6 +34,7 @@
 #include <stdint.h>
 
 #include "dfmi_math.h"
+#include "np_sum.h"
 #include "wdfmi.h"
 
 #pragma clang fp contract(off)
@@ -41,126 +42,59 @@
 namespace dfmi {
 namespace {
 
-constexpr int SPT = 16;      // samples per thread (R <= 16 * threads)
 constexpr int MMAX = 64;     // lmdif residuals (2 * ndata <= 64)
 constexpr int NHMAX = 64;    // harmonics per evaluation (ndata, ndata_psi <= 64)
-constexpr int LEAFMAX = 256; // numpy pairwise leaves (R <= 16384)
+constexpr int LEAFMAX = 512; // numpy pairwise tree nodes (<= 256 leaves: R <= 16384)
 constexpr double kEps = 2.220446049250313e-16;
 constexpr double kPi = 3.141592653589793;
 
 __device__ __forceinline__ double inf_d() { return __builtin_huge_val(); }
 
-// ---------------------------------------------------------------------------
-// numpy pairwise summation (numpy/_core/src/umath/loops_utils.h.src: blocks of
-// <= 128 with 8 accumulators, split at n2 = n/2 - (n/2)%8). np.sum / np.mean of a
-// contiguous float64 vector use exactly this tree.
-// ---------------------------------------------------------------------------
-__device__ double leaf_sum(const double* a, int n) {
-  if (n < 8) {
-    double r = 0.0;
-    for (int i = 0; i < n; ++i) r += a[i];
-    return r;
+// Diagnostics (dfmi_set_tuning("probe", 1)): workgroup 0, thread 0 accumulates
+// s_memrealtime ticks (100 MHz) per phase into probe[slot]; results are unaffected.
+struct Probe {
+  uint64_t* p;
+  uint64_t acc[8];
+  uint64_t last;
+  __device__ void init(uint64_t* ptr) {
+    p = (ptr && blockIdx.x == 0 && threadIdx.x == 0) ? ptr : nullptr;
+    for (int i = 0; i < 8; ++i) acc[i] = 0;
+    last = p ? __builtin_amdgcn_s_memrealtime() : 0;
   }
-  double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
-  int i = 8;
-  const int e = n - (n % 8);
-  for (; i < e; i += 8) {
-    r0 += a[i + 0];
-    r1 += a[i + 1];
-    r2 += a[i + 2];
-    r3 += a[i + 3];
-    r4 += a[i + 4];
-    r5 += a[i + 5];
-    r6 += a[i + 6];
-    r7 += a[i + 7];
-  }
-  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-  for (; i < n; ++i) res += a[i];
-  return res;
-}
-
-// Leaf count of the tree over n, and (off, len) of leaf `want` (left to right).
-__device__ int pw_leaf(int n, int want, int& off, int& len) {
-  int so[24], sn[24];
-  int sp = 1, nl = 0;
-  so[0] = 0;
-  sn[0] = n;
-  off = 0;
-  len = 0;
-  while (sp) {
-    --sp;
-    const int o = so[sp], m = sn[sp];
-    if (m <= 128) {
-      if (nl == want) {
-        off = o;
-        len = m;
-      }
-      ++nl;
-      continue;
-    }
-    int n2 = m / 2;
-    n2 -= n2 % 8;
-    so[sp] = o + n2;
-    sn[sp] = m - n2;
-    ++sp;
-    so[sp] = o;
-    sn[sp] = n2;
-    ++sp;
-  }
-  return nl;
-}
-
-// Post-order combination of the leaf sums: pairwise(left) + pairwise(right).
-__device__ double pw_combine(int n, const double* leafv) {
-  int sn[24], st[24];
-  double left[24];
-  int sp = 1, li = 0;
-  sn[0] = n;
-  st[0] = 0;
-  double ret = 0.0;
-  for (;;) {
-    int top = sp - 1;
-    while (sn[top] > 128) {
-      int n2 = sn[top] / 2;
-      n2 -= n2 % 8;
-      st[top] = 1;
-      sn[sp] = n2;
-      st[sp] = 0;
-      ++sp;
-      top = sp - 1;
-    }
-    ret = leafv[li++];
-    --sp;
-    for (;;) {
-      if (sp == 0) return ret;
-      const int p = sp - 1;
-      if (st[p] == 1) {
-        left[p] = ret;
-        st[p] = 2;
-        int n2 = sn[p] / 2;
-        n2 -= n2 % 8;
-        sn[sp] = sn[p] - n2;
-        st[sp] = 0;
-        ++sp;
-        break;
-      }
-      ret = left[p] + ret;
-      --sp;
+  __device__ __forceinline__ void mark(int slot) {
+    if (p) {
+      const uint64_t t = __builtin_amdgcn_s_memrealtime();
+      acc[slot] += t - last;
+      last = t;
     }
   }
-}
+  __device__ void flush() {
+    if (p)
+      for (int i = 0; i < 8; ++i) p[i] = acc[i];
+  }
+};
 
-// np.sum of an LDS vector, leaves in parallel, tree combined by every thread.
+// np.sum of an LDS vector following a host-built plan of numpy's tree
+// (wdfmi_pairwise_plan): leaves summed in parallel, then the internal nodes level
+// by level (children before parents), every addition exactly numpy's.
+//   plan[0] = leaves nl, plan[1] = levels H, plan[2 .. 2+nl] = leaf offsets,
+//   then H+1 level starts into the node triples (dst, a, b) that follow.
 template <int T>
-__device__ double block_np_sum(const double* a, int n, double* leafv) {
-  int off, len;
-  const int nl = pw_leaf(n, 0, off, len);
-  for (int t = threadIdx.x; t < nl; t += T) {
-    pw_leaf(n, t, off, len);
-    leafv[t] = leaf_sum(a + off, len);
-  }
+__device__ double block_np_sum(const double* a, const int* __restrict__ plan, double* nodes) {
+  const int nl = plan[0], H = plan[1];
+  const int* off = plan + 2;
+  const int* lvl = off + nl + 1;
+  const int* tri = lvl + H + 1;
+  for (int t = threadIdx.x; t < nl; t += T) nodes[t] = dfmi_np_leaf_sum(a + off[t], off[t + 1] - off[t]);
   __syncthreads();
-  const double s = pw_combine(n, leafv);
+  for (int h = 0; h < H; ++h) {
+    for (int j = lvl[h] + threadIdx.x; j < lvl[h + 1]; j += T) {
+      const int* q = tri + 3 * j;
+      nodes[q[0]] = nodes[q[1]] + nodes[q[2]];
+    }
+    __syncthreads();
+  }
+  const double s = nodes[nl > 1 ? 2 * nl - 2 : 0];
   __syncthreads();
   return s;
 }
@@ -208,16 +142,28 @@ __device__ void block_reduce(double (&v)[N], double* red, Op op) {
 struct Geo {
   int R;
   double fs, period, omega;
-  const double* __restrict__ tt;
+  // t_k = k / f_samp, formed in registers: IEEE division rounds exactly like numpy's
+  // np.arange(R) / f_samp, and costs a few VALU ops instead of a dependent load.
+  __device__ __forceinline__ double t(int k) const { return (double)k / fs; }
 };
 
-// Largest i <= hi with t_i <= x (caller guarantees t_0 <= x).
-__device__ __forceinline__ int seek(const Geo& g, double x, int hi) {
+// Largest i <= hi with t_i <= x (caller guarantees t_0 <= x); also returns t_i, t_{i+1}.
+__device__ __forceinline__ int seek(const Geo& g, double x, int hi, double& ti, double& tn) {
   int i = (int)(x * g.fs);
   if (i > hi) i = hi;
   if (i < 0) i = 0;
-  while (i < hi && g.tt[i + 1] <= x) ++i;
-  while (i > 0 && g.tt[i] > x) --i;
+  ti = g.t(i);
+  tn = g.t(i + 1);
+  while (i < hi && tn <= x) {
+    ++i;
+    ti = tn;
+    tn = g.t(i + 1);
+  }
+  while (i > 0 && ti > x) {
+    --i;
+    tn = ti;
+    ti = g.t(i);
+  }
   return i;
 }
 
@@ -226,64 +172,220 @@ __device__ __forceinline__ int seek(const Geo& g, double x, int hi) {
 // t[0]; argsort places index 0 first, so the sorted/padded table is
 //   xp = [t_{R-2}-P, 0, 0, t_1 .. t_{R-2}, P],  fp = [f_{R-2}, f_0, f_{R-1}, f_1 .. f_{R-2}, f_0]
 // and x in [0, t_1) interpolates from the second zero (value f_{R-1}).
-__device__ double interp_per(const Geo& g, double x, const double* f) {
+__device__ __forceinline__ double interp_per(const Geo& g, double x, const double* f) {
   if (x != x) return x;
   const int R = g.R;
   if (x >= g.period) return f[0];
-  const int i = seek(g, x, R - 2);
+  double ti, tn;
+  const int i = seek(g, x, R - 2, ti, tn);
   if (i == 0) {
     if (x == 0.0) return f[R - 1];
-    const double slope = (f[1] - f[R - 1]) / (g.tt[1] - 0.0);
+    const double slope = (f[1] - f[R - 1]) / (tn - 0.0);
     return slope * (x - 0.0) + f[R - 1];
   }
-  const double ti = g.tt[i];
   if (x == ti) return f[i];
   const double fn = (i == R - 2) ? f[0] : f[i + 1];
-  const double slope = (fn - f[i]) / (g.tt[i + 1] - ti);
+  const double slope = (fn - f[i]) / (tn - ti);
   return slope * (x - ti) + f[i];
 }
 
 // np.interp(x, t, f) (no period): left = f[0], right = f[R-1].
-__device__ double interp_lin(const Geo& g, double x, const double* f) {
+__device__ __forceinline__ double interp_lin(const Geo& g, double x, const double* f) {
   if (x != x) return x;
   const int R = g.R;
-  if (x > g.tt[R - 1]) return f[R - 1];
+  if (x > g.period) return f[R - 1];
   if (x < 0.0) return f[0];
-  const int i = seek(g, x, R - 1);
+  double ti, tn;
+  const int i = seek(g, x, R - 1, ti, tn);
   if (i == R - 1) return f[R - 1];
-  const double ti = g.tt[i];
   if (x == ti) return f[i];
-  const double slope = (f[i + 1] - f[i]) / (g.tt[i + 1] - ti);
+  const double slope = (f[i + 1] - f[i]) / (tn - ti);
   return slope * (x - ti) + f[i];
+}
+
+// numpy's x % period for |x| < 2*period without fmod's general loop: x - period is
+// exact there (Sterbenz), x + period rounds exactly as numpy's mod += b.
+__device__ __forceinline__ double pmod(double x, double period) {
+  if (x >= 0.0 && x < period) return x == 0.0 ? 0.0 : x;
+  if (x >= period && x < 2.0 * period) return x == period ? 0.0 : x - period;
+  if (x < 0.0 && x >= -period) return x + period;
+  return dfmi_pymod(x, period);
+}
+
+// ---- batched, branch-free forms of the above (one thread's SPT samples at once) ----
+// The straight-line bodies let the compiler interleave the samples' dependent
+// chains; the exact sequential search only runs when the first guess
+// i = (int)(x * f_samp) does not bracket x (rounding at a grid point: rare).
+
+// numpy's x % period, branch-free for -period <= x < 2*period (exact there).
+__device__ __forceinline__ double pmod_fast(double x, double period, bool& slow) {
+  double r = x;
+  r = (x >= period) ? (x == period ? 0.0 : x - period) : r;
+  r = (x < 0.0) ? x + period : r;
+  r = (x == 0.0) ? 0.0 : r;
+  slow = !(x >= -period && x < 2.0 * period);
+  return r;
+}
+
+// x[s] in [0, period] (numpy's reduced abscissae) -> np.interp(x, t, f, period=t[-1])
+template <int SPT>
+__device__ __forceinline__ void interp_per_batch(const Geo& g, const double (&x)[SPT], const double* f,
+                                                 double (&out)[SPT], int nvalid) {
+  const int R = g.R;
+  int idx[SPT];
+  double ti[SPT], tn[SPT];
+  bool bad = false;
+#pragma unroll
+  for (int s = 0; s < SPT; ++s) {
+    const double xs = (x[s] == x[s]) ? x[s] : 0.0;
+    int i = (int)(xs * g.fs);
+    i = i < 0 ? 0 : (i > R - 2 ? R - 2 : i);
+    ti[s] = (double)i / g.fs;
+    tn[s] = (double)(i + 1) / g.fs;
+    const bool ok = (ti[s] <= xs) && (xs < tn[s] || i == R - 2);
+    bad = bad || (s < nvalid && !ok);
+    idx[s] = i;
+  }
+  if (bad) {
+#pragma unroll
+    for (int s = 0; s < SPT; ++s) {
+      const double xs = (x[s] == x[s]) ? x[s] : 0.0;
+      if (s < nvalid && !((ti[s] <= xs) && (xs < tn[s] || idx[s] == R - 2))) idx[s] = seek(g, xs, R - 2, ti[s], tn[s]);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < SPT; ++s) {
+    const int i = idx[s];
+    const double fl = (i == 0) ? f[R - 1] : f[i];
+    const double fr = (i == R - 2) ? f[0] : f[i + 1];
+    const double slope = (fr - fl) / (tn[s] - ti[s]);
+    double r = slope * (x[s] - ti[s]) + fl;
+    r = (x[s] == ti[s]) ? fl : r;
+    r = (x[s] >= g.period) ? f[0] : r;
+    out[s] = (x[s] != x[s]) ? x[s] : r;
+  }
+}
+
+// np.interp(x, t, f) (no period) for a batch
+template <int SPT>
+__device__ __forceinline__ void interp_lin_batch(const Geo& g, const double (&x)[SPT], const double* f,
+                                                 double (&out)[SPT], int nvalid) {
+  const int R = g.R;
+  int idx[SPT];
+  double ti[SPT], tn[SPT];
+  bool bad = false;
+#pragma unroll
+  for (int s = 0; s < SPT; ++s) {
+    const double xs = (x[s] >= 0.0 && x[s] <= g.period) ? x[s] : 0.0;  // out of range / NaN: selected below
+    int i = (int)(xs * g.fs);
+    i = i < 0 ? 0 : (i > R - 2 ? R - 2 : i);
+    ti[s] = (double)i / g.fs;
+    tn[s] = (double)(i + 1) / g.fs;
+    const bool ok = (ti[s] <= xs) && (xs < tn[s] || i == R - 2);
+    bad = bad || (s < nvalid && !ok);
+    idx[s] = i;
+  }
+  if (bad) {
+#pragma unroll
+    for (int s = 0; s < SPT; ++s) {
+      const double xs = (x[s] >= 0.0 && x[s] <= g.period) ? x[s] : 0.0;
+      if (s < nvalid && !((ti[s] <= xs) && (xs < tn[s] || idx[s] == R - 2))) {
+        idx[s] = seek(g, xs, R - 2, ti[s], tn[s]);
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < SPT; ++s) {
+    const int i = idx[s];
+    const double fl = f[i], fr = f[i + 1];
+    const double slope = (fr - fl) / (tn[s] - ti[s]);
+    double r = slope * (x[s] - ti[s]) + fl;
+    r = (x[s] == ti[s]) ? fl : r;
+    r = (x[s] >= g.period) ? f[R - 1] : r;  // x == t[R-1] and beyond: right value
+    r = (x[s] < 0.0) ? f[0] : r;
+    out[s] = (x[s] != x[s]) ? x[s] : r;
+  }
+}
+
+// sin/cos for |x| < 2^19 without branches: Cody-Waite reduction by pi/2 in three
+// parts, fdlibm kernel polynomials on [-pi/4, pi/4], quadrant by select. Callers
+// use the library sincos for larger arguments (not produced by these fits).
+__device__ __forceinline__ void sincos_fast(double x, double* sn, double* cs) {
+  const double invpio2 = 6.36619772367581382433e-01;
+  const double p1 = 1.57079632673412561417e+00, p2 = 6.07710050630396597660e-11, p3 = 2.02226624871116645580e-21;
+  const double q = rint(x * invpio2);
+  double r = fma(-q, p1, x);
+  r = fma(-q, p2, r);
+  r = fma(-q, p3, r);
+  const double z = r * r;
+  const double ps = fma(z, fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
+                                              2.75573137070700676789e-06), -1.98412698298579493134e-04),
+                             8.33333333332248946124e-03), -1.66666666666666324348e-01);
+  const double sr = fma(r * z, ps, r);
+  const double pc = fma(z, fma(z, fma(z, fma(z, fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+                                              -2.75573143513906633035e-07), 2.48015872894767294178e-05),
+                             -1.38888888888741095749e-03), 4.16666666666666019037e-02);
+  const double cr = fma(z * z, pc, fma(-0.5, z, 1.0));
+  const int qi = ((int)q) & 3;
+  *sn = (qi == 0) ? sr : (qi == 1) ? cr : (qi == 2) ? -sr : -cr;
+  *cs = (qi == 0) ? cr : (qi == 1) ? -sr : (qi == 2) ? -cr : sr;
 }
 
 // W-DFMI phase difference (fitters.py:533-539 / 611-617 / 688-694):
 //   shifted = interp(t - (-psi/omega), t, tab, period), delayed = interp(t - tau, t, shifted, period)
-template <int T>
-__device__ void wdfmi_delta(const Geo& g, const double* tab, double* sh, double tau, double psi,
-                            double (&d)[SPT]) {
+template <int T, int SPT>
+__device__ __forceinline__ void wdfmi_delta(const Geo& g, const double* tab, double* sh, double tau, double psi,
+                                            double (&d)[SPT]) {
   const double c = (-psi) / g.omega;
+  const int nvalid = (g.R - (int)threadIdx.x + T - 1) / T;
+  double x[SPT], y[SPT];
+  bool slow = false;
+#pragma unroll
+  for (int s = 0; s < SPT; ++s) {
+    bool sl;
+    x[s] = pmod_fast(g.t(threadIdx.x + T * s) - c, g.period, sl);
+    slow = slow || sl;
+  }
+  if (slow) {
+#pragma unroll
+    for (int s = 0; s < SPT; ++s) x[s] = dfmi_pymod(g.t(threadIdx.x + T * s) - c, g.period);
+  }
+  interp_per_batch<SPT>(g, x, tab, y, nvalid);
 #pragma unroll
   for (int s = 0; s < SPT; ++s) {
     const int k = threadIdx.x + T * s;
-    if (k < g.R) sh[k] = interp_per(g, dfmi_pymod(g.tt[k] - c, g.period), tab);
+    if (k < g.R) sh[k] = y[s];
   }
   __syncthreads();
+  slow = false;
 #pragma unroll
   for (int s = 0; s < SPT; ++s) {
-    const int k = threadIdx.x + T * s;
-    if (k < g.R) d[s] = interp_per(g, dfmi_pymod(g.tt[k] - tau, g.period), sh) - sh[k];
+    bool sl;
+    x[s] = pmod_fast(g.t(threadIdx.x + T * s) - tau, g.period, sl);
+    slow = slow || sl;
   }
+  if (slow) {
+#pragma unroll
+    for (int s = 0; s < SPT; ++s) x[s] = dfmi_pymod(g.t(threadIdx.x + T * s) - tau, g.period);
+  }
+  interp_per_batch<SPT>(g, x, sh, d, nvalid);
+#pragma unroll
+  for (int s = 0; s < SPT; ++s) d[s] = d[s] - y[s];
   __syncthreads();
 }
 
 // HW-DFMI (fitters.py:848-852): delta = tmpl - interp(t - tau, t, tmpl)
-template <int T>
-__device__ void hw_delta(const Geo& g, const double* tab, double tau, double (&d)[SPT]) {
+template <int T, int SPT>
+__device__ __forceinline__ void hw_delta(const Geo& g, const double* tab, double tau, double (&d)[SPT]) {
+  const int nvalid = (g.R - (int)threadIdx.x + T - 1) / T;
+  double x[SPT];
+#pragma unroll
+  for (int s = 0; s < SPT; ++s) x[s] = g.t(threadIdx.x + T * s) - tau;
+  interp_lin_batch<SPT>(g, x, tab, d, nvalid);
 #pragma unroll
   for (int s = 0; s < SPT; ++s) {
     const int k = threadIdx.x + T * s;
-    if (k < g.R) d[s] = tab[k] - interp_lin(g, g.tt[k] - tau, tab);
+    d[s] = (k < g.R) ? tab[k] - d[s] : 0.0;
   }
 }
 
@@ -298,18 +400,26 @@ struct VP {
   bool full;
 };
 
-template <int T>
-__device__ VP varpro(const Geo& g, double* red, const double (&d)[SPT], const double (&v)[SPT], double (&bi)[SPT],
+template <int T, int SPT>
+__device__ __forceinline__ VP varpro(const Geo& g, double* red, const double (&d)[SPT], const double (&v)[SPT], double (&bi)[SPT],
                      double (&bq)[SPT], bool want_res) {
   double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  bool big = false;
+#pragma unroll
+  for (int q = 0; q < SPT; ++q) {
+    sincos_fast(d[q], &bq[q], &bi[q]);
+    big = big || !(fabs(d[q]) < 524288.0);
+  }
+  if (big) {
+#pragma unroll
+    for (int q = 0; q < SPT; ++q)
+      if (!(fabs(d[q]) < 524288.0)) sincos(d[q], &bq[q], &bi[q]);
+  }
 #pragma unroll
   for (int q = 0; q < SPT; ++q) {
     const int k = threadIdx.x + T * q;
     if (k < g.R) {
-      double sn, cs;
-      sincos(d[q], &sn, &cs);
-      bi[q] = cs;
-      bq[q] = sn;
+      const double cs = bi[q], sn = bq[q];
       s[0] += cs * cs;
       s[1] += cs * sn;
       s[2] += sn * sn;
@@ -338,8 +448,8 @@ __device__ VP varpro(const Geo& g, double* red, const double (&d)[SPT], const do
         t2[1] += w * v[q];
       }
     }
-    block_reduce<T, 2>(t2, red, OpAdd());
-    r22sq = t2[0];
+      block_reduce<T, 2>(t2, red, OpAdd());
+      r22sq = t2[0];
     wv = t2[1];
     // singular values of [[r11, r12], [0, r22]]
     const double r12sq = (b * b) / a;
@@ -364,8 +474,8 @@ __device__ VP varpro(const Geo& g, double* red, const double (&d)[SPT], const do
           t1[0] += e * e;
         }
       }
-      block_reduce<T, 1>(t1, red, OpAdd());
-      r.res = t1[0];
+          block_reduce<T, 1>(t1, red, OpAdd());
+          r.res = t1[0];
     }
   } else {
     // rank <= 1: minimum-norm solution on the dominant right singular vector
@@ -1182,9 +1292,9 @@ __global__ __launch_bounds__(T) void wdfmi_template_kernel(WdfmiLaunch a) {
   double* __restrict__ out = a.tmpl + rec * R;
   for (int k = threadIdx.x; k < R; k += T) buf[k] = w[k];
   __syncthreads();
-  const double dt = a.tt[1] - a.tt[0];
+  const double dt = 1.0 / a.f_samp - 0.0 / a.f_samp;  // t[1] - t[0]
   if (a.method != kHwdfmi) {
-    const double mean = block_np_sum<T>(buf, R, leafv) / (double)R;
+    const double mean = block_np_sum<T>(buf, a.pw_plan, leafv) / (double)R;
     double mx[1] = {0.0};
     for (int k = threadIdx.x; k < R; k += T) {
       const double v = buf[k] - mean;
@@ -1222,21 +1332,37 @@ __global__ __launch_bounds__(T) void wdfmi_template_kernel(WdfmiLaunch a) {
 }
 
 struct LdsMap {
-  double *tab, *sh, *mv, *bins, *hout, *hmeas, *red, *leafv;
+  double *tab, *sh, *vac, *mv, *bins, *hout, *hmeas, *red, *leafv;
 };
 
+// All methods: tab (witness template) | sh (shifted phase / scratch) | vac (the
+// buffer minus its mean) | red | leafv; nls / seq add the model vector, the phase
+// bins and the harmonic vectors.
+__host__ __device__ inline bool needs_harmonics(int method) { return method == kWdfmiNLS || method == kWdfmiSeq; }
+
+__host__ __device__ inline size_t lds_doubles(int method, int R, int L, int threads) {
+  const int Lp = ((L > 0 ? L : 1) + 1) & ~1;
+  size_t n = 3 * (size_t)R + (threads / 64) * 8 + LEAFMAX;
+  if (needs_harmonics(method)) n += (size_t)R + Lp + 4 * NHMAX;
+  return n;
+}
+
 template <int T>
-__device__ LdsMap lds_map(double* lds, int R, int L) {
+__device__ LdsMap lds_map(double* lds, int method, int R, int L) {
   LdsMap m;
   const int Lp = ((L > 0 ? L : 1) + 1) & ~1;
   m.tab = lds;
   m.sh = m.tab + R;
-  m.mv = m.sh + R;
-  m.bins = m.mv + R;
-  m.hout = m.bins + Lp;
-  m.hmeas = m.hout + 2 * NHMAX;
-  m.red = m.hmeas + 2 * NHMAX;
+  m.vac = m.sh + R;
+  m.red = m.vac + R;
   m.leafv = m.red + (T / 64) * 8;
+  m.mv = m.bins = m.hout = m.hmeas = nullptr;
+  if (needs_harmonics(method)) {
+    m.mv = m.leafv + LEAFMAX;
+    m.bins = m.mv + R;
+    m.hout = m.bins + Lp;
+    m.hmeas = m.hout + 2 * NHMAX;
+  }
   return m;
 }
 
@@ -1257,31 +1383,98 @@ __device__ void put_row(const WdfmiLaunch& a, int64_t idx, double amp, double m,
 }
 
 // Buffer prologue: raw samples into registers and LDS, dc = np.mean(buffer).
+// Buffer prologue: dc = np.mean(buffer) (raw samples staged in sh), vac = buffer - dc;
+// with keep_raw the raw samples are also left in mv (WDFMI_NLS demodulates them).
 template <int T>
-__device__ double load_buffer(const WdfmiLaunch& a, const LdsMap& L, const double* __restrict__ xb, double (&xr)[SPT]) {
+__device__ double load_buffer(const WdfmiLaunch& a, const LdsMap& L, const double* __restrict__ xb, bool keep_raw) {
+  for (int k = threadIdx.x; k < a.R; k += T) {
+    const double v = xb[k];
+    L.sh[k] = v;
+    if (keep_raw) L.mv[k] = v;
+  }
+  __syncthreads();
+  const double dc = block_np_sum<T>(L.sh, a.pw_plan, L.leafv) / (double)a.R;
+  for (int k = threadIdx.x; k < a.R; k += T) L.vac[k] = L.sh[k] - dc;
+  __syncthreads();
+  return dc;
+}
+
+// One cost evaluation, shared by every optimiser call site (a single out-of-line
+// copy keeps the kernels small; the per-sample arrays live in its registers).
+enum : int {
+  kEvHW = 1,      // HW-DFMI delta (non-periodic), else the W-DFMI shifted/delayed delta
+  kEvRes = 2,     // VarPro residual sum of squares
+  kEvModel = 4,   // mv[k] = p0 cos(d) - p1 sin(d) (WDFMI_SequentialFitter stage 2)
+  kEvPtp = 8,     // max / min of delta (HWDFMI m)
+  kEvNls = 16,    // mv[k] = amp cos(phi + d), no VarPro (WDFMI_NLSFitter residual)
+};
+
+struct EvalOut {
+  double p0, p1, res, dmax, dmin;
+  bool full;
+};
+
+template <int T, int SPT>
+__device__ __attribute__((noinline)) EvalOut evaluate(const Geo g, const LdsMap L, double tau, double psi, int flags,
+                                                      double amp, double phi) {
+  double d[SPT], v[SPT], bi[SPT], bq[SPT];
+  if (flags & kEvHW) hw_delta<T, SPT>(g, L.tab, tau, d);
+  else wdfmi_delta<T, SPT>(g, L.tab, L.sh, tau, psi, d);
+  EvalOut o;
+  o.p0 = o.p1 = o.res = o.dmax = o.dmin = 0.0;
+  o.full = false;
+  if (flags & kEvNls) {
+#pragma unroll
+    for (int s = 0; s < SPT; ++s) {
+      const int k = threadIdx.x + T * s;
+      if (k < g.R) L.mv[k] = amp * cos(phi + d[s]);
+    }
+    return o;
+  }
 #pragma unroll
   for (int s = 0; s < SPT; ++s) {
     const int k = threadIdx.x + T * s;
-    xr[s] = 0.0;
-    if (k < a.R) {
-      xr[s] = xb[k];
-      L.mv[k] = xr[s];
+    v[s] = (k < g.R) ? L.vac[k] : 0.0;
+  }
+  const VP r = varpro<T, SPT>(g, L.red, d, v, bi, bq, (flags & kEvRes) != 0);
+  o.p0 = r.p0;
+  o.p1 = r.p1;
+  o.res = r.res;
+  o.full = r.full;
+  if (flags & kEvModel) {
+#pragma unroll
+    for (int s = 0; s < SPT; ++s) {
+      const int k = threadIdx.x + T * s;
+      if (k < g.R) L.mv[k] = r.p0 * bi[s] - r.p1 * bq[s];
     }
   }
-  __syncthreads();
-  return block_np_sum<T>(L.mv, a.R, L.leafv) / (double)a.R;
+  if (flags & kEvPtp) {
+    double mx[1] = {-inf_d()}, mn[1] = {inf_d()};
+#pragma unroll
+    for (int s = 0; s < SPT; ++s) {
+      const int k = threadIdx.x + T * s;
+      if (k < g.R) {
+        mx[0] = OpMax()(mx[0], d[s]);
+        mn[0] = OpMin()(mn[0], d[s]);
+      }
+    }
+    block_reduce<T, 1>(mx, L.red, OpMax());
+    block_reduce<T, 1>(mn, L.red, OpMin());
+    o.dmax = mx[0];
+    o.dmin = mn[0];
+  }
+  return o;
 }
 
-template <int T, int METHOD>
+template <int T, int SPT, int METHOD>
 __global__ __launch_bounds__(T) void wdfmi_fit_kernel(WdfmiLaunch a) {
   extern __shared__ double lds[];
   const int R = a.R;
-  const LdsMap L = lds_map<T>(lds, R, a.L);
+  const LdsMap L = lds_map<T>(lds, METHOD, R, a.L);
   Geo g;
   g.R = R;
   g.fs = a.f_samp;
-  g.tt = a.tt;
-  g.period = a.tt[R - 1];
+  g.period = g.t(R - 1);  // t[-1]
   g.omega = (2.0 * kPi) * a.f_mod;
   const double m_scale = (2.0 * kPi) * a.df;
 
@@ -1298,24 +1491,28 @@ __global__ __launch_bounds__(T) void wdfmi_fit_kernel(WdfmiLaunch a) {
   const double* __restrict__ tsrc = a.tmpl + (a.wit_stride == 0 ? 0 : rec) * (int64_t)R;
   for (int k = threadIdx.x; k < R; k += T) L.tab[k] = tsrc[k];
   __syncthreads();
-
-  double xr[SPT], v[SPT], d[SPT], bi[SPT], bq[SPT];
+  Probe pr;
+  pr.init(a.probe);
+  auto ev = [&](double tau, double psi, int flags, double amp = 0.0, double phi = 0.0) -> EvalOut {
+    pr.mark(5);
+    const EvalOut o = evaluate<T, SPT>(g, L, tau, psi, flags, amp, phi);
+    pr.mark(1);
+    if (pr.p) ++pr.acc[7];
+    return o;
+  };
 
   if constexpr (METHOD == kWdfmiOrtho) {
     double guess[2] = {a.tau_init, a.init_psi};
     for (int64_t b = b0; b < b1; ++b) {
-      const double dc = load_buffer<T>(a, L, a.x + rec * a.rec_stride + b * R, xr);
-#pragma unroll
-      for (int s = 0; s < SPT; ++s) v[s] = xr[s] - dc;
+      const double dc = load_buffer<T>(a, L, a.x + rec * a.rec_stride + b * R, false);
+      pr.mark(0);
       auto cost = [&](double tau, double psi) -> double {
-        wdfmi_delta<T>(g, L.tab, L.sh, tau, psi, d);
-        const VP r = varpro<T>(g, L.red, d, v, bi, bq, true);
-        return r.full ? r.res : inf_d();
+        const EvalOut o = ev(tau, psi, kEvRes);
+        return o.full ? o.res : inf_d();
       };
       double x[2];
       const bool ok = nelder_mead2(cost, guess, x);
-      wdfmi_delta<T>(g, L.tab, L.sh, x[0], x[1], d);
-      const VP r = varpro<T>(g, L.red, d, v, bi, bq, true);
+      const EvalOut r = ev(x[0], x[1], kEvRes);
       const double amp = sqrt(r.p0 * r.p0 + r.p1 * r.p1);
       put_row<T>(a, rec * a.nbuf + b, amp, m_scale * x[0], atan2(-r.p1, r.p0), x[1], x[0], dc,
                  r.full ? r.res : 0.0, ok ? 1 : 0);
@@ -1325,68 +1522,40 @@ __global__ __launch_bounds__(T) void wdfmi_fit_kernel(WdfmiLaunch a) {
   } else if constexpr (METHOD == kHwdfmi) {
     double guess = a.tau_init;
     for (int64_t b = b0; b < b1; ++b) {
-      const double dc = load_buffer<T>(a, L, a.x + rec * a.rec_stride + b * R, xr);
-#pragma unroll
-      for (int s = 0; s < SPT; ++s) v[s] = xr[s] - dc;
+      const double dc = load_buffer<T>(a, L, a.x + rec * a.rec_stride + b * R, false);
+      pr.mark(0);
       auto cost = [&](double tau) -> double {
-        hw_delta<T>(g, L.tab, tau, d);
-        const VP r = varpro<T>(g, L.red, d, v, bi, bq, true);
-        return r.full ? r.res : inf_d();
+        const EvalOut o = ev(tau, 0.0, kEvHW | kEvRes);
+        return o.full ? o.res : inf_d();
       };
       const double lo = guess != 0.0 ? guess * 0.8 : -1e-9;
       const double hi = guess != 0.0 ? guess * 1.2 : 1e-9;
       bool bok;
       const double tau = brent(cost, lo, hi, &bok);
-      hw_delta<T>(g, L.tab, tau, d);
-      const VP r = varpro<T>(g, L.red, d, v, bi, bq, true);
-      double mm[2] = {-inf_d(), inf_d()};
-#pragma unroll
-      for (int s = 0; s < SPT; ++s) {
-        const int k = threadIdx.x + T * s;
-        if (k < R) {
-          mm[0] = OpMax()(mm[0], d[s]);
-          mm[1] = OpMin()(mm[1], d[s]);
-        }
-      }
-      double mx1[1] = {mm[0]}, mn1[1] = {mm[1]};
-      block_reduce<T, 1>(mx1, L.red, OpMax());
-      block_reduce<T, 1>(mn1, L.red, OpMin());
+      const EvalOut r = ev(tau, 0.0, kEvHW | kEvRes | kEvPtp);
       const double amp = sqrt(r.p0 * r.p0 + r.p1 * r.p1);
-      put_row<T>(a, rec * a.nbuf + b, amp, (mx1[0] - mn1[0]) / 2.0, atan2(-r.p1, r.p0), 0.0, tau, dc,
+      put_row<T>(a, rec * a.nbuf + b, amp, (r.dmax - r.dmin) / 2.0, atan2(-r.p1, r.p0), 0.0, tau, dc,
                  r.full ? r.res : 0.0, 1);
       guess = tau;
     }
   } else if constexpr (METHOD == kWdfmiSeq) {
     const int nh = a.ndata_psi;
     for (int64_t b = b0; b < b1; ++b) {
-      const double dc = load_buffer<T>(a, L, a.x + rec * a.rec_stride + b * R, xr);
-#pragma unroll
-      for (int s = 0; s < SPT; ++s) v[s] = xr[s] - dc;
+      const double dc = load_buffer<T>(a, L, a.x + rec * a.rec_stride + b * R, false);
+      pr.mark(0);
       // stage 1: tau by Brent on the VarPro cost at psi = init_psi
       auto cost_tau = [&](double tau) -> double {
-        wdfmi_delta<T>(g, L.tab, L.sh, tau, a.init_psi, d);
-        const VP r = varpro<T>(g, L.red, d, v, bi, bq, true);
-        return r.full ? r.res : inf_d();
+        const EvalOut o = ev(tau, a.init_psi, kEvRes);
+        return o.full ? o.res : inf_d();
       };
       const double lo = a.tau_init > 0.0 ? a.tau_init * 0.9 : -1e-9;
       const double hi = a.tau_init > 0.0 ? a.tau_init * 1.1 : 1e-9;
       bool bok;
       const double tau_fit = brent(cost_tau, lo, hi, &bok);
       // stage 2: psi by bounded Brent on the variance of the unwrapped harmonic phase error
-#pragma unroll
-      for (int s = 0; s < SPT; ++s) {
-        const int k = threadIdx.x + T * s;
-        if (k < R) L.mv[k] = v[s];
-      }
-      harmonics<T>(g, nh, a.L, a.btab_psi, a.w0, L.mv, L.bins, L.hmeas);
+      harmonics<T>(g, nh, a.L, a.btab_psi, a.w0, L.vac, L.bins, L.hmeas);
       auto cost_psi = [&](double dpsi) -> double {
-        wdfmi_delta<T>(g, L.tab, L.sh, tau_fit, a.init_psi + dpsi, d);
-        const VP r = varpro<T>(g, L.red, d, v, bi, bq, false);
-#pragma unroll
-        for (int s = 0; s < SPT; ++s) {
-          const int k = threadIdx.x + T * s;
-          if (k < R) L.mv[k] = r.p0 * bi[s] - r.p1 * bq[s];
-        }
+        ev(tau_fit, a.init_psi + dpsi, kEvModel);
         harmonics<T>(g, nh, a.L, a.btab_psi, a.w0, L.mv, L.bins, L.hout);
         // np.angle(alpha_meas * conj(alpha_model)), np.unwrap, np.var (every thread)
         double pe[NHMAX];
@@ -1408,18 +1577,17 @@ __global__ __launch_bounds__(T) void wdfmi_fit_kernel(WdfmiLaunch a) {
           cum = (i == 1) ? corr : cum + corr;
           up[i] = pe[i] + cum;
         }
-        const double mean = leaf_sum(up, nh) / (double)nh;
+        const double mean = dfmi_np_leaf_sum(up, nh) / (double)nh;
         for (int i = 0; i < nh; ++i) {
           const double x = up[i] - mean;
           up[i] = x * x;
         }
-        return leaf_sum(up, nh) / (double)nh;
+        return dfmi_np_leaf_sum(up, nh) / (double)nh;
       };
       const double dpsi = fminbound(cost_psi, -kPi / 2.0, kPi / 2.0);
       const double psi_fit = a.init_psi + dpsi;
       // stage 3: linear fit at (tau, psi)
-      wdfmi_delta<T>(g, L.tab, L.sh, tau_fit, psi_fit, d);
-      const VP r = varpro<T>(g, L.red, d, v, bi, bq, true);
+      const EvalOut r = ev(tau_fit, psi_fit, kEvRes);
       const double amp = sqrt(r.p0 * r.p0 + r.p1 * r.p1);
       put_row<T>(a, rec * a.nbuf + b, amp, m_scale * tau_fit, atan2(-r.p1, r.p0), psi_fit, tau_fit, dc,
                  r.full ? r.res : 0.0, 1);
@@ -1428,16 +1596,12 @@ __global__ __launch_bounds__(T) void wdfmi_fit_kernel(WdfmiLaunch a) {
     const int nd = a.ndata, m = 2 * a.ndata;
     double guess[NP] = {a.init_a, a.tau_init, a.init_phi, a.init_psi};
     for (int64_t b = b0; b < b1; ++b) {
-      const double dc = load_buffer<T>(a, L, a.x + rec * a.rec_stride + b * R, xr);
-      // QI of the raw buffer (mv still holds it)
+      const double dc = load_buffer<T>(a, L, a.x + rec * a.rec_stride + b * R, true);
+      pr.mark(0);
+      // QI of the raw buffer (fitters.py:551-556)
       harmonics<T>(g, nd, a.L, a.btab_nls, a.w0, L.mv, L.bins, L.hmeas);
       auto fcn = [&](const double (&p)[NP], double* fv) {
-        wdfmi_delta<T>(g, L.tab, L.sh, p[1], p[3], d);
-#pragma unroll
-        for (int s = 0; s < SPT; ++s) {
-          const int k = threadIdx.x + T * s;
-          if (k < R) L.mv[k] = p[0] * cos(p[2] + d[s]);
-        }
+        ev(p[1], p[3], kEvNls, p[0], p[2]);
         harmonics<T>(g, nd, a.L, a.btab_nls, a.w0, L.mv, L.bins, L.hout);
         for (int i = 0; i < m; ++i) fv[i] = L.hout[i] - L.hmeas[i];
       };
@@ -1445,15 +1609,16 @@ __global__ __launch_bounds__(T) void wdfmi_fit_kernel(WdfmiLaunch a) {
       double fvec[MMAX];
       const int info = lmdif(fcn, m, x, fvec);
       for (int i = 0; i < m; ++i) fvec[i] = fvec[i] * fvec[i];
-      const double ssq = leaf_sum(fvec, m);
+      const double ssq = dfmi_np_leaf_sum(fvec, m);
       put_row<T>(a, rec * a.nbuf + b, x[0], m_scale * x[1], x[2], x[3], x[1], dc, ssq,
                  (info >= 1 && info <= 4) ? 1 : 0);
       for (int i = 0; i < NP; ++i) guess[i] = x[i];
     }
   }
+  pr.flush();
 }
 
-template <int T>
+template <int T, int SPT>
 hipError_t launch_t(const WdfmiLaunch& a, hipStream_t st) {
   const int64_t ntmpl = a.wit_stride == 0 ? 1 : a.nrec;
   const size_t tl = (size_t)(2 * a.R + LEAFMAX + (T / 64) * 8) * 8;
@@ -1464,16 +1629,16 @@ hipError_t launch_t(const WdfmiLaunch& a, hipStream_t st) {
   const int64_t grid = a.method == kWdfmiSeq ? a.nrec * a.nbuf : a.nrec;
   switch (a.method) {
     case kWdfmiNLS:
-      hipLaunchKernelGGL((wdfmi_fit_kernel<T, kWdfmiNLS>), dim3((unsigned)grid), dim3(T), fl, st, a);
+      hipLaunchKernelGGL((wdfmi_fit_kernel<T, SPT, kWdfmiNLS>), dim3((unsigned)grid), dim3(T), fl, st, a);
       break;
     case kWdfmiOrtho:
-      hipLaunchKernelGGL((wdfmi_fit_kernel<T, kWdfmiOrtho>), dim3((unsigned)grid), dim3(T), fl, st, a);
+      hipLaunchKernelGGL((wdfmi_fit_kernel<T, SPT, kWdfmiOrtho>), dim3((unsigned)grid), dim3(T), fl, st, a);
       break;
     case kWdfmiSeq:
-      hipLaunchKernelGGL((wdfmi_fit_kernel<T, kWdfmiSeq>), dim3((unsigned)grid), dim3(T), fl, st, a);
+      hipLaunchKernelGGL((wdfmi_fit_kernel<T, SPT, kWdfmiSeq>), dim3((unsigned)grid), dim3(T), fl, st, a);
       break;
     default:
-      hipLaunchKernelGGL((wdfmi_fit_kernel<T, kHwdfmi>), dim3((unsigned)grid), dim3(T), fl, st, a);
+      hipLaunchKernelGGL((wdfmi_fit_kernel<T, SPT, kHwdfmi>), dim3((unsigned)grid), dim3(T), fl, st, a);
       break;
   }
   return hipGetLastError();
@@ -1481,18 +1646,14 @@ hipError_t launch_t(const WdfmiLaunch& a, hipStream_t st) {
 
 }  // namespace
 
-size_t wdfmi_lds_bytes(const WdfmiLaunch& a) {
-  const int Lp = ((a.L > 0 ? a.L : 1) + 1) & ~1;
-  return (size_t)(3 * (size_t)a.R + Lp + 4 * NHMAX + (a.threads / 64) * 8 + LEAFMAX) * 8;
-}
+size_t wdfmi_lds_bytes(const WdfmiLaunch& a) { return lds_doubles(a.method, a.R, a.L, a.threads) * 8; }
 
 hipError_t wdfmi_launch(const WdfmiLaunch& a, hipStream_t st) {
   if (a.nrec == 0 || a.nbuf == 0) return hipSuccess;
-  switch (a.threads) {
-    case 256: return launch_t<256>(a, st);
-    case 512: return launch_t<512>(a, st);
-    default: return launch_t<1024>(a, st);
-  }
+  // one wave per SIMD and 16 samples per thread measured fastest at R = 4000 (256 vs
+  // 512 vs 1024 threads: scripts/bench_wdfmi.py --threads); larger R widens the group
+  if (a.R <= 16 * 256) return launch_t<256, 16>(a, st);
+  return launch_t<1024, 16>(a, st);
 }
 
 }  // namespace dfmi

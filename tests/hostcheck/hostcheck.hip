@@ -8,8 +8,12 @@
 #include <vector>
 #include "../../deepfmkit_amd/csrc/dfmi_math.h"
 #include "../../deepfmkit_amd/csrc/lm.h"
+#include "../../deepfmkit_amd/csrc/np_sum.h"
 
 extern "C" {
+
+// numpy summation order (np_sum.h): the plan the W-DFMI kernels run for their means.
+double hc_np_sum(const double* a, int n) { return dfmi_plan_sum_host(a, n); }
 
 void hc_bessel_table(double x, int N, double* out) { dfmi_bessel_table(x, N, out); }
 

@@ -74,3 +74,15 @@ def test_host_lm_on_reference_qi(hc, records_npz, manifest):
     for i, k in ((0, "amp"), (1, "m"), (3, "psi")):
         assert np.abs(p[:, i] - records_npz["config1_c1_" + k]).max() <= 1e-9, k
     assert wrapped(p[:, 2] - records_npz["config1_c1_phi"]).max() <= 1e-9
+
+
+def test_numpy_summation_plan_is_bit_exact(hc):
+    """np_sum.h's plan (the device means of the W-DFMI kernels) == np.sum bit for bit,
+    across the block, split and 8192-chunk boundaries."""
+    hc.hc_np_sum.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    hc.hc_np_sum.restype = ctypes.c_double
+    rng = np.random.default_rng(0)
+    for n in [1, 2, 7, 8, 9, 100, 127, 128, 129, 200, 255, 256, 257, 1000, 3999, 4000, 4001, 5000, 8191, 8192,
+              8193, 12345, 16384, 16385, 30001]:
+        a = rng.standard_normal(n) * 10 ** rng.uniform(-3, 3, n)
+        assert hc.hc_np_sum(a.ctypes.data, n) == np.sum(a), n

@@ -388,16 +388,18 @@ __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int
 // probe (diagnostics, may be null): s_memrealtime at the entry of workgroups 0 and
 // gridDim-1 and at the exit of workgroup 0's wave 0 ([3], [4], [5]).
 template <int MAXSLOT, int LOADS, bool ROWS>
-__global__ __launch_bounds__(kBlockThreads) void demod_bins_kernel(
+__device__ __forceinline__ void bins_kernel_body(
     const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
     const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc, int spacer,
-    uint64_t* __restrict__ probe) {
+    uint64_t* __restrict__ probe, int block0 = 0) {
+  // block0: leading workgroups that play another role (the fused seed kernel, seed.h)
+  const int bid = (int)blockIdx.x - block0;
   if (probe && threadIdx.x == 0) {
-    if (blockIdx.x == 0) probe[3] = __builtin_amdgcn_s_memrealtime();
-    if (blockIdx.x == gridDim.x - 1) probe[4] = __builtin_amdgcn_s_memrealtime();
+    if (bid == 0) probe[3] = __builtin_amdgcn_s_memrealtime();
+    if ((int)blockIdx.x == (int)gridDim.x - 1) probe[4] = __builtin_amdgcn_s_memrealtime();
   }
-  const int nwork = (int)gridDim.x - spacer;
-  if ((int)blockIdx.x >= nwork) return;
+  const int nwork = (int)gridDim.x - block0 - spacer;
+  if (bid < 0 || bid >= nwork) return;
   extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
   const int ntab = 2 * ndata * L;
   for (int i = threadIdx.x; i < ntab; i += kBlockThreads) lds_dyn[i] = tab[i];
@@ -413,10 +415,27 @@ __global__ __launch_bounds__(kBlockThreads) void demod_bins_kernel(
     pbase[j] = 2 * (lane + 64 * j);
     pval[j] = (j < nslot) && (pbase[j] < L);
   }
-  for (int64_t s = (int64_t)blockIdx.x * kWavesPerBlock + wave; s < nseg; s += (int64_t)nwork * kWavesPerBlock)
+  for (int64_t s = (int64_t)bid * kWavesPerBlock + wave; s < nseg; s += (int64_t)nwork * kWavesPerBlock)
     bins_segment<MAXSLOT, LOADS, true, kHarmBlock, ROWS>(x + s * seg_stride, R, L, ndata, lds_dyn, ybin, lane, pval,
                                                            pbase, qi, qi_ld, s, dc);
-  if (probe && threadIdx.x == 0 && blockIdx.x == 0) probe[5] = __builtin_amdgcn_s_memrealtime();
+  if (probe && threadIdx.x == 0 && bid == 0) probe[5] = __builtin_amdgcn_s_memrealtime();
+}
+
+template <int MAXSLOT, int LOADS, bool ROWS>
+__global__ __launch_bounds__(kBlockThreads) void demod_bins_kernel(
+    const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
+    const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc, int spacer,
+    uint64_t* __restrict__ probe) {
+  bins_kernel_body<MAXSLOT, LOADS, ROWS>(x, nseg, seg_stride, R, L, ndata, tab, qi, qi_ld, dc, spacer, probe);
+}
+
+// Same kernel held to <= 128 VGPRs, i.e. 4 waves per SIMD (4 workgroups per CU).
+template <int MAXSLOT, int LOADS, bool ROWS>
+__global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void demod_bins4_kernel(
+    const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
+    const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc, int spacer,
+    uint64_t* __restrict__ probe) {
+  bins_kernel_body<MAXSLOT, LOADS, ROWS>(x, nseg, seg_stride, R, L, ndata, tab, qi, qi_ld, dc, spacer, probe);
 }
 
 // Fallback when no short integer period exists: per-sample angles

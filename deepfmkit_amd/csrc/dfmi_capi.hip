@@ -204,6 +204,8 @@ struct Tuning {
   int demod_kernel = 1;        // 1: bin-in-LDS kernel where it applies, 0: cycle-aligned fold kernel
   int seed_bins = 1;           // 1: seed step with the LDS fold + LDS-resident QI (seed.h seed_bins_kernel)
   int seed_order = 1;          // 1: seed on the caller's stream, bulk demodulation on the side stream
+  int demod_occ4 = 0;          // 1: bin kernel held to 128 VGPRs (4 waves per SIMD)
+  int seed_fused = 1;          // 1: seed + bulk demodulation in one launch on the caller's stream
 };
 Tuning g_tune;
 std::string g_last_demod;     // kernel variant of the last demodulation launch (dfmi_last_demod_kernel)
@@ -272,7 +274,7 @@ int launch_fold_ms(int ms, const double* x, int64_t nseg, int64_t stride, int R,
 template <int MS, bool ROWS>
 int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tab,
                   double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu, size_t lds) {
-  auto kern = dfmi::demod_bins_kernel<MS, 8, ROWS>;
+  auto kern = g_tune.demod_occ4 ? dfmi::demod_bins4_kernel<MS, 8, ROWS> : dfmi::demod_bins_kernel<MS, 8, ROWS>;
   int per_cu = 0;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, dfmi::kBlockThreads, lds));
   if (per_cu < 1) per_cu = 1;
@@ -283,7 +285,7 @@ int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, i
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(dfmi::kBlockThreads), lds, st, x, nseg, stride, R, L, ndata,
                      tab, qi, qi_ld, dc, (int)(spacer < grid ? spacer : 0), g_probe);
   HIPCHK(hipGetLastError());
-  g_last_demod = "demod_bins_kernel<" + std::to_string(MS) + ",8" + (ROWS ? ",rows" : "") +
+  g_last_demod = std::string(g_tune.demod_occ4 ? "demod_bins4_kernel<" : "demod_bins_kernel<") + std::to_string(MS) + ",8" + (ROWS ? ",rows" : "") +
                  (spacer ? ",spacer" + std::to_string(spacer) : "") + ">";
   return DFMI_OK;
 }
@@ -414,6 +416,45 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
 }
 
 // Whole record pipeline on device pointers (fitters.py:370-428).
+// Fused seed + bulk demodulation (seed.h demod_seed_bins_kernel) on one stream.
+// Returns 1 when it does not apply (caller uses the two-kernel path).
+int fused_seed_demod(int dev, const double* x, int64_t nrec, int64_t nbuf, int R, int ndata, int L,
+                     const double* tab, double* rows, int64_t qs, const double* gdev, const dfmi::GuessInline& ginl,
+                     const double* jtab, const dfmi::LMConst& c, double* out, int64_t out_ld, int32_t* fitok,
+                     hipStream_t st) {
+  if (!g_tune.seed_fused || ndata > 16 || L <= 0) return 1;
+  const int nslot = (L + 127) / 128;
+  if (nslot > 8) return 1;
+  using K = void (*)(const double*, int64_t, int64_t, int64_t, int, int, int, const double*, double*, int64_t,
+                     const double*, dfmi::GuessInline, int, const double*, dfmi::LMConst, double*, int64_t, int64_t,
+                     int32_t*, uint64_t*);
+  K kern;
+  if (ndata <= 12)
+    kern = nslot <= 2 ? dfmi::demod_seed_bins_kernel<2, 12> : nslot <= 4 ? dfmi::demod_seed_bins_kernel<4, 12>
+                                                                       : dfmi::demod_seed_bins_kernel<8, 12>;
+  else
+    kern = nslot <= 2 ? dfmi::demod_seed_bins_kernel<2, 16> : nslot <= 4 ? dfmi::demod_seed_bins_kernel<4, 16>
+                                                                       : dfmi::demod_seed_bins_kernel<8, 16>;
+  const size_t lds = ((size_t)2 * ndata * L + (size_t)dfmi::kWavesPerBlock * L) * sizeof(double);
+  int per_cu = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, dfmi::kBlockThreads, lds));
+  if (per_cu < 1) per_cu = 1;
+  if (g_tune.demod_blocks_per_cu > 0 && g_tune.demod_blocks_per_cu < per_cu) per_cu = g_tune.demod_blocks_per_cu;
+  const int64_t slots = (int64_t)g_dev[dev].n_cu * per_cu;
+  const int64_t nseg = nrec * nbuf;
+  if (nrec + 1 > slots / 2) return 1;  // every seed and most of the bulk must be resident at once
+  int64_t bulk = slots - nrec;
+  const int64_t need = (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock;
+  if (bulk > need) bulk = need;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(nrec + bulk)), dim3(dfmi::kBlockThreads), lds, st, x, nseg,
+                     nbuf * (int64_t)R, nrec, R, L, ndata, tab, rows, qs, gdev, ginl, gdev ? 0 : 1, jtab, c, out,
+                     out_ld, nbuf, fitok, g_probe);
+  HIPCHK(hipGetLastError());
+  g_last_demod = "demod_seed_bins_kernel<" + std::to_string(nslot <= 2 ? 2 : nslot <= 4 ? 4 : 8) + "," +
+                 std::to_string(ndata <= 12 ? 12 : 16) + ",rows>";
+  return DFMI_OK;
+}
+
 int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride, int64_t nbuf, int R, int ndata,
                       double w0, int period, const double* init_guess_host, int parallel, int64_t nchunk,
                       const dfmi_lm_config& cfg, const dfmi::LMConst& c, double* out, int32_t* fitok,
@@ -471,6 +512,18 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
     if ((rc = workspace(dev, "dc_seed", (size_t)nrec * 8, &ds_))) return rc;
     const bool seed_bins = rows && L > 0 && g_tune.seed_bins;
     seed_first = seed_bins && g_tune.seed_order == 1;
+    if (seed_first && (nrec == 1 || rec_stride == nbuf * (int64_t)R) && nbuf > 1) {
+      const int64_t qs1 = dfmi_row_stride(ndata);
+      void* rw = nullptr;
+      if ((rc = workspace(dev, "qrow", (size_t)qs1 * nseg * sizeof(double), &rw))) return rc;
+      rc = fused_seed_demod(dev, x, nrec, nbuf, R, ndata, L, tab, (double*)rw, qs1, gdev, ginl, jtab, c, out, out_ld,
+                            fitok, st);
+      if (rc < 0) return rc;
+      if (rc == 0)  // seeds + rows written; the LM follows in stream order
+        return lm_device(dev, (double*)rw, qs1, ndata, nrec, nbuf, 1, nbuf - 1, nchunk, out, nbuf, out_ld, nullptr, c,
+                         jtab, out, out_ld, fitok, st, true);
+      rc = 0;
+    }
     HIPCHK(hipEventRecord(ds.ev_in, st));
     HIPCHK(hipStreamWaitEvent(ds.side, ds.ev_in, 0));
     hipStream_t sst = ds.side;
@@ -553,7 +606,9 @@ const std::map<std::string, Knob>& knobs() {
       {"demod_loads", {&g_tune.demod_loads, {8, 16}}},     {"demod_nt", {&g_tune.demod_nt, {0, 1}}},
       {"demod_blocks_per_cu", {&g_tune.demod_blocks_per_cu, {}}}, {"lm_general", {&g_tune.lm_general, {0, 1}}},
       {"demod_kernel", {&g_tune.demod_kernel, {0, 1}}},    {"seed_bins", {&g_tune.seed_bins, {0, 1}}},
-      {"seed_order", {&g_tune.seed_order, {0, 1}}}};
+      {"seed_order", {&g_tune.seed_order, {0, 1}}},
+      {"demod_occ4", {&g_tune.demod_occ4, {0, 1}}},
+      {"seed_fused", {&g_tune.seed_fused, {0, 1}}}};
   return k;
 }
 }  // namespace

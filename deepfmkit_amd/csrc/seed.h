@@ -146,3 +146,102 @@ __global__ __launch_bounds__(64) void seed_bins_kernel(const double* __restrict_
 }
 
 }  // namespace dfmi
+
+namespace dfmi {
+
+// Seed + bulk demodulation in ONE launch (record pipeline, row layout): workgroups
+// 0..nrec-1 are the seed step of record blockIdx.x (wave 0 folds buffer 0 into LDS
+// bins and contracts it into an LDS row, lane 0 fits it — seed_bins_kernel's work),
+// the others are the persistent bin demodulation of all nseg segments
+// (demod_bins_kernel's work). Lower block indices dispatch first, so the seeds are
+// resident from the start without a second queue, an event, or idle "spacer"
+// workgroups; the LM follows on the same stream. Records are contiguous (segment s
+// at x + s*R). The seed's 162 VGPRs share the
+// bin kernel's 3-waves-per-SIMD register budget (168), so occupancy is unchanged.
+template <int MAXSLOT, int NDMAX>
+__global__ __launch_bounds__(kBlockThreads) void demod_seed_bins_kernel(
+    const double* __restrict__ x, int64_t nseg, int64_t rec_stride, int64_t nrec, int R, int L, int ndata,
+    const double* __restrict__ tab, double* __restrict__ rows, int64_t row_ld, const double* __restrict__ guess,
+    GuessInline ginl, int use_inline, const double* __restrict__ jtab, LMConst c, double* __restrict__ out,
+    int64_t out_ld, int64_t nbuf, int32_t* __restrict__ status, uint64_t* __restrict__ probe) {
+  if ((int64_t)blockIdx.x >= nrec) {
+    bins_kernel_body<MAXSLOT, 8, true>(x, nseg, (int64_t)R, R, L, ndata, tab, rows, row_ld, nullptr, 0, probe,
+                                       (int)nrec);
+    return;
+  }
+  const uint64_t t_in = __builtin_amdgcn_s_memrealtime();
+  extern __shared__ __attribute__((aligned(16))) double sh[];  // basis | bins [L] | row
+  const int64_t r = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __builtin_amdgcn_s_setprio(3);
+  const int ntab = 2 * ndata * L;
+  {
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    const d2v* __restrict__ src = reinterpret_cast<const d2v*>(tab);
+    d2v* dst = reinterpret_cast<d2v*>(sh);
+    const int n2 = ntab / 2;
+    for (int base = 0; base < n2; base += kBlockThreads * 8) {
+      d2v v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = base + u * kBlockThreads + (int)threadIdx.x;
+        v[u] = i < n2 ? src[i] : d2v{0.0, 0.0};
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = base + u * kBlockThreads + (int)threadIdx.x;
+        if (i < n2) dst[i] = v[u];
+      }
+    }
+  }
+  __syncthreads();
+  double* ybin = sh + ntab;
+  double* row = ybin + L;
+  if (wave == 0) {
+    const int nslot = (L + 127) / 128;
+    int pbase[MAXSLOT];
+    bool pval[MAXSLOT];
+#pragma unroll
+    for (int j = 0; j < MAXSLOT; ++j) {
+      pbase[j] = 2 * (lane + 64 * j);
+      pval[j] = (j < nslot) && (pbase[j] < L);
+    }
+    bins_segment<MAXSLOT, 32, false, kHarmBlock, true>(x + r * rec_stride, R, L, ndata, sh, ybin, lane, pval, pbase,
+                                                          row, 0, 0, nullptr);
+  }
+  __syncthreads();
+  const uint64_t t_fold = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x != 0) return;
+  double p[4] = {0.0, 0.0, 0.0, 0.0};
+  if (use_inline) {
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) {
+      if (r == rr) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) p[i] = ginl.v[rr][i];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) p[i] = guess[r * 4 + i];
+  }
+  double ssq;
+  const QRow<1> q{row};
+  const int st = fit_segment_q<NDMAX>(q, ndata, jtab, c, p, ssq);
+  const int64_t sidx = r * nbuf;
+  out[0 * out_ld + sidx] = p[0];
+  out[1 * out_ld + sidx] = p[1];
+  out[2 * out_ld + sidx] = p[2];
+  out[3 * out_ld + sidx] = p[3];
+  out[4 * out_ld + sidx] = q.at(dfmi_row_dc(ndata));
+  out[5 * out_ld + sidx] = ssq;
+  status[sidx] = st;
+  if (probe && r == 0) {
+    probe[0] = t_in;
+    probe[1] = t_fold;
+    probe[2] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+}  // namespace dfmi

@@ -253,9 +253,10 @@ def test_record_rows_path_matches_component_path():
 
 
 def test_seed_stream_order_identical():
-    """The seed step runs on the caller's stream with the bulk demodulation on the
-    side stream (seed_order 1, default) or the other way round (seed_order 0); the
-    results are the same bits."""
+    """The seed step (buffer 0, fitters.py:403-410) runs fused into the bulk
+    demodulation launch (seed_fused 1, default), as its own kernel on the caller's
+    stream beside the bulk on the side stream (seed_fused 0, seed_order 1), or the
+    other way round (seed_order 0); the results are the same bits."""
     import torch
     from deepfmkit_amd import _lib
     from deepfmkit_amd.fitters import nls_records
@@ -267,12 +268,15 @@ def test_seed_stream_order_identical():
     x = (1.0 + torch.cos(0.4 + 6.2 * torch.cos(2 * np.pi * 1000.0 * t + 0.2))).reshape(1, -1)
     x = x + 1e-3 * torch.randn(x.shape, dtype=torch.float64, device="cuda", generator=g)
     res = []
-    for order in (1, 0, 1):
+    for fused, order in ((1, 1), (0, 1), (0, 0), (1, 1)):
+        _lib.check(lib.dfmi_set_tuning(b"seed_fused", fused), "tune")
         _lib.check(lib.dfmi_set_tuning(b"seed_order", order), "tune")
         cols, ok = nls_records(x, 200000.0, 1000.0, R, nbuf, 10)
         res.append((cols.cpu().numpy(), ok.cpu().numpy(), lib.dfmi_last_demod_kernel().decode()))
+    _lib.check(lib.dfmi_set_tuning(b"seed_fused", 1), "tune")
     _lib.check(lib.dfmi_set_tuning(b"seed_order", 1), "tune")
-    assert "spacer" in res[0][2] and "spacer" not in res[1][2], (res[0][2], res[1][2])
+    names = [r[2] for r in res]
+    assert names[0].startswith("demod_seed_bins_kernel") and "spacer" in names[1] and "spacer" not in names[2], names
     for cols, ok, _ in res[1:]:
         np.testing.assert_array_equal(cols, res[0][0])
         np.testing.assert_array_equal(ok, res[0][1])

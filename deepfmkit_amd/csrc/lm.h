@@ -341,7 +341,49 @@ DFMI_HDI void damped_solve(const Eval& e, double lam, double (&dp)[4]) {
 
 DFMI_HDI double norm4(double a, double b, double c, double d) { return sqrt(a * a + b * b + c * c + d * d); }
 
-// fit.py:208-258 (_run_lma_fit). p in/out; returns ssq0 at the final p.
+// fit.py:208-258 (_run_lma_fit), flattened for SIMT: every pass of the loop does
+// ONE damped solve and (unless the step is below min_step_norm) ONE trial
+// evaluation for each active lane, whatever its position on the lambda ladder.
+// The nested form (iterations x ladder) made a wave execute the union of its lanes'
+// ladders at every iteration; here a wave runs max over lanes of the trial count.
+// Per lane the sequence of solves, trials and acceptances is exactly the nested
+// loop's (same arithmetic, same bits).
+template <typename EvalFn>
+DFMI_HDI double lm_descend_flat(EvalFn&& evalf, double (&p)[4], const LMConst& c) {
+  Eval e;
+  evalf(p, e);
+  int it = 0, li = 0;
+  bool active = c.max_steps > 0 && c.n_lambda > 0;
+  while (active) {
+    double dp[4];
+    damped_solve(e, c.lambdas[li], dp);
+    bool accepted = false;
+    if (!(norm4(dp[0], dp[1], dp[2], dp[3]) < c.min_step_norm)) {
+      double pt[4] = {p[0] + dp[0], p[1] + dp[1], p[2] + dp[2], p[3] + dp[3]};
+      Eval et;
+      evalf(pt, et);
+      if (et.ssq < e.ssq) {
+        accepted = true;
+        const double change = norm4(pt[0] - p[0], pt[1] - p[1], pt[2] - p[2], pt[3] - p[3]);
+        p[0] = pt[0];
+        p[1] = pt[1];
+        p[2] = pt[2];
+        p[3] = pt[3];
+        const double best_ssq = et.ssq;
+        e = et;  // coeffs(ndata, data, parm) at the accepted point (fit.py:251)
+        ++it;
+        li = 0;
+        if (((e.ssq - best_ssq) < c.conv_improve && change < c.conv_param_change) || it >= c.max_steps)
+          active = false;
+      }
+    }
+    if (!accepted && ++li >= c.n_lambda) active = false;  // no lambda improved: fit.py:246-247
+  }
+  return e.ssq;
+}
+
+// fit.py:208-258 (_run_lma_fit), nested form (one lane at a time: host build, seed).
+// p in/out; returns ssq0 at the final p.
 template <typename EvalFn>
 DFMI_HDI double lm_descend(EvalFn&& evalf, double (&p)[4], const LMConst& c) {
   Eval e;
@@ -453,10 +495,11 @@ DFMI_HDI void m_grid_seed(QF&& Q, int ndata, const double* __restrict__ jtab, co
 }
 
 // fit.py:322-361 (fit): LM, status + grid retry, normalisation, phi wrap.
-template <typename EvalFn, typename QF>
+template <bool FLAT = true, typename EvalFn, typename QF>
 DFMI_HDI int fit_segment_t(EvalFn&& evalf, QF&& Q, int ndata, const double* __restrict__ jtab, const LMConst& c,
                            double (&p)[4], double& ssq_out) {
-  double ssq = lm_descend(evalf, p, c);
+  auto descend = [&](double (&pp)[4]) { return FLAT ? lm_descend_flat(evalf, pp, c) : lm_descend(evalf, pp, c); };
+  double ssq = descend(p);
   int status;
   if (ssq < c.fitok_threshold) {
     status = 0;
@@ -464,7 +507,7 @@ DFMI_HDI int fit_segment_t(EvalFn&& evalf, QF&& Q, int ndata, const double* __re
     double g[4];
     m_grid_seed(Q, ndata, jtab, c, g);
     if (!(g[0] == 0.0) || !(g[1] == 0.0) || !(g[2] == 0.0) || !(g[3] == 0.0)) {  // np.any
-      const double ssq2 = lm_descend(evalf, g, c);
+      const double ssq2 = descend(g);
       if (ssq2 < ssq) {
         ssq = ssq2;
         p[0] = g[0];
@@ -491,15 +534,15 @@ DFMI_HDI int fit_segment_t(EvalFn&& evalf, QF&& Q, int ndata, const double* __re
 
 // Single-segment entry used by the kernels and by the test-only host build.
 // NDMAX > 0: register path (requires ndata <= NDMAX); NDMAX == 0: general path.
-template <int NDMAX, typename QF>
+template <int NDMAX, typename QF, bool FLAT = true>
 __host__ __device__ __forceinline__ int fit_segment_q(const QF& q, int ndata, const double* __restrict__ jtab,
                                                    const LMConst& c, double (&p)[4], double& ssq_out) {
   if constexpr (NDMAX > 0) {
     auto evalf = [&](const double (&pp)[4], Eval& e) { eval_reg<NDMAX>(q, ndata, pp, e); };
-    return fit_segment_t(evalf, q, ndata, jtab, c, p, ssq_out);
+    return fit_segment_t<FLAT>(evalf, q, ndata, jtab, c, p, ssq_out);
   } else {
     auto evalf = [&](const double (&pp)[4], Eval& e) { eval_gen(q, ndata, pp, e); };
-    return fit_segment_t(evalf, q, ndata, jtab, c, p, ssq_out);
+    return fit_segment_t<FLAT>(evalf, q, ndata, jtab, c, p, ssq_out);
   }
 }
 

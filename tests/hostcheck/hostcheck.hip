@@ -46,7 +46,10 @@ int hc_fit_segments(const double* qi, long n, int ndata, const double* guess, co
   for (long s = 0; s < n; ++s) {
     double p[4] = {guess[s * 4], guess[s * 4 + 1], guess[s * 4 + 2], guess[s * 4 + 3]};
     double ssq;
-    if (force_general)
+    if (force_general == 2 && ndata <= 12) {  // nested (one-lane) descent: must equal the flattened one
+      const dfmi::QGlobal qg{qi + s, n, ndata};
+      status_out[s] = dfmi::fit_segment_q<12, dfmi::QGlobal, false>(qg, ndata, tab.data(), c, p, ssq);
+    } else if (force_general)
       status_out[s] = dfmi::fit_segment<0>(qi + s, n, ndata, tab.data(), c, p, ssq);
     else if (ndata <= 12)
       status_out[s] = dfmi::fit_segment<12>(qi + s, n, ndata, tab.data(), c, p, ssq);

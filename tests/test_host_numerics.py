@@ -86,3 +86,14 @@ def test_numpy_summation_plan_is_bit_exact(hc):
               8193, 12345, 16384, 16385, 30001]:
         a = rng.standard_normal(n) * 10 ** rng.uniform(-3, 3, n)
         assert hc.hc_np_sum(a.ctypes.data, n) == np.sum(a), n
+
+
+@pytest.mark.parametrize("group", ["g5", "g10"])
+def test_flattened_descent_equals_nested(hc, lm_npz, group):
+    """lm.h lm_descend_flat (the SIMT form the kernels run) makes exactly the nested
+    _run_lma_fit loop's solves, trials and acceptances: identical bits."""
+    qi, g = lm_npz[group + "_qi"], lm_npz[group + "_guess"]
+    a = _fit(hc, qi, g, 0)
+    b = _fit(hc, qi, g, 2)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)

@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 OUT=$PWD/gpurun_out/prof_${TAG:-r01}
 mkdir -p "$OUT"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o bench -- \
-    python3 bench.py --no-cpu-baseline --steps 20 --warmup 3 > "$OUT/bench_trace.json" 2> "$OUT/trace.err" || exit $?
+    python3 bench.py --no-cpu-baseline > "$OUT/bench_trace.json" 2> "$OUT/trace.err" || exit $?
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o demod -- \
     python3 bench.py --demod-only --steps 10 --warmup 2 > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err" || exit $?
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o demod -- \

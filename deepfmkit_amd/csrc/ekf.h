@@ -32,7 +32,19 @@ __global__ __launch_bounds__(64) void ekf_kernel(const double* __restrict__ x, i
     for (int j = 0; j < 5; ++j) P[i][j] = (i == j) ? p0[i] : 0.0;
   }
   const double Rv = rv[r];
+  // samples arrive 8 at a time (one 64-B load ahead of the chain that needs them);
+  // the snapshot test counts down instead of a 64-bit modulo per sample
+  int64_t to_snap = R;
+  double xbuf[8];
   for (int64_t k = 0; k < n_samp; ++k) {
+    const int slot = (int)(k & 7);
+    if (slot == 0) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) xbuf[u] = (k + u < n_samp) ? xr[k + u] : 0.0;
+    }
+    double xk = xbuf[0];
+#pragma unroll
+    for (int u = 1; u < 8; ++u) xk = (slot == u) ? xbuf[u] : xk;
     // predict: P = F P F^T + Q with F = I
 #pragma unroll
     for (int i = 0; i < 5; ++i)
@@ -48,7 +60,7 @@ __global__ __launch_bounds__(64) void ekf_kernel(const double* __restrict__ x, i
     sincos(arg, &sa, &ca);
     const double h = a * ca + dc;
     double H[5] = {ca, -a * sa * cth, -a * sa, a * m * sa * sth, 1.0};
-    const double y = xr[k] - h;
+    const double y = xk - h;
     double HP[5];
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
@@ -92,7 +104,8 @@ __global__ __launch_bounds__(64) void ekf_kernel(const double* __restrict__ x, i
     for (int i = 0; i < 5; ++i)
 #pragma unroll
       for (int j = 0; j < 5; ++j) P[i][j] = Pn[i][j];
-    if ((k + 1) % R == 0) {
+    if (--to_snap == 0) {
+      to_snap = R;
       const int64_t b = (k + 1) / R - 1;
       if (b < nbuf) {
 #pragma unroll

@@ -1,0 +1,99 @@
+"""Config 5 (BASELINE.json): the EKF time-domain path (EKFFitter, fitters.py:214-320,
+notebooks/2.0_EKF) on the GPU — one lane per channel, a serial predict/update
+chain over the samples — next to the CPU oracle (oracle/nls_oracle.py ekf_record,
+the restated reference loop, one core).
+
+Workload: `channels` independent snr-mode records (f_samp 200 kHz, f_mod 1 kHz,
+m = 6, 40 dB, n = 20 -> R = 4000 snapshot spacing) of `seconds` each, resident in
+HBM. Timing: HIP events around one dfmi_ekf call (median of `reps`); the per-record
+pre-reductions (mean, var: fitters.py:253, 256) are host inputs here, as in
+fitters.ekf_records. Reported: samples/s per channel (the serial chain's speed) and
+aggregate samples/s. One JSON line per channel count.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=2.0)
+    ap.add_argument("--channels", default="1,64,1024")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--cpu-seconds", type=float, default=0.1, help="oracle sample length (s of signal)")
+    args = ap.parse_args()
+    import torch
+
+    import deepfmkit_amd as dfm
+    from deepfmkit_amd import _lib
+    from oracle import nls_oracle as O
+
+    f_samp, f_mod, n = 200000.0, 1000.0, 20
+    R = int(f_samp / f_mod * n)
+    laser = dfm.LaserConfig()
+    ifo = dfm.InterferometerConfig()
+    dfm.set_laser_df_for_effect(laser, ifo, 6.0)
+    dff = dfm.DeepFitFramework()
+    dff.load_sim(dfm.DFMIObject("ekf", laser, ifo, f_samp=f_samp))
+    dff.simulate("ekf", n_seconds=args.seconds, mode="snr", snr_db=40.0, trial_num=0)
+    x1 = np.asarray(dff.raws["ekf"].samples(), dtype=np.float64)
+    ns = x1.size
+    nbuf = ns // R
+
+    ncpu = int(args.cpu_seconds * f_samp)
+    t0 = time.perf_counter()
+    ref = O.ekf_record(x1[:ncpu], f_samp, f_mod, n)
+    cpu_rate = ncpu / (time.perf_counter() - t0)
+    cpu = {"value": cpu_rate, "unit": "samples/s per channel", "cores": 1, "kind": "port",
+           "sample": f"{ncpu} samples ({args.cpu_seconds} s of signal), oracle restatement of EKFFitter.fit"}
+
+    lib = _lib.load()
+    dev = torch.device("cuda:0")
+    # parity on the oracle's own record (the prefix, with ITS mean and variance as x0[4]
+    # and R: fitters.py:253, 256), through the drop-in facade
+    raw = dfm.DeepRawObject(data=x1[:ncpu])
+    raw.f_samp, raw.f_mod = f_samp, f_mod
+    got = dfm.fitters.ekf_records([raw], n)[0]
+    parity = float(np.max(np.abs(got - ref)))
+    st = torch.cuda.current_stream()
+    p0 = torch.ones(5, dtype=torch.float64, device=dev)
+    qd = torch.tensor([1e-8, 1e-8, 1e-6, 1e-6, 1e-8], dtype=torch.float64, device=dev)
+    for nch in [int(v) for v in args.channels.split(",")]:
+        x = torch.from_numpy(x1).to(dev).reshape(1, -1).expand(nch, -1).contiguous()
+        x0 = torch.tensor([[1.6, 6.0, 0.0, 0.0, float(np.mean(x1))]] * nch, dtype=torch.float64, device=dev)
+        rv = torch.full((nch,), float(np.var(x1)), dtype=torch.float64, device=dev)
+        states = torch.empty((nch, nbuf, 5), dtype=torch.float64, device=dev)
+
+        def call():
+            _lib.check(lib.dfmi_ekf(x.data_ptr(), nch, ns, ns, x0.data_ptr(), p0.data_ptr(), qd.data_ptr(),
+                                    rv.data_ptr(), 2 * np.pi * f_mod, f_samp, R, nbuf, states.data_ptr(),
+                                    _lib.DFMI_MEM_DEVICE, st.cuda_stream), "dfmi_ekf")
+
+        call()
+        torch.cuda.synchronize()
+        times = []
+        for _ in range(args.reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            call()
+            e1.record(st)
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1) / 1e3)
+        t = float(np.median(times))
+        print(json.dumps({"metric": "EKF samples/s", "channels": nch, "samples_per_channel": ns, "seconds": t,
+                          "per_channel_samples_per_s": ns / t, "aggregate_samples_per_s": nch * ns / t,
+                          "max_abs_dstate_vs_oracle": parity, "parity_record": f"{ncpu} samples", "cpu_baseline": cpu,
+                          "data": "snr-mode m=6, 40 dB, 200 kS/s (the package's bit-exact physics.py restatement)"}),
+              flush=True)
+        del x
+
+
+if __name__ == "__main__":
+    main()

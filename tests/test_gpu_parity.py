@@ -147,6 +147,29 @@ def test_ekf_matches_reference(manifest):
             assert err <= 1e-9, (lab, k, err)
 
 
+def test_ekf_long_record_matches_oracle():
+    """Config 5 shape on a longer record than the golden one (0.1 s = 20,000 samples,
+    5 snapshots): the lane-per-channel kernel tracks the restated reference loop to
+    fp64 rounding (the reference itself moves by ~1e-15 under 1-ulp input changes),
+    and several channels in one launch give each channel's answer bit for bit."""
+    import deepfmkit_amd as dfm
+    from oracle import nls_oracle as O
+    laser = dfm.LaserConfig()
+    ifo = dfm.InterferometerConfig()
+    dfm.set_laser_df_for_effect(laser, ifo, 6.0)
+    dff = dfm.DeepFitFramework()
+    dff.load_sim(dfm.DFMIObject("e", laser, ifo, f_samp=200000.0))
+    dff.simulate("e", n_seconds=0.1, mode="snr", snr_db=40.0, trial_num=5)
+    raw = dff.raws["e"]
+    x = np.asarray(raw.samples(), dtype=np.float64)
+    ref = O.ekf_record(x, 200000.0, 1000.0, 20)
+    got = dfm.fitters.ekf_records([raw], 20)[0]
+    assert np.max(np.abs(got - ref)) <= 1e-12, np.max(np.abs(got - ref))
+    many = dfm.fitters.ekf_records([raw] * 3, 20)
+    for k in range(3):
+        np.testing.assert_array_equal(many[k], got)
+
+
 def test_large_batch_known_answer_and_seed_independence():
     """Full-size property checks (config 2 shape, 100k segments of R=4000, on device):
     noiseless A(1+cos(phi+m cos(wt+psi))) is recovered exactly in every segment, and a

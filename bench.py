@@ -196,6 +196,8 @@ def main():
     ms = el / args.steps * 1e3
     total_segments = nseg * world  # units of work; the seed replicas on ranks > 0 are not counted
     value = total_segments * args.steps / el
+    # BASELINE.json configs: 2 = 100k segments on one GPU, 4 = 10M over 8 GPUs (1.25M per GPU)
+    cfg_name = {100_000: "config2", 1_250_000: "config4 shard"}.get(nseg, "config2-shape")
 
     # ---- roofline of the dominant kernel (demod), HIP events on the launch stream ----
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -258,7 +260,7 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic snr-mode DFMI (m=6, 40 dB white noise) generated on device",
-            "config": {"workload": f"config2: {nseg} segments/GPU x R={R} @200 kS/s, ndata={NDATA}, 1 channel, "
+            "config": {"workload": f"{cfg_name}: {nseg} segments/GPU x R={R} @200 kS/s, ndata={NDATA}, 1 channel, "
                                    f"_fit_parallel chunk size 1",
                        "segments_per_gpu": nseg, "R": R, "ndata": NDATA, "parallelism": f"shard{world}"},
             "roofline": roof,

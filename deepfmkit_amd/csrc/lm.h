@@ -30,6 +30,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "dfmi_math.h"
 
 namespace dfmi {
@@ -75,10 +77,8 @@ DFMI_HDI void harmonic_term(Eval& e, int j, double a, bool a_nz, double cph, dou
   const double pt = quarter_turn(j, cph, sph);       // cos(phi + j pi/2)
   const double ptd = quarter_turn(j + 1, cph, sph);  // cos(phi + j pi/2 + pi/2)
   const double common = a * pt * J0;
-  const double mq = common * cj;
-  const double mi = -common * sj;
-  const double rq = Q - mq;
-  const double ri = I - mi;
+  const double rq = fma(-common, cj, Q);  // Q - model_Q (model_Q = common cos(j psi))
+  const double ri = fma(common, sj, I);   // I - model_I (model_I = -common sin(j psi))
   e.ssq = fma(rq, rq, e.ssq);
   e.ssq = fma(ri, ri, e.ssq);
   // d model / d a = model / a (fit.py:126-128), written without the division
@@ -108,6 +108,18 @@ DFMI_HDI void harmonic_term(Eval& e, int j, double a, bool a_nz, double cph, dou
 }
 
 DFMI_HDI void eval_zero(Eval& e) { e = Eval{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; }
+
+// The residual part of harmonic_term only (ssqf, fit.py:152-167): same bits as the
+// ssq harmonic_term accumulates.
+DFMI_HDI void harmonic_ssq(double& ssq, int j, double a, double cph, double sph, double J0, double cj, double sj,
+                           double Q, double I) {
+  const double pt = quarter_turn(j, cph, sph);
+  const double common = a * pt * J0;
+  const double rq = fma(-common, cj, Q);
+  const double ri = fma(common, sj, I);
+  ssq = fma(rq, rq, ssq);
+  ssq = fma(ri, ri, ssq);
+}
 
 // ---------------------------------------------------------------------------
 // Register path
@@ -142,18 +154,32 @@ DFMI_HDI void bessel_regs(double x, int N, double (&J)[NB]) {
   int M = dfmi_bessel_start(N, ax);
   if (M < NB) M = (NB + 1) & ~1;
   const double tox = 2.0 / ax;
-  const double big = ldexp(1.0, DFMI_BES_BIG_EXP);
+  // Runtime part of the pass without the per-order overflow test: power-of-two
+  // rescaling is exact, so a pass that never leaves the finite range gives the same
+  // bits as the rescaled one; only if it overflowed does the checked pass run.
   double fp1 = 0.0, f = 1.0, S = 2.0;  // order M (even) contributes 2 f_M
   for (int k = M; k >= NB; --k) {
-    double fm1 = fma((double)k * tox, f, -fp1);
-    if (fabs(fm1) > big) {
-      fm1 = ldexp(fm1, -DFMI_BES_BIG_EXP);
-      f = ldexp(f, -DFMI_BES_BIG_EXP);
-      S = ldexp(S, -DFMI_BES_BIG_EXP);
-    }
+    const double fm1 = fma((double)k * tox, f, -fp1);
     if (((k - 1) & 1) == 0) S += 2.0 * fm1;
     fp1 = f;
     f = fm1;
+  }
+  if (!(fabs(f) < 1.0e300) || !(fabs(S) < 1.0e300)) {
+    const double big = ldexp(1.0, DFMI_BES_BIG_EXP);
+    fp1 = 0.0;
+    f = 1.0;
+    S = 2.0;
+    for (int k = M; k >= NB; --k) {
+      double fm1 = fma((double)k * tox, f, -fp1);
+      if (fabs(fm1) > big) {
+        fm1 = ldexp(fm1, -DFMI_BES_BIG_EXP);
+        f = ldexp(f, -DFMI_BES_BIG_EXP);
+        S = ldexp(S, -DFMI_BES_BIG_EXP);
+      }
+      if (((k - 1) & 1) == 0) S += 2.0 * fm1;
+      fp1 = f;
+      f = fm1;
+    }
   }
   J[NB - 1] = f;
 #pragma unroll
@@ -190,6 +216,53 @@ DFMI_HDI void eval_reg(const QF& q, int nd, const double (&p)[4], Eval& e) {
     if (j <= nd) harmonic_term(e, j, a, a_nz, cph, sph, J[j - 1], J[j], J[j + 1], cj, sj, q.qc(j - 1), q.qs(j - 1));
     const double cn = fma(cj, c1, -(sj * s1));
     const double sn = fma(sj, c1, cj * s1);
+    cj = cn;
+    sj = sn;
+  }
+}
+
+// Split form of eval_reg for the LM trials: `trial` computes the point's ssq and
+// keeps its Bessel values and trig; `accept` adds J^T J and J^T r from them when the
+// trial is accepted. A rejected trial (about 45 % of them at 40 dB) thus costs only
+// the ssqf part, as in the reference (fit.py:236-243), and the bits are eval_reg's.
+template <int NDMAX>
+struct TrialReg {
+  double J[NDMAX + 2];
+  double cph, sph, c1, s1, ssq;
+};
+
+template <int NDMAX, typename QF>
+DFMI_HDI double eval_reg_trial(const QF& q, int nd, const double (&p)[4], TrialReg<NDMAX>& t) {
+  const double a = p[0], m = p[1], phi = p[2], psi = p[3];
+  sincos(phi, &t.sph, &t.cph);
+  sincos(psi, &t.s1, &t.c1);
+  bessel_regs<NDMAX + 2>(m, nd + 1, t.J);
+  double ssq = 0.0;
+  double cj = t.c1, sj = t.s1;
+#pragma unroll
+  for (int j = 1; j <= NDMAX; ++j) {
+    if (j <= nd) harmonic_ssq(ssq, j, a, t.cph, t.sph, t.J[j], cj, sj, q.qc(j - 1), q.qs(j - 1));
+    const double cn = fma(cj, t.c1, -(sj * t.s1));
+    const double sn = fma(sj, t.c1, cj * t.s1);
+    cj = cn;
+    sj = sn;
+  }
+  t.ssq = ssq;
+  return ssq;
+}
+
+template <int NDMAX, typename QF>
+DFMI_HDI void eval_reg_accept(const QF& q, int nd, const double (&p)[4], const TrialReg<NDMAX>& t, Eval& e) {
+  const double a = p[0];
+  const bool a_nz = (a != 0.0);
+  eval_zero(e);
+  double cj = t.c1, sj = t.s1;
+#pragma unroll
+  for (int j = 1; j <= NDMAX; ++j) {
+    if (j <= nd)
+      harmonic_term(e, j, a, a_nz, t.cph, t.sph, t.J[j - 1], t.J[j], t.J[j + 1], cj, sj, q.qc(j - 1), q.qs(j - 1));
+    const double cn = fma(cj, t.c1, -(sj * t.s1));
+    const double sn = fma(sj, t.c1, cj * t.s1);
     cj = cn;
     sj = sn;
   }
@@ -348,10 +421,14 @@ DFMI_HDI double norm4(double a, double b, double c, double d) { return sqrt(a * 
 // ladders at every iteration; here a wave runs max over lanes of the trial count.
 // Per lane the sequence of solves, trials and acceptances is exactly the nested
 // loop's (same arithmetic, same bits).
-template <typename EvalFn>
-DFMI_HDI double lm_descend_flat(EvalFn&& evalf, double (&p)[4], const LMConst& c) {
+template <typename Ev>
+DFMI_HDI double lm_descend_flat(Ev&& ev, double (&p)[4], const LMConst& c) {
   Eval e;
-  evalf(p, e);
+  {
+    typename std::decay_t<Ev>::Trial t0;
+    ev.trial(p, t0);
+    ev.accept(p, t0, e);
+  }
   int it = 0, li = 0;
   bool active = c.max_steps > 0 && c.n_lambda > 0;
   while (active) {
@@ -360,17 +437,17 @@ DFMI_HDI double lm_descend_flat(EvalFn&& evalf, double (&p)[4], const LMConst& c
     bool accepted = false;
     if (!(norm4(dp[0], dp[1], dp[2], dp[3]) < c.min_step_norm)) {
       double pt[4] = {p[0] + dp[0], p[1] + dp[1], p[2] + dp[2], p[3] + dp[3]};
-      Eval et;
-      evalf(pt, et);
-      if (et.ssq < e.ssq) {
+      typename std::decay_t<Ev>::Trial tt;
+      const double ssq_try = ev.trial(pt, tt);
+      if (ssq_try < e.ssq) {
         accepted = true;
         const double change = norm4(pt[0] - p[0], pt[1] - p[1], pt[2] - p[2], pt[3] - p[3]);
         p[0] = pt[0];
         p[1] = pt[1];
         p[2] = pt[2];
         p[3] = pt[3];
-        const double best_ssq = et.ssq;
-        e = et;  // coeffs(ndata, data, parm) at the accepted point (fit.py:251)
+        const double best_ssq = ssq_try;
+        ev.accept(p, tt, e);  // coeffs(ndata, data, parm) at the accepted point (fit.py:251)
         ++it;
         li = 0;
         if (((e.ssq - best_ssq) < c.conv_improve && change < c.conv_param_change) || it >= c.max_steps)
@@ -381,6 +458,33 @@ DFMI_HDI double lm_descend_flat(EvalFn&& evalf, double (&p)[4], const LMConst& c
   }
   return e.ssq;
 }
+
+// Evaluators for lm_descend_flat: a full evaluation per trial (general path) or
+// the split register-path one.
+template <typename EvalFn>
+struct FullEval {
+  EvalFn f;
+  struct Trial {
+    Eval e;
+  };
+  DFMI_HDI double trial(const double (&p)[4], Trial& t) {
+    f(p, t.e);
+    return t.e.ssq;
+  }
+  DFMI_HDI void accept(const double (&)[4], const Trial& t, Eval& e) { e = t.e; }
+};
+
+template <int NDMAX, typename QF>
+struct SplitEval {
+  const QF& q;
+  int nd;
+  using Trial = TrialReg<NDMAX>;
+  DFMI_HDI double trial(const double (&p)[4], Trial& t) { return eval_reg_trial<NDMAX>(q, nd, p, t); }
+  DFMI_HDI void accept(const double (&p)[4], const Trial& t, Eval& e) {
+    eval_reg_accept<NDMAX>(q, nd, p, t, e);
+    e.ssq = t.ssq;
+  }
+};
 
 // fit.py:208-258 (_run_lma_fit), nested form (one lane at a time: host build, seed).
 // p in/out; returns ssq0 at the final p.
@@ -495,10 +599,15 @@ DFMI_HDI void m_grid_seed(QF&& Q, int ndata, const double* __restrict__ jtab, co
 }
 
 // fit.py:322-361 (fit): LM, status + grid retry, normalisation, phi wrap.
-template <bool FLAT = true, typename EvalFn, typename QF>
-DFMI_HDI int fit_segment_t(EvalFn&& evalf, QF&& Q, int ndata, const double* __restrict__ jtab, const LMConst& c,
-                           double (&p)[4], double& ssq_out) {
-  auto descend = [&](double (&pp)[4]) { return FLAT ? lm_descend_flat(evalf, pp, c) : lm_descend(evalf, pp, c); };
+// Ev: an evaluator for the flattened descent (FullEval / SplitEval); evalf: the full
+// evaluation for the nested one (FLAT = false: host build / equivalence tests).
+template <bool FLAT = true, typename Ev, typename EvalFn, typename QF>
+DFMI_HDI int fit_segment_t(Ev&& ev, EvalFn&& evalf, QF&& Q, int ndata, const double* __restrict__ jtab,
+                           const LMConst& c, double (&p)[4], double& ssq_out) {
+  auto descend = [&](double (&pp)[4]) {
+    if constexpr (FLAT) return lm_descend_flat(ev, pp, c);
+    else return lm_descend(evalf, pp, c);
+  };
   double ssq = descend(p);
   int status;
   if (ssq < c.fitok_threshold) {
@@ -539,10 +648,12 @@ __host__ __device__ __forceinline__ int fit_segment_q(const QF& q, int ndata, co
                                                    const LMConst& c, double (&p)[4], double& ssq_out) {
   if constexpr (NDMAX > 0) {
     auto evalf = [&](const double (&pp)[4], Eval& e) { eval_reg<NDMAX>(q, ndata, pp, e); };
-    return fit_segment_t<FLAT>(evalf, q, ndata, jtab, c, p, ssq_out);
+    SplitEval<NDMAX, QF> ev{q, ndata};
+    return fit_segment_t<FLAT>(ev, evalf, q, ndata, jtab, c, p, ssq_out);
   } else {
     auto evalf = [&](const double (&pp)[4], Eval& e) { eval_gen(q, ndata, pp, e); };
-    return fit_segment_t<FLAT>(evalf, q, ndata, jtab, c, p, ssq_out);
+    FullEval<decltype(evalf)> ev{evalf};
+    return fit_segment_t<FLAT>(ev, evalf, q, ndata, jtab, c, p, ssq_out);
   }
 }
 

@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--segments", type=int, default=100_000, help="segments per GPU")
+    ap.add_argument("--channels", type=int, default=1,
+                    help="records in the batch (config 3: 2 channels, main m=6 and witness m=4.3, each "
+                         "seeded by its own buffer 0), segments split evenly; 1 GPU only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=8000, help="segments in the CPU-baseline sample")
     ap.add_argument("--cpu-procs", type=int, default=16, help="Pool size of the CPU baseline (box share: 16)")
@@ -52,9 +55,10 @@ def parse():
     return ap.parse_args()
 
 
-def gen_shard(torch, dev, seg0, nseg, R, seed, chunk=8192):
+def gen_shard(torch, dev, seg0, nseg, R, seed, chunk=8192, m_true=None):
     """snr-mode signal (physics.py:493-530 formula) for global segments [seg0, seg0+nseg)
     generated on the device: y = 1 + cos(m cos(w t)), white noise at SNR_DB."""
+    M_TRUE = m_true if m_true is not None else globals()["M_TRUE"]
     x = torch.empty(nseg * R, dtype=torch.float64, device=dev)
     w = 2 * np.pi * F_MOD
     # noise power from the (periodic) clean signal power: mean((y - mean y)^2)
@@ -145,33 +149,42 @@ def main():
     lib = _lib.load()
     R = int(F_SAMP / F_MOD * N_CYC)
     nseg = args.segments
-    seg0, nbuf, prepend_seed = shard_plan(rank, world, nseg)
-    body = gen_shard(torch, dev, seg0, nseg, R, seed=1234 + rank)
-    if not prepend_seed:
-        x = body
+    nrec = max(1, args.channels) if world == 1 else 1
+    if nrec > 1:  # config 3: channels as records of one batch (fit_many), each with its own seed
+        if nseg % nrec:
+            raise SystemExit("--segments must be a multiple of --channels")
+        nbuf, prepend_seed = nseg // nrec, False
+        ms_true = [M_TRUE, 4.3] + [M_TRUE] * (nrec - 2)
+        x = torch.cat([gen_shard(torch, dev, 0, nbuf, R, seed=1234 + c, m_true=ms_true[c]) for c in range(nrec)])
     else:
-        head = gen_shard(torch, dev, 0, 1, R, seed=1234)
-        x = torch.cat([head, body])
-        del head
-    del body
+        seg0, nbuf, prepend_seed = shard_plan(rank, world, nseg)
+        body = gen_shard(torch, dev, seg0, nseg, R, seed=1234 + rank)
+        if not prepend_seed:
+            x = body
+        else:
+            head = gen_shard(torch, dev, 0, 1, R, seed=1234)
+            x = torch.cat([head, body])
+            del head
+        del body
     torch.cuda.synchronize()
     w0 = w0_of(F_MOD, F_SAMP)
     cfg = F.lm_config()
-    guess = np.array([1.6, 6.0, 0.0, 0.0])
-    out = torch.empty((6, nbuf), dtype=torch.float64, device=dev)
-    ok = torch.empty(nbuf, dtype=torch.int32, device=dev)
-    qi = torch.empty((2 * NDATA, nbuf), dtype=torch.float64, device=dev)
-    dcb = torch.empty(nbuf, dtype=torch.float64, device=dev)
-    rows = torch.empty((nbuf, lib.dfmi_qi_row_stride(NDATA)), dtype=torch.float64, device=dev)
+    guess = np.ascontiguousarray(np.tile([1.6, 6.0, 0.0, 0.0], (nrec, 1)))  # per-record default seed
+    out = torch.empty((6, nrec * nbuf), dtype=torch.float64, device=dev)
+    ok = torch.empty(nrec * nbuf, dtype=torch.int32, device=dev)
+    nall = nrec * nbuf  # segments in the batch (demodulation / LM-only timings run over all of them)
+    qi = torch.empty((2 * NDATA, nall), dtype=torch.float64, device=dev)
+    dcb = torch.empty(nall, dtype=torch.float64, device=dev)
+    rows = torch.empty((nall, lib.dfmi_qi_row_stride(NDATA)), dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream()
 
     def step():
-        rc = lib.dfmi_nls_record(x.data_ptr(), 1, nbuf * R, nbuf, R, NDATA, w0, 0, _lib.ptr(guess), 1, nbuf - 1,
+        rc = lib.dfmi_nls_record(x.data_ptr(), nrec, nbuf * R, nbuf, R, NDATA, w0, 0, _lib.ptr(guess), 1, nbuf - 1,
                                  cfg, out.data_ptr(), ok.data_ptr(), _lib.DFMI_MEM_DEVICE, stream.cuda_stream)
         _lib.check(rc, "dfmi_nls_record")
 
     def demod():  # the record pipeline's demodulation (row layout): the roofline kernel
-        rc = lib.dfmi_demod_rows(x.data_ptr(), nbuf, R, R, NDATA, w0, 0, rows.data_ptr(), _lib.DFMI_MEM_DEVICE,
+        rc = lib.dfmi_demod_rows(x.data_ptr(), nall, R, R, NDATA, w0, 0, rows.data_ptr(), _lib.DFMI_MEM_DEVICE,
                                  stream.cuda_stream)
         _lib.check(rc, "dfmi_demod_rows")
 
@@ -198,6 +211,8 @@ def main():
     value = total_segments * args.steps / el
     # BASELINE.json configs: 2 = 100k segments on one GPU, 4 = 10M over 8 GPUs (1.25M per GPU)
     cfg_name = {100_000: "config2", 1_250_000: "config4 shard"}.get(nseg, "config2-shape")
+    if nrec == 2:
+        cfg_name = "config3"
 
     # ---- roofline of the dominant kernel (demod), HIP events on the launch stream ----
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -218,17 +233,17 @@ def main():
             dist.destroy_process_group()
         return
     # the LM kernel alone over the same QI (every segment its own chunk), for the record
-    lm_out = torch.empty((4, nbuf), dtype=torch.float64, device=dev)
-    lm_ssq = torch.empty(nbuf, dtype=torch.float64, device=dev)
-    lm_st = torch.empty(nbuf, dtype=torch.int32, device=dev)
+    lm_out = torch.empty((4, nall), dtype=torch.float64, device=dev)
+    lm_ssq = torch.empty(nall, dtype=torch.float64, device=dev)
+    lm_st = torch.empty(nall, dtype=torch.int32, device=dev)
     gdev = torch.tensor([1.0, 6.0, 0.0, 0.0], dtype=torch.float64, device=dev)
 
     def lm_only():
-        rc = lib.dfmi_lm(qi.data_ptr(), nbuf, NDATA, gdev.data_ptr(), 0, nbuf, cfg, lm_out.data_ptr(),
+        rc = lib.dfmi_lm(qi.data_ptr(), nall, NDATA, gdev.data_ptr(), 0, nall, cfg, lm_out.data_ptr(),
                          lm_ssq.data_ptr(), lm_st.data_ptr(), _lib.DFMI_MEM_DEVICE, stream.cuda_stream)
         _lib.check(rc, "dfmi_lm")
 
-    _lib.check(lib.dfmi_demod(x.data_ptr(), nbuf, R, R, NDATA, w0, 0, qi.data_ptr(), dcb.data_ptr(),
+    _lib.check(lib.dfmi_demod(x.data_ptr(), nall, R, R, NDATA, w0, 0, qi.data_ptr(), dcb.data_ptr(),
                               _lib.DFMI_MEM_DEVICE, stream.cuda_stream), "dfmi_demod")
     lm_only()
     ev0.record(stream)
@@ -238,7 +253,7 @@ def main():
     ev1.synchronize()
     lm_ms = ev0.elapsed_time(ev1) / nrep
     bytes_per_seg = 8 * R + 8 * (2 * NDATA + 1)  # read the segment, write QI + dc
-    achieved = nbuf * bytes_per_seg / (demod_ms * 1e-3) / 1e9
+    achieved = nall * bytes_per_seg / (demod_ms * 1e-3) / 1e9
     family = kname.split("<")[0]
     traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_demod.json")
@@ -246,11 +261,11 @@ def main():
         with open(pmc) as f:
             rec = json.load(f)
         if family and family in rec.get("kernel", "") and rec.get("algorithmic_bytes_per_launch") == \
-                nbuf * bytes_per_seg:
+                nall * bytes_per_seg:
             traffic, traffic_src = rec.get("hbm_bytes_per_launch"), "profiles/pmc_demod.json"
     roof = {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-            "avg_launch_ms": round(demod_ms, 4), "algorithmic_bytes_per_launch": nbuf * bytes_per_seg}
+            "avg_launch_ms": round(demod_ms, 4), "algorithmic_bytes_per_launch": nall * bytes_per_seg}
 
     # parity on the timed batch itself: status-0 fraction and a sanity check of the estimates
     st = ok.cpu().numpy()
@@ -260,9 +275,10 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic snr-mode DFMI (m=6, 40 dB white noise) generated on device",
-            "config": {"workload": f"{cfg_name}: {nseg} segments/GPU x R={R} @200 kS/s, ndata={NDATA}, 1 channel, "
-                                   f"_fit_parallel chunk size 1",
-                       "segments_per_gpu": nseg, "R": R, "ndata": NDATA, "parallelism": f"shard{world}"},
+            "config": {"workload": f"{cfg_name}: {nseg} segments/GPU x R={R} @200 kS/s, ndata={NDATA}, "
+                                   f"{nrec} channel{'s' if nrec > 1 else ''}, _fit_parallel chunk size 1",
+                       "segments_per_gpu": nseg, "channels": nrec, "R": R, "ndata": NDATA,
+                       "parallelism": f"shard{world}"},
             "roofline": roof,
             "kernels_ms": {"demod": round(demod_ms, 4), "lm_all_segments": round(lm_ms, 4)},
             "batch_status0_frac": float(np.mean(st == 0)),

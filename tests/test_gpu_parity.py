@@ -305,6 +305,37 @@ def test_seed_stream_order_identical():
         np.testing.assert_array_equal(ok, res[0][1])
 
 
+@pytest.mark.parametrize("nrec,nbuf", [(3, 40), (600, 3), (4, 1), (1, 2)])
+def test_fused_seed_layouts_match_unfused(nrec, nbuf):
+    """The fused seed + demodulation launch (seed_fused 1) against the two-kernel path
+    (seed_fused 0) across record layouts: several records (one seed workgroup each),
+    more records than can be resident as seeds (the fused path steps aside), single-
+    buffer records (no LM), two buffers. Same bits; every record's seed is its own
+    buffer 0 (fitters.py:403-410)."""
+    import torch
+    from deepfmkit_amd import _lib
+    from deepfmkit_amd.fitters import nls_records
+    lib = _lib.load()
+    R = 4000
+    t = torch.arange(nbuf * R, dtype=torch.float64, device="cuda") / 200000.0
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    ms = torch.linspace(4.0, 8.0, nrec, dtype=torch.float64, device="cuda")[:, None]
+    x = 1.0 + torch.cos(0.3 + ms * torch.cos(2 * np.pi * 1000.0 * t[None, :] + 0.1))
+    x = (x + 1e-3 * torch.randn(x.shape, dtype=torch.float64, device="cuda", generator=g)).contiguous()
+    res = []
+    for fused in (1, 0):
+        _lib.check(lib.dfmi_set_tuning(b"seed_fused", fused), "tune")
+        cols, ok = nls_records(x, 200000.0, 1000.0, R, nbuf, 10, init_guess=(1.0, 6.0, 0.0, 0.0))
+        res.append((cols.cpu().numpy(), ok.cpu().numpy()))
+    _lib.check(lib.dfmi_set_tuning(b"seed_fused", 1), "tune")
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    np.testing.assert_array_equal(res[0][1], res[1][1])
+    m = res[0][0][1].reshape(nrec, nbuf)
+    assert np.all(np.abs(m - ms.cpu().numpy()) < 1e-3)
+    assert np.all(res[0][1] == 0)
+
+
 def test_raw_file_to_fit_file_end_to_end(tmp_path):
     """raw_data file -> load_raw (host, and straight to the GPU) -> fit -> to_txt ->
     load_fit: the device-loaded record fits to the same bits as the host-loaded one,

@@ -206,6 +206,7 @@ struct Tuning {
   int seed_order = 1;          // 1: seed on the caller's stream, bulk demodulation on the side stream
   int demod_occ4 = 0;          // 1: bin kernel held to 128 VGPRs (4 waves per SIMD)
   int seed_fused = 1;          // 1: seed + bulk demodulation in one launch on the caller's stream
+  int wdfmi_accel = 3;         // W-DFMI: bit 0 time axis without division, bit 1 template slopes in LDS
 };
 Tuning g_tune;
 std::string g_last_demod;     // kernel variant of the last demodulation launch (dfmi_last_demod_kernel)
@@ -608,7 +609,8 @@ const std::map<std::string, Knob>& knobs() {
       {"demod_kernel", {&g_tune.demod_kernel, {0, 1}}},    {"seed_bins", {&g_tune.seed_bins, {0, 1}}},
       {"seed_order", {&g_tune.seed_order, {0, 1}}},
       {"demod_occ4", {&g_tune.demod_occ4, {0, 1}}},
-      {"seed_fused", {&g_tune.seed_fused, {0, 1}}}};
+      {"seed_fused", {&g_tune.seed_fused, {0, 1}}},
+      {"wdfmi_accel", {&g_tune.wdfmi_accel, {0, 1, 2, 3}}}};
   return k;
 }
 }  // namespace
@@ -890,6 +892,7 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
   a.ndata = cfg->ndata;
   a.ndata_psi = cfg->ndata_psi;
   a.threads = R <= 4096 ? 256 : 1024;
+  a.accel = g_tune.wdfmi_accel;
   a.probe = g_probe;
   a.nrec = nrec;
   a.nbuf = nbuf;

@@ -29,6 +29,13 @@ struct WdfmiLaunch {
   int32_t* fitok;                // nrec*nbuf
   uint64_t* probe;               // diagnostics timestamps (null: off)
   const int* pw_plan;            // numpy summation plan over R (np_sum.h dfmi_pairwise_plan)
+  // bit 0: time axis by multiply + fma correction (when exact), bit 1: the template's
+  // slope table in LDS (when it fits); dfmi_set_tuning("wdfmi_accel"), default 3
+  int32_t accel;
+  // set by wdfmi_launch: the time axis k / f_samp formed as q = k * t_rcp plus one
+  // fma correction when that reproduces the division for every k in [0, R] (t_fast)
+  int32_t t_fast;
+  double t_rcp;
 };
 
 // Dynamic LDS bytes the fit kernel of this launch needs.

@@ -33,6 +33,9 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <cmath>
+#include <type_traits>
+
 #include "dfmi_math.h"
 #include "np_sum.h"
 #include "wdfmi.h"
@@ -141,10 +144,26 @@ __device__ void block_reduce(double (&v)[N], double* red, Op op) {
 // ---------------------------------------------------------------------------
 struct Geo {
   int R;
-  double fs, period, omega;
-  // t_k = k / f_samp, formed in registers: IEEE division rounds exactly like numpy's
-  // np.arange(R) / f_samp, and costs a few VALU ops instead of a dependent load.
-  __device__ __forceinline__ double t(int k) const { return (double)k / fs; }
+  bool fast;  // WdfmiLaunch::t_fast
+  double fs, rfs, period, omega;
+  const double* slp;  // LDS: the template's interval slopes (null: divide per sample)
+  // t_k = k / f_samp, formed in registers, rounded exactly like numpy's
+  // np.arange(R) / f_samp: q = k * (1/f_samp) corrected by one fma of its residual
+  // (Markstein) where the host verified that this equals the IEEE quotient for every
+  // k in [0, R], else the division itself (~12 fp64 instructions).
+  template <bool FAST>
+  __device__ __forceinline__ double tt(int k) const {
+    const double kd = (double)k;
+    if constexpr (FAST) {
+      const double q = kd * rfs;
+      return fma(fma(-q, fs, kd), rfs, q);
+    } else {
+      return kd / fs;
+    }
+  }
+  // runtime choice (prologues, the rare exact search); the per-sample loops take the
+  // compile-time form, dispatched once per evaluation, so they stay straight-line
+  __device__ __forceinline__ double t(int k) const { return fast ? tt<true>(k) : tt<false>(k); }
 };
 
 // Largest i <= hi with t_i <= x (caller guarantees t_0 <= x); also returns t_i, t_{i+1}.
@@ -167,52 +186,7 @@ __device__ __forceinline__ int seek(const Geo& g, double x, int hi, double& ti, 
   return i;
 }
 
-// np.interp(x, t, f, period=t[-1]) for x already reduced into [0, period]
-// (numpy's x % period). numpy sorts xp = t % period: t[R-1] % period = 0 ties with
-// t[0]; argsort places index 0 first, so the sorted/padded table is
-//   xp = [t_{R-2}-P, 0, 0, t_1 .. t_{R-2}, P],  fp = [f_{R-2}, f_0, f_{R-1}, f_1 .. f_{R-2}, f_0]
-// and x in [0, t_1) interpolates from the second zero (value f_{R-1}).
-__device__ __forceinline__ double interp_per(const Geo& g, double x, const double* f) {
-  if (x != x) return x;
-  const int R = g.R;
-  if (x >= g.period) return f[0];
-  double ti, tn;
-  const int i = seek(g, x, R - 2, ti, tn);
-  if (i == 0) {
-    if (x == 0.0) return f[R - 1];
-    const double slope = (f[1] - f[R - 1]) / (tn - 0.0);
-    return slope * (x - 0.0) + f[R - 1];
-  }
-  if (x == ti) return f[i];
-  const double fn = (i == R - 2) ? f[0] : f[i + 1];
-  const double slope = (fn - f[i]) / (tn - ti);
-  return slope * (x - ti) + f[i];
-}
-
-// np.interp(x, t, f) (no period): left = f[0], right = f[R-1].
-__device__ __forceinline__ double interp_lin(const Geo& g, double x, const double* f) {
-  if (x != x) return x;
-  const int R = g.R;
-  if (x > g.period) return f[R - 1];
-  if (x < 0.0) return f[0];
-  double ti, tn;
-  const int i = seek(g, x, R - 1, ti, tn);
-  if (i == R - 1) return f[R - 1];
-  if (x == ti) return f[i];
-  const double slope = (f[i + 1] - f[i]) / (tn - ti);
-  return slope * (x - ti) + f[i];
-}
-
-// numpy's x % period for |x| < 2*period without fmod's general loop: x - period is
-// exact there (Sterbenz), x + period rounds exactly as numpy's mod += b.
-__device__ __forceinline__ double pmod(double x, double period) {
-  if (x >= 0.0 && x < period) return x == 0.0 ? 0.0 : x;
-  if (x >= period && x < 2.0 * period) return x == period ? 0.0 : x - period;
-  if (x < 0.0 && x >= -period) return x + period;
-  return dfmi_pymod(x, period);
-}
-
-// ---- batched, branch-free forms of the above (one thread's SPT samples at once) ----
+// ---- np.interp, batched and branch-free (one thread's SPT samples at once) ----
 // The straight-line bodies let the compiler interleave the samples' dependent
 // chains; the exact sequential search only runs when the first guess
 // i = (int)(x * f_samp) does not bracket x (rounding at a grid point: rare).
@@ -227,8 +201,13 @@ __device__ __forceinline__ double pmod_fast(double x, double period, bool& slow)
   return r;
 }
 
-// x[s] in [0, period] (numpy's reduced abscissae) -> np.interp(x, t, f, period=t[-1])
-template <int SPT>
+// x[s] in [0, period] (numpy's reduced abscissae) -> np.interp(x, t, f, period=t[-1]).
+// numpy sorts xp = t % period: t[R-1] % period = 0 ties with t[0]; argsort places
+// index 0 first, so the sorted/padded table is
+//   xp = [t_{R-2}-P, 0, 0, t_1 .. t_{R-2}, P],  fp = [f_{R-2}, f_0, f_{R-1}, f_1 .. f_{R-2}, f_0]
+// and x in [0, t_1) interpolates from the second zero (value f_{R-1}).
+// SLP: take the slopes from g.slp (the template's table) instead of dividing per sample.
+template <int SPT, bool FAST, bool SLP>
 __device__ __forceinline__ void interp_per_batch(const Geo& g, const double (&x)[SPT], const double* f,
                                                  double (&out)[SPT], int nvalid) {
   const int R = g.R;
@@ -240,8 +219,8 @@ __device__ __forceinline__ void interp_per_batch(const Geo& g, const double (&x)
     const double xs = (x[s] == x[s]) ? x[s] : 0.0;
     int i = (int)(xs * g.fs);
     i = i < 0 ? 0 : (i > R - 2 ? R - 2 : i);
-    ti[s] = (double)i / g.fs;
-    tn[s] = (double)(i + 1) / g.fs;
+    ti[s] = g.tt<FAST>(i);
+    tn[s] = g.tt<FAST>(i + 1);
     const bool ok = (ti[s] <= xs) && (xs < tn[s] || i == R - 2);
     bad = bad || (s < nvalid && !ok);
     idx[s] = i;
@@ -258,7 +237,7 @@ __device__ __forceinline__ void interp_per_batch(const Geo& g, const double (&x)
     const int i = idx[s];
     const double fl = (i == 0) ? f[R - 1] : f[i];
     const double fr = (i == R - 2) ? f[0] : f[i + 1];
-    const double slope = (fr - fl) / (tn[s] - ti[s]);
+    const double slope = SLP ? g.slp[i] : (fr - fl) / (tn[s] - ti[s]);
     double r = slope * (x[s] - ti[s]) + fl;
     r = (x[s] == ti[s]) ? fl : r;
     r = (x[s] >= g.period) ? f[0] : r;
@@ -266,8 +245,8 @@ __device__ __forceinline__ void interp_per_batch(const Geo& g, const double (&x)
   }
 }
 
-// np.interp(x, t, f) (no period) for a batch
-template <int SPT>
+// np.interp(x, t, f) (no period; left = f[0], right = f[R-1]) for a batch
+template <int SPT, bool FAST, bool SLP>
 __device__ __forceinline__ void interp_lin_batch(const Geo& g, const double (&x)[SPT], const double* f,
                                                  double (&out)[SPT], int nvalid) {
   const int R = g.R;
@@ -279,8 +258,8 @@ __device__ __forceinline__ void interp_lin_batch(const Geo& g, const double (&x)
     const double xs = (x[s] >= 0.0 && x[s] <= g.period) ? x[s] : 0.0;  // out of range / NaN: selected below
     int i = (int)(xs * g.fs);
     i = i < 0 ? 0 : (i > R - 2 ? R - 2 : i);
-    ti[s] = (double)i / g.fs;
-    tn[s] = (double)(i + 1) / g.fs;
+    ti[s] = g.tt<FAST>(i);
+    tn[s] = g.tt<FAST>(i + 1);
     const bool ok = (ti[s] <= xs) && (xs < tn[s] || i == R - 2);
     bad = bad || (s < nvalid && !ok);
     idx[s] = i;
@@ -298,7 +277,7 @@ __device__ __forceinline__ void interp_lin_batch(const Geo& g, const double (&x)
   for (int s = 0; s < SPT; ++s) {
     const int i = idx[s];
     const double fl = f[i], fr = f[i + 1];
-    const double slope = (fr - fl) / (tn[s] - ti[s]);
+    const double slope = SLP ? g.slp[i] : (fr - fl) / (tn[s] - ti[s]);
     double r = slope * (x[s] - ti[s]) + fl;
     r = (x[s] == ti[s]) ? fl : r;
     r = (x[s] >= g.period) ? f[R - 1] : r;  // x == t[R-1] and beyond: right value
@@ -333,7 +312,7 @@ __device__ __forceinline__ void sincos_fast(double x, double* sn, double* cs) {
 
 // W-DFMI phase difference (fitters.py:533-539 / 611-617 / 688-694):
 //   shifted = interp(t - (-psi/omega), t, tab, period), delayed = interp(t - tau, t, shifted, period)
-template <int T, int SPT>
+template <int T, int SPT, bool FAST, bool SLP>
 __device__ __forceinline__ void wdfmi_delta(const Geo& g, const double* tab, double* sh, double tau, double psi,
                                             double (&d)[SPT]) {
   const double c = (-psi) / g.omega;
@@ -343,14 +322,14 @@ __device__ __forceinline__ void wdfmi_delta(const Geo& g, const double* tab, dou
 #pragma unroll
   for (int s = 0; s < SPT; ++s) {
     bool sl;
-    x[s] = pmod_fast(g.t(threadIdx.x + T * s) - c, g.period, sl);
+    x[s] = pmod_fast(g.tt<FAST>(threadIdx.x + T * s) - c, g.period, sl);
     slow = slow || sl;
   }
   if (slow) {
 #pragma unroll
-    for (int s = 0; s < SPT; ++s) x[s] = dfmi_pymod(g.t(threadIdx.x + T * s) - c, g.period);
+    for (int s = 0; s < SPT; ++s) x[s] = dfmi_pymod(g.tt<FAST>(threadIdx.x + T * s) - c, g.period);
   }
-  interp_per_batch<SPT>(g, x, tab, y, nvalid);
+  interp_per_batch<SPT, FAST, SLP>(g, x, tab, y, nvalid);
 #pragma unroll
   for (int s = 0; s < SPT; ++s) {
     const int k = threadIdx.x + T * s;
@@ -361,27 +340,27 @@ __device__ __forceinline__ void wdfmi_delta(const Geo& g, const double* tab, dou
 #pragma unroll
   for (int s = 0; s < SPT; ++s) {
     bool sl;
-    x[s] = pmod_fast(g.t(threadIdx.x + T * s) - tau, g.period, sl);
+    x[s] = pmod_fast(g.tt<FAST>(threadIdx.x + T * s) - tau, g.period, sl);
     slow = slow || sl;
   }
   if (slow) {
 #pragma unroll
-    for (int s = 0; s < SPT; ++s) x[s] = dfmi_pymod(g.t(threadIdx.x + T * s) - tau, g.period);
+    for (int s = 0; s < SPT; ++s) x[s] = dfmi_pymod(g.tt<FAST>(threadIdx.x + T * s) - tau, g.period);
   }
-  interp_per_batch<SPT>(g, x, sh, d, nvalid);
+  interp_per_batch<SPT, FAST, false>(g, x, sh, d, nvalid);
 #pragma unroll
   for (int s = 0; s < SPT; ++s) d[s] = d[s] - y[s];
   __syncthreads();
 }
 
 // HW-DFMI (fitters.py:848-852): delta = tmpl - interp(t - tau, t, tmpl)
-template <int T, int SPT>
+template <int T, int SPT, bool FAST, bool SLP>
 __device__ __forceinline__ void hw_delta(const Geo& g, const double* tab, double tau, double (&d)[SPT]) {
   const int nvalid = (g.R - (int)threadIdx.x + T - 1) / T;
   double x[SPT];
 #pragma unroll
-  for (int s = 0; s < SPT; ++s) x[s] = g.t(threadIdx.x + T * s) - tau;
-  interp_lin_batch<SPT>(g, x, tab, d, nvalid);
+  for (int s = 0; s < SPT; ++s) x[s] = g.tt<FAST>(threadIdx.x + T * s) - tau;
+  interp_lin_batch<SPT, FAST, SLP>(g, x, tab, d, nvalid);
 #pragma unroll
   for (int s = 0; s < SPT; ++s) {
     const int k = threadIdx.x + T * s;
@@ -1332,7 +1311,7 @@ __global__ __launch_bounds__(T) void wdfmi_template_kernel(WdfmiLaunch a) {
 }
 
 struct LdsMap {
-  double *tab, *sh, *vac, *mv, *bins, *hout, *hmeas, *red, *leafv;
+  double *tab, *sh, *vac, *mv, *bins, *hout, *hmeas, *red, *leafv, *slp;
 };
 
 // All methods: tab (witness template) | sh (shifted phase / scratch) | vac (the
@@ -1340,15 +1319,27 @@ struct LdsMap {
 // bins and the harmonic vectors.
 __host__ __device__ inline bool needs_harmonics(int method) { return method == kWdfmiNLS || method == kWdfmiSeq; }
 
-__host__ __device__ inline size_t lds_doubles(int method, int R, int L, int threads) {
+__host__ __device__ inline size_t lds_doubles_base(int method, int R, int L, int threads) {
   const int Lp = ((L > 0 ? L : 1) + 1) & ~1;
   size_t n = 3 * (size_t)R + (threads / 64) * 8 + LEAFMAX;
   if (needs_harmonics(method)) n += (size_t)R + Lp + 4 * NHMAX;
   return n;
 }
 
+// The template's slope table (R - 1 doubles) rides along where the workgroup's LDS
+// still has room for it (ortho / hw at R = 4000; not nls / seq).
+constexpr size_t kLdsDoubles = 160 * 1024 / 8;
+__host__ __device__ inline bool slopes_in_lds(const WdfmiLaunch& a) {
+  return (a.accel & 2) && lds_doubles_base(a.method, a.R, a.L, a.threads) + (size_t)a.R <= kLdsDoubles;
+}
+
+__host__ __device__ inline size_t lds_doubles(const WdfmiLaunch& a) {
+  return lds_doubles_base(a.method, a.R, a.L, a.threads) + (slopes_in_lds(a) ? (size_t)a.R : 0);
+}
+
 template <int T>
-__device__ LdsMap lds_map(double* lds, int method, int R, int L) {
+__device__ LdsMap lds_map(double* lds, const WdfmiLaunch& a) {
+  const int method = a.method, R = a.R, L = a.L;
   LdsMap m;
   const int Lp = ((L > 0 ? L : 1) + 1) & ~1;
   m.tab = lds;
@@ -1357,12 +1348,15 @@ __device__ LdsMap lds_map(double* lds, int method, int R, int L) {
   m.red = m.vac + R;
   m.leafv = m.red + (T / 64) * 8;
   m.mv = m.bins = m.hout = m.hmeas = nullptr;
+  double* end = m.leafv + LEAFMAX;
   if (needs_harmonics(method)) {
-    m.mv = m.leafv + LEAFMAX;
+    m.mv = end;
     m.bins = m.mv + R;
     m.hout = m.bins + Lp;
     m.hmeas = m.hout + 2 * NHMAX;
+    end = m.hmeas + 2 * NHMAX;
   }
+  m.slp = slopes_in_lds(a) ? end : nullptr;
   return m;
 }
 
@@ -1418,8 +1412,16 @@ template <int T, int SPT>
 __device__ __attribute__((noinline)) EvalOut evaluate(const Geo g, const LdsMap L, double tau, double psi, int flags,
                                                       double amp, double phi) {
   double d[SPT], v[SPT], bi[SPT], bq[SPT];
-  if (flags & kEvHW) hw_delta<T, SPT>(g, L.tab, tau, d);
-  else wdfmi_delta<T, SPT>(g, L.tab, L.sh, tau, psi, d);
+  auto delta = [&](auto fast, auto slp) {
+    constexpr bool F = decltype(fast)::value, S = decltype(slp)::value;
+    if (flags & kEvHW) hw_delta<T, SPT, F, S>(g, L.tab, tau, d);
+    else wdfmi_delta<T, SPT, F, S>(g, L.tab, L.sh, tau, psi, d);
+  };
+  using yes = std::true_type;
+  using no = std::false_type;
+  if (g.fast && g.slp) delta(yes(), yes());
+  else if (g.fast) delta(yes(), no());
+  else delta(no(), no());  // the slope table without the fast time axis: not worth a variant
   EvalOut o;
   o.p0 = o.p1 = o.res = o.dmax = o.dmin = 0.0;
   o.full = false;
@@ -1470,10 +1472,13 @@ template <int T, int SPT, int METHOD>
 __global__ __launch_bounds__(T) void wdfmi_fit_kernel(WdfmiLaunch a) {
   extern __shared__ double lds[];
   const int R = a.R;
-  const LdsMap L = lds_map<T>(lds, METHOD, R, a.L);
+  const LdsMap L = lds_map<T>(lds, a);
   Geo g;
   g.R = R;
+  g.fast = a.t_fast != 0;
   g.fs = a.f_samp;
+  g.rfs = a.t_rcp;
+  g.slp = nullptr;
   g.period = g.t(R - 1);  // t[-1]
   g.omega = (2.0 * kPi) * a.f_mod;
   const double m_scale = (2.0 * kPi) * a.df;
@@ -1491,6 +1496,20 @@ __global__ __launch_bounds__(T) void wdfmi_fit_kernel(WdfmiLaunch a) {
   const double* __restrict__ tsrc = a.tmpl + (a.wit_stride == 0 ? 0 : rec) * (int64_t)R;
   for (int k = threadIdx.x; k < R; k += T) L.tab[k] = tsrc[k];
   __syncthreads();
+  if (L.slp) {
+    // np.interp's interval slopes (fp[j+1] - fp[j]) / (xp[j+1] - xp[j]) of the template
+    // table, formed once per record: HW-DFMI's clamped table, else the periodic one
+    // (interp_per_batch's sorted/padded layout: interval 0 starts at the second zero
+    // with f_{R-1}, interval R-2 ends at the period with f_0).
+    const bool per = METHOD != kHwdfmi;
+    for (int i = threadIdx.x; i < R - 1; i += T) {
+      const double fl = (per && i == 0) ? L.tab[R - 1] : L.tab[i];
+      const double fr = (per && i == R - 2) ? L.tab[0] : L.tab[i + 1];
+      L.slp[i] = (fr - fl) / (g.t(i + 1) - g.t(i));
+    }
+    __syncthreads();
+    g.slp = L.slp;
+  }
   Probe pr;
   pr.init(a.probe);
   auto ev = [&](double tau, double psi, int flags, double amp = 0.0, double phi = 0.0) -> EvalOut {
@@ -1646,10 +1665,17 @@ hipError_t launch_t(const WdfmiLaunch& a, hipStream_t st) {
 
 }  // namespace
 
-size_t wdfmi_lds_bytes(const WdfmiLaunch& a) { return lds_doubles(a.method, a.R, a.L, a.threads) * 8; }
+size_t wdfmi_lds_bytes(const WdfmiLaunch& a) { return lds_doubles(a) * 8; }
 
-hipError_t wdfmi_launch(const WdfmiLaunch& a, hipStream_t st) {
-  if (a.nrec == 0 || a.nbuf == 0) return hipSuccess;
+hipError_t wdfmi_launch(const WdfmiLaunch& in, hipStream_t st) {
+  if (in.nrec == 0 || in.nbuf == 0) return hipSuccess;
+  WdfmiLaunch a = in;
+  a.t_rcp = 1.0 / a.f_samp;
+  a.t_fast = (a.accel & 1) ? 1 : 0;
+  for (int k = 0; k <= a.R && a.t_fast; ++k) {
+    const double kd = (double)k, q = kd * a.t_rcp;
+    if (std::fma(std::fma(-q, a.f_samp, kd), a.t_rcp, q) != kd / a.f_samp) a.t_fast = 0;
+  }
   // one wave per SIMD and 16 samples per thread measured fastest at R = 4000 (256 vs
   // 512 vs 1024 threads: scripts/bench_wdfmi.py --threads); larger R widens the group
   if (a.R <= 16 * 256) return launch_t<256, 16>(a, st);

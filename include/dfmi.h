@@ -164,12 +164,15 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
                    const double* witness, int64_t wit_stride, const dfmi_wdfmi_config* cfg, double* out,
                    int32_t* fitok, int32_t mem, void* stream);
 
-/* Performance tuning hook (results are unaffected): "demod_kernel" (0 cycle-aligned
- * fold, 1 pipelined cycle-aligned fold, 2 bins in LDS [default], 3 pipelined bins),
- * "demod_unr" (cycles/chunks per batch of the pipelined variants), "demod_loads"
- * (8 | 16 vector loads in flight per lane), "demod_nt" (0 | 1 non-temporal stream
- * loads), "demod_blocks_per_cu" (0 = occupancy limit), "lm_general" (1 = two-pass LM
- * path for every ndata). Process-wide. */
+/* Performance tuning hook, process-wide (results are unaffected unless noted):
+ * "demod_kernel" (1 phase bins in LDS where they apply [default], 0 cycle-aligned
+ * fold), "demod_loads" (8 | 16 vector loads in flight per lane), "demod_nt" (0 | 1
+ * non-temporal stream loads), "demod_blocks_per_cu" (0 = occupancy limit),
+ * "demod_occ4" (1 = bin kernel held to 4 waves per SIMD), "lm_general" (1 = two-pass
+ * LM path for every ndata), "seed_bins" (1 = seed fold in LDS; moves fits < 1e-10),
+ * "seed_order" / "seed_fused" (seed step scheduling), "wdfmi_accel" (bit 0: W-DFMI
+ * time axis without division, bit 1: template slopes in LDS; both exact), "probe"
+ * (1 = diagnostics timestamps, dfmi_probe_read). */
 int dfmi_set_tuning(const char* key, int64_t value);
 
 /* Current value of a tuning key (see dfmi_set_tuning). */

@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--nbuf", type=int, default=9)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cpu", type=int, default=1, help="time the oracle on one record (1 core)")
-    ap.add_argument("--threads", default="", help="comma list of wdfmi_threads values to compare")
+    ap.add_argument("--accel", default="", help="comma list of wdfmi_accel tuning values to compare (default: 3)")
     args = ap.parse_args()
 
     import torch
@@ -74,9 +74,8 @@ def main():
                 W.fit_hwdfmi(rec[: nb * R], wit, f_samp, f_mod, f_ref, dl, int(n))
             cpu = {"value": nb / (time.perf_counter() - t0), "unit": "buffers/s", "cores": 1, "kind": "port",
                    "sample": f"{nb} buffers, oracle restatement of the reference loop (numpy/scipy algorithms)"}
-        for nrec, thr in [(int(v), t) for v in args.records.split(",") for t in (args.threads.split(",") if args.threads else [""])]:
-            if thr:
-                _lib.check(_lib.load().dfmi_set_tuning(b"wdfmi_threads", int(thr)), "dfmi_set_tuning")
+        for nrec, acc in [(int(v), t) for v in args.records.split(",") for t in (args.accel.split(",") if args.accel else [""])]:
+            _lib.check(_lib.load().dfmi_set_tuning(b"wdfmi_accel", int(acc) if acc else 3), "dfmi_set_tuning")
             x = torch.from_numpy(np.ascontiguousarray(np.broadcast_to(rec, (nrec, rec.size)))).to(dev)
             w = torch.from_numpy(np.ascontiguousarray(wit[:R])).to(dev)
             F.wdfmi_records(method, x, w, f_samp, f_mod, R, args.nbuf, **kw)  # warm-up (tables, code objects)
@@ -93,7 +92,7 @@ def main():
             t = float(np.median(times))
             nb_tot = nrec * args.nbuf
             line = {"metric": "W-DFMI buffers fitted/sec", "method": method, "value": nb_tot / t, "unit": "buffers/s",
-                    "records": nrec, "threads": int(thr) if thr else None, "nbuf": args.nbuf, "R": R, "seconds": t,
+                    "records": nrec, "accel": int(acc) if acc else 3, "nbuf": args.nbuf, "R": R, "seconds": t,
                     "per_buffer_latency_ms": (t / args.nbuf if method != "wdfmi_seq" else t) * 1e3,
                     "fitok_frac": float(ok.float().mean().item()), "cpu_baseline": cpu,
                     "data": "reference W-DFMI 'cos' case (tests/golden/wdfmi.npz) tiled to nbuf buffers"}

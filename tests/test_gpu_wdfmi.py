@@ -137,6 +137,26 @@ def test_records_batch_is_independent(method):
         np.testing.assert_array_equal(okm[r * nbuf:(r + 1) * nbuf], ok1)
 
 
+@pytest.mark.parametrize("case", ["cos", "dist"])
+@pytest.mark.parametrize("method", METHODS)
+def test_accel_paths_bit_identical(case, method):
+    """The time axis without division (multiply + fma correction, host-verified exact)
+    and the template's LDS slope table reproduce numpy's arithmetic: every
+    dfmi_set_tuning("wdfmi_accel") setting gives the same bits."""
+    from deepfmkit_amd import _lib
+    lib = _lib.load()
+    outs = []
+    try:
+        for acc in (0, 1, 2, 3):
+            _lib.check(lib.dfmi_set_tuning(b"wdfmi_accel", acc), "dfmi_set_tuning")
+            outs.append(gpu_fit(case, method))
+    finally:
+        _lib.check(lib.dfmi_set_tuning(b"wdfmi_accel", 3), "dfmi_set_tuning")
+    for cols, ok, _ in outs[1:]:
+        np.testing.assert_array_equal(cols, outs[0][0])
+        np.testing.assert_array_equal(ok, outs[0][1])
+
+
 @pytest.mark.parametrize("method", ["wdfmi_nls", "wdfmi_seq"])
 def test_direct_harmonics_match_folded(method):
     """period=-1 forms every angle per sample (the path for f_samp/f_mod without an

@@ -22,6 +22,7 @@
 #include "lm.h"
 #include "seed.h"
 #include "np_sum.h"
+#include "moments.h"
 #include "wdfmi.h"
 
 namespace {
@@ -44,6 +45,7 @@ int fail(int code, const std::string& msg) {
 struct DevBuf {
   void* p = nullptr;
   size_t n = 0;
+  int64_t aux = 0;  // pwplan: leaves of the plan
 };
 
 struct DeviceState {
@@ -53,7 +55,7 @@ struct DeviceState {
   std::map<std::string, DevBuf> ws;                                  // named workspaces
   std::map<std::tuple<int, int, uint64_t>, DevBuf> basis;            // (L, ndata, w0 bits)
   std::map<std::tuple<int, uint64_t, uint64_t, uint64_t>, DevBuf> gridtab;  // (ndata, min, max, step)
-  std::map<int, DevBuf> pwplan;                                     // R -> numpy pairwise-sum plan
+  std::map<int64_t, DevBuf> pwplan;                                 // n -> numpy pairwise-sum plan
   hipStream_t side = nullptr;  // seed step runs here, concurrently with the bulk demod
   hipEvent_t ev_in = nullptr, ev_seed = nullptr, ev_bulk = nullptr;
 };
@@ -103,6 +105,22 @@ int workspace(int dev, const char* name, size_t bytes, void** out) {
     b.n = bytes;
   }
   *out = b.p;
+  return DFMI_OK;
+}
+
+// Device copy of numpy's summation plan over n elements (np_sum.h), cached per n;
+// n_leaves (optional) = plan[0].
+int pairwise_plan(int dev, int64_t n, const int** out, int64_t* n_leaves) {
+  DevBuf& pb = g_dev[dev].pwplan[n];
+  if (!pb.p) {
+    const std::vector<int> plan = dfmi_pairwise_plan((int)n);
+    HIPCHK(hipMalloc(&pb.p, plan.size() * sizeof(int)));
+    pb.n = plan.size() * sizeof(int);
+    HIPCHK(hipMemcpy(pb.p, plan.data(), pb.n, hipMemcpyHostToDevice));
+    pb.aux = plan[0];
+  }
+  *out = (const int*)pb.p;
+  if (n_leaves) *n_leaves = pb.aux;
   return DFMI_OK;
 }
 
@@ -613,6 +631,107 @@ const std::map<std::string, Knob>& knobs() {
       {"wdfmi_accel", {&g_tune.wdfmi_accel, {0, 1, 2, 3}}}};
   return k;
 }
+// np.mean / np.var of nrec device records on st (moments.hip), numpy-exact.
+int moments_dev(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, double* mean, int64_t mean_stride,
+                double* var, int64_t var_stride, hipStream_t st) {
+  const int* plan;
+  int64_t nl;
+  int rc = pairwise_plan(dev, n, &plan, &nl);
+  if (rc) return rc;
+  void* nodes;
+  if ((rc = workspace(dev, "m_nodes", (size_t)nrec * 2 * nl * 8, &nodes))) return rc;
+  HIPCHK(dfmi::moments_launch(dx, nrec, rs, n, plan, nl, (double*)nodes, mean, mean_stride, var, var_stride, st));
+  return DFMI_OK;
+}
+
+// EKFFitter.fit (fitters.py:214-320) for nrec channels. Either x0 (nrec x 5, dc
+// included) and r_val (nrec) come from the caller (dfmi_ekf), or init4 (a, m, phi,
+// psi for every record) does and the pre-reductions run on the device (dfmi_ekf_fit):
+// x0[4] = np.mean(data) (fitters.py:253), R_val = np.var(data) unless given (:256).
+int ekf_impl(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, const double* x0, const double* init4,
+             const double* p0_diag, const double* q_diag, const double* r_val, double w_m, double f_samp, int32_t R,
+             int64_t nbuf, double* states, int32_t mem, void* stream) {
+  if (nrec < 0 || n_samp < 0 || R <= 0 || nbuf < 0) return fail(DFMI_ERR_ARG, "bad ekf geometry");
+  if (nrec > 1 && rec_stride < n_samp) return fail(DFMI_ERR_ARG, "rec_stride < n_samp");
+  if (init4 && n_samp > INT32_MAX) return fail(DFMI_ERR_ARG, "n_samp >= 2^31");
+  int dev;
+  int rc = ensure_init(&dev);
+  if (rc) return rc;
+  if (nrec == 0) return DFMI_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t rs = nrec > 1 ? rec_stride : n_samp;
+  const double *dx = x, *dx0 = x0, *dp0 = p0_diag, *dq = q_diag, *dr = r_val;
+  double* dstates = states;
+  const size_t sb = (size_t)nrec * nbuf * 5 * 8;
+  const bool host = mem != DFMI_MEM_DEVICE;
+  if (host) {
+    void *a, *c2, *d, *f;
+    const size_t xb = (size_t)((nrec - 1) * rs + n_samp) * 8;
+    if ((rc = workspace(dev, "e_x", xb > 0 ? xb : 8, &a))) return rc;
+    if ((rc = workspace(dev, "e_p0", 5 * 8, &c2))) return rc;
+    if ((rc = workspace(dev, "e_q", 5 * 8, &d))) return rc;
+    if ((rc = workspace(dev, "e_st", sb > 0 ? sb : 8, &f))) return rc;
+    if (xb) HIPCHK(hipMemcpyAsync(a, x, xb, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(c2, p0_diag, 5 * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d, q_diag, 5 * 8, hipMemcpyHostToDevice, st));
+    dx = (const double*)a;
+    dp0 = (const double*)c2;
+    dq = (const double*)d;
+    dstates = (double*)f;
+  }
+  if (init4) {
+    // x0 = [init4, mean] and r_val (given or np.var) formed on the device
+    void *b, *e;
+    if ((rc = workspace(dev, "e_x0", (size_t)nrec * 5 * 8, &b))) return rc;
+    if ((rc = workspace(dev, "e_r", (size_t)nrec * 8, &e))) return rc;
+    // host-side staging: init4 in every row, then the device fills x0[r*5+4] and r
+    // (an empty record keeps numpy's NaN mean / variance)
+    std::vector<double> hx0((size_t)nrec * 5), hr((size_t)nrec, NAN);
+    double i4[4];
+    if (host) memcpy(i4, init4, sizeof(i4));
+    else HIPCHK(hipMemcpy(i4, init4, sizeof(i4), hipMemcpyDeviceToHost));
+    for (int64_t r = 0; r < nrec; ++r) {
+      for (int i = 0; i < 4; ++i) hx0[r * 5 + i] = i4[i];
+      hx0[r * 5 + 4] = NAN;
+    }
+    if (r_val) {
+      double rv;
+      if (host) rv = *r_val;
+      else HIPCHK(hipMemcpy(&rv, r_val, 8, hipMemcpyDeviceToHost));
+      for (auto& v : hr) v = rv;
+    }
+    HIPCHK(hipMemcpyAsync(b, hx0.data(), hx0.size() * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(e, hr.data(), hr.size() * 8, hipMemcpyHostToDevice, st));
+    if (n_samp >= 1) {
+      if ((rc = moments_dev(dev, dx, nrec, rs, n_samp, (double*)b + 4, 5, r_val ? nullptr : (double*)e, 1, st)))
+        return rc;
+    }
+    // the staging vectors must outlive the async copies
+    HIPCHK(hipStreamSynchronize(st));
+    dx0 = (const double*)b;
+    dr = (const double*)e;
+  } else if (host) {
+    void *b, *e;
+    if ((rc = workspace(dev, "e_x0", (size_t)nrec * 5 * 8, &b))) return rc;
+    if ((rc = workspace(dev, "e_r", (size_t)nrec * 8, &e))) return rc;
+    HIPCHK(hipMemcpyAsync(b, x0, (size_t)nrec * 5 * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(e, r_val, (size_t)nrec * 8, hipMemcpyHostToDevice, st));
+    dx0 = (const double*)b;
+    dr = (const double*)e;
+  }
+  if (sb) HIPCHK(hipMemsetAsync(dstates, 0, sb, st));
+  const int block = 64;
+  const int64_t grid = (nrec + block - 1) / block;
+  hipLaunchKernelGGL(dfmi::ekf_kernel, dim3((unsigned)grid), dim3(block), 0, st, dx, nrec, rs, n_samp, dx0, dp0, dq,
+                     dr, w_m, f_samp, (int)R, nbuf, dstates);
+  HIPCHK(hipGetLastError());
+  if (host) {
+    if (sb) HIPCHK(hipMemcpyAsync(states, dstates, sb, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  return DFMI_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -909,16 +1028,7 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
   a.L = 0;
   if (nh > 0 && cfg->period >= 0) a.L = cfg->period > 0 ? cfg->period : detect_period_impl(a.w0, R, nh);
   if (a.L > R) a.L = 0;
-  {
-    DevBuf& pb = g_dev[dev].pwplan[R];
-    if (!pb.p) {
-      const std::vector<int> plan = dfmi_pairwise_plan(R);
-      HIPCHK(hipMalloc(&pb.p, plan.size() * sizeof(int)));
-      pb.n = plan.size() * sizeof(int);
-      HIPCHK(hipMemcpy(pb.p, plan.data(), pb.n, hipMemcpyHostToDevice));
-    }
-    a.pw_plan = (const int*)pb.p;
-  }
+  if ((rc = pairwise_plan(dev, R, &a.pw_plan, nullptr))) return rc;
   const size_t lds = dfmi::wdfmi_lds_bytes(a);
   if (lds > g_dev[dev].lds_per_block)
     return fail(DFMI_ERR_UNSUPPORTED, "W-DFMI: R too large for the LDS budget (" + std::to_string(lds) + " B)");
@@ -969,46 +1079,48 @@ int dfmi_ekf(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
              int64_t nbuf, double* states, int32_t mem, void* stream) {
   std::lock_guard<std::mutex> lk(g_mu);
   g_err.clear();
-  if (nrec < 0 || n_samp < 0 || R <= 0 || nbuf < 0) return fail(DFMI_ERR_ARG, "bad ekf geometry");
-  if (nrec > 1 && rec_stride < n_samp) return fail(DFMI_ERR_ARG, "rec_stride < n_samp");
+  return ekf_impl(x, nrec, rec_stride, n_samp, x0, nullptr, p0_diag, q_diag, r_val, w_m, f_samp, R, nbuf, states, mem,
+                  stream);
+}
+
+int dfmi_ekf_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, const double* init4,
+                 const double* p0_diag, const double* q_diag, const double* r_val, double w_m, double f_samp,
+                 int32_t R, int64_t nbuf, double* states, int32_t mem, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_err.clear();
+  if (!init4) return fail(DFMI_ERR_ARG, "null init4");
+  return ekf_impl(x, nrec, rec_stride, n_samp, nullptr, init4, p0_diag, q_diag, r_val, w_m, f_samp, R, nbuf, states,
+                  mem, stream);
+}
+
+int dfmi_record_moments(const double* x, int64_t nrec, int64_t rec_stride, int64_t n, double* mean, double* var,
+                        int32_t mem, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_err.clear();
+  if (nrec < 0 || n < 1 || n > INT32_MAX) return fail(DFMI_ERR_ARG, "bad moments geometry (1 <= n < 2^31)");
+  if (nrec > 1 && rec_stride < n) return fail(DFMI_ERR_ARG, "rec_stride < n");
+  if (nrec > 0 && (!x || !mean)) return fail(DFMI_ERR_ARG, "null pointer");
   int dev;
   int rc = ensure_init(&dev);
   if (rc) return rc;
   if (nrec == 0) return DFMI_OK;
   hipStream_t st = (hipStream_t)stream;
-  const int64_t rs = nrec > 1 ? rec_stride : n_samp;
-  const double *dx = x, *dx0 = x0, *dp0 = p0_diag, *dq = q_diag, *dr = r_val;
-  double* dstates = states;
-  const size_t sb = (size_t)nrec * nbuf * 5 * 8;
+  const int64_t rs = nrec > 1 ? rec_stride : n;
+  const double* dx = x;
+  double *dm = mean, *dv = var;
   if (mem != DFMI_MEM_DEVICE) {
-    void *a, *b, *c2, *d, *e, *f;
-    const size_t xb = (size_t)((nrec - 1) * rs + n_samp) * 8;
-    if ((rc = workspace(dev, "e_x", xb > 0 ? xb : 8, &a))) return rc;
-    if ((rc = workspace(dev, "e_x0", (size_t)nrec * 5 * 8, &b))) return rc;
-    if ((rc = workspace(dev, "e_p0", 5 * 8, &c2))) return rc;
-    if ((rc = workspace(dev, "e_q", 5 * 8, &d))) return rc;
-    if ((rc = workspace(dev, "e_r", (size_t)nrec * 8, &e))) return rc;
-    if ((rc = workspace(dev, "e_st", sb > 0 ? sb : 8, &f))) return rc;
-    if (xb) HIPCHK(hipMemcpyAsync(a, x, xb, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(b, x0, (size_t)nrec * 5 * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(c2, p0_diag, 5 * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(d, q_diag, 5 * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(e, r_val, (size_t)nrec * 8, hipMemcpyHostToDevice, st));
+    void *a, *b;
+    if ((rc = workspace(dev, "m_x", (size_t)((nrec - 1) * rs + n) * 8, &a))) return rc;
+    if ((rc = workspace(dev, "m_out", (size_t)nrec * 16, &b))) return rc;
+    HIPCHK(hipMemcpyAsync(a, x, (size_t)((nrec - 1) * rs + n) * 8, hipMemcpyHostToDevice, st));
     dx = (const double*)a;
-    dx0 = (const double*)b;
-    dp0 = (const double*)c2;
-    dq = (const double*)d;
-    dr = (const double*)e;
-    dstates = (double*)f;
+    dm = (double*)b;
+    dv = var ? dm + nrec : nullptr;
   }
-  if (sb) HIPCHK(hipMemsetAsync(dstates, 0, sb, st));
-  const int block = 64;
-  const int64_t grid = (nrec + block - 1) / block;
-  hipLaunchKernelGGL(dfmi::ekf_kernel, dim3((unsigned)grid), dim3(block), 0, st, dx, nrec, rs, n_samp, dx0, dp0, dq,
-                     dr, w_m, f_samp, (int)R, nbuf, dstates);
-  HIPCHK(hipGetLastError());
+  if ((rc = moments_dev(dev, dx, nrec, rs, n, dm, 1, dv, 1, st))) return rc;
   if (mem != DFMI_MEM_DEVICE) {
-    if (sb) HIPCHK(hipMemcpyAsync(states, dstates, sb, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(mean, dm, (size_t)nrec * 8, hipMemcpyDeviceToHost, st));
+    if (var) HIPCHK(hipMemcpyAsync(var, dv, (size_t)nrec * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
   }
   return DFMI_OK;

@@ -88,21 +88,24 @@ inline std::vector<int> dfmi_pairwise_plan(int n) {
   std::vector<int> plan = {nl, H};
   for (int k = 0; k < nl; ++k) plan.push_back(leaves[k]);
   plan.push_back(n);
+  // internal nodes bucketed by height (build order within a height); O(nodes) for
+  // long records, whose chunk chain makes H ~ n / 8192
+  std::vector<std::vector<int>> byh(H + 1);
+  for (size_t k = 0; k < nodes.size(); ++k)
+    if (nodes[k].a >= 0) byh[nodes[k].h].push_back((int)k);
   std::vector<int> starts, tri;
   int cnt = 0;
   for (int h = 1; h <= H; ++h) {
     starts.push_back(cnt);
-    for (size_t k = 0; k < nodes.size(); ++k)
-      if (nodes[k].a >= 0 && nodes[k].h == h) id[k] = next++, ++cnt;
+    for (int k : byh[h]) id[k] = next++, ++cnt;
   }
   starts.push_back(cnt);
   for (int h = 1; h <= H; ++h)
-    for (size_t k = 0; k < nodes.size(); ++k)
-      if (nodes[k].a >= 0 && nodes[k].h == h) {
-        tri.push_back(id[k]);
-        tri.push_back(id[nodes[k].a]);
-        tri.push_back(id[nodes[k].b]);
-      }
+    for (int k : byh[h]) {
+      tri.push_back(id[k]);
+      tri.push_back(id[nodes[k].a]);
+      tri.push_back(id[nodes[k].b]);
+    }
   plan.insert(plan.end(), starts.begin(), starts.end());
   plan.insert(plan.end(), tri.begin(), tri.end());
   return plan;

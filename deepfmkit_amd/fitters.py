@@ -189,13 +189,16 @@ def ekf_records(raws, n, **kwargs):
     qd = np.ascontiguousarray(kwargs.get("Q_diag", [1e-8, 1e-8, 1e-6, 1e-6, 1e-8]), dtype=np.float64)
     r_val = kwargs.get("R_val", None)
     x = np.ascontiguousarray(np.stack(xs))
-    x0 = np.ascontiguousarray([init + [np.mean(xx)] for xx in xs], dtype=np.float64)  # fitters.py:253
-    rv = np.ascontiguousarray([np.var(xx) if r_val is None else r_val for xx in xs], dtype=np.float64)  # :256
+    init4 = np.ascontiguousarray(init, dtype=np.float64)
+    # x0[4] = np.mean(data) (fitters.py:253) and, without R_val, np.var(data) (:256):
+    # formed on the device by dfmi_ekf_fit, in numpy's summation order
+    rv = None if r_val is None else np.ascontiguousarray([r_val], dtype=np.float64)
     states = np.zeros((len(xs), max(nbuf, 0), 5))
     w_m = 2 * np.pi * f_mod
-    rc = lib.dfmi_ekf(_lib.ptr(x), len(xs), n_samp, n_samp, _lib.ptr(x0), _lib.ptr(p0), _lib.ptr(qd), _lib.ptr(rv),
-                      w_m, float(f_samp), R, max(nbuf, 0), _lib.ptr(states), _lib.DFMI_MEM_HOST, None)
-    _lib.check(rc, "dfmi_ekf")
+    rc = lib.dfmi_ekf_fit(_lib.ptr(x), len(xs), n_samp, n_samp, _lib.ptr(init4), _lib.ptr(p0), _lib.ptr(qd),
+                          None if rv is None else _lib.ptr(rv), w_m, float(f_samp), R, max(nbuf, 0), _lib.ptr(states),
+                          _lib.DFMI_MEM_HOST, None)
+    _lib.check(rc, "dfmi_ekf_fit")
     return states
 
 

@@ -24,7 +24,9 @@
  *                    chunk with the warm start of _process_fit_chunk (fitters.py:13-60)
  *   dfmi_nls_record  StandardNLSFitter._fit_sequential / _fit_parallel
  *                    (fitters.py:370-428) for one or more records (channels)
- *   dfmi_ekf         EKFFitter.fit (fitters.py:214-320)
+ *   dfmi_ekf         EKFFitter.fit (fitters.py:214-320), pre-reductions by the caller
+ *   dfmi_ekf_fit     EKFFitter.fit whole: np.mean / np.var on the device (fitters.py:253, 256)
+ *   dfmi_record_moments  np.mean / np.var of records in numpy's summation order
  *   dfmi_wdfmi_fit   WDFMI_NLSFitter / WDFMI_OrthogonalFitter / WDFMI_SequentialFitter /
  *                    HWDFMI_Fitter .fit (fitters.py:481-891)
  */
@@ -124,6 +126,21 @@ int dfmi_nls_record(const double* x, int64_t nrec, int64_t rec_stride, int64_t n
 int dfmi_ekf(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, const double* x0,
              const double* p0_diag, const double* q_diag, const double* r_val, double w_m, double f_samp,
              int32_t R, int64_t nbuf, double* states, int32_t mem, void* stream);
+
+/* EKFFitter.fit (fitters.py:214-320) whole: as dfmi_ekf, with the two whole-record
+ * pre-reductions on the device, bit-exact with numpy: x0 = [init4[0..3],
+ * np.mean(record)] (fitters.py:253) and the measurement variance r_val[0] for every
+ * record, or np.var(record) when r_val is NULL (fitters.py:256). init4 (4 doubles:
+ * init_a, init_m, init_phi, init_psi) and r_val live in `mem` like x. n_samp < 2^31. */
+int dfmi_ekf_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, const double* init4,
+                 const double* p0_diag, const double* q_diag, const double* r_val, double w_m, double f_samp,
+                 int32_t R, int64_t nbuf, double* states, int32_t mem, void* stream);
+
+/* np.mean / np.var of nrec float64 records x[r*rec_stride .. + n] (1 <= n < 2^31),
+ * bit-exact with numpy's pairwise summation (numpy 2.x _methods._mean / _var); var
+ * may be NULL. One workgroup per record. */
+int dfmi_record_moments(const double* x, int64_t nrec, int64_t rec_stride, int64_t n, double* mean, double* var,
+                        int32_t mem, void* stream);
 
 /* ---- Witness-based fitters (EXPERIMENTAL in the reference) ----
  * Replace, per record (main channel + witness channel):

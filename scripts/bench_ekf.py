@@ -5,10 +5,10 @@ the restated reference loop, one core).
 
 Workload: `channels` independent snr-mode records (f_samp 200 kHz, f_mod 1 kHz,
 m = 6, 40 dB, n = 20 -> R = 4000 snapshot spacing) of `seconds` each, resident in
-HBM. Timing: HIP events around one dfmi_ekf call (median of `reps`); the per-record
-pre-reductions (mean, var: fitters.py:253, 256) are host inputs here, as in
-fitters.ekf_records. Reported: samples/s per channel (the serial chain's speed) and
-aggregate samples/s. One JSON line per channel count.
+HBM. Timing: HIP events around one dfmi_ekf_fit call (median of `reps`), which
+includes the per-record pre-reductions (np.mean, np.var: fitters.py:253, 256) on the
+device. Reported: samples/s per channel (the serial chain's speed) and aggregate
+samples/s. One JSON line per channel count.
 """
 import argparse
 import json
@@ -65,16 +65,16 @@ def main():
     st = torch.cuda.current_stream()
     p0 = torch.ones(5, dtype=torch.float64, device=dev)
     qd = torch.tensor([1e-8, 1e-8, 1e-6, 1e-6, 1e-8], dtype=torch.float64, device=dev)
+    init4 = torch.tensor([1.6, 6.0, 0.0, 0.0], dtype=torch.float64, device=dev)
     for nch in [int(v) for v in args.channels.split(",")]:
         x = torch.from_numpy(x1).to(dev).reshape(1, -1).expand(nch, -1).contiguous()
-        x0 = torch.tensor([[1.6, 6.0, 0.0, 0.0, float(np.mean(x1))]] * nch, dtype=torch.float64, device=dev)
-        rv = torch.full((nch,), float(np.var(x1)), dtype=torch.float64, device=dev)
         states = torch.empty((nch, nbuf, 5), dtype=torch.float64, device=dev)
 
         def call():
-            _lib.check(lib.dfmi_ekf(x.data_ptr(), nch, ns, ns, x0.data_ptr(), p0.data_ptr(), qd.data_ptr(),
-                                    rv.data_ptr(), 2 * np.pi * f_mod, f_samp, R, nbuf, states.data_ptr(),
-                                    _lib.DFMI_MEM_DEVICE, st.cuda_stream), "dfmi_ekf")
+            # EKFFitter.fit whole: np.mean / np.var of every channel on the device, then the chain
+            _lib.check(lib.dfmi_ekf_fit(x.data_ptr(), nch, ns, ns, init4.data_ptr(), p0.data_ptr(), qd.data_ptr(),
+                                        None, 2 * np.pi * f_mod, f_samp, R, nbuf, states.data_ptr(),
+                                        _lib.DFMI_MEM_DEVICE, st.cuda_stream), "dfmi_ekf_fit")
 
         call()
         torch.cuda.synchronize()

@@ -117,3 +117,24 @@ def test_wdfmi_argument_errors_before_any_device_work():
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         assert call() == -3  # DFMI_ERR_NODEV
+
+
+def test_moments_and_ekf_fit_argument_errors():
+    """dfmi_record_moments / dfmi_ekf_fit check their arguments on the host; with valid
+    arguments and no GPU they fail loudly (no host-side numpy fallback)."""
+    from deepfmkit_amd import _lib
+    lib = _lib.load()
+    x = np.zeros(100)
+    m, v = np.zeros(2), np.zeros(2)
+    H = _lib.DFMI_MEM_HOST
+    assert lib.dfmi_record_moments(_lib.ptr(x), 2, 50, 0, _lib.ptr(m), _lib.ptr(v), H, None) == -1
+    assert lib.dfmi_record_moments(_lib.ptr(x), 2, 40, 50, _lib.ptr(m), _lib.ptr(v), H, None) == -1
+    assert lib.dfmi_record_moments(_lib.ptr(x), 2, 50, 50, None, _lib.ptr(v), H, None) == -1
+    st = np.zeros((1, 5))
+    p0, qd = np.ones(5), np.ones(5)
+    assert lib.dfmi_ekf_fit(_lib.ptr(x), 1, 100, 100, None, _lib.ptr(p0), _lib.ptr(qd), None, 1.0, 1.0, 100, 1,
+                            _lib.ptr(st), H, None) == -1
+    import pytest
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        assert lib.dfmi_record_moments(_lib.ptr(x), 2, 50, 50, _lib.ptr(m), _lib.ptr(v), H, None) == -3

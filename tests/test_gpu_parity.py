@@ -170,6 +170,61 @@ def test_ekf_long_record_matches_oracle():
         np.testing.assert_array_equal(many[k], got)
 
 
+@pytest.mark.parametrize("n", [1, 7, 8, 127, 129, 4000, 8191, 8192, 8193, 30001, 400000])
+def test_record_moments_bit_exact(n):
+    """dfmi_record_moments == np.mean / np.var bit for bit (numpy's pairwise tree, its
+    8192-element buffer chunks, (x - mean)^2 rounded per operation), for 3 strided
+    records, from host and from device memory."""
+    import torch
+    from deepfmkit_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(n)
+    stride = n + 5
+    x = rng.standard_normal(3 * stride) * 10 ** rng.uniform(-2, 2, 3 * stride) + 1.7
+    mean, var = np.zeros(3), np.zeros(3)
+    _lib.check(lib.dfmi_record_moments(_lib.ptr(x), 3, stride, n, _lib.ptr(mean), _lib.ptr(var),
+                                       _lib.DFMI_MEM_HOST, None), "dfmi_record_moments")
+    for r in range(3):
+        xr = x[r * stride: r * stride + n]
+        assert mean[r] == np.mean(xr), (n, r)
+        assert var[r] == np.var(xr), (n, r)
+    dx = torch.from_numpy(x).cuda()
+    dm, dv = torch.zeros(3, dtype=torch.float64, device="cuda"), torch.zeros(3, dtype=torch.float64, device="cuda")
+    st = torch.cuda.current_stream()
+    _lib.check(lib.dfmi_record_moments(dx.data_ptr(), 3, stride, n, dm.data_ptr(), dv.data_ptr(),
+                                       _lib.DFMI_MEM_DEVICE, st.cuda_stream), "dfmi_record_moments")
+    np.testing.assert_array_equal(dm.cpu().numpy(), mean)
+    np.testing.assert_array_equal(dv.cpu().numpy(), var)
+
+
+@pytest.mark.parametrize("r_val", [None, 0.001])
+def test_ekf_device_prereductions_equal_host_numpy(r_val):
+    """dfmi_ekf_fit (np.mean / np.var on the device, fitters.py:253, 256) == dfmi_ekf
+    handed numpy's own mean and variance: the same states, bit for bit."""
+    import deepfmkit_amd as dfm
+    from deepfmkit_amd import _lib
+    lib = _lib.load()
+    laser = dfm.LaserConfig()
+    ifo = dfm.InterferometerConfig()
+    dfm.set_laser_df_for_effect(laser, ifo, 6.0)
+    dff = dfm.DeepFitFramework()
+    dff.load_sim(dfm.DFMIObject("e", laser, ifo, f_samp=200000.0))
+    dff.simulate("e", n_seconds=0.1, mode="snr", snr_db=40.0, trial_num=3)
+    raw = dff.raws["e"]
+    x = np.ascontiguousarray(raw.samples(), dtype=np.float64)
+    got = dfm.fitters.ekf_records([raw], 20, **({} if r_val is None else {"R_val": r_val}))[0]
+    x0 = np.array([1.6, 6.0, 0.0, 0.0, np.mean(x)])
+    rv = np.array([np.var(x) if r_val is None else r_val])
+    p0 = np.ones(5)
+    qd = np.array([1e-8, 1e-8, 1e-6, 1e-6, 1e-8])
+    nbuf = x.size // 4000
+    ref = np.zeros((nbuf, 5))
+    _lib.check(lib.dfmi_ekf(_lib.ptr(x), 1, x.size, x.size, _lib.ptr(x0), _lib.ptr(p0), _lib.ptr(qd), _lib.ptr(rv),
+                            2 * np.pi * 1000.0, 200000.0, 4000, nbuf, _lib.ptr(ref), _lib.DFMI_MEM_HOST, None),
+               "dfmi_ekf")
+    np.testing.assert_array_equal(got, ref)
+
+
 def test_large_batch_known_answer_and_seed_independence():
     """Full-size property checks (config 2 shape, 100k segments of R=4000, on device):
     noiseless A(1+cos(phi+m cos(wt+psi))) is recovered exactly in every segment, and a

@@ -83,7 +83,7 @@ def test_numpy_summation_plan_is_bit_exact(hc):
     hc.hc_np_sum.restype = ctypes.c_double
     rng = np.random.default_rng(0)
     for n in [1, 2, 7, 8, 9, 100, 127, 128, 129, 200, 255, 256, 257, 1000, 3999, 4000, 4001, 5000, 8191, 8192,
-              8193, 12345, 16384, 16385, 30001]:
+              8193, 12345, 16384, 16385, 30001, 400000, 400001]:
         a = rng.standard_normal(n) * 10 ** rng.uniform(-3, 3, n)
         assert hc.hc_np_sum(a.ctypes.data, n) == np.sum(a), n
 

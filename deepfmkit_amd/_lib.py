@@ -24,7 +24,7 @@ SYMBOLS = ("dfmi_lm_config_default", "dfmi_demod", "dfmi_lm", "dfmi_nls_record",
            "dfmi_last_demod_kernel", "dfmi_qi_row_stride", "dfmi_qi_row_dc", "dfmi_demod_rows",
            "dfmi_probe_read", "dfmi_get_tuning", "dfmi_txt_parse_header", "dfmi_txt_shape", "dfmi_txt_read",
            "dfmi_fit_txt_write", "dfmi_py_repr", "dfmi_txt_last_error", "dfmi_wdfmi_fit", "dfmi_ekf_fit",
-           "dfmi_record_moments")
+           "dfmi_record_moments", "dfmi_synth_asd")
 
 
 class DFMIError(RuntimeError):
@@ -99,6 +99,8 @@ def load():
         lib.dfmi_ekf_fit.restype = ctypes.c_int
         lib.dfmi_record_moments.argtypes = [P, i64, i64, i64, P, P, i32, P]
         lib.dfmi_record_moments.restype = ctypes.c_int
+        lib.dfmi_synth_asd.argtypes = [P, i64, i64, dbl, P, i32, P]
+        lib.dfmi_synth_asd.restype = ctypes.c_int
         lib.dfmi_wdfmi_fit.argtypes = [P, i64, i64, i64, i32, P, i64, ctypes.POINTER(WdfmiConfig), P, P, i32, P]
         lib.dfmi_wdfmi_fit.restype = ctypes.c_int
         lib.dfmi_detect_period.argtypes = [dbl, i32, i32]

@@ -23,6 +23,7 @@
 #include "seed.h"
 #include "np_sum.h"
 #include "moments.h"
+#include "synth.h"
 #include "wdfmi.h"
 
 namespace {
@@ -1091,6 +1092,30 @@ int dfmi_ekf_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_sa
   if (!init4) return fail(DFMI_ERR_ARG, "null init4");
   return ekf_impl(x, nrec, rec_stride, n_samp, nullptr, init4, p0_diag, q_diag, r_val, w_m, f_samp, R, nbuf, states,
                   mem, stream);
+}
+
+int dfmi_synth_asd(const dfmi_synth_trial* trials, int64_t ntrial, int64_t n_samp, double f_samp, double* out,
+                   int32_t mem, void* stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_err.clear();
+  if (ntrial < 0 || n_samp < 2 || !(f_samp > 0.0)) return fail(DFMI_ERR_ARG, "bad synthesis geometry (n_samp >= 2)");
+  if (ntrial > 0 && (!trials || !out)) return fail(DFMI_ERR_ARG, "null pointer");
+  int dev;
+  int rc = ensure_init(&dev);
+  if (rc) return rc;
+  if (ntrial == 0) return DFMI_OK;
+  hipStream_t st = (hipStream_t)stream;
+  void *dt, *scr, *dout = out;
+  const size_t ob = (size_t)ntrial * n_samp * 8;
+  if ((rc = workspace(dev, "s_trials", (size_t)ntrial * sizeof(dfmi_synth_trial), &dt))) return rc;
+  if ((rc = workspace(dev, "s_scratch", dfmi::synth_scratch_bytes(ntrial, n_samp), &scr))) return rc;
+  if (mem != DFMI_MEM_DEVICE && (rc = workspace(dev, "s_out", ob, &dout))) return rc;
+  HIPCHK(hipMemcpyAsync(dt, trials, (size_t)ntrial * sizeof(dfmi_synth_trial), hipMemcpyHostToDevice, st));
+  HIPCHK(dfmi::synth_launch((const dfmi_synth_trial*)dt, ntrial, n_samp, f_samp, scr, (double*)dout, st));
+  if (mem != DFMI_MEM_DEVICE) HIPCHK(hipMemcpyAsync(out, dout, ob, hipMemcpyDeviceToHost, st));
+  // the trial table is a caller (host) array: done with it only once the copy ran
+  HIPCHK(hipStreamSynchronize(st));
+  return DFMI_OK;
 }
 
 int dfmi_record_moments(const double* x, int64_t nrec, int64_t rec_stride, int64_t n, double* mean, double* var,

@@ -23,6 +23,11 @@ from .data import DeepRawObject
 log = logging.getLogger(__name__)
 
 
+def cosine_waveform(t_phase):
+    """The default frequency-modulation waveform (reference physics.py:15-51)."""
+    return np.cos(t_phase)
+
+
 class LaserConfig:
     """Laser source parameters (reference physics.py:15-51)."""
 
@@ -34,7 +39,7 @@ class LaserConfig:
         self.f_mod = 1000
         self.df = 3e9
         self.psi = psi if psi else 0.0
-        self.waveform_func: Callable[..., np.ndarray] = lambda t_phase: np.cos(t_phase)
+        self.waveform_func: Callable[..., np.ndarray] = cosine_waveform
         self.waveform_kwargs: Dict[str, Any] = {}
         self.f_n = 0.0
         self.df_n = 0.0
@@ -201,3 +206,91 @@ def exact_model_signal(cfg, t, noise, is_dynamic):
     if np.isscalar(truth):
         truth = np.full_like(t, truth, dtype=float)
     return sig, phase, truth
+
+
+# --- asd-mode trials on the device (dfmi_synth_asd) ---------------------------
+
+SYNTH_TRIAL_DTYPE = np.dtype([("seed", "<u4"), ("dynamic", "<i4")] + [(k, "<f8") for k in (
+    "omega_mod", "psi", "df", "cphi", "w_arm", "arml_mod_amp", "arml_mod_psi", "dl0", "c_light", "tau_m", "tau_r",
+    "w0c", "amp", "vis", "s_amp", "s_df")])  # include/dfmi.h dfmi_synth_trial
+
+
+def device_synth_supported(cfg) -> bool:
+    """dfmi_synth_asd covers the default cosine waveform with white (or zero)
+    amplitude / df noise and no frequency / arm-length noise sources."""
+    laser, ifo = cfg.laser, cfg.ifo
+    return (laser.waveform_func is cosine_waveform and not laser.waveform_kwargs and laser.f_n == 0.0
+            and ifo.arml_mod_n == 0.0)
+
+
+def synth_trial_fields(cfg, trial_num, dynamic=True):
+    """One dfmi_synth_trial: the scalar sub-expressions of asd_noise_arrays and
+    exact_model_signal, evaluated here exactly as those numpy expressions do."""
+    laser, ifo = cfg.laser, cfg.ifo
+    seed = 1 + int(trial_num) * 4
+    if not 0 <= seed <= 2 ** 32 - 1:
+        raise ValueError("Seed must be between 0 and 2**32 - 1")
+    fs_cfg = cfg.f_samp
+    t01 = np.arange(2) / cfg.f_samp
+    dt = t01[1] - t01[0]
+    fs = 1 / dt
+    f0 = (sc.c / laser.wavelength) + 0.0
+    rec = np.zeros((), dtype=SYNTH_TRIAL_DTYPE)
+    rec["seed"], rec["dynamic"] = seed, 1 if dynamic else 0
+    rec["omega_mod"] = 2 * np.pi * laser.f_mod
+    rec["psi"] = laser.psi
+    rec["df"] = laser.df
+    rec["cphi"] = 2 * np.pi / fs
+    rec["w_arm"] = 2 * np.pi * ifo.arml_mod_f
+    rec["arml_mod_amp"] = ifo.arml_mod_amp
+    rec["arml_mod_psi"] = ifo.arml_mod_psi
+    rec["dl0"] = ifo.phi * laser.wavelength / (2 * np.pi)
+    rec["c_light"] = sc.c
+    rec["tau_m"] = ifo.meas_arml / sc.c
+    rec["tau_r"] = ifo.ref_arml / sc.c
+    rec["w0c"] = 2 * np.pi * f0
+    rec["amp"] = laser.amp
+    rec["vis"] = laser.visibility
+    rec["s_amp"] = laser.amp_n * np.sqrt(fs_cfg / 2.0) if laser.amp_n != 0.0 else 0.0
+    rec["s_df"] = laser.df_n * np.sqrt(fs_cfg / 2.0) if laser.df_n != 0.0 else 0.0
+    return rec
+
+
+def synthesize_asd_trials(cfgs, trial_nums, n_seconds, dynamic=True):
+    """The main channel of SignalGenerator.generate(cfg, n_seconds, mode='asd',
+    trial_num=t) for every (cfg, t), generated on the GPU (dfmi_synth_asd) into one
+    (ntrial, N) CUDA tensor. All cfgs share f_samp; each must be
+    device_synth_supported."""
+    import torch
+
+    from . import _lib
+    from .fitters import _torch_stream
+    f_samp = float(cfgs[0].f_samp)
+    if any(float(c.f_samp) != f_samp for c in cfgs):
+        raise ValueError("synthesize_asd_trials: trials must share f_samp")
+    bad = [i for i, c in enumerate(cfgs) if not device_synth_supported(c)]
+    if bad:
+        raise ValueError(f"trials {bad[:5]} need the host generator (custom waveform or coloured noise)")
+    n = int(n_seconds * f_samp)
+    # trials of one experiment share their configuration values and differ in the
+    # seed: the scalar fields are formed once per distinct configuration
+    index, recs, which = {}, [], []
+    for c in cfgs:
+        la, fo = c.laser, c.ifo
+        key = (la.f_mod, la.psi, la.df, la.wavelength, la.amp, la.visibility, la.amp_n, la.df_n, fo.arml_mod_f,
+               fo.arml_mod_amp, fo.arml_mod_psi, fo.phi, fo.meas_arml, fo.ref_arml)
+        u = index.get(key)
+        if u is None:
+            u = index[key] = len(recs)
+            recs.append(synth_trial_fields(c, 0, dynamic))
+        which.append(u)
+    seeds = 1 + np.asarray(trial_nums, dtype=np.int64) * 4
+    if seeds.size and (seeds.min() < 0 or seeds.max() > 2 ** 32 - 1):
+        raise ValueError("Seed must be between 0 and 2**32 - 1")
+    tab = np.stack(recs)[np.asarray(which, dtype=np.int64)]
+    tab["seed"] = seeds.astype(np.uint32)
+    out = torch.empty((len(cfgs), n), dtype=torch.float64, device="cuda")
+    lib = _lib.load()
+    _lib.check(lib.dfmi_synth_asd(tab.ctypes.data, len(cfgs), n, f_samp, out.data_ptr(), _lib.DFMI_MEM_DEVICE,
+                                  _torch_stream()), "dfmi_synth_asd")
+    return out

@@ -3,8 +3,9 @@
 `run_single_trial` / `run_efficiency_trial` keep the reference's
 Configure-Simulate-Fit shape and call `DeepFitFramework.fit` (one tiny GPU
 call per trial). `run_efficiency_trials` is the batched form (SURVEY.md §8f
-item 2): it simulates every trial on the host and fits all of them in ONE
-engine call — each trial is one record of one buffer, with its own seed.
+item 2): it generates every trial's record on the GPU (dfmi_synth_asd) and fits
+all of them in ONE engine call — each trial is one record of one buffer, with
+its own seed.
 """
 from __future__ import annotations
 
@@ -66,32 +67,59 @@ def run_efficiency_trial(params: dict) -> float:
     return np.nan
 
 
-def run_efficiency_trials(params_list):
-    """Batched run_efficiency_trial: same results, one GPU call for all trials that
-    share (f_samp, f_mod, n_seconds, ndata)."""
-    from .physics import SignalGenerator
+class _TrialCfg:
+    """The fields of DFMIObject("main_trial", laser, ifo) the device generator reads
+    (run_single_trial's channel, default f_samp), without the object's set-up cost."""
+    __slots__ = ("laser", "ifo", "f_samp")
+
+    def __init__(self, laser, ifo):
+        self.laser, self.ifo, self.f_samp = laser, ifo, _DEFAULT_F_SAMP
+
+
+_DEFAULT_F_SAMP = DFMIObject("_", LaserConfig(), InterferometerConfig()).f_samp
+
+
+def run_efficiency_trials(params_list, synth="device"):
+    """Batched run_efficiency_trial: one GPU fit call for all trials that share
+    (f_samp, f_mod, n_seconds, ndata), each trial a record with its own seed.
+
+    synth="device": the trials' asd-mode records are generated on the GPU
+    (physics.synthesize_asd_trials -> dfmi_synth_asd: numpy's RandomState stream and
+    the exact-delay model restated; records within ~1e-15 of numpy's, the device's
+    cos / sin / log being the only difference) and stay in HBM for the fit; trials the
+    device generator does not cover (custom waveform) use the host generator.
+    synth="host": the package's numpy generator for every trial (results then equal
+    run_efficiency_trial's bit for bit)."""
+    from .physics import SignalGenerator, device_synth_supported, synthesize_asd_trials
+    if synth not in ("device", "host"):
+        raise ValueError("synth must be 'device' or 'host'")
     out = np.full(len(params_list), np.nan)
     groups = {}
     for i, p in enumerate(params_list):
         lc = p["laser_config"]
-        key = (float(lc.f_mod), float(p["n_seconds"]), int(p["ndata"]))
-        groups.setdefault(key, []).append(i)
-    for (f_mod, n_seconds, ndata), idx in groups.items():
-        recs, guesses, f_samp = [], [], None
-        for i in idx:
-            p = params_list[i]
-            cfg = DFMIObject("main_trial", p["laser_config"], p["ifo_config"])
-            f_samp = cfg.f_samp
-            raw = SignalGenerator().generate(cfg, n_seconds, mode="asd", trial_num=p["trial_num"])["main"]
-            recs.append(np.asarray(raw.samples(), dtype=np.float64))
-            guesses.append((1.6, p["m_true"], 0.0, 0.0))
+        cfg = _TrialCfg(lc, p["ifo_config"]) if synth == "device" else DFMIObject("main_trial", lc, p["ifo_config"])
+        dev = synth == "device" and device_synth_supported(cfg)
+        if synth == "device" and not dev:
+            cfg = DFMIObject("main_trial", lc, p["ifo_config"])
+        key = (float(cfg.f_samp), float(lc.f_mod), float(p["n_seconds"]), int(p["ndata"]), dev)
+        groups.setdefault(key, []).append((i, cfg))
+    for (f_samp, f_mod, n_seconds, ndata, dev), members in groups.items():
+        idx = [i for i, _ in members]
+        guesses = np.array([(1.6, params_list[i]["m_true"], 0.0, 0.0) for i in idx])
         n = int(f_mod * n_seconds)
         R = int(f_samp / f_mod * n)
-        nbuf = int(recs[0].size / R)
+        nbuf = int(int(n_seconds * f_samp) / R)
         if nbuf == 0:
             continue
-        cols, _ = _fitters.nls_records([r[: nbuf * R] for r in recs], f_samp, f_mod, R, nbuf, ndata,
-                                       np.array(guesses), parallel=False)
-        m = np.asarray(cols[1]).reshape(len(idx), nbuf)[:, 0]
-        out[np.array(idx)] = m
+        if dev:
+            x = synthesize_asd_trials([c for _, c in members], [params_list[i]["trial_num"] for i in idx], n_seconds)
+            recs = x[:, : nbuf * R]
+        else:
+            recs = []
+            for i, cfg in members:
+                raw = SignalGenerator().generate(cfg, n_seconds, mode="asd", trial_num=params_list[i]["trial_num"])
+                recs.append(np.asarray(raw["main"].samples(), dtype=np.float64)[: nbuf * R])
+        cols, _ = _fitters.nls_records(recs, f_samp, f_mod, R, nbuf, ndata, guesses, parallel=False)
+        m = cols[1].cpu().numpy() if hasattr(cols, "cpu") else np.asarray(cols[1])
+        out[np.array(idx)] = m.reshape(len(idx), nbuf)[:, 0]
     return out

@@ -27,6 +27,8 @@
  *   dfmi_ekf         EKFFitter.fit (fitters.py:214-320), pre-reductions by the caller
  *   dfmi_ekf_fit     EKFFitter.fit whole: np.mean / np.var on the device (fitters.py:253, 256)
  *   dfmi_record_moments  np.mean / np.var of records in numpy's summation order
+ *   dfmi_synth_asd   SignalGenerator asd mode (physics.py:423-722, white noise) per
+ *                    trial, the input side of workers.run_efficiency_trial batches
  *   dfmi_wdfmi_fit   WDFMI_NLSFitter / WDFMI_OrthogonalFitter / WDFMI_SequentialFitter /
  *                    HWDFMI_Fitter .fit (fitters.py:481-891)
  */
@@ -141,6 +143,39 @@ int dfmi_ekf_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_sa
  * may be NULL. One workgroup per record. */
 int dfmi_record_moments(const double* x, int64_t nrec, int64_t rec_stride, int64_t n, double* mean, double* var,
                         int32_t mem, void* stream);
+
+/* ---- Trial synthesis (input side of the batched efficiency trials) ----
+ * One asd-mode channel per trial, as SignalGenerator.generate(mode='asd') makes it
+ * (reference physics.py:423-473, white noise sources 532-613, exact-delay model
+ * 615-722) for the default cosine waveform: numpy's legacy RandomState(seed) stream
+ * (MT19937 + polar gauss) restated on the device. Every field is the reference's
+ * scalar expression, evaluated by the caller with Python/numpy floats. */
+typedef struct dfmi_synth_trial {
+  uint32_t seed;        /* 1 + trial_num * 4 (asd_noise_arrays' RandomState) */
+  int32_t dynamic;      /* 1: main channel (arm-length modulation term), 0: witness */
+  double omega_mod;     /* 2 * np.pi * laser.f_mod */
+  double psi;           /* laser.psi */
+  double df;            /* laser.df */
+  double cphi;          /* 2 * np.pi / fs, fs = 1 / (t[1] - t[0]) */
+  double w_arm;         /* 2 * np.pi * ifo.arml_mod_f */
+  double arml_mod_amp;  /* ifo.arml_mod_amp */
+  double arml_mod_psi;  /* ifo.arml_mod_psi */
+  double dl0;           /* ifo.phi * laser.wavelength / (2 * np.pi) */
+  double c_light;       /* scipy.constants.c */
+  double tau_m;         /* ifo.meas_arml / c */
+  double tau_r;         /* ifo.ref_arml / c */
+  double w0c;           /* 2 * np.pi * (c / laser.wavelength + 0.0) */
+  double amp;           /* laser.amp */
+  double vis;           /* laser.visibility */
+  double s_amp;         /* laser.amp_n * np.sqrt(f_samp / 2.0), 0: no draws */
+  double s_df;          /* laser.df_n * np.sqrt(f_samp / 2.0), 0: no draws */
+} dfmi_synth_trial;
+
+/* out[r*n_samp + k] = trial r's signal sample k (t_k = k / f_samp), one lane per
+ * trial. trials: host array; out in `mem`. Records agree with numpy's to ~1e-15
+ * (the device's cos / sin / log), bit-exact elsewhere. */
+int dfmi_synth_asd(const dfmi_synth_trial* trials, int64_t ntrial, int64_t n_samp, double f_samp, double* out,
+                   int32_t mem, void* stream);
 
 /* ---- Witness-based fitters (EXPERIMENTAL in the reference) ----
  * Replace, per record (main channel + witness channel):

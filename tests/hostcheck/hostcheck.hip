@@ -9,11 +9,38 @@
 #include "../../deepfmkit_amd/csrc/dfmi_math.h"
 #include "../../deepfmkit_amd/csrc/lm.h"
 #include "../../deepfmkit_amd/csrc/np_sum.h"
+#include "../../deepfmkit_amd/csrc/synth.h"
+
+namespace {
+struct HKey {
+  uint32_t* p;
+  uint32_t& operator()(int i) const { return p[i]; }
+};
+struct HVec {
+  double* p;
+  double& operator()(int64_t k) const { return p[k]; }
+};
+}  // namespace
 
 extern "C" {
 
 // numpy summation order (np_sum.h): the plan the W-DFMI kernels run for their means.
 double hc_np_sum(const double* a, int n) { return dfmi_plan_sum_host(a, n); }
+
+// synth.h on the host: n gaussians of RandomState(seed) (legacy normal, scale 1)
+void hc_mt_gauss(uint32_t seed, int64_t n, double* out) {
+  std::vector<uint32_t> key(dfmi::kMtN);
+  dfmi::Mt<HKey> mt{HKey{key.data()}, 0, false, 0.0};
+  mt.seed(seed);
+  for (int64_t k = 0; k < n; ++k) out[k] = mt.next_gauss();
+}
+
+// synth.h's whole trial on the host (host libm cos / sin / log)
+void hc_synth_trial(const dfmi_synth_trial* p, int64_t n, double f_samp, double* out) {
+  std::vector<uint32_t> key(dfmi::kMtN);
+  std::vector<double> a(n), d(n), ph(n);
+  dfmi::synth_trial(*p, n, f_samp, HKey{key.data()}, HVec{a.data()}, HVec{d.data()}, HVec{ph.data()}, HVec{out});
+}
 
 void hc_bessel_table(double x, int N, double* out) { dfmi_bessel_table(x, N, out); }
 

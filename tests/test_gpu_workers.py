@@ -2,7 +2,9 @@
 run_efficiency_trial results (tests/golden/workers.json, made by
 tests/golden/make_workers_golden.py): one Configure-Simulate-Fit trial per call
 (run_efficiency_trial), and the batched form (run_efficiency_trials: every trial a
-record of one GPU call, each with its own seed) giving the same bits.
+record of one GPU call, each with its own seed): with the host generator it gives
+the same bits; with the device generator (dfmi_synth_asd) the records agree with
+numpy's to ~1e-15 and the fits with the reference's within the tolerance.
 
 Tolerance: |m - m_ref| <= 1e-9 (status-0 fits)."""
 import json
@@ -46,8 +48,52 @@ def test_run_efficiency_trial_matches_reference():
 def test_batched_trials_equal_single_trials():
     from deepfmkit_amd import workers
     ps = [params_of(t) for t in G["trials"]]
-    batched = workers.run_efficiency_trials(ps)
+    batched = workers.run_efficiency_trials(ps, synth="host")
     single = np.array([workers.run_efficiency_trial(p) for p in ps])
     np.testing.assert_array_equal(batched, single)
     ref = np.array([t["m_fit"] for t in G["trials"]])
     assert np.max(np.abs(batched - ref)) <= 1e-9
+
+
+def test_device_synthesis_matches_host_generator():
+    """dfmi_synth_asd vs the package's numpy generator (bit-exact with the reference's,
+    tests/test_host_numerics.py pins the restatement itself bit for bit on the host):
+    the device's cos / sin / log differ from libm by an ulp at most. The model's phase is
+    the carrier term w0c * (tau_m - tau_r) ~ 1.2e6 rad plus a difference of two
+    interpolated phi_mod values of order 1e6 rad, whose ulp is 2.3e-10: one ulp of
+    any cos upstream moves a sample by that much. Records agree within 1e-9 absolute
+    (a few ulps of the phase; signal ~ 2), most samples exactly; covers df noise and
+    the arm-length modulation term too."""
+    import deepfmkit_amd as dfm
+    from deepfmkit_amd import physics as P
+    cfgs, tns, hosts = [], [], []
+    for (m, an, dn, tn, arm) in [(6.0, 1e-4, 0.0, 0, 0.0), (8.0, 3e-4, 2e3, 3, 0.0), (6.0, 0.0, 0.0, 2, 1e-7),
+                                 (20.0, 1e-3, 0.0, 7, 0.0)]:
+        laser = dfm.LaserConfig()
+        laser.f_mod = 1000.0
+        laser.amp_n, laser.df_n = an, dn
+        ifo = dfm.InterferometerConfig()
+        ifo.arml_mod_amp = arm
+        dfm.set_laser_df_for_effect(laser, ifo, m)
+        cfg = dfm.DFMIObject("main_trial", laser, ifo)
+        cfgs.append(cfg)
+        tns.append(tn)
+        hosts.append(np.asarray(P.SignalGenerator().generate(cfg, 0.02, mode="asd", trial_num=tn)["main"].samples()))
+    dev = P.synthesize_asd_trials(cfgs, tns, 0.02).cpu().numpy()
+    for k, h in enumerate(hosts):
+        assert np.max(np.abs(dev[k] - h)) <= 1e-9, (k, np.max(np.abs(dev[k] - h)))
+        assert np.mean(dev[k] == h) >= 0.5, (k, np.mean(dev[k] == h))
+
+
+def test_device_synthesized_trials_match_reference():
+    """run_efficiency_trials with records generated on the device: m within 1e-9 of
+    the reference's run_efficiency_trial (the BASELINE tolerance) and of the
+    host-generated batch: the LM stops once |dp| < 1e-9 (fit.py:254-256), so the
+    records' phase-ulp differences move m by up to that step (1.2e-10 measured)."""
+    from deepfmkit_amd import workers
+    ps = [params_of(t) for t in G["trials"]]
+    dev = workers.run_efficiency_trials(ps, synth="device")
+    host = workers.run_efficiency_trials(ps, synth="host")
+    ref = np.array([t["m_fit"] for t in G["trials"]])
+    assert np.max(np.abs(dev - ref)) <= 1e-9, np.abs(dev - ref)
+    assert np.max(np.abs(dev - host)) <= 1e-9, np.abs(dev - host)

@@ -97,3 +97,31 @@ def test_flattened_descent_equals_nested(hc, lm_npz, group):
     b = _fit(hc, qi, g, 2)
     for x, y in zip(a, b):
         np.testing.assert_array_equal(x, y)
+
+
+def test_trial_synthesis_restatement_bit_exact(hc):
+    """synth.h (dfmi_synth_asd's generator) built for the host, where cos / sin / log
+    are numpy's own libm: numpy's legacy RandomState normal stream and whole asd-mode
+    trials (amplitude + df noise, arm-length modulation) bit for bit."""
+    import deepfmkit_amd as dfm
+    from deepfmkit_amd import physics as P
+    hc.hc_mt_gauss.argtypes = [ctypes.c_uint32, ctypes.c_int64, ctypes.c_void_p]
+    hc.hc_synth_trial.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p]
+    for seed in (0, 1, 5, 12345, 2 ** 32 - 1):
+        out = np.zeros(3001)
+        hc.hc_mt_gauss(seed, 3001, out.ctypes.data)
+        np.testing.assert_array_equal(out, np.random.RandomState(seed).normal(size=3001))
+    for (m, an, dn, ns, tn, arm) in [(6.0, 1e-4, 0.0, 0.02, 0, 0.0), (8.0, 3e-4, 2e3, 0.02, 3, 0.0),
+                                     (6.0, 0.0, 0.0, 0.01, 2, 1e-7), (20.0, 1e-3, 0.0, 0.05, 7, 0.0)]:
+        laser = dfm.LaserConfig()
+        laser.f_mod = 1000.0
+        laser.amp_n, laser.df_n = an, dn
+        ifo = dfm.InterferometerConfig()
+        ifo.arml_mod_amp = arm
+        dfm.set_laser_df_for_effect(laser, ifo, m)
+        cfg = dfm.DFMIObject("main_trial", laser, ifo)
+        x = np.asarray(P.SignalGenerator().generate(cfg, ns, mode="asd", trial_num=tn)["main"].samples())
+        rec = P.synth_trial_fields(cfg, tn)
+        out = np.zeros(x.size)
+        hc.hc_synth_trial(rec.ctypes.data, x.size, cfg.f_samp, out.ctypes.data)
+        np.testing.assert_array_equal(out, x)

@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=8000, help="segments in the CPU-baseline sample")
     ap.add_argument("--cpu-procs", type=int, default=16, help="Pool size of the CPU baseline (box share: 16)")
     ap.add_argument("--demod-only", action="store_true", help="profile helper: time only the demod kernel")
+    ap.add_argument("--tune", default="", help="A/B helper: dfmi_set_tuning knobs as key=value[,key=value]")
     return ap.parse_args()
 
 
@@ -147,6 +148,9 @@ def main():
     from deepfmkit_amd.fitters import StandardNLSFitter, w0_of
 
     lib = _lib.load()
+    for kv in filter(None, args.tune.split(",")):
+        k, v = kv.split("=")
+        _lib.check(lib.dfmi_set_tuning(k.encode(), int(v)), "dfmi_set_tuning")
     R = int(F_SAMP / F_MOD * N_CYC)
     nseg = args.segments
     nrec = max(1, args.channels) if world == 1 else 1
@@ -285,6 +289,8 @@ def main():
             "batch_m_mean": float(res[1].mean())}
     if args.demod_only:
         line["metric"] = "demod only (profile helper)"
+    if args.tune:
+        line["tuning"] = args.tune
     if pre is not None:
         raw, ref, procs, base = pre
         df = StandardNLSFitter({"n": N_CYC}).fit(raw, parallel=True, n_cores=procs)  # same chunking, on GPU

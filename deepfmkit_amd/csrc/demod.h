@@ -350,19 +350,37 @@ __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int
       if (p0 >= L) p0 -= L;
     }
   }
-  for (; c < nch; ++c) {
-    double v[2];
-    VecT<2>::load(xs + c * 128, v);
-    add_chunk(p0, v);
-    p0 += 128;
-    if (p0 >= L) p0 -= L;
-  }
-  if (tail) {  // partial chunk: element-wise (R may be odd)
+  {
+    // the remaining (< LOADS) full chunks and the partial tail chunk as ONE more load
+    // group (issued together, then added in chunk order as before: same bits); one
+    // HBM round trip instead of one per chunk
+    const int rem = nch - c;
+    double v[LOADS][2];
+#pragma unroll
+    for (int u = 0; u < LOADS; ++u) {
+      if (u < rem) {
+        if constexpr (NT) VecT<2>::load_nt(xs + (c + u) * 128, v[u]);
+        else VecT<2>::load(xs + (c + u) * 128, v[u]);
+      }
+    }
     const int t0 = 2 * lane;
-    int p = p0 + t0;
-    if (p >= L) p -= L;
-    if (t0 < tail) ybin[p] += xs[nch * 128];
-    if (t0 + 1 < tail) ybin[p + 1] += xs[nch * 128 + 1];
+    double tv0 = 0.0, tv1 = 0.0;
+    if (t0 < tail) tv0 = xs[nch * 128];  // partial chunk: element-wise (R may be odd)
+    if (t0 + 1 < tail) tv1 = xs[nch * 128 + 1];
+#pragma unroll
+    for (int u = 0; u < LOADS; ++u) {
+      if (u < rem) {
+        add_chunk(p0, v[u]);
+        p0 += 128;
+        if (p0 >= L) p0 -= L;
+      }
+    }
+    if (tail) {
+      int p = p0 + t0;
+      if (p >= L) p -= L;
+      if (t0 < tail) ybin[p] += tv0;
+      if (t0 + 1 < tail) ybin[p + 1] += tv1;
+    }
   }
   double y[MAXSLOT][2];
 #pragma unroll

@@ -226,6 +226,7 @@ struct Tuning {
   int demod_occ4 = 0;          // 1: bin kernel held to 128 VGPRs (4 waves per SIMD)
   int seed_fused = 1;          // 1: seed + bulk demodulation in one launch on the caller's stream
   int wdfmi_accel = 3;         // W-DFMI: bit 0 time axis without division, bit 1 template slopes in LDS
+  int bins_loads = 8;          // bin kernels (L <= 256): 1-KB chunk loads in flight per wave (8 | 16)
 };
 Tuning g_tune;
 std::string g_last_demod;     // kernel variant of the last demodulation launch (dfmi_last_demod_kernel)
@@ -295,6 +296,8 @@ template <int MS, bool ROWS>
 int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tab,
                   double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu, size_t lds) {
   auto kern = g_tune.demod_occ4 ? dfmi::demod_bins4_kernel<MS, 8, ROWS> : dfmi::demod_bins_kernel<MS, 8, ROWS>;
+  const bool l16 = MS == 2 && g_tune.bins_loads == 16 && !g_tune.demod_occ4;
+  if (l16) kern = dfmi::demod_bins_kernel<MS, 16, ROWS>;
   int per_cu = 0;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, dfmi::kBlockThreads, lds));
   if (per_cu < 1) per_cu = 1;
@@ -305,7 +308,7 @@ int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, i
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(dfmi::kBlockThreads), lds, st, x, nseg, stride, R, L, ndata,
                      tab, qi, qi_ld, dc, (int)(spacer < grid ? spacer : 0), g_probe);
   HIPCHK(hipGetLastError());
-  g_last_demod = std::string(g_tune.demod_occ4 ? "demod_bins4_kernel<" : "demod_bins_kernel<") + std::to_string(MS) + ",8" + (ROWS ? ",rows" : "") +
+  g_last_demod = std::string(g_tune.demod_occ4 ? "demod_bins4_kernel<" : "demod_bins_kernel<") + std::to_string(MS) + (l16 ? ",16" : ",8") + (ROWS ? ",rows" : "") +
                  (spacer ? ",spacer" + std::to_string(spacer) : "") + ">";
   return DFMI_OK;
 }
@@ -450,8 +453,10 @@ int fused_seed_demod(int dev, const double* x, int64_t nrec, int64_t nbuf, int R
                      int32_t*, uint64_t*);
   K kern;
   if (ndata <= 12)
-    kern = nslot <= 2 ? dfmi::demod_seed_bins_kernel<2, 12> : nslot <= 4 ? dfmi::demod_seed_bins_kernel<4, 12>
-                                                                       : dfmi::demod_seed_bins_kernel<8, 12>;
+    kern = nslot <= 2 ? (g_tune.bins_loads == 16 ? dfmi::demod_seed_bins_kernel<2, 12, 16>
+                                                 : dfmi::demod_seed_bins_kernel<2, 12>)
+           : nslot <= 4 ? dfmi::demod_seed_bins_kernel<4, 12>
+                        : dfmi::demod_seed_bins_kernel<8, 12>;
   else
     kern = nslot <= 2 ? dfmi::demod_seed_bins_kernel<2, 16> : nslot <= 4 ? dfmi::demod_seed_bins_kernel<4, 16>
                                                                        : dfmi::demod_seed_bins_kernel<8, 16>;
@@ -471,7 +476,8 @@ int fused_seed_demod(int dev, const double* x, int64_t nrec, int64_t nbuf, int R
                      out_ld, nbuf, fitok, g_probe);
   HIPCHK(hipGetLastError());
   g_last_demod = "demod_seed_bins_kernel<" + std::to_string(nslot <= 2 ? 2 : nslot <= 4 ? 4 : 8) + "," +
-                 std::to_string(ndata <= 12 ? 12 : 16) + ",rows>";
+                 std::to_string(ndata <= 12 ? 12 : 16) +
+                 (nslot <= 2 && ndata <= 12 && g_tune.bins_loads == 16 ? ",16" : "") + ",rows>";
   return DFMI_OK;
 }
 
@@ -629,7 +635,8 @@ const std::map<std::string, Knob>& knobs() {
       {"seed_order", {&g_tune.seed_order, {0, 1}}},
       {"demod_occ4", {&g_tune.demod_occ4, {0, 1}}},
       {"seed_fused", {&g_tune.seed_fused, {0, 1}}},
-      {"wdfmi_accel", {&g_tune.wdfmi_accel, {0, 1, 2, 3}}}};
+      {"wdfmi_accel", {&g_tune.wdfmi_accel, {0, 1, 2, 3}}},
+      {"bins_loads", {&g_tune.bins_loads, {8, 16}}}};
   return k;
 }
 // np.mean / np.var of nrec device records on st (moments.hip), numpy-exact.

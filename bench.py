@@ -138,10 +138,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     want_base = rank == 0 and world == 1 and not args.no_cpu_baseline and not args.demod_only
     pre = cpu_baseline(args) if want_base else None
-    if world > 1:
-        dist.init_process_group("gloo" if not torch.cuda.is_available() else "nccl")
+    # one process per GPU: bind the device first, so RCCL's barrier / all_reduce run
+    # on this rank's GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world > 1:
+        # RCCL; DFMI_DIST_BACKEND=gloo rehearses N ranks that share one card (RCCL
+        # refuses two ranks on one device)
+        backend = os.environ.get("DFMI_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from deepfmkit_amd import _lib
     from deepfmkit_amd import fit as F

@@ -286,30 +286,6 @@ __device__ __forceinline__ void interp_lin_batch(const Geo& g, const double (&x)
   }
 }
 
-// sin/cos for |x| < 2^19 without branches: Cody-Waite reduction by pi/2 in three
-// parts, fdlibm kernel polynomials on [-pi/4, pi/4], quadrant by select. Callers
-// use the library sincos for larger arguments (not produced by these fits).
-__device__ __forceinline__ void sincos_fast(double x, double* sn, double* cs) {
-  const double invpio2 = 6.36619772367581382433e-01;
-  const double p1 = 1.57079632673412561417e+00, p2 = 6.07710050630396597660e-11, p3 = 2.02226624871116645580e-21;
-  const double q = rint(x * invpio2);
-  double r = fma(-q, p1, x);
-  r = fma(-q, p2, r);
-  r = fma(-q, p3, r);
-  const double z = r * r;
-  const double ps = fma(z, fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
-                                              2.75573137070700676789e-06), -1.98412698298579493134e-04),
-                             8.33333333332248946124e-03), -1.66666666666666324348e-01);
-  const double sr = fma(r * z, ps, r);
-  const double pc = fma(z, fma(z, fma(z, fma(z, fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
-                                              -2.75573143513906633035e-07), 2.48015872894767294178e-05),
-                             -1.38888888888741095749e-03), 4.16666666666666019037e-02);
-  const double cr = fma(z * z, pc, fma(-0.5, z, 1.0));
-  const int qi = ((int)q) & 3;
-  *sn = (qi == 0) ? sr : (qi == 1) ? cr : (qi == 2) ? -sr : -cr;
-  *cs = (qi == 0) ? cr : (qi == 1) ? -sr : (qi == 2) ? -cr : sr;
-}
-
 // W-DFMI phase difference (fitters.py:533-539 / 611-617 / 688-694):
 //   shifted = interp(t - (-psi/omega), t, tab, period), delayed = interp(t - tau, t, shifted, period)
 template <int T, int SPT, bool FAST, bool SLP>
@@ -386,7 +362,7 @@ __device__ __forceinline__ VP varpro(const Geo& g, double* red, const double (&d
   bool big = false;
 #pragma unroll
   for (int q = 0; q < SPT; ++q) {
-    sincos_fast(d[q], &bq[q], &bi[q]);
+    dfmi_sincos_fast(d[q], &bq[q], &bi[q]);
     big = big || !(fabs(d[q]) < 524288.0);
   }
   if (big) {

@@ -312,7 +312,10 @@ __global__ __launch_bounds__(kBlockThreads) void demod_fold_kernel(
 // One segment of the bin-in-LDS fold: the wave's L bins (ybin, LDS) are zeroed,
 // every 1-KB chunk is added into them, and fold_finish contracts the lane-owned
 // bins with the basis T (LDS or global) into column / row `col` of qi (and dc).
-template <int MAXSLOT, int LOADS, bool NT, int HB, bool ROWS>
+// ROLL: the full load groups are software-pipelined — group g+1 is issued before
+// group g is added into the bins, so the wave keeps LOADS chunks in flight while it
+// adds (same additions in the same order: same bits).
+template <int MAXSLOT, int LOADS, bool NT, int HB, bool ROWS, bool ROLL = false>
 __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int R, int L, int ndata,
                                              const double* __restrict__ T, double* __restrict__ ybin, int lane,
                                              const bool (&pval)[MAXSLOT], const int (&pbase)[MAXSLOT],
@@ -336,18 +339,42 @@ __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int
   const double* __restrict__ xs = xs0 + 2 * lane;
   int p0 = 0;  // bin of the chunk's first sample: (128 c) mod L
   int c = 0;
-  for (; c + LOADS <= nch; c += LOADS) {
-    double v[LOADS][2];
+  auto load_group = [&](int c0, double (&v)[LOADS][2]) {
 #pragma unroll
     for (int u = 0; u < LOADS; ++u) {
-      if constexpr (NT) VecT<2>::load_nt(xs + (c + u) * 128, v[u]);
-      else VecT<2>::load(xs + (c + u) * 128, v[u]);
+      if constexpr (NT) VecT<2>::load_nt(xs + (c0 + u) * 128, v[u]);
+      else VecT<2>::load(xs + (c0 + u) * 128, v[u]);
     }
+  };
+  auto add_group = [&](const double (&v)[LOADS][2]) {
 #pragma unroll
     for (int u = 0; u < LOADS; ++u) {
       add_chunk(p0, v[u]);
       p0 += 128;
       if (p0 >= L) p0 -= L;
+    }
+  };
+  if constexpr (ROLL) {
+    if (LOADS <= nch) {
+      double cur[LOADS][2];
+      load_group(0, cur);
+      for (c = LOADS; c + LOADS <= nch; c += LOADS) {
+        double nxt[LOADS][2];
+        load_group(c, nxt);
+        add_group(cur);
+#pragma unroll
+        for (int u = 0; u < LOADS; ++u) {
+          cur[u][0] = nxt[u][0];
+          cur[u][1] = nxt[u][1];
+        }
+      }
+      add_group(cur);
+    }
+  } else {
+    for (; c + LOADS <= nch; c += LOADS) {
+      double v[LOADS][2];
+      load_group(c, v);
+      add_group(v);
     }
   }
   {
@@ -405,7 +432,7 @@ __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int
 // only idle workgroups, never segments that would wait behind it.
 // probe (diagnostics, may be null): s_memrealtime at the entry of workgroups 0 and
 // gridDim-1 and at the exit of workgroup 0's wave 0 ([3], [4], [5]).
-template <int MAXSLOT, int LOADS, bool ROWS>
+template <int MAXSLOT, int LOADS, bool ROWS, bool ROLL = false>
 __device__ __forceinline__ void bins_kernel_body(
     const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
     const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc, int spacer,
@@ -434,17 +461,17 @@ __device__ __forceinline__ void bins_kernel_body(
     pval[j] = (j < nslot) && (pbase[j] < L);
   }
   for (int64_t s = (int64_t)bid * kWavesPerBlock + wave; s < nseg; s += (int64_t)nwork * kWavesPerBlock)
-    bins_segment<MAXSLOT, LOADS, true, kHarmBlock, ROWS>(x + s * seg_stride, R, L, ndata, lds_dyn, ybin, lane, pval,
-                                                           pbase, qi, qi_ld, s, dc);
+    bins_segment<MAXSLOT, LOADS, true, kHarmBlock, ROWS, ROLL>(x + s * seg_stride, R, L, ndata, lds_dyn, ybin, lane,
+                                                                 pval, pbase, qi, qi_ld, s, dc);
   if (probe && threadIdx.x == 0 && bid == 0) probe[5] = __builtin_amdgcn_s_memrealtime();
 }
 
-template <int MAXSLOT, int LOADS, bool ROWS>
+template <int MAXSLOT, int LOADS, bool ROWS, bool ROLL = false>
 __global__ __launch_bounds__(kBlockThreads) void demod_bins_kernel(
     const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
     const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc, int spacer,
     uint64_t* __restrict__ probe) {
-  bins_kernel_body<MAXSLOT, LOADS, ROWS>(x, nseg, seg_stride, R, L, ndata, tab, qi, qi_ld, dc, spacer, probe);
+  bins_kernel_body<MAXSLOT, LOADS, ROWS, ROLL>(x, nseg, seg_stride, R, L, ndata, tab, qi, qi_ld, dc, spacer, probe);
 }
 
 // Same kernel held to <= 128 VGPRs, i.e. 4 waves per SIMD (4 workgroups per CU).

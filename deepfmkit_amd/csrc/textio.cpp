@@ -17,14 +17,19 @@
 // std::to_chars in CPython's repr() layout, so a file written here is byte-identical
 // to the reference's writer (the header text comes formatted from Python, which
 // knows the header fields' Python types) and every value reads back bit-exact.
+#include <algorithm>
+#include <array>
 #include <charconv>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <system_error>
 #include <thread>
 #include <vector>
+
+#include <sys/stat.h>
 
 #include "../../include/dfmi.h"
 
@@ -32,42 +37,40 @@ namespace {
 
 thread_local std::string g_txt_err;
 
+int default_threads() {
+  const unsigned h = std::thread::hardware_concurrency();
+  return h == 0 ? 1 : (h > 16 ? 16 : (int)h);
+}
+
 int txt_fail(int code, const std::string& msg) {
   g_txt_err = msg;
   return code;
 }
 
+// The whole file in memory (not zero-filled first: the read overwrites it all).
+struct Buf {
+  std::unique_ptr<char[]> p;
+  size_t n = 0;
+  const char* data() const { return p.get(); }
+  size_t size() const { return n; }
+};
+
 struct File {
-  std::vector<char> buf;
+  Buf buf;
   int load(const char* path) {
     FILE* f = std::fopen(path, "rb");
     if (!f) return txt_fail(DFMI_ERR_ARG, std::string("cannot open ") + path);
     std::fseek(f, 0, SEEK_END);
     const long n = std::ftell(f);
     std::fseek(f, 0, SEEK_SET);
-    buf.resize(n > 0 ? (size_t)n : 0);
-    const size_t got = n > 0 ? std::fread(buf.data(), 1, (size_t)n, f) : 0;
+    buf.n = n > 0 ? (size_t)n : 0;
+    buf.p.reset(new char[buf.n > 0 ? buf.n : 1]);
+    const size_t got = n > 0 ? std::fread(buf.p.get(), 1, (size_t)n, f) : 0;
     std::fclose(f);
     if ((long)got != n) return txt_fail(DFMI_ERR_ARG, std::string("short read: ") + path);
     return DFMI_OK;
   }
 };
-
-// Start offsets of lines [first, ...) after skipping `skip` lines; a final line
-// without '\n' counts.
-void line_starts(const std::vector<char>& b, int skip, std::vector<size_t>* starts) {
-  size_t i = 0;
-  const size_t n = b.size();
-  for (int k = 0; k < skip && i < n; ++k) {
-    const void* p = std::memchr(b.data() + i, '\n', n - i);
-    i = p ? (size_t)((const char*)p - b.data()) + 1 : n;
-  }
-  while (i < n) {
-    starts->push_back(i);
-    const void* p = std::memchr(b.data() + i, '\n', n - i);
-    i = p ? (size_t)((const char*)p - b.data()) + 1 : n;
-  }
-}
 
 // Fields of one line. SINGLE_SPACE: every ' ' separates (pandas sep=' ': two
 // spaces make an empty field). WHITESPACE: runs of blanks separate, leading and
@@ -124,17 +127,17 @@ double parse_double(const char* a, const char* b) {
 // through it, so the raw reader reproduces it bit for bit — pinned against pandas
 // itself by tests/test_textio.py. Returns false if [a, b) is not a number.
 const double* pow10_table() {
-  static double e[309];
-  static bool init = false;
-  if (!init) {
+  // built once, thread-safely (the parse threads call this concurrently)
+  static const std::array<double, 309> e = [] {
+    std::array<double, 309> t{};
     for (int i = 0; i <= 308; ++i) {
       char buf[16];
       std::snprintf(buf, sizeof buf, "1e%d", i);
-      e[i] = std::strtod(buf, nullptr);
+      t[(size_t)i] = std::strtod(buf, nullptr);
     }
-    init = true;
-  }
-  return e;
+    return t;
+  }();
+  return e.data();
 }
 
 bool pandas_xstrtod(const char* p, const char* end, double* out) {
@@ -232,6 +235,84 @@ bool is_blank(const char* s, const char* e) {
   return true;
 }
 
+// Every line after `skip`, indexed and classified in parallel over byte ranges cut
+// at line ends: st = line start offsets, nf = fields of a data line, -1 for a
+// blank or comment line (the caller applies the row rules that need the order,
+// e.g. genfromtxt's "same field count as the first row").
+struct Scan {
+  std::vector<size_t> st;
+  std::vector<int> nf;
+};
+
+// File identity for the shape -> read hand-over: size + modification time.
+struct Stamp {
+  long long size = -1, sec = 0, nsec = 0;
+  bool operator==(const Stamp& o) const { return size == o.size && sec == o.sec && nsec == o.nsec; }
+};
+
+bool stamp_of(const char* path, Stamp* s) {
+  struct stat st;
+  if (stat(path, &st) != 0) return false;
+  s->size = (long long)st.st_size;
+  s->sec = (long long)st.st_mtim.tv_sec;
+  s->nsec = (long long)st.st_mtim.tv_nsec;
+  return true;
+}
+
+void scan_lines(const Buf& b, int skip, int mode, int threads, Scan* sc) {
+  const size_t n = b.size();
+  size_t i0 = 0;
+  for (int k = 0; k < skip && i0 < n; ++k) {
+    const void* p = std::memchr(b.data() + i0, '\n', n - i0);
+    i0 = p ? (size_t)((const char*)p - b.data()) + 1 : n;
+  }
+  const int nt = (threads > 1 && n - i0 > ((size_t)1 << 20)) ? threads : 1;
+  // range t starts at the first line start at or after i0 + t*(n-i0)/nt
+  std::vector<size_t> cut((size_t)nt + 1, n);
+  cut[0] = i0;
+  for (int t = 1; t < nt; ++t) {
+    size_t c = i0 + (n - i0) / (size_t)nt * (size_t)t;
+    const void* p = std::memchr(b.data() + c - 1, '\n', n - (c - 1));
+    cut[(size_t)t] = p ? (size_t)((const char*)p - b.data()) + 1 : n;
+  }
+  for (int t = 1; t <= nt; ++t) cut[(size_t)t] = std::max(cut[(size_t)t], cut[(size_t)t - 1]);
+  std::vector<std::vector<size_t>> lst((size_t)nt);
+  std::vector<std::vector<int>> lnf((size_t)nt);
+  auto work = [&](int t) {
+    size_t i = cut[(size_t)t];
+    const size_t hi = cut[(size_t)t + 1];
+    auto& S = lst[(size_t)t];
+    auto& F = lnf[(size_t)t];
+    while (i < hi) {
+      const void* p = std::memchr(b.data() + i, '\n', n - i);
+      const size_t nx = p ? (size_t)((const char*)p - b.data()) + 1 : n;
+      const char* s0 = b.data() + i;
+      const char* e = b.data() + nx;
+      if (e > s0 && e[-1] == '\n') --e;
+      S.push_back(i);
+      F.push_back((is_blank(s0, e) || is_comment(s0, e, mode))
+                      ? -1
+                      : for_fields(s0, e, mode, [](int, const char*, const char*) {}));
+      i = nx;
+    }
+  };
+  if (nt == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nt; ++t) pool.emplace_back(work, t);
+    for (auto& th : pool) th.join();
+  }
+  size_t tot = 0;
+  for (auto& v : lst) tot += v.size();
+  sc->st.reserve(tot);
+  sc->nf.reserve(tot);
+  for (int t = 0; t < nt; ++t) {
+    sc->st.insert(sc->st.end(), lst[(size_t)t].begin(), lst[(size_t)t].end());
+    sc->nf.insert(sc->nf.end(), lnf[(size_t)t].begin(), lnf[(size_t)t].end());
+  }
+}
+
 // CPython repr(float): shortest round-trip digits; fixed notation when the
 // decimal exponent is in [-4, 16), with ".0" for integral values; otherwise
 // d[.ddd]e±XX with at least two exponent digits.
@@ -298,6 +379,17 @@ std::string digits_only(const std::string& line) {
   return o;
 }
 
+// What dfmi_txt_shape loaded, for the dfmi_txt_read of the same file that follows
+// on this thread (textio.read_columns calls them in that order); dropped by the read.
+struct Loaded {
+  File f;
+  Scan sc;
+  std::string path;
+  int skip = -1, mode = -1;
+  Stamp stamp;
+};
+thread_local Loaded g_loaded;
+
 }  // namespace
 
 extern "C" {
@@ -349,19 +441,24 @@ int dfmi_txt_parse_header(const char* path, int32_t kind, dfmi_txt_header* hdr) 
 int dfmi_txt_shape(const char* path, int32_t skip, int32_t mode, int64_t* rows, int32_t* cols) {
   g_txt_err.clear();
   if (!path || !rows || !cols || skip < 0) return txt_fail(DFMI_ERR_ARG, "bad argument");
-  File f;
-  int rc = f.load(path);
+  Loaded& L = g_loaded;
+  L = Loaded();
+  int rc = L.f.load(path);
   if (rc) return rc;
-  std::vector<size_t> st;
-  line_starts(f.buf, skip, &st);
+  scan_lines(L.f.buf, skip, mode, default_threads(), &L.sc);
+  if (stamp_of(path, &L.stamp)) {  // kept for the dfmi_txt_read that follows
+    L.path = path;
+    L.skip = skip;
+    L.mode = mode;
+  }
+  const File& f = L.f;
+  const Scan& sc = L.sc;
+  (void)f;
   int64_t nr = 0;
   int32_t nc = 0, first = -1;
-  for (size_t i = 0; i < st.size(); ++i) {
-    const char* s = f.buf.data() + st[i];
-    const char* e = f.buf.data() + (i + 1 < st.size() ? st[i + 1] : f.buf.size());
-    if (e > s && e[-1] == '\n') --e;
-    if (is_blank(s, e) || is_comment(s, e, mode)) continue;
-    const int k = for_fields(s, e, mode, [](int, const char*, const char*) {});
+  for (size_t i = 0; i < sc.st.size(); ++i) {
+    const int k = sc.nf[i];
+    if (k < 0) continue;
     if (mode == DFMI_TXT_WHITESPACE) {
       if (first < 0) first = k;
       if (k != first) continue;  // genfromtxt(invalid_raise=False) drops such rows
@@ -378,12 +475,25 @@ int dfmi_txt_read(const char* path, int32_t skip, int32_t mode, int32_t ncol, co
                   int64_t rows, int32_t threads) {
   g_txt_err.clear();
   if (!path || skip < 0 || ncol < 0 || (ncol && (!cols || !out)) || rows < 0) return txt_fail(DFMI_ERR_ARG, "bad argument");
+  // the file and its line scan as dfmi_txt_shape left them (same path, size and
+  // modification time, same skip / mode), else loaded and scanned here
   File f;
-  int rc = f.load(path);
-  if (rc) return rc;
-  std::vector<size_t> st;
-  line_starts(f.buf, skip, &st);
-  // pass 1 (serial, cheap): which lines are data rows, and their row index
+  Scan sc;
+  Stamp now;
+  Loaded& L = g_loaded;
+  if (!L.path.empty() && L.path == path && L.skip == skip && L.mode == mode && stamp_of(path, &now) &&
+      now == L.stamp) {
+    f = std::move(L.f);
+    sc = std::move(L.sc);
+  } else {
+    int rc = f.load(path);
+    if (rc) return rc;
+    // pass 1: line index and classification (parallel)
+    scan_lines(f.buf, skip, mode, threads, &sc);
+  }
+  L = Loaded();
+  // then the row numbers in file order (serial over the per-line field counts)
+  const std::vector<size_t>& st = sc.st;
   std::vector<int64_t> row_of(st.size(), -1);
   int64_t nr = 0;
   int first = -1;
@@ -393,11 +503,9 @@ int dfmi_txt_read(const char* path, int32_t skip, int32_t mode, int32_t ncol, co
     return e;
   };
   for (size_t i = 0; i < st.size(); ++i) {
-    const char* s = f.buf.data() + st[i];
-    const char* e = line_end(i);
-    if (is_blank(s, e) || is_comment(s, e, mode)) continue;
+    const int k = sc.nf[i];
+    if (k < 0) continue;
     if (mode == DFMI_TXT_WHITESPACE) {
-      const int k = for_fields(s, e, mode, [](int, const char*, const char*) {});
       if (first < 0) first = k;
       if (k != first) continue;
     }
@@ -443,28 +551,37 @@ int dfmi_fit_txt_write(const char* path, const char* header, const double* ssq, 
   g_txt_err.clear();
   if (!path || !header || n < 0 || (n && (!ssq || !amp || !m || !phi || !psi || !dc)))
     return txt_fail(DFMI_ERR_ARG, "bad argument");
-  std::string o(header);
-  o.reserve(o.size() + (size_t)n * 120);
-  auto num = [&](double v) { py_repr(v, &o); };
-  for (int64_t i = 0; i < n; ++i) {  // data.py:198-207: str(v) + ' ' per column, then '\n'
-    num(ssq[i]);
-    o += ' ';
-    num(amp[i]);
-    o += ' ';
-    num(m[i]);
-    o += ' ';
-    num(phi[i]);
-    o += ' ';
-    num(psi[i]);
-    o += ' ';
-    num(dc[i]);
-    o += " \n";
+  // data.py:198-207: str(v) + ' ' per column, then '\n'; row ranges formatted in
+  // parallel into their own strings, written in order
+  const int nt = n >= 4096 ? default_threads() : 1;
+  std::vector<std::string> part((size_t)nt);
+  auto fmt = [&](int t) {
+    const int64_t lo = n * t / nt, hi = n * (t + 1) / nt;
+    std::string& o = part[(size_t)t];
+    o.reserve((size_t)(hi - lo) * 120);
+    for (int64_t i = lo; i < hi; ++i) {
+      const double v[6] = {ssq[i], amp[i], m[i], phi[i], psi[i], dc[i]};
+      for (int c = 0; c < 6; ++c) {
+        py_repr(v[c], &o);
+        o += ' ';
+      }
+      o += '\n';
+    }
+  };
+  if (nt == 1) {
+    fmt(0);
+  } else {
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nt; ++t) pool.emplace_back(fmt, t);
+    for (auto& th : pool) th.join();
   }
   FILE* f = std::fopen(path, "wb");
   if (!f) return txt_fail(DFMI_ERR_ARG, std::string("cannot write ") + path);
-  const size_t w = std::fwrite(o.data(), 1, o.size(), f);
-  std::fclose(f);
-  if (w != o.size()) return txt_fail(DFMI_ERR_ARG, std::string("short write: ") + path);
+  const size_t hl = std::strlen(header);
+  bool ok = std::fwrite(header, 1, hl, f) == hl;
+  for (const auto& o : part) ok = ok && std::fwrite(o.data(), 1, o.size(), f) == o.size();
+  ok = (std::fclose(f) == 0) && ok;
+  if (!ok) return txt_fail(DFMI_ERR_ARG, std::string("short write: ") + path);
   return DFMI_OK;
 }
 

@@ -229,7 +229,7 @@ __global__ __launch_bounds__(256) void segwave_con(const double* __restrict__ x,
       y[c & 1][1] += v.y;
     }
     if constexpr (STORE == 0) {
-      dfmi::fold_finish<2, 2, false, HB>(y, pval, pbase, S, L, ndata, T, lane, qi, nseg, seg, dcv);
+      dfmi::fold_finish<2, 2, HB>(y, pval, pbase, S, L, ndata, T, lane, qi, nseg, seg, dcv);
     } else if constexpr (STORE == 1) {
       double acc[2 * HB] = {};
       for (int hb = 0; hb < 2; ++hb) {

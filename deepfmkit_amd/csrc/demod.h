@@ -315,12 +315,17 @@ __global__ __launch_bounds__(kBlockThreads) void demod_fold_kernel(
 // ROLL: the full load groups are software-pipelined — group g+1 is issued before
 // group g is added into the bins, so the wave keeps LOADS chunks in flight while it
 // adds (same additions in the same order: same bits).
-template <int MAXSLOT, int LOADS, bool NT, int HB, bool ROWS, bool ROLL = false>
+// PFN > 0: the segment's first PFN chunks arrive prefetched in pf (nch >= PFN), and
+// the next segment's first PFN chunks (at `next`, if not null) are issued into pf
+// before this segment's contraction, so the wave has loads in flight while it
+// contracts.
+template <int MAXSLOT, int LOADS, bool NT, int HB, bool ROWS, bool ROLL = false, int PFN = 0>
 __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int R, int L, int ndata,
                                              const double* __restrict__ T, double* __restrict__ ybin, int lane,
                                              const bool (&pval)[MAXSLOT], const int (&pbase)[MAXSLOT],
                                              double* __restrict__ qi, int64_t qi_ld, int64_t col,
-                                             double* __restrict__ dc) {
+                                             double* __restrict__ dc, double (*pf)[2] = nullptr,
+                                             const double* __restrict__ next = nullptr) {
   typedef double d2v __attribute__((ext_vector_type(2)));
   const int nch = R >> 7;           // full 128-sample chunks
   const int tail = R - (nch << 7);  // samples of the last, partial chunk
@@ -354,6 +359,15 @@ __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int
       if (p0 >= L) p0 -= L;
     }
   };
+  if constexpr (PFN > 0) {
+#pragma unroll
+    for (int u = 0; u < PFN; ++u) {
+      add_chunk(p0, pf[u]);
+      p0 += 128;
+      if (p0 >= L) p0 -= L;
+    }
+    c = PFN;
+  }
   if constexpr (ROLL) {
     if (LOADS <= nch) {
       double cur[LOADS][2];
@@ -409,6 +423,16 @@ __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int
       if (t0 + 1 < tail) ybin[p + 1] += tv1;
     }
   }
+  if constexpr (PFN > 0) {
+    if (next) {
+      const double* __restrict__ xn = next + 2 * lane;
+#pragma unroll
+      for (int u = 0; u < PFN; ++u) {
+        if constexpr (NT) VecT<2>::load_nt(xn + u * 128, pf[u]);
+        else VecT<2>::load(xn + u * 128, pf[u]);
+      }
+    }
+  }
   double y[MAXSLOT][2];
 #pragma unroll
   for (int j = 0; j < MAXSLOT; ++j) {
@@ -432,7 +456,7 @@ __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int
 // only idle workgroups, never segments that would wait behind it.
 // probe (diagnostics, may be null): s_memrealtime at the entry of workgroups 0 and
 // gridDim-1 and at the exit of workgroup 0's wave 0 ([3], [4], [5]).
-template <int MAXSLOT, int LOADS, bool ROWS, bool ROLL = false>
+template <int MAXSLOT, int LOADS, bool ROWS, bool ROLL = false, int PFN = 0>
 __device__ __forceinline__ void bins_kernel_body(
     const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
     const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc, int spacer,
@@ -460,18 +484,34 @@ __device__ __forceinline__ void bins_kernel_body(
     pbase[j] = 2 * (lane + 64 * j);
     pval[j] = (j < nslot) && (pbase[j] < L);
   }
-  for (int64_t s = (int64_t)bid * kWavesPerBlock + wave; s < nseg; s += (int64_t)nwork * kWavesPerBlock)
-    bins_segment<MAXSLOT, LOADS, true, kHarmBlock, ROWS, ROLL>(x + s * seg_stride, R, L, ndata, lds_dyn, ybin, lane,
-                                                                 pval, pbase, qi, qi_ld, s, dc);
+  const int64_t s0 = (int64_t)bid * kWavesPerBlock + wave, ds = (int64_t)nwork * kWavesPerBlock;
+  if (PFN > 0 && (R >> 7) >= PFN) {
+    // software pipeline across this wave's segments (see bins_segment PFN)
+    double pf[PFN > 0 ? PFN : 1][2];
+    if (s0 < nseg) {
+      const double* __restrict__ x0 = x + s0 * seg_stride + 2 * lane;
+#pragma unroll
+      for (int u = 0; u < PFN; ++u) VecT<2>::load_nt(x0 + u * 128, pf[u]);
+    }
+    for (int64_t s = s0; s < nseg; s += ds)
+      bins_segment<MAXSLOT, LOADS, true, kHarmBlock, ROWS, ROLL, PFN>(
+          x + s * seg_stride, R, L, ndata, lds_dyn, ybin, lane, pval, pbase, qi, qi_ld, s, dc, pf,
+          s + ds < nseg ? x + (s + ds) * seg_stride : nullptr);
+  } else {
+    for (int64_t s = s0; s < nseg; s += ds)
+      bins_segment<MAXSLOT, LOADS, true, kHarmBlock, ROWS, ROLL>(x + s * seg_stride, R, L, ndata, lds_dyn, ybin,
+                                                                   lane, pval, pbase, qi, qi_ld, s, dc);
+  }
   if (probe && threadIdx.x == 0 && bid == 0) probe[5] = __builtin_amdgcn_s_memrealtime();
 }
 
-template <int MAXSLOT, int LOADS, bool ROWS, bool ROLL = false>
+template <int MAXSLOT, int LOADS, bool ROWS, bool ROLL = false, int PFN = 0>
 __global__ __launch_bounds__(kBlockThreads) void demod_bins_kernel(
     const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
     const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc, int spacer,
     uint64_t* __restrict__ probe) {
-  bins_kernel_body<MAXSLOT, LOADS, ROWS, ROLL>(x, nseg, seg_stride, R, L, ndata, tab, qi, qi_ld, dc, spacer, probe);
+  bins_kernel_body<MAXSLOT, LOADS, ROWS, ROLL, PFN>(x, nseg, seg_stride, R, L, ndata, tab, qi, qi_ld, dc, spacer,
+                                                    probe);
 }
 
 // Same kernel held to <= 128 VGPRs, i.e. 4 waves per SIMD (4 workgroups per CU).

@@ -228,6 +228,8 @@ struct Tuning {
   int wdfmi_accel = 3;         // W-DFMI: bit 0 time axis without division, bit 1 template slopes in LDS
   int bins_loads = 8;          // bin kernels (L <= 256): 1-KB chunk loads in flight per wave (8 | 16)
   int bins_roll = 0;           // bin kernels (L <= 256): next load group issued before the current one is added
+  int bins_prefetch = 4;       // bin kernels (L <= 256): next segment's first 4 (1: 4, 6) chunks in flight during
+                               // the contraction (+1.4 % on the step vs 0; 6 ties 4)
 };
 Tuning g_tune;
 std::string g_last_demod;     // kernel variant of the last demodulation launch (dfmi_last_demod_kernel)
@@ -301,6 +303,9 @@ int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, i
   if (l16) kern = dfmi::demod_bins_kernel<MS, 16, ROWS>;
   const bool roll = MS == 2 && !l16 && g_tune.bins_roll && !g_tune.demod_occ4;
   if (roll) kern = dfmi::demod_bins_kernel<MS, 8, ROWS, true>;
+  const bool pf = MS == 2 && !l16 && !roll && g_tune.bins_prefetch && !g_tune.demod_occ4;
+  if (pf) kern = g_tune.bins_prefetch == 6 ? dfmi::demod_bins_kernel<MS, 8, ROWS, false, 6>
+                                           : dfmi::demod_bins_kernel<MS, 8, ROWS, false, 4>;
   int per_cu = 0;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, dfmi::kBlockThreads, lds));
   if (per_cu < 1) per_cu = 1;
@@ -311,7 +316,7 @@ int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, i
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(dfmi::kBlockThreads), lds, st, x, nseg, stride, R, L, ndata,
                      tab, qi, qi_ld, dc, (int)(spacer < grid ? spacer : 0), g_probe);
   HIPCHK(hipGetLastError());
-  g_last_demod = std::string(g_tune.demod_occ4 ? "demod_bins4_kernel<" : "demod_bins_kernel<") + std::to_string(MS) + (l16 ? ",16" : ",8") + (ROWS ? ",rows" : "") + (roll ? ",roll" : "") +
+  g_last_demod = std::string(g_tune.demod_occ4 ? "demod_bins4_kernel<" : "demod_bins_kernel<") + std::to_string(MS) + (l16 ? ",16" : ",8") + (ROWS ? ",rows" : "") + (roll ? ",roll" : "") + (pf ? (g_tune.bins_prefetch == 6 ? ",pf6" : ",pf4") : "") +
                  (spacer ? ",spacer" + std::to_string(spacer) : "") + ">";
   return DFMI_OK;
 }
@@ -458,6 +463,8 @@ int fused_seed_demod(int dev, const double* x, int64_t nrec, int64_t nbuf, int R
   if (ndata <= 12)
     kern = nslot <= 2 ? (g_tune.bins_loads == 16 ? dfmi::demod_seed_bins_kernel<2, 12, 16>
                          : g_tune.bins_roll       ? dfmi::demod_seed_bins_kernel<2, 12, 8, true>
+                         : g_tune.bins_prefetch == 6 ? dfmi::demod_seed_bins_kernel<2, 12, 8, false, 6>
+                         : g_tune.bins_prefetch   ? dfmi::demod_seed_bins_kernel<2, 12, 8, false, 4>
                                                   : dfmi::demod_seed_bins_kernel<2, 12>)
            : nslot <= 4 ? dfmi::demod_seed_bins_kernel<4, 12>
                         : dfmi::demod_seed_bins_kernel<8, 12>;
@@ -482,7 +489,9 @@ int fused_seed_demod(int dev, const double* x, int64_t nrec, int64_t nbuf, int R
   g_last_demod = "demod_seed_bins_kernel<" + std::to_string(nslot <= 2 ? 2 : nslot <= 4 ? 4 : 8) + "," +
                  std::to_string(ndata <= 12 ? 12 : 16) +
                  (nslot <= 2 && ndata <= 12 && g_tune.bins_loads == 16 ? ",16" : "") +
-                 (nslot <= 2 && ndata <= 12 && g_tune.bins_loads != 16 && g_tune.bins_roll ? ",roll" : "") + ",rows>";
+                 (nslot <= 2 && ndata <= 12 && g_tune.bins_loads != 16 && g_tune.bins_roll ? ",roll" : "") +
+                 (nslot <= 2 && ndata <= 12 && g_tune.bins_loads != 16 && !g_tune.bins_roll && g_tune.bins_prefetch
+                      ? (g_tune.bins_prefetch == 6 ? ",pf6" : ",pf4") : "") + ",rows>";
   return DFMI_OK;
 }
 
@@ -642,7 +651,8 @@ const std::map<std::string, Knob>& knobs() {
       {"seed_fused", {&g_tune.seed_fused, {0, 1}}},
       {"wdfmi_accel", {&g_tune.wdfmi_accel, {0, 1, 2, 3}}},
       {"bins_loads", {&g_tune.bins_loads, {8, 16}}},
-      {"bins_roll", {&g_tune.bins_roll, {0, 1}}}};
+      {"bins_roll", {&g_tune.bins_roll, {0, 1}}},
+      {"bins_prefetch", {&g_tune.bins_prefetch, {0, 1, 4, 6}}}};
   return k;
 }
 // np.mean / np.var of nrec device records on st (moments.hip), numpy-exact.

@@ -224,7 +224,8 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
  * LM path for every ndata), "seed_bins" (1 = seed fold in LDS; moves fits < 1e-10),
  * "seed_order" / "seed_fused" (seed step scheduling), "bins_loads" (8 | 16 chunk loads
  * in flight in the bin kernels), "bins_roll" (1 = software-pipelined load groups),
- * "wdfmi_accel" (bit 0: W-DFMI
+ * "bins_prefetch" (0 | 4 [default] | 6: chunks of the next segment loaded during a
+ * segment's contraction), "wdfmi_accel" (bit 0: W-DFMI
  * time axis without division, bit 1: template slopes in LDS; both exact), "probe"
  * (1 = diagnostics timestamps, dfmi_probe_read). */
 int dfmi_set_tuning(const char* key, int64_t value);

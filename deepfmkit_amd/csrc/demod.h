@@ -387,8 +387,17 @@ __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int
   } else {
     for (; c + LOADS <= nch; c += LOADS) {
       double v[LOADS][2];
-      load_group(c, v);
-      add_group(v);
+#pragma unroll
+      for (int u = 0; u < LOADS; ++u) {
+        if constexpr (NT) VecT<2>::load_nt(xs + (c + u) * 128, v[u]);
+        else VecT<2>::load(xs + (c + u) * 128, v[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < LOADS; ++u) {
+        add_chunk(p0, v[u]);
+        p0 += 128;
+        if (p0 >= L) p0 -= L;
+      }
     }
   }
   {

@@ -7,11 +7,15 @@ all remaining segments seeded from it — i.e. (amp, m, phi, psi, dc, ssq, fitok
 for every segment. Workload at N=1: BASELINE config 2 — 100,000 segments of
 R = 4000 samples (200 kS/s, f_mod = 1 kHz, n = 20), ndata = 10, fp64.
 
-Multi-GPU (torchrun, one process per GPU): every rank owns a contiguous shard of
-`--segments` segments of one long record (weak scaling, no data-path collective);
-each rank also demodulates/fits the record's buffer 0 to get the seed, exactly
-what every reference Pool worker receives. Timing: barrier + synchronize on both
-sides of exactly K steps, MAX over ranks (all_reduce MAX of the elapsed time).
+Multi-GPU (torchrun, one process per GPU): BASELINE config 4 by default — ONE
+record of 10,000,000 segments split into contiguous shards of 10M/world segments
+(strong scaling; 1.25M = 40 GB per GPU at 8); with --segments, that many per GPU
+(weak scaling). No data-path collective: each rank also demodulates/fits the
+record's buffer 0 to get the seed, exactly what every reference Pool worker
+receives, and regenerates it bit for bit (the input is the counter-based
+dfmi_synth_snr record: sample i is a function of (seed, i) only). Timing: barrier
++ synchronize on both sides of exactly K steps, MAX over ranks (all_reduce MAX of
+the elapsed time).
 
 Extra JSON fields: roofline (demod kernel, HIP events on the launch stream),
 cpu_baseline (oracle restatement of _fit_parallel with a Pool on the host's
@@ -35,6 +39,8 @@ METRIC = "segments fitted/sec (m,phi,psi,amp) @200 kS/s, 1/2/4/8 GPU; max|Δphi|
 F_SAMP, F_MOD, N_CYC, NDATA = 200000.0, 1000.0, 20, 10
 M_TRUE, SNR_DB = 6.0, 40.0
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+CONFIG4_SEGMENTS = 10_000_000  # BASELINE.json config 4: 10M segments over the node's GPUs
+SEED = 1234  # key of the counter-based generator (one record for every rank)
 
 
 def parse():
@@ -44,48 +50,71 @@ def parse():
     # (0.658 vs 0.630 ms/step measured on the same box)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--segments", type=int, default=100_000, help="segments per GPU")
+    ap.add_argument("--segments", type=int, default=None,
+                    help="segments per GPU (default: 100,000 = config 2 on one GPU; with WORLD_SIZE > 1, "
+                         "10,000,000 / world = config 4, one 10M-segment record split over the ranks)")
     ap.add_argument("--channels", type=int, default=1,
                     help="records in the batch (config 3: 2 channels, main m=6 and witness m=4.3, each "
                          "seeded by its own buffer 0), segments split evenly; 1 GPU only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=8000, help="segments in the CPU-baseline sample")
-    ap.add_argument("--cpu-procs", type=int, default=16, help="Pool size of the CPU baseline (box share: 16)")
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="segments in the CPU-baseline sample (default max(8000, 500 per process))")
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="Pool size of the CPU baseline (0: every CPU this process may use, bench.cpu_share)")
     ap.add_argument("--demod-only", action="store_true", help="profile helper: time only the demod kernel")
     ap.add_argument("--tune", default="", help="A/B helper: dfmi_set_tuning knobs as key=value[,key=value]")
     return ap.parse_args()
 
 
-def gen_shard(torch, dev, seg0, nseg, R, seed, chunk=8192, m_true=None):
-    """snr-mode signal (physics.py:493-530 formula) for global segments [seg0, seg0+nseg)
-    generated on the device: y = 1 + cos(m cos(w t)), white noise at SNR_DB."""
-    M_TRUE = m_true if m_true is not None else globals()["M_TRUE"]
-    x = torch.empty(nseg * R, dtype=torch.float64, device=dev)
-    w = 2 * np.pi * F_MOD
-    # noise power from the (periodic) clean signal power: mean((y - mean y)^2)
-    t1 = torch.arange(R, dtype=torch.float64, device=dev) / F_SAMP
-    y1 = 1.0 + torch.cos(M_TRUE * torch.cos(w * t1))
-    std = float(torch.sqrt(((y1 - y1.mean()) ** 2).mean() / 10 ** (SNR_DB / 10.0)))
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed)
-    for s in range(0, nseg, chunk):
-        n = min(chunk, nseg - s)
-        t = (torch.arange(n * R, dtype=torch.float64, device=dev) + float((seg0 + s) * R)) / F_SAMP
-        y = 1.0 + torch.cos(M_TRUE * torch.cos(w * t))
-        y += std * torch.randn(n * R, dtype=torch.float64, device=dev, generator=g)
-        x[s * R:(s + n) * R] = y
+def gen_shard(torch, dev, seg0, nseg, R, seed, chunk=None, m_true=None, stream=0, out=None):
+    """Global segments [seg0, seg0+nseg) of the snr-mode record (physics.py:493-530
+    formula: A(1 + C cos(phi + m cos(w t + psi))) + white noise at SNR_DB) generated on
+    the device by the counter-based dfmi_synth_snr: sample i of the record depends only
+    on (seed, stream, i), so every rank regenerates any segment (buffer 0 included) bit
+    for bit at any world size."""
+    from deepfmkit_amd.physics import SnrSpec, synth_snr
+    spec = SnrSpec(seed=seed, stream=stream, f_samp=F_SAMP, f_mod=F_MOD, m=M_TRUE if m_true is None else m_true,
+                   snr_db=SNR_DB)
+    x = torch.empty(nseg * R, dtype=torch.float64, device=dev) if out is None else out
+    synth_snr(spec, seg0 * R, nseg * R, out=x)
     return x
 
 
 def shard_plan(rank, world, nseg):
-    """Static weak-scaling shard of one long record: rank r owns global segments
+    """Static shard of one long record: rank r owns global segments
     [r*nseg, (r+1)*nseg). Rank 0's shard starts with the record's buffer 0, which
     seeds every chunk (fitters.py:403-410); the other ranks prepend that buffer
-    and fit it themselves (no collective). Returns (first global segment,
-    buffers in the local batch, whether the seed buffer is prepended)."""
+    (regenerated bit for bit by the counter-based generator) and fit it themselves
+    (no collective). Returns (first global segment, buffers in the local batch,
+    whether the seed buffer is prepended)."""
     if rank == 0:
         return 0, nseg, False
     return rank * nseg, nseg + 1, True
+
+
+def cpu_share():
+    """The host CPUs this process may use: affinity, capped by a cgroup CPU quota
+    (a GPU box's share is far below os.cpu_count(), which counts the whole machine)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    share = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return share, {"os_cpu_count": os.cpu_count(), "affinity": aff, "cgroup_quota": quota, "model": model}
 
 
 def cpu_baseline(args):
@@ -98,21 +127,24 @@ def cpu_baseline(args):
     from oracle import nls_oracle as O
 
     R = int(F_SAMP / F_MOD * N_CYC)
-    nseg = args.cpu_sample
+    share, host = cpu_share()
+    procs = args.cpu_procs if args.cpu_procs > 0 else share
+    nseg = args.cpu_sample if args.cpu_sample else max(8000, 500 * procs)
     laser, ifo = dfm.LaserConfig(), dfm.InterferometerConfig()
     dfm.set_laser_df_for_effect(laser, ifo, M_TRUE)
     sim = dfm.DFMIObject("cpu", laser, ifo, f_samp=F_SAMP)
     raw = dfm.SignalGenerator().generate(sim, nseg * R / F_SAMP, mode="snr", snr_db=SNR_DB, trial_num=0)["main"]
     x = raw.samples()
-    procs = max(1, min(args.cpu_procs, os.cpu_count() or 1))
     with get_context("fork").Pool(procs) as pool:
         O.fit_record_parallel(x[: 4 * R * procs], F_SAMP, F_MOD, N_CYC, n_cores=procs, pool=pool)  # warm
         t0 = time.perf_counter()
         ref = O.fit_record_parallel(x, F_SAMP, F_MOD, N_CYC, n_cores=procs, pool=pool)
         dt = time.perf_counter() - t0
     base = {"value": round(nseg / dt, 1), "unit": "segments/s", "cores": procs, "kind": "port",
-            "sample": f"{nseg} segments of config 2 (R=4000, ndata=10, m=6, 40 dB), numpy restatement of "
-                      f"StandardNLSFitter._fit_parallel with multiprocessing.Pool({procs}); {dt:.2f} s wall"}
+            "sample": f"{nseg} segments of config 2 (R=4000, ndata=10, m=6, 40 dB; the reference's own snr "
+                      f"generator, RandomState(0)), numpy restatement of StandardNLSFitter._fit_parallel with "
+                      f"multiprocessing.Pool({procs}); {dt:.2f} s wall",
+            "host": host}
     return raw, ref, procs, base
 
 
@@ -160,24 +192,32 @@ def main():
         k, v = kv.split("=")
         _lib.check(lib.dfmi_set_tuning(k.encode(), int(v)), "dfmi_set_tuning")
     R = int(F_SAMP / F_MOD * N_CYC)
-    nseg = args.segments
+    # config 4 (BASELINE.json): ONE 10,000,000-segment record split over the ranks
+    # (total work fixed: strong scaling); config 2: 100,000 segments on one GPU;
+    # an explicit --segments is per GPU (weak scaling)
+    config4 = world > 1 and args.segments is None
+    if config4:
+        if CONFIG4_SEGMENTS % world:
+            raise SystemExit(f"config 4: {CONFIG4_SEGMENTS} segments do not split over {world} ranks")
+        nseg = CONFIG4_SEGMENTS // world
+    else:
+        nseg = args.segments if args.segments is not None else 100_000
     nrec = max(1, args.channels) if world == 1 else 1
     if nrec > 1:  # config 3: channels as records of one batch (fit_many), each with its own seed
         if nseg % nrec:
             raise SystemExit("--segments must be a multiple of --channels")
         nbuf, prepend_seed = nseg // nrec, False
         ms_true = [M_TRUE, 4.3] + [M_TRUE] * (nrec - 2)
-        x = torch.cat([gen_shard(torch, dev, 0, nbuf, R, seed=1234 + c, m_true=ms_true[c]) for c in range(nrec)])
+        x = torch.empty(nrec * nbuf * R, dtype=torch.float64, device=dev)
+        for c in range(nrec):  # channel c: its own Philox stream under the seed
+            gen_shard(torch, dev, 0, nbuf, R, seed=SEED, m_true=ms_true[c], stream=c,
+                      out=x[c * nbuf * R:(c + 1) * nbuf * R])
     else:
         seg0, nbuf, prepend_seed = shard_plan(rank, world, nseg)
-        body = gen_shard(torch, dev, seg0, nseg, R, seed=1234 + rank)
-        if not prepend_seed:
-            x = body
-        else:
-            head = gen_shard(torch, dev, 0, 1, R, seed=1234)
-            x = torch.cat([head, body])
-            del head
-        del body
+        x = torch.empty(nbuf * R, dtype=torch.float64, device=dev)
+        if prepend_seed:  # the record's buffer 0, bit for bit what rank 0 holds
+            gen_shard(torch, dev, 0, 1, R, seed=SEED, out=x[:R])
+        gen_shard(torch, dev, seg0, nseg, R, seed=SEED, out=x[(nbuf - nseg) * R:])
     torch.cuda.synchronize()
     w0 = w0_of(F_MOD, F_SAMP)
     cfg = F.lm_config()
@@ -200,42 +240,23 @@ def main():
                                  stream.cuda_stream)
         _lib.check(rc, "dfmi_demod_rows")
 
-    fn = demod if args.demod_only else step
-    for _ in range(args.warmup):
-        fn()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        fn()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
-    ms = el / args.steps * 1e3
-    total_segments = nseg * world  # units of work; the seed replicas on ranks > 0 are not counted
-    value = total_segments * args.steps / el
-    # BASELINE.json configs: 2 = 100k segments on one GPU, 4 = 10M over 8 GPUs (1.25M per GPU)
-    cfg_name = {100_000: "config2", 1_250_000: "config4 shard"}.get(nseg, "config2-shape")
-    if nrec == 2:
-        cfg_name = "config3"
-
     # ---- roofline of the dominant kernel (demod), HIP events on the launch stream ----
+    # (measured BEFORE the timed window: these ~2 x nrep untimed launches also bring the
+    # GPU to its steady clocks, so a short driver window carries no ramp-up)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     demod()
-    nrep = max(5, args.steps)
+    nrep = max(20, args.steps)
     ev0.record(stream)
     for _ in range(nrep):
         demod()
     ev1.record(stream)
     ev1.synchronize()
     demod_ms = ev0.elapsed_time(ev1) / nrep
+    demod_ms_max = demod_ms
+    if world > 1:  # the slowest rank's dominant kernel (every rank runs the same shape)
+        tt = torch.tensor([demod_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        demod_ms_max = float(tt.item())
     kname = lib.dfmi_last_demod_kernel().decode()
     if args.demod_only:  # profile helper: nothing but the timed demodulation kernel
         if rank == 0:
@@ -264,6 +285,36 @@ def main():
     ev1.record(stream)
     ev1.synchronize()
     lm_ms = ev0.elapsed_time(ev1) / nrep
+    fn = demod if args.demod_only else step
+    for _ in range(args.warmup):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    ms = el / args.steps * 1e3
+    total_segments = nseg * world  # units of work; the seed replicas on ranks > 0 are not counted
+    value = total_segments * args.steps / el
+    # BASELINE.json configs: 2 = 100k segments on one GPU, 3 = two channels,
+    # 4 = 10M over the ranks (1.25M per GPU at 8)
+    if config4:
+        cfg_name = "config4"
+    elif nrec == 2:
+        cfg_name = "config3"
+    else:
+        cfg_name = {100_000: "config2", 1_250_000: "config4 shard"}.get(nseg, "config2-shape")
+
     bytes_per_seg = 8 * R + 8 * (2 * NDATA + 1)  # read the segment, write QI + dc
     achieved = nall * bytes_per_seg / (demod_ms * 1e-3) / 1e9
     family = kname.split("<")[0]
@@ -278,6 +329,9 @@ def main():
     roof = {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
             "avg_launch_ms": round(demod_ms, 4), "algorithmic_bytes_per_launch": nall * bytes_per_seg}
+    if world > 1:
+        roof["avg_launch_ms_max_over_ranks"] = round(demod_ms_max, 4)
+        roof["frac_min_over_ranks"] = round(nall * bytes_per_seg / (demod_ms_max * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
 
     # parity on the timed batch itself: status-0 fraction and a sanity check of the estimates
     st = ok.cpu().numpy()
@@ -285,9 +339,13 @@ def main():
 
     line = {"metric": METRIC, "value": round(value, 1), "unit": "segments/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic snr-mode DFMI (m=6, 40 dB white noise) generated on device",
-            "config": {"workload": f"{cfg_name}: {nseg} segments/GPU x R={R} @200 kS/s, ndata={NDATA}, "
+            "scaling": "strong" if config4 else "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic snr-mode DFMI (m=6, 40 dB white noise) generated on device by the counter-based "
+                    "dfmi_synth_snr (Philox4x32-10 keyed by (seed, sample index): every rank regenerates buffer 0 "
+                    "bit for bit)",
+            "config": {"workload": f"{cfg_name}: {nseg} segments/GPU"
+                                   + (f" ({nseg * world} total, one record)" if world > 1 else "")
+                                   + f" x R={R} @200 kS/s, ndata={NDATA}, "
                                    f"{nrec} channel{'s' if nrec > 1 else ''}, _fit_parallel chunk size 1",
                        "segments_per_gpu": nseg, "channels": nrec, "R": R, "ndata": NDATA,
                        "parallelism": f"shard{world}"},

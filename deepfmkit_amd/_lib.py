@@ -24,7 +24,7 @@ SYMBOLS = ("dfmi_lm_config_default", "dfmi_demod", "dfmi_lm", "dfmi_nls_record",
            "dfmi_last_demod_kernel", "dfmi_qi_row_stride", "dfmi_qi_row_dc", "dfmi_demod_rows",
            "dfmi_probe_read", "dfmi_get_tuning", "dfmi_txt_parse_header", "dfmi_txt_shape", "dfmi_txt_read",
            "dfmi_fit_txt_write", "dfmi_py_repr", "dfmi_txt_last_error", "dfmi_wdfmi_fit", "dfmi_ekf_fit",
-           "dfmi_record_moments", "dfmi_synth_asd")
+           "dfmi_record_moments", "dfmi_synth_asd", "dfmi_synth_snr", "dfmi_bessel_eval")
 
 
 class DFMIError(RuntimeError):
@@ -67,6 +67,23 @@ class WdfmiConfig(ctypes.Structure):
     ]
 
 
+class SnrParams(ctypes.Structure):
+    """Mirror of dfmi_snr_params (include/dfmi.h)."""
+    _fields_ = [
+        ("seed", ctypes.c_uint64),
+        ("stream", ctypes.c_uint32),
+        ("period", ctypes.c_int32),
+        ("f_samp", ctypes.c_double),
+        ("f_mod", ctypes.c_double),
+        ("amp", ctypes.c_double),
+        ("visibility", ctypes.c_double),
+        ("m", ctypes.c_double),
+        ("phi", ctypes.c_double),
+        ("psi", ctypes.c_double),
+        ("noise_std", ctypes.c_double),
+    ]
+
+
 WDFMI_METHODS = {"wdfmi_nls": 0, "wdfmi_ortho": 1, "wdfmi_seq": 2, "hwdfmi": 3}
 
 _lock = threading.Lock()
@@ -101,6 +118,10 @@ def load():
         lib.dfmi_record_moments.restype = ctypes.c_int
         lib.dfmi_synth_asd.argtypes = [P, i64, i64, dbl, P, i32, P]
         lib.dfmi_synth_asd.restype = ctypes.c_int
+        lib.dfmi_synth_snr.argtypes = [ctypes.POINTER(SnrParams), i64, i64, P, i32, P]
+        lib.dfmi_synth_snr.restype = ctypes.c_int
+        lib.dfmi_bessel_eval.argtypes = [P, i64, i32, i32, P, i32, P]
+        lib.dfmi_bessel_eval.restype = ctypes.c_int
         lib.dfmi_wdfmi_fit.argtypes = [P, i64, i64, i64, i32, P, i64, ctypes.POINTER(WdfmiConfig), P, P, i32, P]
         lib.dfmi_wdfmi_fit.restype = ctypes.c_int
         lib.dfmi_detect_period.argtypes = [dbl, i32, i32]

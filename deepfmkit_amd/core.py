@@ -268,8 +268,11 @@ class DeepFitFramework:
         """Fit several channels in ONE engine call (lane/segment batch across channels).
 
         Equivalent to `for l in labels: self.fit(l, method, **kwargs)` (which is how
-        notebooks/0.1_quickstart-2-ch fits its two channels); channels must share
-        f_samp, f_mod and length. Returns {label: DeepFitObject}."""
+        notebooks/0.1_quickstart-2-ch fits its two channels), including the fit labels
+        f"{label}_{method}" under which self.fits / self.fits_df store the results; channels
+        that share f_samp, f_mod and length go through one engine call. Raises fit()'s
+        ValueError when the record length is not a multiple of R (fitters.py:375, 412).
+        Returns {label: DeepFitObject}."""
         raws = [self.raws[l] for l in labels]
         r0 = raws[0]
         if any(r.f_samp != r0.f_samp or r.f_mod != r0.f_mod or r.n_samples() != r0.n_samples() for r in raws):
@@ -298,5 +301,5 @@ class DeepFitFramework:
         df_all = _fitters.frame_from(cols, ok)
         for i, (l, raw) in enumerate(zip(labels, raws)):
             df = df_all.iloc[i * nbuf:(i + 1) * nbuf].reset_index(drop=True)
-            out[l] = self._finish(f"fit_{l}", l, raw, method, df, n, R, fs, nbuf)
+            out[l] = self._finish(f"{l}_{method}", l, raw, method, df, n, R, fs, nbuf)  # fit()'s default label
         return out

@@ -26,10 +26,34 @@
 #include "synth.h"
 #include "wdfmi.h"
 
+namespace dfmi {
+hipError_t snr_gen_launch(const dfmi_snr_params& p, int64_t idx0, int64_t n, double* out, int n_cu, hipStream_t st);
+hipError_t bessel_eval_launch(const double* x, int64_t nx, int nmax, int method, double* out, hipStream_t st);
+}
+
 namespace {
 
 thread_local std::string g_err;
-std::mutex g_mu;
+std::mutex g_mu;  // the device map, HIP initialisation and the tuning/probe globals
+
+// One C-ABI call on this thread: clears the error, remembers the caller's stream
+// (workspaces are per stream: two DFMI_MEM_DEVICE calls in flight on different
+// streams never share scratch) and, once ensure_init has picked the device, holds
+// that DEVICE's lock — calls on different devices from different host threads run
+// concurrently; calls on one device are serialised while they enqueue.
+struct CallScope;
+thread_local CallScope* t_call = nullptr;
+struct CallScope {
+  std::unique_lock<std::mutex> dev_lk;
+  hipStream_t stream;
+  explicit CallScope(void* s = nullptr) : stream((hipStream_t)s) {
+    g_err.clear();
+    t_call = this;
+  }
+  ~CallScope() { t_call = nullptr; }
+  CallScope(const CallScope&) = delete;
+  CallScope& operator=(const CallScope&) = delete;
+};
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -57,6 +81,8 @@ struct DeviceState {
   std::map<std::tuple<int, int, uint64_t>, DevBuf> basis;            // (L, ndata, w0 bits)
   std::map<std::tuple<int, uint64_t, uint64_t, uint64_t>, DevBuf> gridtab;  // (ndata, min, max, step)
   std::map<int64_t, DevBuf> pwplan;                                 // n -> numpy pairwise-sum plan
+  std::map<std::pair<const void*, int>, int> occupancy;              // (kernel, LDS bytes) -> blocks per CU
+  std::mutex mu;               // held by the call that drives this device (CallScope)
   hipStream_t side = nullptr;  // seed step runs here, concurrently with the bulk demod
   hipEvent_t ev_in = nullptr, ev_seed = nullptr, ev_bulk = nullptr;
 };
@@ -64,7 +90,26 @@ struct DeviceState {
 std::map<int, DeviceState> g_dev;
 int g_ndev = -1;
 
+thread_local DeviceState* t_ds = nullptr;  // the device of the current call
+
+int ensure_init_locked(int* dev_out);
+
+// Picks (and on first use initialises) the current HIP device and takes its lock
+// for the rest of the current CallScope.
 int ensure_init(int* dev_out) {
+  DeviceState* ds = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    int rc = ensure_init_locked(dev_out);
+    if (rc) return rc;
+    ds = &g_dev[*dev_out];
+  }
+  if (t_call && !t_call->dev_lk.owns_lock()) t_call->dev_lk = std::unique_lock<std::mutex>(ds->mu);
+  t_ds = ds;
+  return DFMI_OK;
+}
+
+int ensure_init_locked(int* dev_out) {
   if (g_ndev < 0) {
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
@@ -97,7 +142,10 @@ int ensure_init(int* dev_out) {
 }
 
 int workspace(int dev, const char* name, size_t bytes, void** out) {
-  DevBuf& b = g_dev[dev].ws[name];
+  (void)dev;
+  std::string key(name);
+  if (t_call && t_call->stream) key += "@" + std::to_string((uintptr_t)t_call->stream);
+  DevBuf& b = t_ds->ws[key];
   if (b.n < bytes) {
     if (b.p) HIPCHK(hipFree(b.p));
     b.p = nullptr;
@@ -112,7 +160,7 @@ int workspace(int dev, const char* name, size_t bytes, void** out) {
 // Device copy of numpy's summation plan over n elements (np_sum.h), cached per n;
 // n_leaves (optional) = plan[0].
 int pairwise_plan(int dev, int64_t n, const int** out, int64_t* n_leaves) {
-  DevBuf& pb = g_dev[dev].pwplan[n];
+  DevBuf& pb = t_ds->pwplan[n];
   if (!pb.p) {
     const std::vector<int> plan = dfmi_pairwise_plan((int)n);
     HIPCHK(hipMalloc(&pb.p, plan.size() * sizeof(int)));
@@ -135,7 +183,7 @@ uint64_t bits(double v) {
 // ndata + c = sin(...), p < L. fit.py:55-64 forms the angle as ((n+1)*w0)*t.
 int basis_table(int dev, int L, int ndata, double w0, hipStream_t st, const double** out) {
   auto key = std::make_tuple(L, ndata, bits(w0));
-  DevBuf& b = g_dev[dev].basis[key];
+  DevBuf& b = t_ds->basis[key];
   if (!b.p) {
     std::vector<double> h((size_t)2 * ndata * L);
     for (int c = 0; c < ndata; ++c) {
@@ -166,7 +214,7 @@ void grid_geometry(const dfmi_lm_config& c, int* n, double* delta) {
 
 int grid_table(int dev, int ndata, const dfmi_lm_config& c, const double** out) {
   auto key = std::make_tuple(ndata, bits(c.m_grid_min), bits(c.m_grid_max), bits(c.m_grid_step));
-  DevBuf& b = g_dev[dev].gridtab[key];
+  DevBuf& b = t_ds->gridtab[key];
   if (!b.p) {
     int n;
     double delta;
@@ -228,13 +276,28 @@ struct Tuning {
   int wdfmi_accel = 3;         // W-DFMI: bit 0 time axis without division, bit 1 template slopes in LDS
   int bins_loads = 8;          // bin kernels (L <= 256): 1-KB chunk loads in flight per wave (8 | 16)
   int bins_roll = 0;           // bin kernels (L <= 256): next load group issued before the current one is added
-  int bins_prefetch = 4;       // bin kernels (L <= 256): next segment's first 4 (1: 4, 6) chunks in flight during
+  int bins_prefetch = 4;       // bin kernels (L <= 256): next segment's first 4 (or 6; 0 = off) chunks in flight during
                                // the contraction (+1.4 % on the step vs 0; 6 ties 4)
 };
 Tuning g_tune;
-std::string g_last_demod;     // kernel variant of the last demodulation launch (dfmi_last_demod_kernel)
-int g_idle_blocks = 0;        // bin kernel: trailing workgroups that take no segments (seed_order 1)
+thread_local std::string g_last_demod;  // kernel variant of the last demodulation launch (dfmi_last_demod_kernel)
+thread_local int g_idle_blocks = 0;  // bin kernel: trailing workgroups that take no segments (seed_order 1)
 uint64_t* g_probe = nullptr;  // diagnostics timestamps (dfmi_set_tuning("probe", 1), dfmi_probe_read)
+
+// hipOccupancyMaxActiveBlocksPerMultiprocessor, cached per (kernel, LDS bytes): the
+// query costs host time on every call otherwise.
+template <typename K>
+int occupancy(K kern, int threads, size_t lds, int* per_cu) {
+  const auto key = std::make_pair((const void*)kern, (int)lds * 4096 + threads);
+  auto it = t_ds->occupancy.find(key);
+  if (it == t_ds->occupancy.end()) {
+    int v = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kern, threads, lds));
+    it = t_ds->occupancy.emplace(key, v).first;
+  }
+  *per_cu = it->second;
+  return DFMI_OK;
+}
 
 int64_t persistent_grid(int n_cu, int per_cu, int64_t need) {
   int64_t grid = (int64_t)n_cu * per_cu;
@@ -272,7 +335,7 @@ int launch_fold_t(const double* x, int64_t nseg, int64_t stride, int R, int L, i
   const size_t lds = LDS ? (size_t)2 * ndata * L * sizeof(double) : 0;
   auto kern = dfmi::demod_fold_kernel<VEC, MS, LDS, LOADS, NT>;
   int per_cu = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, dfmi::kBlockThreads, lds));
+  if (int orc = occupancy(kern, dfmi::kBlockThreads, lds, &per_cu)) return orc;
   if (per_cu < 1) per_cu = 1;
   if (g_tune.demod_blocks_per_cu > 0 && g_tune.demod_blocks_per_cu < per_cu) per_cu = g_tune.demod_blocks_per_cu;
   const int64_t grid = persistent_grid(n_cu, per_cu, (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock);
@@ -307,7 +370,7 @@ int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, i
   if (pf) kern = g_tune.bins_prefetch == 6 ? dfmi::demod_bins_kernel<MS, 8, ROWS, false, 6>
                                            : dfmi::demod_bins_kernel<MS, 8, ROWS, false, 4>;
   int per_cu = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, dfmi::kBlockThreads, lds));
+  if (int orc = occupancy(kern, dfmi::kBlockThreads, lds, &per_cu)) return orc;
   if (per_cu < 1) per_cu = 1;
   if (g_tune.demod_blocks_per_cu > 0 && g_tune.demod_blocks_per_cu < per_cu) per_cu = g_tune.demod_blocks_per_cu;
   const int spacer = g_idle_blocks;  // one of the grid's slots each (seed_order 1)
@@ -352,7 +415,7 @@ bool rows_supported(int dev, const double* x, int64_t stride, int R, int ndata, 
   if (L == 0) L = detect_period_impl(w0, R, ndata);
   if (L <= 0) return false;
   const bool vec2 = (L % 2 == 0) && (stride % 2 == 0) && (((uintptr_t)x & 15) == 0);
-  return bins_applicable(vec2, L, ndata, g_dev[dev].lds_per_block);
+  return bins_applicable(vec2, L, ndata, t_ds->lds_per_block);
 }
 
 // Device-pointer demodulation (all pointers on the current device).
@@ -366,7 +429,7 @@ int demod_device(int dev, const double* x, int64_t nseg, int64_t stride, int R, 
   struct {
     int n_cu;
     size_t lds_per_block;
-  } ds = {g_dev[dev].n_cu, g_dev[dev].lds_per_block};
+  } ds = {t_ds->n_cu, t_ds->lds_per_block};
   if (L > 0) {
     const bool vec2 = (L % 2 == 0) && (stride % 2 == 0) && (((uintptr_t)x & 15) == 0);
     const int VEC = vec2 ? 2 : 1;
@@ -473,10 +536,10 @@ int fused_seed_demod(int dev, const double* x, int64_t nrec, int64_t nbuf, int R
                                                                        : dfmi::demod_seed_bins_kernel<8, 16>;
   const size_t lds = ((size_t)2 * ndata * L + (size_t)dfmi::kWavesPerBlock * L) * sizeof(double);
   int per_cu = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, dfmi::kBlockThreads, lds));
+  if (int orc = occupancy(kern, dfmi::kBlockThreads, lds, &per_cu)) return orc;
   if (per_cu < 1) per_cu = 1;
   if (g_tune.demod_blocks_per_cu > 0 && g_tune.demod_blocks_per_cu < per_cu) per_cu = g_tune.demod_blocks_per_cu;
-  const int64_t slots = (int64_t)g_dev[dev].n_cu * per_cu;
+  const int64_t slots = (int64_t)t_ds->n_cu * per_cu;
   const int64_t nseg = nrec * nbuf;
   if (nrec + 1 > slots / 2) return 1;  // every seed and most of the bulk must be resident at once
   int64_t bulk = slots - nrec;
@@ -501,7 +564,7 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
                       hipStream_t st) {
   const int64_t nseg = nrec * nbuf;
   if (nseg == 0) return DFMI_OK;
-  DeviceState& ds = g_dev[dev];
+  DeviceState& ds = *t_ds;
   void* qiw = nullptr;
   int rc = workspace(dev, "qi", (size_t)2 * ndata * nseg * sizeof(double), &qiw);
   if (rc) return rc;
@@ -652,7 +715,7 @@ const std::map<std::string, Knob>& knobs() {
       {"wdfmi_accel", {&g_tune.wdfmi_accel, {0, 1, 2, 3}}},
       {"bins_loads", {&g_tune.bins_loads, {8, 16}}},
       {"bins_roll", {&g_tune.bins_roll, {0, 1}}},
-      {"bins_prefetch", {&g_tune.bins_prefetch, {0, 1, 4, 6}}}};
+      {"bins_prefetch", {&g_tune.bins_prefetch, {0, 4, 6}}}};
   return k;
 }
 // np.mean / np.var of nrec device records on st (moments.hip), numpy-exact.
@@ -781,7 +844,7 @@ void dfmi_lm_config_default(dfmi_lm_config* cfg) {
 int32_t dfmi_detect_period(double w0, int32_t R, int32_t ndata) { return detect_period_impl(w0, R, ndata); }
 
 int dfmi_device_count(void) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  CallScope cs;
   int dev;
   int rc = ensure_init(&dev);
   if (rc) return 0;
@@ -795,8 +858,7 @@ const char* dfmi_version(void) { return "dfmi 0.2 gfx950"; }
 const char* dfmi_last_demod_kernel(void) { return g_last_demod.c_str(); }
 
 int dfmi_probe_read(int64_t* out, int32_t n) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  g_err.clear();
+  CallScope cs;
   if (!g_probe) return fail(DFMI_ERR_ARG, "probe not enabled (dfmi_set_tuning(\"probe\", 1))");
   if (n < 0 || n > 16 || (n && !out)) return fail(DFMI_ERR_ARG, "bad probe read");
   HIPCHK(hipDeviceSynchronize());
@@ -805,8 +867,7 @@ int dfmi_probe_read(int64_t* out, int32_t n) {
 }
 
 int dfmi_get_tuning(const char* key, int64_t* value) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  g_err.clear();
+  CallScope cs;
   if (!key || !value) return fail(DFMI_ERR_ARG, "null argument");
   const std::string k(key);
   if (k == "probe") {
@@ -820,8 +881,7 @@ int dfmi_get_tuning(const char* key, int64_t* value) {
 }
 
 int dfmi_set_tuning(const char* key, int64_t value) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  g_err.clear();
+  CallScope cs;
   if (!key) return fail(DFMI_ERR_ARG, "null key");
   const std::string k(key);
   if (k == "probe") {
@@ -853,8 +913,7 @@ int dfmi_set_tuning(const char* key, int64_t value) {
 
 int dfmi_demod(const double* x, int64_t nseg, int64_t seg_stride, int32_t R, int32_t ndata, double w0,
                int32_t period, double* qi, double* dc, int32_t mem, void* stream) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  g_err.clear();
+  CallScope cs(stream);
   if (nseg < 0 || R <= 0 || ndata <= 0 || seg_stride < R) return fail(DFMI_ERR_ARG, "bad demod geometry");
   if (nseg > 0 && (!x || !qi || !dc)) return fail(DFMI_ERR_ARG, "null pointer");
   int dev;
@@ -883,8 +942,7 @@ int32_t dfmi_qi_row_dc(int32_t ndata) { return ndata > 0 ? dfmi_row_dc((int)ndat
 
 int dfmi_demod_rows(const double* x, int64_t nseg, int64_t seg_stride, int32_t R, int32_t ndata, double w0,
                     int32_t period, double* rows, int32_t mem, void* stream) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  g_err.clear();
+  CallScope cs(stream);
   if (nseg < 0 || R <= 0 || ndata <= 0 || seg_stride < R) return fail(DFMI_ERR_ARG, "bad demod geometry");
   if (nseg > 0 && (!x || !rows)) return fail(DFMI_ERR_ARG, "null pointer");
   int dev;
@@ -915,8 +973,7 @@ int dfmi_demod_rows(const double* x, int64_t nseg, int64_t seg_stride, int32_t R
 int dfmi_lm(const double* qi, int64_t nseg, int32_t ndata, const double* guess, int32_t guess_per_segment,
             int64_t nchunk, const dfmi_lm_config* cfg, double* params, double* ssq, int32_t* status, int32_t mem,
             void* stream) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  g_err.clear();
+  CallScope cs(stream);
   if (nseg < 0 || ndata <= 0) return fail(DFMI_ERR_ARG, "bad lm geometry");
   if (nseg > 0 && (!qi || !guess || !params || !ssq || !status)) return fail(DFMI_ERR_ARG, "null pointer");
   dfmi_lm_config dcfg;
@@ -968,8 +1025,7 @@ int dfmi_lm(const double* qi, int64_t nseg, int32_t ndata, const double* guess, 
 int dfmi_nls_record(const double* x, int64_t nrec, int64_t rec_stride, int64_t nbuf, int32_t R, int32_t ndata,
                     double w0, int32_t period, const double* init_guess, int32_t parallel, int64_t nchunk,
                     const dfmi_lm_config* cfg, double* out, int32_t* fitok, int32_t mem, void* stream) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  g_err.clear();
+  CallScope cs(stream);
   if (nrec < 0 || nbuf < 0 || R <= 0 || ndata <= 0) return fail(DFMI_ERR_ARG, "bad record geometry");
   if (nrec > 1 && rec_stride < nbuf * (int64_t)R) return fail(DFMI_ERR_ARG, "rec_stride < nbuf*R");
   if (nrec * nbuf > 0 && (!x || !init_guess || !out || !fitok)) return fail(DFMI_ERR_ARG, "null pointer");
@@ -1008,8 +1064,7 @@ int dfmi_nls_record(const double* x, int64_t nrec, int64_t rec_stride, int64_t n
 int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nbuf, int32_t R,
                    const double* witness, int64_t wit_stride, const dfmi_wdfmi_config* cfg, double* out,
                    int32_t* fitok, int32_t mem, void* stream) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  g_err.clear();
+  CallScope cs(stream);
   if (!cfg) return fail(DFMI_ERR_ARG, "null config");
   if (cfg->method < DFMI_WDFMI_NLS || cfg->method > DFMI_HWDFMI) return fail(DFMI_ERR_ARG, "unknown W-DFMI method");
   if (nrec < 0 || nbuf < 0 || R < 4) return fail(DFMI_ERR_ARG, "bad record geometry (R >= 4)");
@@ -1054,7 +1109,7 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
   if (a.L > R) a.L = 0;
   if ((rc = pairwise_plan(dev, R, &a.pw_plan, nullptr))) return rc;
   const size_t lds = dfmi::wdfmi_lds_bytes(a);
-  if (lds > g_dev[dev].lds_per_block)
+  if (lds > t_ds->lds_per_block)
     return fail(DFMI_ERR_UNSUPPORTED, "W-DFMI: R too large for the LDS budget (" + std::to_string(lds) + " B)");
   if (nh > 0 && a.L > 0) {
     const double* bt;
@@ -1101,8 +1156,7 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
 int dfmi_ekf(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, const double* x0,
              const double* p0_diag, const double* q_diag, const double* r_val, double w_m, double f_samp, int32_t R,
              int64_t nbuf, double* states, int32_t mem, void* stream) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  g_err.clear();
+  CallScope cs(stream);
   return ekf_impl(x, nrec, rec_stride, n_samp, x0, nullptr, p0_diag, q_diag, r_val, w_m, f_samp, R, nbuf, states, mem,
                   stream);
 }
@@ -1110,8 +1164,7 @@ int dfmi_ekf(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
 int dfmi_ekf_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, const double* init4,
                  const double* p0_diag, const double* q_diag, const double* r_val, double w_m, double f_samp,
                  int32_t R, int64_t nbuf, double* states, int32_t mem, void* stream) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  g_err.clear();
+  CallScope cs(stream);
   if (!init4) return fail(DFMI_ERR_ARG, "null init4");
   return ekf_impl(x, nrec, rec_stride, n_samp, nullptr, init4, p0_diag, q_diag, r_val, w_m, f_samp, R, nbuf, states,
                   mem, stream);
@@ -1119,8 +1172,7 @@ int dfmi_ekf_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_sa
 
 int dfmi_synth_asd(const dfmi_synth_trial* trials, int64_t ntrial, int64_t n_samp, double f_samp, double* out,
                    int32_t mem, void* stream) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  g_err.clear();
+  CallScope cs(stream);
   if (ntrial < 0 || n_samp < 2 || !(f_samp > 0.0)) return fail(DFMI_ERR_ARG, "bad synthesis geometry (n_samp >= 2)");
   if (ntrial > 0 && (!trials || !out)) return fail(DFMI_ERR_ARG, "null pointer");
   int dev;
@@ -1141,10 +1193,60 @@ int dfmi_synth_asd(const dfmi_synth_trial* trials, int64_t ntrial, int64_t n_sam
   return DFMI_OK;
 }
 
+int dfmi_synth_snr(const dfmi_snr_params* prm, int64_t idx0, int64_t n, double* out, int32_t mem, void* stream) {
+  CallScope cs(stream);
+  if (!prm || n < 0 || idx0 < 0) return fail(DFMI_ERR_ARG, "bad snr synthesis arguments");
+  if (!(prm->f_samp > 0.0) || prm->period < 0) return fail(DFMI_ERR_ARG, "f_samp must be > 0, period >= 0");
+  if (n > 0 && !out) return fail(DFMI_ERR_ARG, "null pointer");
+  int dev;
+  int rc = ensure_init(&dev);
+  if (rc) return rc;
+  if (n == 0) return DFMI_OK;
+  hipStream_t st = (hipStream_t)stream;
+  double* dout = out;
+  if (mem != DFMI_MEM_DEVICE && (rc = workspace(dev, "g_out", (size_t)n * 8, (void**)&dout))) return rc;
+  HIPCHK(dfmi::snr_gen_launch(*prm, idx0, n, dout, t_ds->n_cu, st));
+  if (mem != DFMI_MEM_DEVICE) {
+    HIPCHK(hipMemcpyAsync(out, dout, (size_t)n * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  return DFMI_OK;
+}
+
+int dfmi_bessel_eval(const double* x, int64_t nx, int32_t nmax, int32_t method, double* out, int32_t mem,
+                     void* stream) {
+  CallScope cs(stream);
+  if (nx < 0 || nmax < 0 || method < 0 || method > 2) return fail(DFMI_ERR_ARG, "bad bessel_eval arguments");
+  if ((method == 1 && nmax > 13) || (method == 2 && nmax > 17))
+    return fail(DFMI_ERR_ARG, "register path: nmax <= 13 (method 1) / 17 (method 2)");
+  if (nx > 0 && (!x || !out)) return fail(DFMI_ERR_ARG, "null pointer");
+  int dev;
+  int rc = ensure_init(&dev);
+  if (rc) return rc;
+  if (nx == 0) return DFMI_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const size_t ob = (size_t)nx * (nmax + 1) * 8;
+  const double* dx = x;
+  double* dout = out;
+  if (mem != DFMI_MEM_DEVICE) {
+    void *a, *b;
+    if ((rc = workspace(dev, "b_x", (size_t)nx * 8, &a))) return rc;
+    if ((rc = workspace(dev, "b_out", ob, &b))) return rc;
+    HIPCHK(hipMemcpyAsync(a, x, (size_t)nx * 8, hipMemcpyHostToDevice, st));
+    dx = (const double*)a;
+    dout = (double*)b;
+  }
+  HIPCHK(dfmi::bessel_eval_launch(dx, nx, nmax, method, dout, st));
+  if (mem != DFMI_MEM_DEVICE) {
+    HIPCHK(hipMemcpyAsync(out, dout, ob, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  return DFMI_OK;
+}
+
 int dfmi_record_moments(const double* x, int64_t nrec, int64_t rec_stride, int64_t n, double* mean, double* var,
                         int32_t mem, void* stream) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  g_err.clear();
+  CallScope cs(stream);
   if (nrec < 0 || n < 1 || n > INT32_MAX) return fail(DFMI_ERR_ARG, "bad moments geometry (1 <= n < 2^31)");
   if (nrec > 1 && rec_stride < n) return fail(DFMI_ERR_ARG, "rec_stride < n");
   if (nrec > 0 && (!x || !mean)) return fail(DFMI_ERR_ARG, "null pointer");

@@ -49,9 +49,16 @@ def _is_device_tensor(x):
     return hasattr(x, "data_ptr") and getattr(x, "is_cuda", False)
 
 
-def _torch_stream():
+def _torch_stream(device=None):
     import torch
-    return torch.cuda.current_stream().cuda_stream
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _on_device(x):
+    """Context that makes x's GPU the current HIP device for the library call: the C ABI
+    launches on hipGetDevice(), so a tensor on cuda:1 must be fitted with cuda:1 current."""
+    import torch
+    return torch.cuda.device(x.device)
 
 
 def w0_of(f_mod, f_samp):
@@ -91,9 +98,10 @@ def nls_records(records, f_samp, f_mod, R, nbuf, ndata=10, init_guess=(1.6, 6.0,
             raise ValueError("device records must be contiguous float64 rows")
         out = torch.empty((6, nseg), dtype=torch.float64, device=x.device)
         ok = torch.empty(nseg, dtype=torch.int32, device=x.device)
-        rc = lib.dfmi_nls_record(x.data_ptr(), nrec, rec_stride, nbuf, R, ndata, w0, 0, _lib.ptr(g),
-                                 1 if parallel else 0, max(nchunk, 1), cfg, out.data_ptr(), ok.data_ptr(),
-                                 _lib.DFMI_MEM_DEVICE, _torch_stream())
+        with _on_device(x):
+            rc = lib.dfmi_nls_record(x.data_ptr(), nrec, rec_stride, nbuf, R, ndata, w0, 0, _lib.ptr(g),
+                                     1 if parallel else 0, max(nchunk, 1), cfg, out.data_ptr(), ok.data_ptr(),
+                                     _lib.DFMI_MEM_DEVICE, _torch_stream(x.device))
         _lib.check(rc, "dfmi_nls_record")
         return out, ok
     x = np.ascontiguousarray(x, dtype=np.float64)
@@ -255,8 +263,11 @@ def wdfmi_records(method, mains, witnesses, f_samp, f_mod, R, nbuf, df=0.0, f_re
         import torch
         out = torch.empty((7, nseg), dtype=torch.float64, device=x.device)
         ok = torch.empty(nseg, dtype=torch.int32, device=x.device)
-        rc = lib.dfmi_wdfmi_fit(x.data_ptr(), nrec, rec_stride, nbuf, R, w.data_ptr(), wit_stride, cfg,
-                                out.data_ptr(), ok.data_ptr(), _lib.DFMI_MEM_DEVICE, _torch_stream())
+        if w.device != x.device:
+            raise ValueError("main and witness records must be on the same device")
+        with _on_device(x):
+            rc = lib.dfmi_wdfmi_fit(x.data_ptr(), nrec, rec_stride, nbuf, R, w.data_ptr(), wit_stride, cfg,
+                                    out.data_ptr(), ok.data_ptr(), _lib.DFMI_MEM_DEVICE, _torch_stream(x.device))
     else:
         out = np.empty((7, nseg))
         ok = np.empty(nseg, dtype=np.int32)

@@ -294,3 +294,61 @@ def synthesize_asd_trials(cfgs, trial_nums, n_seconds, dynamic=True):
     _lib.check(lib.dfmi_synth_asd(tab.ctypes.data, len(cfgs), n, f_samp, out.data_ptr(), _lib.DFMI_MEM_DEVICE,
                                   _torch_stream()), "dfmi_synth_asd")
     return out
+
+
+# --- counter-based snr-mode records (dfmi_synth_snr) ---------------------------
+class SnrSpec:
+    """Parameters of an unbounded snr-mode record whose sample i is a pure function of
+    (spec, i) (include/dfmi.h dfmi_synth_snr): the signal of physics.py:493-518
+    (is_dynamic=False) plus Philox4x32-10 white noise whose std follows
+    physics.py:520-530 (signal power over one modulation cycle / 10^(snr/10)).
+
+    Used where a record must be split over ranks (BASELINE config 4): every rank
+    regenerates any segment — buffer 0 included — bit for bit."""
+
+    def __init__(self, seed=1234, stream=0, f_samp=200000.0, f_mod=1000.0, amp=1.0, visibility=1.0, m=6.0,
+                 phi=0.0, psi=0.0, snr_db=40.0):
+        self.seed, self.stream = int(seed), int(stream)
+        self.f_samp, self.f_mod = float(f_samp), float(f_mod)
+        self.amp, self.visibility, self.m, self.phi, self.psi = (float(amp), float(visibility), float(m),
+                                                                float(phi), float(psi))
+        self.snr_db = snr_db
+        ratio = self.f_samp / self.f_mod
+        self.period = int(round(ratio)) if abs(ratio - round(ratio)) < 1e-9 and ratio < 2 ** 31 else 0
+
+    def noise_std(self):
+        if self.snr_db is None:
+            return 0.0
+        n = self.period if self.period > 0 else int(self.f_samp)
+        t = np.arange(n) / self.f_samp
+        clean = self.amp * (1 + self.visibility * np.cos(self.phi + self.m * np.cos(2 * np.pi * self.f_mod * t
+                                                                                      + self.psi)))
+        ac = clean - np.mean(clean)
+        return float(np.sqrt(np.mean(ac ** 2) / 10 ** (self.snr_db / 10.0)))
+
+    def params(self):
+        from . import _lib
+        return _lib.SnrParams(self.seed, self.stream, self.period, self.f_samp, self.f_mod, self.amp,
+                              self.visibility, self.m, self.phi, self.psi, self.noise_std())
+
+
+def synth_snr(spec: SnrSpec, idx0, n, out=None):
+    """Samples [idx0, idx0 + n) of the record `spec` (dfmi_synth_snr, on the GPU).
+
+    out: a contiguous float64 CUDA tensor (filled on its device's current stream) or
+    None (returns a numpy array)."""
+    from . import _lib
+    lib = _lib.load()
+    prm = spec.params()
+    if out is not None and getattr(out, "is_cuda", False):
+        import torch
+        if out.dtype != torch.float64 or not out.is_contiguous() or out.numel() < n:
+            raise ValueError("out must be a contiguous float64 CUDA tensor with >= n elements")
+        with torch.cuda.device(out.device):
+            _lib.check(lib.dfmi_synth_snr(prm, int(idx0), int(n), out.data_ptr(), _lib.DFMI_MEM_DEVICE,
+                                          torch.cuda.current_stream(out.device).cuda_stream), "dfmi_synth_snr")
+        return out
+    host = np.empty(int(n), dtype=np.float64) if out is None else out
+    _lib.check(lib.dfmi_synth_snr(prm, int(idx0), int(n), _lib.ptr(host), _lib.DFMI_MEM_HOST, None),
+               "dfmi_synth_snr")
+    return host

@@ -108,9 +108,14 @@ def run_efficiency_trials(params_list, synth="device"):
         guesses = np.array([(1.6, params_list[i]["m_true"], 0.0, 0.0) for i in idx])
         n = int(f_mod * n_seconds)
         R = int(f_samp / f_mod * n)
-        nbuf = int(int(n_seconds * f_samp) / R)
+        N = int(n_seconds * f_samp)
+        nbuf = int(N / R) if R > 0 else 0
         if nbuf == 0:
-            continue
+            continue  # the reference logs "nbuf is zero" and returns an empty fit -> nan
+        if N % R != 0:
+            # run_efficiency_trial raises here: _fit_sequential reshapes the whole
+            # record with reshape(-1, R) (fitters.py:375)
+            raise ValueError(f"cannot reshape array of size {N} into shape ({R})")
         if dev:
             x = synthesize_asd_trials([c for _, c in members], [params_list[i]["trial_num"] for i in idx], n_seconds)
             recs = x[:, : nbuf * R]

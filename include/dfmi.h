@@ -177,6 +177,35 @@ typedef struct dfmi_synth_trial {
 int dfmi_synth_asd(const dfmi_synth_trial* trials, int64_t ntrial, int64_t n_samp, double f_samp, double* out,
                    int32_t mem, void* stream);
 
+/* ---- Counter-based snr-mode input (bench / tests of sharded records) ----
+ * The signal of SignalGenerator._generate_with_snr (physics.py:475-530, ideal signal
+ * physics.py:493-518, is_dynamic=False) for samples [idx0, idx0 + n) of an unbounded
+ * record: sample i = amp*(1 + visibility*cos(phi + m*cos(2*pi*f_mod*t + psi)))
+ * + noise_std*z_i with t = (i mod period)/f_samp (period 0: t = i/f_samp) and z_i a
+ * standard normal from Philox4x32-10 (key = seed, counter = (i>>1, stream, 0),
+ * Box-Muller: z_2j = r*cos(2*pi*u2), z_2j+1 = r*sin(2*pi*u2)). Sample i depends only
+ * on (params, i): any rank can regenerate any segment bit for bit at any world size.
+ * Replaces the reference's RandomState(trial_num).randn stream, which cannot be split
+ * (noise_std is the caller's physics.py:520-530 value). out[k] = sample idx0 + k. */
+typedef struct dfmi_snr_params {
+  uint64_t seed;
+  uint32_t stream;     /* independent streams under one seed (e.g. channels) */
+  int32_t period;      /* samples per modulation cycle (f_samp/f_mod when integer), or 0 */
+  double f_samp, f_mod;
+  double amp, visibility, m, phi, psi;
+  double noise_std;
+} dfmi_snr_params;
+
+int dfmi_synth_snr(const dfmi_snr_params* prm, int64_t idx0, int64_t n, double* out, int32_t mem, void* stream);
+
+/* Diagnostics (GPU parity of scipy.special.jv, fit.py:106-108, 160, 275-276): the
+ * device Bessel code the fit kernels inline, on caller points.
+ * out[i*(nmax+1) + k] = J_k(x[i]), k <= nmax. method 0: the general path's two-pass
+ * Miller walk (any nmax); 1: the register path of ndata <= 12 (nmax <= 13);
+ * 2: the register path of ndata <= 16 (nmax <= 17). */
+int dfmi_bessel_eval(const double* x, int64_t nx, int32_t nmax, int32_t method, double* out, int32_t mem,
+                     void* stream);
+
 /* ---- Witness-based fitters (EXPERIMENTAL in the reference) ----
  * Replace, per record (main channel + witness channel):
  *   DFMI_WDFMI_NLS    WDFMI_NLSFitter.fit        fitters.py:481-570 (least_squares(method='lm'))

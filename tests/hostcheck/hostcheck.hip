@@ -44,6 +44,20 @@ void hc_synth_trial(const dfmi_synth_trial* p, int64_t n, double f_samp, double*
 
 void hc_bessel_table(double x, int N, double* out) { dfmi_bessel_table(x, N, out); }
 
+// the LM register path's single Miller pass (lm.h bessel_regs): NB = 14 (ndata <= 12)
+// or 18 (ndata <= 16), J_0..J_{NB-1}
+void hc_bessel_regs(double x, int nb, double* out) {
+  if (nb == 14) {
+    double J[14];
+    dfmi::bessel_regs<14>(x, 13, J);
+    for (int k = 0; k < 14; ++k) out[k] = J[k];
+  } else {
+    double J[18];
+    dfmi::bessel_regs<18>(x, 17, J);
+    for (int k = 0; k < 18; ++k) out[k] = J[k];
+  }
+}
+
 // qi component-major (qi[c*n + s]); guess n x 4; constants in the reference order.
 int hc_fit_segments(const double* qi, long n, int ndata, const double* guess, const double* consts,
                     const double* lambdas, int n_lambda, double* p_out, double* ssq_out, int* status_out,

@@ -1,0 +1,115 @@
+"""GPU checks of device numerics that the record tests reach only indirectly.
+
+- scipy.special.jv (the reference's Bessel, fit.py:106-108, 160, 275-276) vs the
+  DEVICE Bessel code the fit kernels inline (dfmi_bessel_eval): the general path's
+  two-pass Miller walk over n <= 64, |x| <= 64 and both register-path variants, on
+  the golden grid (tests/golden/bessel.npz), with the host check's bounds
+  (tests/test_host_numerics.py).
+- the bin kernels' prefetch setting (bins_prefetch 0 | 4 | 6) is a schedule, not
+  arithmetic: rows and record fits are bit-identical across settings on a batch
+  large enough that every wave handles several segments (the prefetch path).
+- a record on a non-current GPU is fitted on its own device (multi-GPU hosts only).
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _bessel(x, nmax, method):
+    from deepfmkit_amd import _lib
+    lib = _lib.load()
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    out = np.zeros((x.size, nmax + 1))
+    _lib.check(lib.dfmi_bessel_eval(_lib.ptr(x), x.size, nmax, method, _lib.ptr(out), _lib.DFMI_MEM_HOST, None),
+               "dfmi_bessel_eval")
+    return out.T
+
+
+def test_device_bessel_walk_vs_scipy():
+    d = np.load(os.path.join(GOLDEN, "bessel.npz"))
+    x, jv = d["x"], d["jv"]
+    ours = _bessel(x, int(d["n"].max()), 0)
+    err = np.abs(ours - jv)
+    assert err[:13].max() <= 1e-15          # orders used at ndata = 10
+    assert err.max() <= 3e-15               # every order <= 64
+    assert (err.max(0) / np.abs(jv).max(0)).max() <= 2e-14
+
+
+@pytest.mark.parametrize("method,nmax", [(1, 13), (2, 17)])
+def test_device_bessel_register_path_vs_scipy(method, nmax):
+    d = np.load(os.path.join(GOLDEN, "bessel.npz"))
+    x, jv = d["x"], d["jv"][: nmax + 1]
+    assert np.abs(_bessel(x, nmax, method) - jv).max() <= 1e-15
+
+
+def test_bessel_eval_rejects_bad_orders():
+    from deepfmkit_amd import _lib
+    lib = _lib.load()
+    x = np.zeros(4)
+    out = np.zeros(4 * 20)
+    assert lib.dfmi_bessel_eval(_lib.ptr(x), 4, 14, 1, _lib.ptr(out), _lib.DFMI_MEM_HOST, None) == -1
+
+
+@pytest.fixture
+def restore_prefetch():
+    from deepfmkit_amd import _lib
+    lib = _lib.load()
+    yield lib
+    _lib.check(lib.dfmi_set_tuning(b"bins_prefetch", 4), "dfmi_set_tuning")
+
+
+def test_bins_prefetch_settings_bit_identical(restore_prefetch):
+    import torch
+    from deepfmkit_amd import _lib
+    from deepfmkit_amd.fitters import nls_records, w0_of
+    lib = restore_prefetch
+    nseg, R, nd = 20_000, 4000, 10  # > the resident waves: every wave runs several segments
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    t = torch.arange(R, dtype=torch.float64, device="cuda") / 200000.0
+    clean = 1.0 + torch.cos(6.0 * torch.cos(2 * np.pi * 1000.0 * t))
+    x = (clean.repeat(nseg) + 0.01 * torch.randn(nseg * R, dtype=torch.float64, device="cuda", generator=g))
+    qs = lib.dfmi_qi_row_stride(nd)
+    st = torch.cuda.current_stream().cuda_stream
+    rows, fits = {}, {}
+    for pf in (0, 4, 6):
+        _lib.check(lib.dfmi_set_tuning(b"bins_prefetch", pf), "dfmi_set_tuning")
+        r = torch.full((nseg, qs), float("nan"), dtype=torch.float64, device="cuda")
+        _lib.check(lib.dfmi_demod_rows(x.data_ptr(), nseg, R, R, nd, w0_of(1000.0, 200000.0), 0, r.data_ptr(),
+                                       _lib.DFMI_MEM_DEVICE, st), "dfmi_demod_rows")
+        rows[pf] = r.cpu().numpy()
+        assert ("pf" + str(pf)) in lib.dfmi_last_demod_kernel().decode() or pf == 0
+        cols, ok = nls_records(x.reshape(1, -1), 200000.0, 1000.0, R, nseg, nd)  # fused seed + bins + LM
+        fits[pf] = (cols.cpu().numpy(), ok.cpu().numpy())
+    for pf in (0, 6):
+        np.testing.assert_array_equal(rows[pf], rows[4])
+        np.testing.assert_array_equal(fits[pf][0], fits[4][0])
+        np.testing.assert_array_equal(fits[pf][1], fits[4][1])
+    assert lib.dfmi_set_tuning(b"bins_prefetch", 1) == -1  # only 0 | 4 | 6
+
+
+def test_record_on_non_current_device():
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("one GPU")
+    from deepfmkit_amd.fitters import nls_records
+    R, nseg = 4000, 64
+    t = torch.arange(R, dtype=torch.float64) / 200000.0
+    x = (1.0 + torch.cos(6.0 * torch.cos(2 * np.pi * 1000.0 * t))).repeat(nseg).reshape(1, -1)
+    ref, _ = nls_records(x.to("cuda:0"), 200000.0, 1000.0, R, nseg, 10)
+    torch.cuda.set_device(0)
+    other, _ = nls_records(x.to("cuda:1"), 200000.0, 1000.0, R, nseg, 10)
+    assert other.device.index == 1
+    np.testing.assert_array_equal(other.cpu().numpy(), ref.cpu().numpy())

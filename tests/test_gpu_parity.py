@@ -124,7 +124,7 @@ def test_asd_two_channel_batch():
     for key in ("dynamic_channel", "reference_channel"):
         fo = out[key]
         ours = dict(amp=fo.amp, m=fo.m, phi=fo.phi, psi=fo.psi, dc=fo.dc, ssq=fo.ssq,
-                    fitok=dff.fits_df[f"fit_{key}"]["fitok"].to_numpy())
+                    fitok=dff.fits_df[f"{key}_nls"]["fitok"].to_numpy())
         ref = {k: d[f"{key}_{k}"] for k in FIT_COLS}
         compare_fit(ours, ref, tol=1e-9)
 

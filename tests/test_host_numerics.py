@@ -19,6 +19,7 @@ def hc():
     lib = ctypes.CDLL(HC)
     P = ctypes.c_void_p
     lib.hc_bessel_table.argtypes = [ctypes.c_double, ctypes.c_int, P]
+    lib.hc_bessel_regs.argtypes = [ctypes.c_double, ctypes.c_int, P]
     lib.hc_fit_segments.argtypes = [P, ctypes.c_long, ctypes.c_int, P, P, P, ctypes.c_int, P, P, P, ctypes.c_int]
     return lib
 
@@ -37,6 +38,19 @@ def test_bessel_vs_scipy_table(hc):
     assert err[:13].max() <= 1e-15          # orders used at ndata = 10
     assert err.max() <= 3e-15               # every order <= 64
     assert (err.max(0) / np.abs(jv).max(0)).max() <= 2e-14
+
+
+@pytest.mark.parametrize("nb", [14, 18])
+def test_bessel_regs_vs_scipy_table(hc, nb):
+    """The LM register path's single Miller pass (lm.h bessel_regs) vs scipy.special.jv."""
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "bessel.npz"))
+    x, jv = d["x"], d["jv"][:nb]
+    out = np.zeros(nb)
+    ours = np.zeros_like(jv)
+    for i, xv in enumerate(x):
+        hc.hc_bessel_regs(float(xv), nb, out.ctypes.data)
+        ours[:, i] = out
+    assert np.abs(ours - jv).max() <= 1e-15
 
 
 def _fit(hc, qi, guess, force_general=0):

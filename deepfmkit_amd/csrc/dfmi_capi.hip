@@ -497,8 +497,12 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
                     : (nd_sel <= 12   ? dfmi::lm_chunks_kernel<12, false>
                        : nd_sel <= 16 ? dfmi::lm_chunks_kernel<16, false>
                                      : dfmi::lm_chunks_kernel<0, false>);
+  // ndata == 10 (the reference default): the exact-ndata register variant (no masking)
+  constexpr int kNd10 = dfmi::kExactNd | 10;
+  if (nd_sel == 10) kern = chain ? dfmi::lm_chunks_kernel<kNd10, true> : dfmi::lm_chunks_kernel<kNd10, false>;
   if (rows) {
-    kern = nd_sel <= 12   ? dfmi::lm_chunks_kernel<12, false, true>
+    kern = nd_sel == 10   ? dfmi::lm_chunks_kernel<kNd10, false, true>
+           : nd_sel <= 12 ? dfmi::lm_chunks_kernel<12, false, true>
            : nd_sel <= 16 ? dfmi::lm_chunks_kernel<16, false, true>
                           : dfmi::lm_chunks_kernel<0, false, true>;
     if (nd_sel <= 16) lds = (size_t)qi_ld * 65 * sizeof(double);  // the wave's rows, transposed

@@ -17,15 +17,17 @@
 // component-major (qi[c·ld + s]) so a wave loads each component coalesced.
 //
 // Two code paths, chosen per launch from ndata:
-//  * register path (ndata <= NDMAX, NDMAX = 12 or 16): QI, J_0..J_{NDMAX+1}(m)
-//    and cos/sin(j psi) live in registers; the Bessel values come from ONE
-//    backward Miller pass that stores the low orders as it goes; harmonics are
-//    accumulated in ascending j like the reference's vector expressions.
+//  * register path (ndata <= NDMAX, NDMAX = 12 or 16): the model's structure is
+//    used to cut the work per evaluation (see "Register path" below): J_0..J_{NDMAX+1}(m)
+//    from ONE backward Miller pass, cos/sin(j psi) by the Chebyshev recurrence, the
+//    J^T J / J^T r sums in closed per-harmonic form (the psi column is orthogonal
+//    to the other three: J^T J is block-diagonal, so the damped solve is a 3x3 LDL^T
+//    plus one division), branch-free Cody-Waite sincos.
 //  * general path (any ndata, e.g. 30/62): the two-pass Miller walk of
-//    dfmi_math.h hands out J values in descending order, nothing is stored.
-// A trial point's evaluation always includes J^T J and J^T r: the reference
-// recomputes coeffs() at an accepted trial point (fit.py:250-251), which here
-// is the evaluation already in hand (same numbers, one Bessel pass less).
+//    dfmi_math.h hands out J values in descending order, nothing is stored; the
+//    literal per-residual Jacobian and the pivoting 4x4 solve (msolve's dgesv).
+// The reference recomputes coeffs() at an accepted trial point (fit.py:250-251);
+// here that is the trial's stored Bessel values and trig plus the Jacobian part.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -109,18 +111,6 @@ DFMI_HDI void harmonic_term(Eval& e, int j, double a, bool a_nz, double cph, dou
 
 DFMI_HDI void eval_zero(Eval& e) { e = Eval{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; }
 
-// The residual part of harmonic_term only (ssqf, fit.py:152-167): same bits as the
-// ssq harmonic_term accumulates.
-DFMI_HDI void harmonic_ssq(double& ssq, int j, double a, double cph, double sph, double J0, double cj, double sj,
-                           double Q, double I) {
-  const double pt = quarter_turn(j, cph, sph);
-  const double common = a * pt * J0;
-  const double rq = fma(-common, cj, Q);
-  const double ri = fma(common, sj, I);
-  ssq = fma(rq, rq, ssq);
-  ssq = fma(ri, ri, ssq);
-}
-
 // ---------------------------------------------------------------------------
 // Register path
 // ---------------------------------------------------------------------------
@@ -200,72 +190,196 @@ DFMI_HDI void bessel_regs(double x, int N, double (&J)[NB]) {
   }
 }
 
-template <int NDMAX, typename QF>
-DFMI_HDI void eval_reg(const QF& q, int nd, const double (&p)[4], Eval& e) {
-  const double a = p[0], m = p[1], phi = p[2], psi = p[3];
-  double sph, cph, s1, c1;
-  sincos(phi, &sph, &cph);
-  sincos(psi, &s1, &c1);
-  double J[NDMAX + 2];
-  bessel_regs<NDMAX + 2>(m, nd + 1, J);
-  const bool a_nz = (a != 0.0);
-  eval_zero(e);
-  double cj = c1, sj = s1;  // cos(j psi), sin(j psi) at j = 1
-#pragma unroll
-  for (int j = 1; j <= NDMAX; ++j) {
-    if (j <= nd) harmonic_term(e, j, a, a_nz, cph, sph, J[j - 1], J[j], J[j + 1], cj, sj, q.qc(j - 1), q.qs(j - 1));
-    const double cn = fma(cj, c1, -(sj * s1));
-    const double sn = fma(sj, c1, cj * s1);
-    cj = cn;
-    sj = sn;
-  }
-}
+// Structure of the model (fit.py:68-150) per harmonic j, with P = cos(phi + j pi/2),
+// D = cos(phi + j pi/2 + pi/2), c = a P J_j, dJ = (J_{j-1} - J_{j+1}) / 2 and
+// (cj, sj) = (cos j psi, sin j psi):
+//   residuals    rq = Q_j - c cj,  ri = I_j + c sj
+//   Jacobian     d/d(a, m, phi) of (model_Q, model_I) = u_k (cj, -sj),
+//                u = (P J_j [0 if a == 0: fit.py:126-128], a P dJ, a D J_j);
+//                d/dpsi = -j c (sj, cj)
+// hence, with w = cj^2 + sj^2 (= 1 up to rounding):
+//   (J^T J)_kl = sum u_k u_l w (k, l < 3),  (J^T J)_33 = sum (j c)^2 w,
+//   (J^T J)_k3 = 0 exactly (the psi column is orthogonal to the others),
+//   (J^T r)_k  = sum u_k (cj rq - sj ri),   (J^T r)_3 = -sum j c (sj rq + cj ri).
+// The reference forms J^T J by a BLAS product of the 2 ndata x 4 Jacobian, whose k3
+// entries are rounding residue (~1e-17 of the diagonal); the solve below treats them
+// as the zeros they are. Differences to the literal evaluation: rounding only (the
+// register path agrees with the literal general path within the parity tolerances,
+// tests/test_host_numerics.py).
+// Scheduling fence between the unrolled harmonics of the register path: without it the
+// machine scheduler hoists every harmonic's products ahead of the accumulations (the
+// J^T J pass then held ~190 VGPRs, pushing the LM kernel to one wave per SIMD).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define DFMI_HARMONIC_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define DFMI_HARMONIC_FENCE() ((void)0)
+#endif
 
-// Split form of eval_reg for the LM trials: `trial` computes the point's ssq and
-// keeps its Bessel values and trig; `accept` adds J^T J and J^T r from them when the
-// trial is accepted. A rejected trial (about 45 % of them at 40 dB) thus costs only
-// the ssqf part, as in the reference (fit.py:236-243), and the bits are eval_reg's.
-template <int NDMAX>
+// Register-path variant tags: NDMAX = n (any ndata <= n, harmonics above ndata masked)
+// or kExactNd | n (ndata == n exactly: no masking; dispatched for the default 10).
+constexpr int kExactNd = 1 << 8;
+constexpr int nd_cap(int v) { return v & (kExactNd - 1); }
+constexpr bool nd_exact(int v) { return (v & kExactNd) != 0; }
+
+template <int V>
 struct TrialReg {
-  double J[NDMAX + 2];
+  double J[nd_cap(V) + 2];
   double cph, sph, c1, s1, ssq;
 };
 
-template <int NDMAX, typename QF>
-DFMI_HDI double eval_reg_trial(const QF& q, int nd, const double (&p)[4], TrialReg<NDMAX>& t) {
-  const double a = p[0], m = p[1], phi = p[2], psi = p[3];
-  sincos(phi, &t.sph, &t.cph);
-  sincos(psi, &t.s1, &t.c1);
-  bessel_regs<NDMAX + 2>(m, nd + 1, t.J);
-  double ssq = 0.0;
-  double cj = t.c1, sj = t.s1;
-#pragma unroll
-  for (int j = 1; j <= NDMAX; ++j) {
-    if (j <= nd) harmonic_ssq(ssq, j, a, t.cph, t.sph, t.J[j], cj, sj, q.qc(j - 1), q.qs(j - 1));
-    const double cn = fma(cj, t.c1, -(sj * t.s1));
-    const double sn = fma(sj, t.c1, cj * t.s1);
-    cj = cn;
-    sj = sn;
+// QI of harmonic j (1-based) for the unrolled loops: every load is issued
+// unconditionally (no per-harmonic branch: a branch around each load serialises the
+// loads' latency), from a clamped index, and masked to 0 above ndata.
+template <int V, typename QF>
+DFMI_HDI void qi_pair(const QF& q, int nd, int j, double& Q, double& I) {
+  if constexpr (nd_exact(V)) {
+    Q = q.qc(j - 1);
+    I = q.qs(j - 1);
+  } else {
+    const bool on = j <= nd;
+    const int h = on ? j - 1 : 0;
+    const double qv = q.qc(h), iv = q.qs(h);
+    Q = on ? qv : 0.0;
+    I = on ? iv : 0.0;
   }
-  t.ssq = ssq;
-  return ssq;
 }
 
-template <int NDMAX, typename QF>
-DFMI_HDI void eval_reg_accept(const QF& q, int nd, const double (&p)[4], const TrialReg<NDMAX>& t, Eval& e) {
-  const double a = p[0];
-  const bool a_nz = (a != 0.0);
-  eval_zero(e);
-  double cj = t.c1, sj = t.s1;
+// 1.0 for harmonics j <= ndata, 0.0 above (masks the model terms of the unrolled loops)
+template <int V>
+DFMI_HDI double hmask(int nd, int j) {
+  if constexpr (nd_exact(V)) return 1.0;
+  else return j <= nd ? 1.0 : 0.0;
+}
+
+// ssqf (fit.py:152-167) at p; keeps the point's Bessel values and trig in t for the
+// Jacobian of an accepted trial (eval_reg_accept). Harmonics accumulate into two
+// partial sums (odd / even j): two independent fma chains.
+template <int V, typename QF>
+DFMI_HDI double eval_reg_trial(const QF& q, int nd, const double (&p)[4], TrialReg<V>& t) {
+  constexpr int NDMAX = nd_cap(V);
+  double Q[NDMAX], I[NDMAX];
+#pragma unroll
+  for (int j = 1; j <= NDMAX; ++j) qi_pair<V>(q, nd, j, Q[j - 1], I[j - 1]);
+  dfmi_sincos(p[2], &t.sph, &t.cph);
+  dfmi_sincos(p[3], &t.s1, &t.c1);
+  bessel_regs<NDMAX + 2>(p[1], nd_exact(V) ? NDMAX + 1 : nd + 1, t.J);
+  const double ac = p[0] * t.cph, as = p[0] * t.sph;
+  const double tc = 2.0 * t.c1;
+  double so = 0.0, se = 0.0;
+  double cj = t.c1, sj = t.s1, cm = 1.0, sm = 0.0;  // (j psi), ((j-1) psi)
 #pragma unroll
   for (int j = 1; j <= NDMAX; ++j) {
-    if (j <= nd)
-      harmonic_term(e, j, a, a_nz, t.cph, t.sph, t.J[j - 1], t.J[j], t.J[j + 1], cj, sj, q.qc(j - 1), q.qs(j - 1));
-    const double cn = fma(cj, t.c1, -(sj * t.s1));
-    const double sn = fma(sj, t.c1, cj * t.s1);
+    const double c = quarter_turn(j, ac, as) * t.J[j] * hmask<V>(nd, j);  // a cos(phi + j pi/2) J_j
+    const double rq = fma(-c, cj, Q[j - 1]);
+    const double ri = fma(c, sj, I[j - 1]);
+    double& acc = (j & 1) ? so : se;
+    acc = fma(rq, rq, acc);
+    acc = fma(ri, ri, acc);
+    // cos / sin((j+1) psi) = 2 cos(psi) cos / sin(j psi) - cos / sin((j-1) psi)
+    const double cn = fma(tc, cj, -cm), sn = fma(tc, sj, -sm);
+    cm = cj;
+    sm = sj;
     cj = cn;
     sj = sn;
   }
+  t.ssq = so + se;
+  return t.ssq;
+}
+
+// coeffs (fit.py:68-150) at the trial point of t: J^T J and J^T r in the closed form
+// above; e.ssq is the trial's.
+template <int V, typename QF>
+DFMI_HDI void eval_reg_accept(const QF& q, int nd, const double (&p)[4], const TrialReg<V>& t, Eval& e) {
+  constexpr int NDMAX = nd_cap(V);
+  double Q[NDMAX], I[NDMAX];
+#pragma unroll
+  for (int j = 1; j <= NDMAX; ++j) qi_pair<V>(q, nd, j, Q[j - 1], I[j - 1]);
+  const double a = p[0];
+  const double ac = a * t.cph, as = a * t.sph;
+  const double tc = 2.0 * t.c1;
+  // d model / d a = 0 at a == 0 (fit.py:126-128): a select, not a branch (a branch here
+  // splits the pass in two and keeps every harmonic's temporaries live across it)
+  const double cph0 = (a != 0.0) ? t.cph : 0.0, sph0 = (a != 0.0) ? t.sph : 0.0;
+  double a00 = 0.0, a01 = 0.0, a02 = 0.0, a11 = 0.0, a12 = 0.0, a22 = 0.0, a33 = 0.0;
+  double g0 = 0.0, g1 = 0.0, g2 = 0.0, g3 = 0.0;
+  double cj = t.c1, sj = t.s1, cm = 1.0, sm = 0.0;
+#pragma unroll
+  for (int j = 1; j <= NDMAX; ++j) {
+    const double Jj = t.J[j] * hmask<V>(nd, j);  // 0 above ndata: every term below vanishes
+    const double aP = quarter_turn(j, ac, as), aD = quarter_turn(j + 1, ac, as);
+    const double c = aP * Jj;
+    const double u0 = quarter_turn(j, cph0, sph0) * Jj;
+    const double u1 = aP * (0.5 * (t.J[j - 1] - t.J[j + 1])) * hmask<V>(nd, j);
+    const double u2 = aD * Jj;
+    const double rq = fma(-c, cj, Q[j - 1]);
+    const double ri = fma(c, sj, I[j - 1]);
+    const double A = fma(cj, rq, -(sj * ri));
+    const double B = fma(sj, rq, cj * ri);
+    const double w = fma(cj, cj, sj * sj);
+    const double v0 = u0 * w, v1 = u1 * w, v2 = u2 * w;
+    a00 = fma(v0, u0, a00);
+    a01 = fma(v0, u1, a01);
+    a02 = fma(v0, u2, a02);
+    a11 = fma(v1, u1, a11);
+    a12 = fma(v1, u2, a12);
+    a22 = fma(v2, u2, a22);
+    const double jc = (double)j * c;
+    a33 = fma(jc * w, jc, a33);
+    g0 = fma(u0, A, g0);
+    g1 = fma(u1, A, g1);
+    g2 = fma(u2, A, g2);
+    g3 = fma(-jc, B, g3);
+    const double cn = fma(tc, cj, -cm), sn = fma(tc, sj, -sm);
+    cm = cj;
+    sm = sj;
+    cj = cn;
+    sj = sn;
+    DFMI_HARMONIC_FENCE();
+  }
+  e = Eval{t.ssq, a00, a01, a02, 0.0, a11, a12, 0.0, a22, 0.0, a33, g0, g1, g2, g3};
+}
+
+// 1/d to within an ulp or two: v_rcp_f64 + two Newton steps on the device (the
+// IEEE division sequence costs ~3x the instructions); exact division on the host.
+DFMI_HDI double rcp_nr(double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(r, fma(-d, r, 1.0), r);
+  r = fma(r, fma(-d, r, 1.0), r);
+  return r;
+#else
+  return 1.0 / d;
+#endif
+}
+
+// msolve (fit.py:169-206) for the register path's block-diagonal J^T J: the (a, m, phi)
+// block by LDL^T (symmetric positive semi-definite: no pivoting needed), psi by one
+// division. numpy raises LinAlgError -> dp = 0 when dgesv meets an exactly-zero
+// pivot; the block form meets an exactly-zero pivot in the same structural cases
+// (a = 0 or m = 0: whole rows of J^T J vanish), tested by the edge vectors of
+// tests/golden/lm_vectors.npz.
+DFMI_HDI void damped_solve_block(const Eval& e, double lam, double (&dp)[4]) {
+  const double d0 = fma(lam, e.a00, e.a00);
+  const double A11 = fma(lam, e.a11, e.a11), A22 = fma(lam, e.a22, e.a22), A33 = fma(lam, e.a33, e.a33);
+  const double r0 = rcp_nr(d0);
+  const double l10 = e.a01 * r0, l20 = e.a02 * r0;
+  const double d1 = fma(-l10, e.a01, A11);
+  const double r1 = rcp_nr(d1);
+  const double t21 = fma(-l20, e.a01, e.a12);
+  const double l21 = t21 * r1;
+  const double d2 = fma(-l21, t21, fma(-l20, e.a02, A22));
+  const double r2 = rcp_nr(d2);
+  const double y1 = fma(-l10, e.g0, e.g1);
+  const double y2 = fma(-l21, y1, fma(-l20, e.g0, e.g2));
+  const double x2 = y2 * r2;
+  const double x1 = fma(-l21, x2, y1 * r1);
+  const double x0 = fma(-l20, x2, fma(-l10, x1, e.g0 * r0));
+  const double x3 = e.g3 * rcp_nr(A33);
+  const bool singular = (d0 == 0.0) || (d1 == 0.0) || (d2 == 0.0) || (A33 == 0.0);
+  dp[0] = singular ? 0.0 : x0;
+  dp[1] = singular ? 0.0 : x1;
+  dp[2] = singular ? 0.0 : x2;
+  dp[3] = singular ? 0.0 : x3;
 }
 
 // ---------------------------------------------------------------------------
@@ -412,7 +526,11 @@ DFMI_HDI void damped_solve(const Eval& e, double lam, double (&dp)[4]) {
   if (singular) dp[0] = dp[1] = dp[2] = dp[3] = 0.0;
 }
 
-DFMI_HDI double norm4(double a, double b, double c, double d) { return sqrt(a * a + b * b + c * c + d * d); }
+DFMI_HDI double sumsq4(double a, double b, double c, double d) { return fma(a, a, fma(b, b, fma(c, c, d * d))); }
+
+// np.linalg.norm(v) < thr without the square root (thr <= 0: never; the squares
+// compare the same numbers up to rounding at the boundary).
+DFMI_HDI bool norm_below(double ss, double thr) { return thr > 0.0 && ss < thr * thr; }
 
 // fit.py:208-258 (_run_lma_fit), flattened for SIMT: every pass of the loop does
 // ONE damped solve and (unless the step is below min_step_norm) ONE trial
@@ -420,7 +538,9 @@ DFMI_HDI double norm4(double a, double b, double c, double d) { return sqrt(a * 
 // The nested form (iterations x ladder) made a wave execute the union of its lanes'
 // ladders at every iteration; here a wave runs max over lanes of the trial count.
 // Per lane the sequence of solves, trials and acceptances is exactly the nested
-// loop's (same arithmetic, same bits).
+// loop's (lm_descend below: same arithmetic, same bits).
+// Ev: trial(p, t) -> ssqf at p; accept(p, t, e) -> coeffs at p from the trial's
+// state; solve(e, lambda, dp) -> msolve.
 template <typename Ev>
 DFMI_HDI double lm_descend_flat(Ev&& ev, double (&p)[4], const LMConst& c) {
   Eval e;
@@ -433,15 +553,15 @@ DFMI_HDI double lm_descend_flat(Ev&& ev, double (&p)[4], const LMConst& c) {
   bool active = c.max_steps > 0 && c.n_lambda > 0;
   while (active) {
     double dp[4];
-    damped_solve(e, c.lambdas[li], dp);
+    ev.solve(e, c.lambdas[li], dp);
     bool accepted = false;
-    if (!(norm4(dp[0], dp[1], dp[2], dp[3]) < c.min_step_norm)) {
+    if (!norm_below(sumsq4(dp[0], dp[1], dp[2], dp[3]), c.min_step_norm)) {
       double pt[4] = {p[0] + dp[0], p[1] + dp[1], p[2] + dp[2], p[3] + dp[3]};
       typename std::decay_t<Ev>::Trial tt;
       const double ssq_try = ev.trial(pt, tt);
       if (ssq_try < e.ssq) {
         accepted = true;
-        const double change = norm4(pt[0] - p[0], pt[1] - p[1], pt[2] - p[2], pt[3] - p[3]);
+        const double change2 = sumsq4(pt[0] - p[0], pt[1] - p[1], pt[2] - p[2], pt[3] - p[3]);
         p[0] = pt[0];
         p[1] = pt[1];
         p[2] = pt[2];
@@ -450,7 +570,8 @@ DFMI_HDI double lm_descend_flat(Ev&& ev, double (&p)[4], const LMConst& c) {
         ev.accept(p, tt, e);  // coeffs(ndata, data, parm) at the accepted point (fit.py:251)
         ++it;
         li = 0;
-        if (((e.ssq - best_ssq) < c.conv_improve && change < c.conv_param_change) || it >= c.max_steps)
+        if (((e.ssq - best_ssq) < c.conv_improve && norm_below(change2, c.conv_param_change)) ||
+            it >= c.max_steps)
           active = false;
       }
     }
@@ -459,8 +580,9 @@ DFMI_HDI double lm_descend_flat(Ev&& ev, double (&p)[4], const LMConst& c) {
   return e.ssq;
 }
 
-// Evaluators for lm_descend_flat: a full evaluation per trial (general path) or
-// the split register-path one.
+// Evaluators for the descents: a full literal evaluation per trial + the pivoting
+// 4x4 solve (general path), or the structured register path (trial = ssqf only, the
+// Jacobian added on acceptance, block-diagonal solve).
 template <typename EvalFn>
 struct FullEval {
   EvalFn f;
@@ -472,41 +594,46 @@ struct FullEval {
     return t.e.ssq;
   }
   DFMI_HDI void accept(const double (&)[4], const Trial& t, Eval& e) { e = t.e; }
+  DFMI_HDI void solve(const Eval& e, double lam, double (&dp)[4]) { damped_solve(e, lam, dp); }
 };
 
 template <int NDMAX, typename QF>
-struct SplitEval {
+struct SplitEval {  // NDMAX: a register-path variant tag (nd_cap / nd_exact)
   const QF& q;
   int nd;
   using Trial = TrialReg<NDMAX>;
   DFMI_HDI double trial(const double (&p)[4], Trial& t) { return eval_reg_trial<NDMAX>(q, nd, p, t); }
-  DFMI_HDI void accept(const double (&p)[4], const Trial& t, Eval& e) {
-    eval_reg_accept<NDMAX>(q, nd, p, t, e);
-    e.ssq = t.ssq;
-  }
+  DFMI_HDI void accept(const double (&p)[4], const Trial& t, Eval& e) { eval_reg_accept<NDMAX>(q, nd, p, t, e); }
+  DFMI_HDI void solve(const Eval& e, double lam, double (&dp)[4]) { damped_solve_block(e, lam, dp); }
 };
 
-// fit.py:208-258 (_run_lma_fit), nested form (one lane at a time: host build, seed).
-// p in/out; returns ssq0 at the final p.
-template <typename EvalFn>
-DFMI_HDI double lm_descend(EvalFn&& evalf, double (&p)[4], const LMConst& c) {
+// fit.py:208-258 (_run_lma_fit), nested form (one lane at a time: the host build's
+// check that the flattened descent takes the same path). p in/out; returns ssq0 at
+// the final p.
+template <typename Ev>
+DFMI_HDI double lm_descend(Ev&& ev, double (&p)[4], const LMConst& c) {
   Eval e;
-  evalf(p, e);
+  {
+    typename std::decay_t<Ev>::Trial t0;
+    ev.trial(p, t0);
+    ev.accept(p, t0, e);
+  }
   for (int it = 0; it < c.max_steps; ++it) {
     const double po0 = p[0], po1 = p[1], po2 = p[2], po3 = p[3];
     bool found = false;
     double pt[4];
-    Eval et;
+    typename std::decay_t<Ev>::Trial tt;
+    double ssq_try = 0.0;
     for (int li = 0; li < c.n_lambda; ++li) {
       double dp[4];
-      damped_solve(e, c.lambdas[li], dp);
-      if (norm4(dp[0], dp[1], dp[2], dp[3]) < c.min_step_norm) continue;
+      ev.solve(e, c.lambdas[li], dp);
+      if (norm_below(sumsq4(dp[0], dp[1], dp[2], dp[3]), c.min_step_norm)) continue;
       pt[0] = p[0] + dp[0];
       pt[1] = p[1] + dp[1];
       pt[2] = p[2] + dp[2];
       pt[3] = p[3] + dp[3];
-      evalf(pt, et);
-      if (et.ssq < e.ssq) {
+      ssq_try = ev.trial(pt, tt);
+      if (ssq_try < e.ssq) {
         found = true;
         break;
       }
@@ -516,10 +643,10 @@ DFMI_HDI double lm_descend(EvalFn&& evalf, double (&p)[4], const LMConst& c) {
     p[1] = pt[1];
     p[2] = pt[2];
     p[3] = pt[3];
-    const double best_ssq = et.ssq;
-    e = et;  // coeffs(ndata, data, parm) at the accepted point (fit.py:251)
-    const double change = norm4(p[0] - po0, p[1] - po1, p[2] - po2, p[3] - po3);
-    if ((e.ssq - best_ssq) < c.conv_improve && change < c.conv_param_change) break;
+    const double best_ssq = ssq_try;
+    ev.accept(p, tt, e);  // coeffs(ndata, data, parm) at the accepted point (fit.py:251)
+    const double change2 = sumsq4(p[0] - po0, p[1] - po1, p[2] - po2, p[3] - po3);
+    if ((e.ssq - best_ssq) < c.conv_improve && norm_below(change2, c.conv_param_change)) break;
   }
   return e.ssq;
 }
@@ -599,14 +726,15 @@ DFMI_HDI void m_grid_seed(QF&& Q, int ndata, const double* __restrict__ jtab, co
 }
 
 // fit.py:322-361 (fit): LM, status + grid retry, normalisation, phi wrap.
-// Ev: an evaluator for the flattened descent (FullEval / SplitEval); evalf: the full
-// evaluation for the nested one (FLAT = false: host build / equivalence tests).
-template <bool FLAT = true, typename Ev, typename EvalFn, typename QF>
-DFMI_HDI int fit_segment_t(Ev&& ev, EvalFn&& evalf, QF&& Q, int ndata, const double* __restrict__ jtab,
-                           const LMConst& c, double (&p)[4], double& ssq_out) {
+// Ev: the evaluator (FullEval / SplitEval); FLAT = false runs the nested descent
+// (host build / equivalence tests). Q: QI accessor for the m-grid re-seed (runtime
+// harmonic index: memory, never a register array).
+template <bool FLAT = true, typename Ev, typename QF>
+DFMI_HDI int fit_segment_t(Ev&& ev, QF&& Q, int ndata, const double* __restrict__ jtab, const LMConst& c,
+                           double (&p)[4], double& ssq_out) {
   auto descend = [&](double (&pp)[4]) {
     if constexpr (FLAT) return lm_descend_flat(ev, pp, c);
-    else return lm_descend(evalf, pp, c);
+    else return lm_descend(ev, pp, c);
   };
   double ssq = descend(p);
   int status;
@@ -643,18 +771,26 @@ DFMI_HDI int fit_segment_t(Ev&& ev, EvalFn&& evalf, QF&& Q, int ndata, const dou
 
 // Single-segment entry used by the kernels and by the test-only host build.
 // NDMAX > 0: register path (requires ndata <= NDMAX); NDMAX == 0: general path.
+// qe: QI accessor of the LM evaluations (compile-time harmonic index after
+// unrolling); qm: QI in memory for the m-grid re-seed (runtime harmonic index).
+template <int NDMAX, typename QE, typename QM, bool FLAT = true>
+__host__ __device__ __forceinline__ int fit_segment_q2(const QE& qe, const QM& qm, int ndata,
+                                                    const double* __restrict__ jtab, const LMConst& c,
+                                                    double (&p)[4], double& ssq_out) {
+  if constexpr (NDMAX > 0) {
+    SplitEval<NDMAX, QE> ev{qe, ndata};
+    return fit_segment_t<FLAT>(ev, qm, ndata, jtab, c, p, ssq_out);
+  } else {
+    auto evalf = [&](const double (&pp)[4], Eval& e) { eval_gen(qe, ndata, pp, e); };
+    FullEval<decltype(evalf)> ev{evalf};
+    return fit_segment_t<FLAT>(ev, qm, ndata, jtab, c, p, ssq_out);
+  }
+}
+
 template <int NDMAX, typename QF, bool FLAT = true>
 __host__ __device__ __forceinline__ int fit_segment_q(const QF& q, int ndata, const double* __restrict__ jtab,
                                                    const LMConst& c, double (&p)[4], double& ssq_out) {
-  if constexpr (NDMAX > 0) {
-    auto evalf = [&](const double (&pp)[4], Eval& e) { eval_reg<NDMAX>(q, ndata, pp, e); };
-    SplitEval<NDMAX, QF> ev{q, ndata};
-    return fit_segment_t<FLAT>(ev, evalf, q, ndata, jtab, c, p, ssq_out);
-  } else {
-    auto evalf = [&](const double (&pp)[4], Eval& e) { eval_gen(q, ndata, pp, e); };
-    FullEval<decltype(evalf)> ev{evalf};
-    return fit_segment_t<FLAT>(ev, evalf, q, ndata, jtab, c, p, ssq_out);
-  }
+  return fit_segment_q2<NDMAX, QF, QF, FLAT>(q, q, ndata, jtab, c, p, ssq_out);
 }
 
 // Component-major QI (qi[c·ld + s], qptr = qi + s). QI is re-read per evaluation
@@ -755,7 +891,7 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
     int st;
     double dcv;
     if constexpr (STAGE) {
-      const QRow<65> q{lds_q + threadIdx.x};
+      const QRow<65> q{lds_q + threadIdx.x};  // QI read from LDS at every evaluation
       st = fit_segment_q<NDMAX>(q, ndata, jtab, c, p, ssq);
       dcv = q.at(dfmi_row_dc(ndata));
     } else {
@@ -770,7 +906,8 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
   } else {
     auto one = [&](int64_t sidx) {
       double ssq;
-      const int st = fit_segment<NDMAX>(qi + sidx, qi_ld, ndata, jtab, c, p, ssq);
+      int st;
+      st = fit_segment<NDMAX>(qi + sidx, qi_ld, ndata, jtab, c, p, ssq);
       put(sidx, st, ssq);
     };
     if constexpr (!CHAIN) {

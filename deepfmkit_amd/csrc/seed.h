@@ -14,6 +14,14 @@
 
 namespace dfmi {
 
+// The seed fit runs the GENERAL LM path (literal coeffs + pivoting msolve, two-pass
+// Bessel walk: no stored Bessel / trig state) in every seed kernel: in the fused
+// kernel the seed shares the bulk demodulation's 168-VGPR budget (3 waves per SIMD),
+// which the register path's trial state would exceed; one lane's fit beside a
+// ~0.5 ms demodulation costs no wall time either way. Same path in every variant,
+// so the seed (and with it every chunk's start) does not depend on the scheduling.
+constexpr int kSeedPath = 0;
+
 template <int NDMAX>
 __global__ __launch_bounds__(64) void seed_kernel(const double* __restrict__ x, int64_t rec_stride, int R, int L,
                                                   int ndata, double w0, const double* __restrict__ tab,
@@ -43,7 +51,7 @@ __global__ __launch_bounds__(64) void seed_kernel(const double* __restrict__ x, 
     for (int i = 0; i < 4; ++i) p[i] = guess[r * 4 + i];
   }
   double ssq;
-  const int st = fit_segment<NDMAX>(qis + r, nrec, ndata, jtab, c, p, ssq);
+  const int st = fit_segment<kSeedPath>(qis + r, nrec, ndata, jtab, c, p, ssq);
   const int64_t sidx = r * nbuf;
   out[0 * out_ld + sidx] = p[0];
   out[1 * out_ld + sidx] = p[1];
@@ -129,7 +137,7 @@ __global__ __launch_bounds__(64) void seed_bins_kernel(const double* __restrict_
   }
   double ssq;
   const QRow<1> q{row};
-  const int st = fit_segment_q<NDMAX>(q, ndata, jtab, c, p, ssq);
+  const int st = fit_segment_q<kSeedPath>(q, ndata, jtab, c, p, ssq);
   const int64_t sidx = r * nbuf;
   out[0 * out_ld + sidx] = p[0];
   out[1 * out_ld + sidx] = p[1];
@@ -228,7 +236,7 @@ __global__ __launch_bounds__(kBlockThreads) void demod_seed_bins_kernel(
   }
   double ssq;
   const QRow<1> q{row};
-  const int st = fit_segment_q<NDMAX>(q, ndata, jtab, c, p, ssq);
+  const int st = fit_segment_q<kSeedPath>(q, ndata, jtab, c, p, ssq);
   const int64_t sidx = r * nbuf;
   out[0 * out_ld + sidx] = p[0];
   out[1 * out_ld + sidx] = p[1];

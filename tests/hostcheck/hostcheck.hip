@@ -92,6 +92,8 @@ int hc_fit_segments(const double* qi, long n, int ndata, const double* guess, co
       status_out[s] = dfmi::fit_segment_q<12, dfmi::QGlobal, false>(qg, ndata, tab.data(), c, p, ssq);
     } else if (force_general)
       status_out[s] = dfmi::fit_segment<0>(qi + s, n, ndata, tab.data(), c, p, ssq);
+    else if (ndata == 10)  // the exact-ndata variant the device dispatches for ndata = 10
+      status_out[s] = dfmi::fit_segment<dfmi::kExactNd | 10>(qi + s, n, ndata, tab.data(), c, p, ssq);
     else if (ndata <= 12)
       status_out[s] = dfmi::fit_segment<12>(qi + s, n, ndata, tab.data(), c, p, ssq);
     else if (ndata <= 16)

@@ -8,7 +8,7 @@ Tolerances (fp64), stated in SURVEY.md §8d / BASELINE.md:
 import numpy as np
 import pytest
 
-from conftest import check_lm_group, compare_fit, make_record, sha, wrapped
+from conftest import check_lm_group, compare_fit, make_record, record_tol, sha, wrapped
 
 pytestmark = pytest.mark.gpu
 
@@ -94,8 +94,11 @@ def test_records_through_fitter(manifest, records_npz, mode):
             df = StandardNLSFitter({"n": e["n"]}).fit(raw, parallel=True, n_cores=4, **kw)
         ref = ref_cols(records_npz, e["name"], mode)
         # noise-dominated records (SNR <= 0 dB) are status 2 almost everywhere; their
-        # status must match, their parameters are reported, not gated
-        compare_fit(df_cols(df), ref, tol=1e-9)
+        # status must match, their parameters are reported, not gated.
+        # Status-0 segments: 1e-9, widened only where the reference's own ssq resolution
+        # is coarser (record_tol: the SNR 0 dB record's status-0 segments, ssq ~1e-3)
+        tol = record_tol(e["ndata"], records_npz[f"{e['name']}_qi"], ref)
+        compare_fit(df_cols(df), ref, tol=tol)
 
 
 def test_facade_tau_and_time(manifest, records_npz):

@@ -20,6 +20,7 @@
 #include "dfmi_math.h"
 #include "ekf.h"
 #include "lm.h"
+#include "lm_refill.h"
 #include "seed.h"
 #include "np_sum.h"
 #include "moments.h"
@@ -278,6 +279,9 @@ struct Tuning {
   int bins_roll = 0;           // bin kernels (L <= 256): next load group issued before the current one is added
   int bins_prefetch = 4;       // bin kernels (L <= 256): next segment's first 4 (or 6; 0 = off) chunks in flight during
                                // the contraction (+1.4 % on the step vs 0; 6 ties 4)
+  int lm_refill = 0;           // LM (chunk size 1): 1 = tiles with lane refill (lm_refill.h; measured slower, off), 0 = one segment per lane
+  int lm_waves_per_simd = 1;   // lm_refill: resident tiles per SIMD the grid is sized for (tile = items / waves)
+  int lm_tile_min = 64;        // lm_refill: smallest tile (segments per wave)
 };
 Tuning g_tune;
 thread_local std::string g_last_demod;  // kernel variant of the last demodulation launch (dfmi_last_demod_kernel)
@@ -500,6 +504,26 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
   // ndata == 10 (the reference default): the exact-ndata register variant (no masking)
   constexpr int kNd10 = dfmi::kExactNd | 10;
   if (nd_sel == 10) kern = chain ? dfmi::lm_chunks_kernel<kNd10, true> : dfmi::lm_chunks_kernel<kNd10, false>;
+  if (!chain && g_tune.lm_refill && nd_sel <= 16 && guess_dev) {
+    // tiles of up to kRefillTmax segments, one wave each, lanes refilled from the tile
+    const int64_t total = nrec * nitems;
+    const int64_t waves = (int64_t)t_ds->n_cu * 4 * (g_tune.lm_waves_per_simd > 0 ? g_tune.lm_waves_per_simd : 1);
+    int64_t tile = (total + waves - 1) / waves;
+    if (tile < g_tune.lm_tile_min) tile = g_tune.lm_tile_min;
+    if (tile > dfmi::kRefillTmax) tile = dfmi::kRefillTmax;
+    const int64_t ntile = (total + tile - 1) / tile;
+    const size_t rl = dfmi::lm_refill_lds(rows ? (int)qi_ld : dfmi_row_stride(ndata), (int)tile);
+    const bool w2 = g_tune.lm_waves_per_simd >= 2;
+    auto rk = rows ? (nd_sel == 10 ? (w2 ? dfmi::lm_refill_kernel<kNd10, true, 2> : dfmi::lm_refill_kernel<kNd10, true>)
+                      : nd_sel <= 12 ? dfmi::lm_refill_kernel<12, true> : dfmi::lm_refill_kernel<16, true>)
+                   : (nd_sel == 10 ? (w2 ? dfmi::lm_refill_kernel<kNd10, false, 2> : dfmi::lm_refill_kernel<kNd10, false>)
+                      : nd_sel <= 12 ? dfmi::lm_refill_kernel<12, false> : dfmi::lm_refill_kernel<16, false>);
+    hipLaunchKernelGGL(rk, dim3((unsigned)ntile), dim3(64), rl, st, qi, qi_ld, ndata, nrec, nbuf, first, nitems,
+                       (int)tile, guess_dev, g_rec, g_comp, jtab, c, out, out_ld, status,
+                       (unsigned long long*)g_probe);
+    HIPCHK(hipGetLastError());
+    return DFMI_OK;
+  }
   if (rows) {
     kern = nd_sel == 10   ? dfmi::lm_chunks_kernel<kNd10, false, true>
            : nd_sel <= 12 ? dfmi::lm_chunks_kernel<12, false, true>
@@ -719,7 +743,10 @@ const std::map<std::string, Knob>& knobs() {
       {"wdfmi_accel", {&g_tune.wdfmi_accel, {0, 1, 2, 3}}},
       {"bins_loads", {&g_tune.bins_loads, {8, 16}}},
       {"bins_roll", {&g_tune.bins_roll, {0, 1}}},
-      {"bins_prefetch", {&g_tune.bins_prefetch, {0, 4, 6}}}};
+      {"bins_prefetch", {&g_tune.bins_prefetch, {0, 4, 6}}},
+      {"lm_refill", {&g_tune.lm_refill, {0, 1}}},
+      {"lm_waves_per_simd", {&g_tune.lm_waves_per_simd, {1, 2, 3, 4}}},
+      {"lm_tile_min", {&g_tune.lm_tile_min, {16, 32, 48, 64, 96, 128}}}};
   return k;
 }
 // np.mean / np.var of nrec device records on st (moments.hip), numpy-exact.

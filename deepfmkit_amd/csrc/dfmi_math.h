@@ -172,9 +172,28 @@ DFMI_HD void dfmi_bessel_table(double x, int N, double* out) {
   }
 }
 
+// fmod(a, b) for b > 0 and |a| < 2^40 b, exactly (fmod's result is always representable,
+// so one fma with the right integer quotient k gives it with no rounding): k from
+// a * (1/b), whose relative error cannot move trunc by more than one, then corrected by
+// the sign / range of the remainder. The library fmod is an iterative (bitwise) loop on
+// the device.
+DFMI_HD double dfmi_fmod_pos(double a, double b) {
+  double k = trunc(a * (1.0 / b));
+  double r = fma(-k, b, a);
+  if (a >= 0.0) {
+    if (r < 0.0) k -= 1.0;
+    else if (r >= b) k += 1.0;
+  } else {
+    if (r > 0.0) k += 1.0;
+    else if (r <= -b) k -= 1.0;
+  }
+  r = fma(-k, b, a);
+  return r == 0.0 ? copysign(0.0, a) : r;
+}
+
 // numpy float64 modulo (npy_divmod): result has the sign of the divisor.
 DFMI_HD double dfmi_pymod(double a, double b) {
-  double mod = fmod(a, b);
+  double mod = (b > 0.0 && fabs(a) < 1.0995116277760000e12 * b) ? dfmi_fmod_pos(a, b) : fmod(a, b);
   if (mod != 0.0) {
     if ((b < 0.0) != (mod < 0.0)) mod += b;
   } else {

@@ -339,6 +339,72 @@ DFMI_HDI void eval_reg_accept(const QF& q, int nd, const double (&p)[4], const T
   e = Eval{t.ssq, a00, a01, a02, 0.0, a11, a12, 0.0, a22, 0.0, a33, g0, g1, g2, g3};
 }
 
+// ssqf AND coeffs at p in one pass (fit.py:152-167 + fit.py:68-150): eval_reg_trial's
+// residual sum followed by eval_reg_accept's closed-form J^T J / J^T r, fused into one
+// unrolled loop over the harmonics. Same expressions, same bits as the two-pass form
+// (c = aP J_j and the residuals are formed identically; the mask is 0 or 1).
+// Used by the refill kernel (lm_refill.h), where lanes sit at different points of
+// their descents: a pass that always forms the Jacobian costs one evaluation, while
+// the split form costs a trial plus, whenever ANY lane of the wave accepts, an accept.
+template <int V, typename QF>
+DFMI_HDI void eval_reg_full(const QF& q, int nd, const double (&p)[4], Eval& e) {
+  constexpr int NDMAX = nd_cap(V);
+  double Q[NDMAX], I[NDMAX];
+#pragma unroll
+  for (int j = 1; j <= NDMAX; ++j) qi_pair<V>(q, nd, j, Q[j - 1], I[j - 1]);
+  double sph, cph, s1, c1;
+  dfmi_sincos(p[2], &sph, &cph);
+  dfmi_sincos(p[3], &s1, &c1);
+  double J[NDMAX + 2];
+  bessel_regs<NDMAX + 2>(p[1], nd_exact(V) ? NDMAX + 1 : nd + 1, J);
+  const double a = p[0];
+  const double ac = a * cph, as = a * sph;
+  const double tc = 2.0 * c1;
+  const double cph0 = (a != 0.0) ? cph : 0.0, sph0 = (a != 0.0) ? sph : 0.0;
+  double so = 0.0, se = 0.0;
+  double a00 = 0.0, a01 = 0.0, a02 = 0.0, a11 = 0.0, a12 = 0.0, a22 = 0.0, a33 = 0.0;
+  double g0 = 0.0, g1 = 0.0, g2 = 0.0, g3 = 0.0;
+  double cj = c1, sj = s1, cm = 1.0, sm = 0.0;
+#pragma unroll
+  for (int j = 1; j <= NDMAX; ++j) {
+    const double mk = hmask<V>(nd, j);
+    const double Jj = J[j] * mk;
+    const double aP = quarter_turn(j, ac, as), aD = quarter_turn(j + 1, ac, as);
+    const double c = aP * Jj;
+    const double rq = fma(-c, cj, Q[j - 1]);
+    const double ri = fma(c, sj, I[j - 1]);
+    double& acc = (j & 1) ? so : se;
+    acc = fma(rq, rq, acc);
+    acc = fma(ri, ri, acc);
+    const double u0 = quarter_turn(j, cph0, sph0) * Jj;
+    const double u1 = aP * (0.5 * (J[j - 1] - J[j + 1])) * mk;
+    const double u2 = aD * Jj;
+    const double A = fma(cj, rq, -(sj * ri));
+    const double B = fma(sj, rq, cj * ri);
+    const double w = fma(cj, cj, sj * sj);
+    const double v0 = u0 * w, v1 = u1 * w, v2 = u2 * w;
+    a00 = fma(v0, u0, a00);
+    a01 = fma(v0, u1, a01);
+    a02 = fma(v0, u2, a02);
+    a11 = fma(v1, u1, a11);
+    a12 = fma(v1, u2, a12);
+    a22 = fma(v2, u2, a22);
+    const double jc = (double)j * c;
+    a33 = fma(jc * w, jc, a33);
+    g0 = fma(u0, A, g0);
+    g1 = fma(u1, A, g1);
+    g2 = fma(u2, A, g2);
+    g3 = fma(-jc, B, g3);
+    const double cn = fma(tc, cj, -cm), sn = fma(tc, sj, -sm);
+    cm = cj;
+    sm = sj;
+    cj = cn;
+    sj = sn;
+    DFMI_HARMONIC_FENCE();
+  }
+  e = Eval{so + se, a00, a01, a02, 0.0, a11, a12, 0.0, a22, 0.0, a33, g0, g1, g2, g3};
+}
+
 // 1/d to within an ulp or two: v_rcp_f64 + two Newton steps on the device (the
 // IEEE division sequence costs ~3x the instructions); exact division on the host.
 DFMI_HDI double rcp_nr(double d) {

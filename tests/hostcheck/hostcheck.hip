@@ -44,6 +44,11 @@ void hc_synth_trial(const dfmi_synth_trial* p, int64_t n, double f_samp, double*
 
 void hc_bessel_table(double x, int N, double* out) { dfmi_bessel_table(x, N, out); }
 
+// dfmi_pymod (numpy / Python float modulo, the phi wrap of fit.py:357) elementwise
+void hc_pymod(const double* a, int64_t n, double b, double* out) {
+  for (int64_t k = 0; k < n; ++k) out[k] = dfmi_pymod(a[k], b);
+}
+
 // the LM register path's single Miller pass (lm.h bessel_regs): NB = 14 (ndata <= 12)
 // or 18 (ndata <= 16), J_0..J_{NB-1}
 void hc_bessel_regs(double x, int nb, double* out) {

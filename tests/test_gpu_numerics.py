@@ -113,3 +113,60 @@ def test_record_on_non_current_device():
     other, _ = nls_records(x.to("cuda:1"), 200000.0, 1000.0, R, nseg, 10)
     assert other.device.index == 1
     np.testing.assert_array_equal(other.cpu().numpy(), ref.cpu().numpy())
+
+
+@pytest.fixture
+def restore_lm_tuning():
+    from deepfmkit_amd import _lib
+    lib = _lib.load()
+    yield lib
+    for k, v in ((b"lm_refill", 0), (b"lm_waves_per_simd", 1), (b"lm_tile_min", 64)):
+        _lib.check(lib.dfmi_set_tuning(k, v), "dfmi_set_tuning")
+
+
+@pytest.mark.parametrize("nrec", [1, 3])
+def test_lm_refill_bit_identical(restore_lm_tuning, nrec):
+    """The lane-refill LM (csrc/lm_refill.h; tiles of segments per wave, a lane takes the
+    tile's next segment when its fit ends) runs every lane through the same solves, trials
+    and acceptances as the one-segment-per-lane kernel: same bits, for the record
+    pipeline's row layout (incl. tiles that span records, the seeds' dc carry, noisy
+    segments that take the m-grid retry) and for dfmi_lm's component-major input."""
+    import torch
+    from deepfmkit_amd import _lib
+    from deepfmkit_amd import fit as F
+    from deepfmkit_amd.fitters import nls_records
+    lib = restore_lm_tuning
+    nbuf, R, nd = 3001, 4000, 10
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    t = torch.arange(R, dtype=torch.float64, device="cuda") / 200000.0
+    recs = []
+    for r in range(nrec):
+        clean = 1.0 + torch.cos(0.3 * r + (6.0 + r) * torch.cos(2 * np.pi * 1000.0 * t))
+        noise = torch.randn(nbuf * R, dtype=torch.float64, device="cuda", generator=g)
+        sig = clean.repeat(nbuf) + 0.01 * noise
+        sig[7 * R: 9 * R] = 0.8 * noise[7 * R: 9 * R]  # two noise-only buffers: status 1/2 + m-grid retry
+        recs.append(sig)
+    x = torch.stack(recs).contiguous()
+    res = {}
+    for setting in ((0, 1, 64), (1, 1, 64), (1, 2, 64), (1, 1, 16)):
+        for k, v in zip((b"lm_refill", b"lm_waves_per_simd", b"lm_tile_min"), setting):
+            _lib.check(lib.dfmi_set_tuning(k, v), "dfmi_set_tuning")
+        cols, ok = nls_records(x, 200000.0, 1000.0, R, nbuf, nd)
+        qi = torch.empty((2 * nd, nbuf), dtype=torch.float64, device="cuda")
+        dc = torch.empty(nbuf, dtype=torch.float64, device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+        _lib.check(lib.dfmi_demod(x.data_ptr(), nbuf, R, R, nd, 2 * np.pi * 1000.0 / 200000.0, 0, qi.data_ptr(),
+                                  dc.data_ptr(), _lib.DFMI_MEM_DEVICE, st), "dfmi_demod")
+        gd = torch.tensor([1.0, 6.0, 0.0, 0.0], dtype=torch.float64, device="cuda")
+        p = torch.empty((4, nbuf), dtype=torch.float64, device="cuda")
+        ssq = torch.empty(nbuf, dtype=torch.float64, device="cuda")
+        stt = torch.empty(nbuf, dtype=torch.int32, device="cuda")
+        _lib.check(lib.dfmi_lm(qi.data_ptr(), nbuf, nd, gd.data_ptr(), 0, nbuf, F.lm_config(), p.data_ptr(),
+                               ssq.data_ptr(), stt.data_ptr(), _lib.DFMI_MEM_DEVICE, st), "dfmi_lm")
+        res[setting] = [a.cpu().numpy() for a in (cols, ok, p, ssq, stt)]
+    base = res[(0, 1, 64)]
+    assert (base[1] != 0).any() and (base[4] != 0).any()  # the retry path ran
+    for setting, arrs in res.items():
+        for a, b in zip(arrs, base):
+            np.testing.assert_array_equal(a, b, err_msg=str(setting))

@@ -21,7 +21,27 @@ def hc():
     lib.hc_bessel_table.argtypes = [ctypes.c_double, ctypes.c_int, P]
     lib.hc_bessel_regs.argtypes = [ctypes.c_double, ctypes.c_int, P]
     lib.hc_fit_segments.argtypes = [P, ctypes.c_long, ctypes.c_int, P, P, P, ctypes.c_int, P, P, P, ctypes.c_int]
+    lib.hc_pymod.argtypes = [P, ctypes.c_int64, ctypes.c_double, P]
     return lib
+
+
+def test_pymod_matches_python_float_modulo(hc):
+    """dfmi_pymod (the phi wrap (phi + pi) % (2 pi) - pi, fit.py:357) with the one-fma
+    fmod of dfmi_fmod_pos: bit for bit Python's float %, incl. exact multiples, signed
+    zeros, values just below/above multiples of 2 pi and the large-|a| library path."""
+    rng = np.random.default_rng(7)
+    two_pi = 2 * np.pi
+    k = rng.integers(-50, 50, 4000).astype(np.float64)
+    a = np.concatenate([
+        rng.uniform(-100, 100, 20000), rng.uniform(-1e6, 1e6, 5000), rng.normal(0, 1e-12, 2000),
+        k * two_pi, np.nextafter(k * two_pi, np.inf), np.nextafter(k * two_pi, -np.inf),
+        [0.0, -0.0, 1e-300, -1e-300, 1e-20, -1e-20, 3.141592653589793, -3.141592653589793, 1e15, -1e15, 1e300,
+         -1e300, np.inf, -np.inf, np.nan]])
+    out = np.empty_like(a)
+    hc.hc_pymod(a.ctypes.data, a.size, two_pi, out.ctypes.data)
+    want = np.array([float(v) % two_pi for v in a])
+    np.testing.assert_array_equal(np.signbit(out), np.signbit(want))
+    np.testing.assert_array_equal(out, want)
 
 
 def test_bessel_vs_scipy_table(hc):

@@ -7,7 +7,8 @@
 //     legacy_gauss with its cached second value, normal = 0.0 + scale * gauss;
 //   asd_noise_arrays (reference physics.py:532-613, white sources: amplitude, df;
 //     seed 1 + trial_num * 4, sources drawn in the reference's order);
-//   _run_simulation_physics (physics.py:615-722): g = cos(omega_mod t + psi) / max|g|,
+//   _run_simulation_physics (physics.py:615-722): g = waveform(omega_mod t + psi) / max|g|
+//     (cos, or the second-harmonic distortion waveform of waveforms.py:4-23),
 //     phi_mod = (2 pi / fs) * cumsum((df + n_df) * g), the exact-delay np.interp at
 //     t - (tau_m + tau_dl) and t - tau_r, phase, (amp + n_amp) * (1 + vis cos(phase)).
 // Every function rounds operation by operation (no FMA contraction, whatever the
@@ -162,9 +163,14 @@ DFMI_SY_HD double interp_grid(double x, const Arr& f, int64_t n, double f_samp) 
 DFMI_SY_HD double synth_gmax_step(double m, double g) { return (g > m || g != g || m != m) ? (m != m ? m : g) : m; }
 
 // g_t of sample k (before the max-normalisation)
+// (waveform_func(phase_axis, **waveform_kwargs), phase_axis = omega_mod t + psi:
+// the default cos, or second_harmonic_distortion's cos(tp) + d_amp cos(2 tp + d_phase))
 DFMI_SY_HD double synth_g(const dfmi_synth_trial& p, int64_t k, double f_samp) {
 #pragma clang fp contract(off)
-  return cos(p.omega_mod * ((double)k / f_samp) + p.psi);
+  const double tp = p.omega_mod * ((double)k / f_samp) + p.psi;
+  const double g1 = cos(tp);
+  if (p.waveform == 1) return g1 + p.d_amp * cos(2.0 * tp + p.d_phase);
+  return g1;
 }
 
 // df_noisy * g_normalised of sample k: the cumsum's summand

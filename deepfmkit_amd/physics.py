@@ -212,15 +212,28 @@ def exact_model_signal(cfg, t, noise, is_dynamic):
 
 SYNTH_TRIAL_DTYPE = np.dtype([("seed", "<u4"), ("dynamic", "<i4")] + [(k, "<f8") for k in (
     "omega_mod", "psi", "df", "cphi", "w_arm", "arml_mod_amp", "arml_mod_psi", "dl0", "c_light", "tau_m", "tau_r",
-    "w0c", "amp", "vis", "s_amp", "s_df")])  # include/dfmi.h dfmi_synth_trial
+    "w0c", "amp", "vis", "s_amp", "s_df")] + [("waveform", "<i4"), ("waveform_pad", "<i4"), ("d_amp", "<f8"),
+                                                 ("d_phase", "<f8")])  # include/dfmi.h dfmi_synth_trial
+
+
+def _device_waveform(laser):
+    """(code, d_amp, d_phase) of a waveform dfmi_synth_asd evaluates, or None."""
+    from . import waveforms
+    kw = dict(laser.waveform_kwargs or {})
+    if laser.waveform_func is cosine_waveform and not kw:
+        return 0, 0.0, 0.0
+    if laser.waveform_func is waveforms.second_harmonic_distortion and set(kw) <= {"distortion_amp",
+                                                                                 "distortion_phase"}:
+        return 1, float(kw.get("distortion_amp", 0.0)), float(kw.get("distortion_phase", 0.0))
+    return None
 
 
 def device_synth_supported(cfg) -> bool:
-    """dfmi_synth_asd covers the default cosine waveform with white (or zero)
-    amplitude / df noise and no frequency / arm-length noise sources."""
+    """dfmi_synth_asd covers the default cosine waveform and the second-harmonic
+    distortion waveform (waveforms.py) with white (or zero) amplitude / df noise and no
+    frequency / arm-length noise sources."""
     laser, ifo = cfg.laser, cfg.ifo
-    return (laser.waveform_func is cosine_waveform and not laser.waveform_kwargs and laser.f_n == 0.0
-            and ifo.arml_mod_n == 0.0)
+    return _device_waveform(laser) is not None and laser.f_n == 0.0 and ifo.arml_mod_n == 0.0
 
 
 def synth_trial_fields(cfg, trial_num, dynamic=True):
@@ -253,6 +266,10 @@ def synth_trial_fields(cfg, trial_num, dynamic=True):
     rec["vis"] = laser.visibility
     rec["s_amp"] = laser.amp_n * np.sqrt(fs_cfg / 2.0) if laser.amp_n != 0.0 else 0.0
     rec["s_df"] = laser.df_n * np.sqrt(fs_cfg / 2.0) if laser.df_n != 0.0 else 0.0
+    wf = _device_waveform(laser)
+    if wf is None:
+        raise ValueError("dfmi_synth_asd does not evaluate this waveform")
+    rec["waveform"], rec["d_amp"], rec["d_phase"] = wf
     return rec
 
 
@@ -278,7 +295,7 @@ def synthesize_asd_trials(cfgs, trial_nums, n_seconds, dynamic=True):
     for c in cfgs:
         la, fo = c.laser, c.ifo
         key = (la.f_mod, la.psi, la.df, la.wavelength, la.amp, la.visibility, la.amp_n, la.df_n, fo.arml_mod_f,
-               fo.arml_mod_amp, fo.arml_mod_psi, fo.phi, fo.meas_arml, fo.ref_arml)
+               fo.arml_mod_amp, fo.arml_mod_psi, fo.phi, fo.meas_arml, fo.ref_arml, _device_waveform(la))
         u = index.get(key)
         if u is None:
             u = index[key] = len(recs)

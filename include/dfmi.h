@@ -147,7 +147,8 @@ int dfmi_record_moments(const double* x, int64_t nrec, int64_t rec_stride, int64
 /* ---- Trial synthesis (input side of the batched efficiency trials) ----
  * One asd-mode channel per trial, as SignalGenerator.generate(mode='asd') makes it
  * (reference physics.py:423-473, white noise sources 532-613, exact-delay model
- * 615-722) for the default cosine waveform: numpy's legacy RandomState(seed) stream
+ * 615-722) for the default cosine waveform or the second-harmonic distortion waveform:
+ * numpy's legacy RandomState(seed) stream
  * (MT19937 + polar gauss) restated on the device. Every field is the reference's
  * scalar expression, evaluated by the caller with Python/numpy floats. */
 typedef struct dfmi_synth_trial {
@@ -169,6 +170,11 @@ typedef struct dfmi_synth_trial {
   double vis;           /* laser.visibility */
   double s_amp;         /* laser.amp_n * np.sqrt(f_samp / 2.0), 0: no draws */
   double s_df;          /* laser.df_n * np.sqrt(f_samp / 2.0), 0: no draws */
+  int32_t waveform;     /* 0: cos(tp) (the default waveform); 1: second_harmonic_distortion
+                           (waveforms.py:4-23): cos(tp) + d_amp * cos(2 * tp + d_phase) */
+  int32_t waveform_pad;
+  double d_amp;         /* waveform 1: distortion_amp */
+  double d_phase;       /* waveform 1: distortion_phase */
 } dfmi_synth_trial;
 
 /* out[r*n_samp + k] = trial r's signal sample k (t_k = k / f_samp), one lane per

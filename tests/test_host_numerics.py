@@ -159,3 +159,37 @@ def test_trial_synthesis_restatement_bit_exact(hc):
         out = np.zeros(x.size)
         hc.hc_synth_trial(rec.ctypes.data, x.size, cfg.f_samp, out.ctypes.data)
         np.testing.assert_array_equal(out, x)
+
+
+def test_trial_synthesis_second_harmonic_waveform_bit_exact(hc):
+    """The second-harmonic distortion waveform (waveforms.second_harmonic_distortion,
+    reference waveforms.py:4-23) in synth.h, host build vs the numpy generator, main and
+    witness (is_dynamic False) channels, incl. distortion_amp = 0 and kwargs omitted."""
+    import deepfmkit_amd as dfm
+    from deepfmkit_amd import physics as P
+    from deepfmkit_amd import waveforms as W
+    hc.hc_synth_trial.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p]
+    for (m, da, dp, an, tn, kw) in [(6.0, 0.05, 0.3, 1e-4, 0, True), (9.0, 0.0, 0.0, 0.0, 1, True),
+                                    (5.0, 0.2, -1.2, 2e-4, 4, True), (7.0, 0.0, 0.0, 1e-4, 2, False)]:
+        laser = dfm.LaserConfig()
+        laser.amp_n = an
+        laser.waveform_func = W.second_harmonic_distortion
+        laser.waveform_kwargs = {"distortion_amp": da, "distortion_phase": dp} if kw else {}
+        ifo = dfm.InterferometerConfig()
+        dfm.set_laser_df_for_effect(laser, ifo, m)
+        cfg = dfm.DFMIObject("main_trial", laser, ifo)
+        wit_ifo = dfm.InterferometerConfig()
+        wit_ifo.meas_arml = 0.15
+        wit = dfm.DFMIObject("witness_trial", laser, wit_ifo)
+        assert P.device_synth_supported(cfg)
+        chans = P.SignalGenerator().generate(cfg, 0.02, mode="asd", trial_num=tn, witness_config=wit)
+        for c, key, dyn in ((cfg, "main", True), (wit, "witness", False)):
+            x = np.asarray(chans[key].samples())
+            rec = P.synth_trial_fields(c, tn, dynamic=dyn)
+            assert int(rec["waveform"]) == 1
+            out = np.zeros(x.size)
+            hc.hc_synth_trial(rec.ctypes.data, x.size, c.f_samp, out.ctypes.data)
+            np.testing.assert_array_equal(out, x)
+    laser = dfm.LaserConfig()
+    laser.waveform_func = W.triangle_wave
+    assert not P.device_synth_supported(dfm.DFMIObject("x", laser, dfm.InterferometerConfig()))

@@ -838,10 +838,15 @@ int ekf_impl(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
     dr = (const double*)e;
   }
   if (sb) HIPCHK(hipMemsetAsync(dstates, 0, sb, st));
+  void* wtw = nullptr;
+  if ((rc = workspace(dev, "e_wt", (size_t)(n_samp > 0 ? n_samp : 1) * 8, &wtw))) return rc;
+  if (n_samp > 0)
+    hipLaunchKernelGGL(dfmi::ekf_phase_kernel, dim3((unsigned)((n_samp + 255) / 256)), dim3(256), 0, st,
+                       (double*)wtw, n_samp, w_m, f_samp);
   const int block = 64;
   const int64_t grid = (nrec + block - 1) / block;
   hipLaunchKernelGGL(dfmi::ekf_kernel, dim3((unsigned)grid), dim3(block), 0, st, dx, nrec, rs, n_samp, dx0, dp0, dq,
-                     dr, w_m, f_samp, (int)R, nbuf, dstates);
+                     dr, (const double*)wtw, (int)R, nbuf, dstates);
   HIPCHK(hipGetLastError());
   if (host) {
     if (sb) HIPCHK(hipMemcpyAsync(states, dstates, sb, hipMemcpyDeviceToHost, st));

@@ -226,9 +226,30 @@ DFMI_HD void dfmi_sincos_fast(double x, double* sn, double* cs) {
   *cs = (qi == 0) ? cr : (qi == 1) ? -sr : (qi == 2) ? -cr : sr;
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// The library's large-argument sincos (Payne-Hanek: table loads from global memory)
+// kept out of line: inlined, its loads make the compiler wait for every vector memory
+// operation in flight (prefetched samples included) where its branch rejoins the fast
+// path, on every call, taken or not.
+static __device__ __noinline__ double2 dfmi_sincos_lib(double x) {
+  double s, c;
+  sincos(x, &s, &c);
+  return make_double2(s, c);
+}
+#endif
+
 // sincos with the fast path where it is exact to the kernel polynomials' accuracy
 // (|x| < 2^19, every argument of these fits) and the library otherwise.
 DFMI_HD void dfmi_sincos(double x, double* sn, double* cs) {
-  if (fabs(x) < 524288.0) dfmi_sincos_fast(x, sn, cs);
-  else sincos(x, sn, cs);
+  if (fabs(x) < 524288.0) {
+    dfmi_sincos_fast(x, sn, cs);
+  } else {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double2 v = dfmi_sincos_lib(x);
+    *sn = v.x;
+    *cs = v.y;
+#else
+    sincos(x, sn, cs);
+#endif
+  }
 }

@@ -96,6 +96,18 @@ def _frame_means(df):
     return df.mean().to_dict()
 
 
+def _trial_means(cols, names, ntrial, nbuf):
+    """_frame_means of each trial's nbuf-row frame with the columns `names` (cols: one
+    (ntrial * nbuf,) array per column, trial-major). One row per trial (the Experiment
+    default: the record is one buffer of n_fit_buffers cycles): the mean of one value is
+    that value (as float), no DataFrame needed."""
+    if nbuf == 1:
+        arrs = [np.asarray(c, dtype=np.float64) for c in cols]
+        return [{k: float(a[j]) for k, a in zip(names, arrs)} for j in range(ntrial)]
+    return [_frame_means(pd.DataFrame({k: np.asarray(c)[j * nbuf:(j + 1) * nbuf] for k, c in zip(names, cols)},
+                                      columns=names)) for j in range(ntrial)]
+
+
 def _synthesize(trials):
     """Every trial's channels: the GPU generator for the trials it covers (grouped by
     record length), the host generator (physics.SignalGenerator) for the rest."""
@@ -195,30 +207,32 @@ def _fit_batched(trials: List[_Trial], analysis, num_fit_buffers):
             cols, ok = _fitters.nls_records(_stack([t.x_main for t in ts]), f_samp, f_mod, R, nbuf,
                                             int(kw.get("ndata", 10)), g, parallel=False)
             cols, ok = _host(cols), _host(ok)
+            dfs = np.repeat(np.array([trials[i].main.laser.df for i in idx], dtype=np.float64), nbuf)
+            names = _fitters.COLUMNS + ["tau"]
+            means = _trial_means([cols[0], cols[1], cols[2], cols[3], cols[4], cols[5], ok.astype(np.int64),
+                                  _tau_col(cols[1], dfs)], names, len(idx), nbuf)
             for j, i in enumerate(idx):
-                sl = slice(j * nbuf, (j + 1) * nbuf)
-                df = _fitters.frame_from(cols[:, sl], ok[sl])
-                df["tau"] = _tau_col(df["m"], trials[i].main.laser.df)
-                out[i] = _frame_means(df)
+                out[i] = means[j]
         elif method == "ekf":
             raws = [_Raw(_host(t.x_main), t.main) for t in ts]
             states = _fitters.ekf_records(raws, n, **{k: v for k, v in kw.items() if k != "parallel"})
+            st = states.reshape(-1, 5)
+            dfs = np.repeat(np.array([trials[i].main.laser.df for i in idx], dtype=np.float64), nbuf)
+            means = _trial_means([st[:, 0], st[:, 1], st[:, 2], st[:, 3], st[:, 4], np.zeros(st.shape[0]),
+                                  np.ones(st.shape[0], dtype=np.int64), _tau_col(st[:, 1], dfs)],
+                                 _fitters.COLUMNS + ["tau"], len(idx), nbuf)
             for j, i in enumerate(idx):
-                st = states[j]
-                df = pd.DataFrame({"amp": st[:, 0], "m": st[:, 1], "phi": st[:, 2], "psi": st[:, 3], "dc": st[:, 4],
-                                   "ssq": np.zeros(nbuf), "fitok": np.ones(nbuf, dtype=int)},
-                                  columns=_fitters.COLUMNS)
-                df["tau"] = _tau_col(df["m"], trials[i].main.laser.df)
-                out[i] = _frame_means(df)
+                out[i] = means[j]
         else:
             wkw = dict(zip(("df", "f_ref", "tau_init", "ndata", "init_a", "init_phi", "init_psi"), key[3:]))
             mains = _stack([t.x_main[: nbuf * R] for t in ts])
             wits = _stack([t.x_wit[:R] for t in ts])
             cols, ok = _fitters.wdfmi_records(method, mains, wits, f_samp, f_mod, R, nbuf, **wkw)
             cols, ok = _host(cols), _host(ok)
+            means = _trial_means([cols[k] for k in range(7)] + [ok.astype(np.int64)], _fitters.WDFMI_COLUMNS,
+                                 len(idx), nbuf)
             for j, i in enumerate(idx):
-                sl = slice(j * nbuf, (j + 1) * nbuf)
-                out[i] = _frame_means(_fitters.wdfmi_frame(cols[:, sl], ok[sl]))
+                out[i] = means[j]
     return out
 
 

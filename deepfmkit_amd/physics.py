@@ -273,39 +273,69 @@ def synth_trial_fields(cfg, trial_num, dynamic=True):
     return rec
 
 
+def synth_trial_table(cfgs, trial_nums, dynamic=True):
+    """dfmi_synth_trial rows for many (cfg, trial_num): synth_trial_fields' expressions
+    evaluated elementwise over the trials (numpy's vector ops round exactly as its scalar
+    ones: the same bits as the per-trial form, tests/test_host_numerics.py)."""
+    n = len(cfgs)
+    if any(not device_synth_supported(c) for c in cfgs):
+        bad = [i for i, c in enumerate(cfgs) if not device_synth_supported(c)]
+        raise ValueError(f"trials {bad[:5]} need the host generator (custom waveform or coloured noise)")
+    f_samp = float(cfgs[0].f_samp)
+    if any(float(c.f_samp) != f_samp for c in cfgs):
+        raise ValueError("synthesize_asd_trials: trials must share f_samp")
+    seeds = 1 + np.asarray(trial_nums, dtype=np.int64) * 4
+    if seeds.size and (seeds.min() < 0 or seeds.max() > 2 ** 32 - 1):
+        raise ValueError("Seed must be between 0 and 2**32 - 1")
+
+    def col(get):
+        return np.fromiter((get(c) for c in cfgs), dtype=np.float64, count=n)
+
+    f_mod, psi, df = col(lambda c: c.laser.f_mod), col(lambda c: c.laser.psi), col(lambda c: c.laser.df)
+    wl, amp, vis = col(lambda c: c.laser.wavelength), col(lambda c: c.laser.amp), col(lambda c: c.laser.visibility)
+    amp_n, df_n = col(lambda c: c.laser.amp_n), col(lambda c: c.laser.df_n)
+    arm_f, arm_a, arm_p = (col(lambda c: c.ifo.arml_mod_f), col(lambda c: c.ifo.arml_mod_amp),
+                           col(lambda c: c.ifo.arml_mod_psi))
+    phi, meas, ref = col(lambda c: c.ifo.phi), col(lambda c: c.ifo.meas_arml), col(lambda c: c.ifo.ref_arml)
+    wf = [_device_waveform(c.laser) for c in cfgs]
+    t01 = np.arange(2) / f_samp
+    fs = 1 / (t01[1] - t01[0])
+    tab = np.zeros(n, dtype=SYNTH_TRIAL_DTYPE)
+    tab["seed"], tab["dynamic"] = seeds.astype(np.uint32), 1 if dynamic else 0
+    tab["omega_mod"] = 2 * np.pi * f_mod
+    tab["psi"] = psi
+    tab["df"] = df
+    tab["cphi"] = 2 * np.pi / fs
+    tab["w_arm"] = 2 * np.pi * arm_f
+    tab["arml_mod_amp"] = arm_a
+    tab["arml_mod_psi"] = arm_p
+    tab["dl0"] = phi * wl / (2 * np.pi)
+    tab["c_light"] = sc.c
+    tab["tau_m"] = meas / sc.c
+    tab["tau_r"] = ref / sc.c
+    tab["w0c"] = 2 * np.pi * ((sc.c / wl) + 0.0)
+    tab["amp"] = amp
+    tab["vis"] = vis
+    tab["s_amp"] = np.where(amp_n != 0.0, amp_n * np.sqrt(f_samp / 2.0), 0.0)
+    tab["s_df"] = np.where(df_n != 0.0, df_n * np.sqrt(f_samp / 2.0), 0.0)
+    tab["waveform"] = [w[0] for w in wf]
+    tab["d_amp"] = [w[1] for w in wf]
+    tab["d_phase"] = [w[2] for w in wf]
+    return tab
+
+
 def synthesize_asd_trials(cfgs, trial_nums, n_seconds, dynamic=True):
-    """The main channel of SignalGenerator.generate(cfg, n_seconds, mode='asd',
-    trial_num=t) for every (cfg, t), generated on the GPU (dfmi_synth_asd) into one
-    (ntrial, N) CUDA tensor. All cfgs share f_samp; each must be
-    device_synth_supported."""
+    """The main channel (dynamic=True) or a witness channel (dynamic=False) of
+    SignalGenerator.generate(cfg, n_seconds, mode='asd', trial_num=t) for every (cfg, t),
+    generated on the GPU (dfmi_synth_asd) into one (ntrial, N) CUDA tensor. All cfgs
+    share f_samp; each must be device_synth_supported."""
     import torch
 
     from . import _lib
     from .fitters import _torch_stream
+    tab = synth_trial_table(cfgs, trial_nums, dynamic)
     f_samp = float(cfgs[0].f_samp)
-    if any(float(c.f_samp) != f_samp for c in cfgs):
-        raise ValueError("synthesize_asd_trials: trials must share f_samp")
-    bad = [i for i, c in enumerate(cfgs) if not device_synth_supported(c)]
-    if bad:
-        raise ValueError(f"trials {bad[:5]} need the host generator (custom waveform or coloured noise)")
     n = int(n_seconds * f_samp)
-    # trials of one experiment share their configuration values and differ in the
-    # seed: the scalar fields are formed once per distinct configuration
-    index, recs, which = {}, [], []
-    for c in cfgs:
-        la, fo = c.laser, c.ifo
-        key = (la.f_mod, la.psi, la.df, la.wavelength, la.amp, la.visibility, la.amp_n, la.df_n, fo.arml_mod_f,
-               fo.arml_mod_amp, fo.arml_mod_psi, fo.phi, fo.meas_arml, fo.ref_arml, _device_waveform(la))
-        u = index.get(key)
-        if u is None:
-            u = index[key] = len(recs)
-            recs.append(synth_trial_fields(c, 0, dynamic))
-        which.append(u)
-    seeds = 1 + np.asarray(trial_nums, dtype=np.int64) * 4
-    if seeds.size and (seeds.min() < 0 or seeds.max() > 2 ** 32 - 1):
-        raise ValueError("Seed must be between 0 and 2**32 - 1")
-    tab = np.stack(recs)[np.asarray(which, dtype=np.int64)]
-    tab["seed"] = seeds.astype(np.uint32)
     out = torch.empty((len(cfgs), n), dtype=torch.float64, device="cuda")
     lib = _lib.load()
     _lib.check(lib.dfmi_synth_asd(tab.ctypes.data, len(cfgs), n, f_samp, out.data_ptr(), _lib.DFMI_MEM_DEVICE,

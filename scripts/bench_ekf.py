@@ -54,6 +54,29 @@ def main():
     cpu = {"value": cpu_rate, "unit": "samples/s per channel", "cores": 1, "kind": "port",
            "sample": f"{ncpu} samples ({args.cpu_seconds} s of signal), oracle restatement of EKFFitter.fit"}
 
+    # second CPU baseline: the scalar C restatement of the same loop
+    # (oracle/csrc/ekf_scalar.c, libm sin / cos, one core) over the whole record
+    import ctypes
+    cl = ctypes.CDLL(os.path.join(ROOT, "oracle", "libekf_scalar.so"))
+    P_ = ctypes.c_void_p
+    cl.ekf_scalar.argtypes = [P_, ctypes.c_int64, P_, P_, P_, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                              ctypes.c_int64, ctypes.c_int64, P_]
+    cx0 = np.array([1.6, 6.0, 0.0, 0.0, np.mean(x1)])
+    cp0, cq = np.ones(5), np.array([1e-8, 1e-8, 1e-6, 1e-6, 1e-8])
+    cst = np.zeros((nbuf, 5))
+    t0 = time.perf_counter()
+    cl.ekf_scalar(x1.ctypes.data, ns, cx0.ctypes.data, cp0.ctypes.data, cq.ctypes.data, float(np.var(x1)),
+                  2 * np.pi * f_mod, f_samp, R, nbuf, cst.ctypes.data)
+    c_rate = ns / (time.perf_counter() - t0)
+    refc = O.ekf_record(x1[:ncpu], f_samp, f_mod, n)
+    cpart = np.zeros((ncpu // R, 5))
+    cx0p = np.array([1.6, 6.0, 0.0, 0.0, np.mean(x1[:ncpu])])
+    cl.ekf_scalar(x1.ctypes.data, ncpu, cx0p.ctypes.data, cp0.ctypes.data, cq.ctypes.data, float(np.var(x1[:ncpu])),
+                  2 * np.pi * f_mod, f_samp, R, ncpu // R, cpart.ctypes.data)
+    cpu_c = {"value": c_rate, "unit": "samples/s per channel", "cores": 1, "kind": "port",
+             "sample": f"{ns} samples, oracle/csrc/ekf_scalar.c (gcc -O2, libm), the numpy loop's operation order",
+             "max_abs_dstate_vs_oracle": float(np.max(np.abs(cpart - refc)))}
+
     lib = _lib.load()
     dev = torch.device("cuda:0")
     # parity on the oracle's own record (the prefix, with ITS mean and variance as x0[4]
@@ -90,6 +113,7 @@ def main():
         print(json.dumps({"metric": "EKF samples/s", "channels": nch, "samples_per_channel": ns, "seconds": t,
                           "per_channel_samples_per_s": ns / t, "aggregate_samples_per_s": nch * ns / t,
                           "max_abs_dstate_vs_oracle": parity, "parity_record": f"{ncpu} samples", "cpu_baseline": cpu,
+                          "cpu_baseline_c_scalar": cpu_c,
                           "data": "snr-mode m=6, 40 dB, 200 kS/s (the package's bit-exact physics.py restatement)"}),
               flush=True)
         del x

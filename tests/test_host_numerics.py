@@ -193,3 +193,33 @@ def test_trial_synthesis_second_harmonic_waveform_bit_exact(hc):
     laser = dfm.LaserConfig()
     laser.waveform_func = W.triangle_wave
     assert not P.device_synth_supported(dfm.DFMIObject("x", laser, dfm.InterferometerConfig()))
+
+
+def test_synth_trial_table_equals_per_trial_fields():
+    """physics.synth_trial_table (vectorised over trials) == synth_trial_fields per trial,
+    every field bit for bit (both waveforms, noise on/off, arm-length modulation)."""
+    import deepfmkit_amd as dfm
+    from deepfmkit_amd import physics as P
+    from deepfmkit_amd import waveforms as W
+    cfgs, nums = [], []
+    rng = np.random.default_rng(2)
+    for i in range(40):
+        laser = dfm.LaserConfig()
+        laser.amp = 1.0 + rng.normal(0, 0.1)
+        laser.psi = rng.uniform(-1, 1)
+        laser.amp_n = [0.0, 1e-4][i % 2]
+        laser.df_n = [0.0, 3e3][(i // 2) % 2]
+        if i % 3 == 0:
+            laser.waveform_func = W.second_harmonic_distortion
+            laser.waveform_kwargs = {"distortion_amp": rng.uniform(0, 0.1), "distortion_phase": rng.uniform(-1, 1)}
+        ifo = dfm.InterferometerConfig()
+        ifo.phi = rng.uniform(0, 6)
+        ifo.arml_mod_amp = [0.0, 1e-7][i % 2]
+        dfm.set_laser_df_for_effect(laser, ifo, rng.uniform(3, 12))
+        cfgs.append(dfm.DFMIObject("main_trial", laser, ifo))
+        nums.append(int(rng.integers(0, 10 ** 6)))
+    for dyn in (True, False):
+        tab = P.synth_trial_table(cfgs, nums, dyn)
+        for c, t, row in zip(cfgs, nums, tab):
+            one = P.synth_trial_fields(c, t, dyn)
+            assert one.tobytes() == row.tobytes()

@@ -170,3 +170,23 @@ def test_lm_refill_bit_identical(restore_lm_tuning, nrec):
     for setting, arrs in res.items():
         for a, b in zip(arrs, base):
             np.testing.assert_array_equal(a, b, err_msg=str(setting))
+
+
+def test_init_m_with_parallel_is_accepted():
+    """Deliberate divergence: the reference raises TypeError for init_m
+    together with parallel=True (fitters.py:366 forwards **kwargs still holding init_m
+    to _fit_parallel); here the seed's m is taken from init_m, and the result equals the
+    oracle's _fit_parallel (chunk size 1) seeded the same way."""
+    import deepfmkit_amd as dfm
+    from oracle import nls_oracle as O
+    laser, ifo = dfm.LaserConfig(), dfm.InterferometerConfig()
+    dfm.set_laser_df_for_effect(laser, ifo, 11.0)
+    dff = dfm.DeepFitFramework()
+    dff.load_sim(dfm.DFMIObject("p", laser, ifo, f_samp=200000.0))
+    dff.simulate("p", n_seconds=0.2, mode="snr", snr_db=40.0, trial_num=4)
+    raw = dff.raws["p"]
+    df = dfm.StandardNLSFitter({"n": 20}).fit(raw, parallel=True, init_m=11.0)
+    x = np.asarray(raw.samples(), dtype=np.float64)
+    ref = O.fit_record_parallel(x, 200000.0, 1000.0, 20, init_m=11.0, n_cores=9)
+    assert (df["fitok"].to_numpy() == ref[:, 6]).all()
+    assert np.abs(df["m"].to_numpy() - ref[:, 1]).max() <= 1e-9

@@ -21,6 +21,7 @@
 #include "ekf.h"
 #include "lm.h"
 #include "lm_refill.h"
+#include "lm_phase.h"
 #include "seed.h"
 #include "np_sum.h"
 #include "moments.h"
@@ -282,6 +283,10 @@ struct Tuning {
   int lm_refill = 0;           // LM (chunk size 1): 1 = tiles with lane refill (lm_refill.h; measured slower, off), 0 = one segment per lane
   int lm_waves_per_simd = 1;   // lm_refill: resident tiles per SIMD the grid is sized for (tile = items / waves)
   int lm_tile_min = 64;        // lm_refill: smallest tile (segments per wave)
+  int lm_phase = 0;            // row-layout LM: 1 = two phases with compaction (lm_phase.h; measured 3 % slower on
+                               // the step, off), 0 = one kernel
+  int lm_pa = 3;               // lm_phase: descent passes in phase A
+  int lm_pa_w2 = 1;            // lm_phase, ndata 10: phase A held to 2 waves per SIMD
 };
 Tuning g_tune;
 thread_local std::string g_last_demod;  // kernel variant of the last demodulation launch (dfmi_last_demod_kernel)
@@ -524,6 +529,31 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
     HIPCHK(hipGetLastError());
     return DFMI_OK;
   }
+  if (rows && g_tune.lm_phase && nd_sel <= 16 && guess_dev && nd_sel > 0) {
+    // two phases: <= lm_pa passes for every segment, then the compacted rest (lm_phase.h)
+    const int64_t total = nrec * nitems;
+    void *wl = nullptr, *wm = nullptr, *wc = nullptr;
+    int rc;
+    if ((rc = workspace(dev, "lm_list", (size_t)dfmi::kLmSt * total * sizeof(double), &wl))) return rc;
+    if ((rc = workspace(dev, "lm_meta", (size_t)total * sizeof(int4), &wm))) return rc;
+    if ((rc = workspace(dev, "lm_count", 64, &wc))) return rc;
+    HIPCHK(hipMemsetAsync(wc, 0, 8, st));
+    const size_t tl = (size_t)qi_ld * 65 * sizeof(double);
+    auto ka = nd_sel == 10 ? (g_tune.lm_pa_w2 ? dfmi::lm_phase_a_kernel<kNd10, 2> : dfmi::lm_phase_a_kernel<kNd10, 1>)
+              : nd_sel <= 12 ? dfmi::lm_phase_a_kernel<12> : dfmi::lm_phase_a_kernel<16>;
+    auto kb = nd_sel == 10 ? dfmi::lm_phase_b_kernel<kNd10> : nd_sel <= 12 ? dfmi::lm_phase_b_kernel<12>
+                                                                            : dfmi::lm_phase_b_kernel<16>;
+    hipLaunchKernelGGL(ka, dim3((unsigned)((total + 63) / 64)), dim3(64), tl, st, qi, qi_ld, ndata, nrec, nbuf, first,
+                       nitems, g_tune.lm_pa, guess_dev, g_rec, g_comp, jtab, c, out, out_ld, status, (double*)wl,
+                       (int4*)wm, total, (unsigned long long*)wc);
+    HIPCHK(hipGetLastError());
+    int64_t gb = (int64_t)t_ds->n_cu * 4;
+    if (gb > (total + 63) / 64) gb = (total + 63) / 64;
+    hipLaunchKernelGGL(kb, dim3((unsigned)gb), dim3(64), tl, st, qi, qi_ld, ndata, jtab, c, out, out_ld, status,
+                       (const double*)wl, (const int4*)wm, total, (const unsigned long long*)wc);
+    HIPCHK(hipGetLastError());
+    return DFMI_OK;
+  }
   if (rows) {
     kern = nd_sel == 10   ? dfmi::lm_chunks_kernel<kNd10, false, true>
            : nd_sel <= 12 ? dfmi::lm_chunks_kernel<12, false, true>
@@ -746,7 +776,10 @@ const std::map<std::string, Knob>& knobs() {
       {"bins_prefetch", {&g_tune.bins_prefetch, {0, 4, 6}}},
       {"lm_refill", {&g_tune.lm_refill, {0, 1}}},
       {"lm_waves_per_simd", {&g_tune.lm_waves_per_simd, {1, 2, 3, 4}}},
-      {"lm_tile_min", {&g_tune.lm_tile_min, {16, 32, 48, 64, 96, 128}}}};
+      {"lm_tile_min", {&g_tune.lm_tile_min, {16, 32, 48, 64, 96, 128}}},
+      {"lm_phase", {&g_tune.lm_phase, {0, 1}}},
+      {"lm_pa", {&g_tune.lm_pa, {}}},
+      {"lm_pa_w2", {&g_tune.lm_pa_w2, {0, 1}}}};
   return k;
 }
 // np.mean / np.var of nrec device records on st (moments.hip), numpy-exact.

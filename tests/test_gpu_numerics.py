@@ -120,13 +120,14 @@ def restore_lm_tuning():
     from deepfmkit_amd import _lib
     lib = _lib.load()
     yield lib
-    for k, v in ((b"lm_refill", 0), (b"lm_waves_per_simd", 1), (b"lm_tile_min", 64)):
+    for k, v in ((b"lm_refill", 0), (b"lm_waves_per_simd", 1), (b"lm_tile_min", 64), (b"lm_phase", 0),
+                 (b"lm_pa", 3)):
         _lib.check(lib.dfmi_set_tuning(k, v), "dfmi_set_tuning")
 
 
 @pytest.mark.parametrize("nrec", [1, 3])
 def test_lm_refill_bit_identical(restore_lm_tuning, nrec):
-    """The lane-refill LM (csrc/lm_refill.h; tiles of segments per wave, a lane takes the
+    """The two-phase LM (csrc/lm_phase.h) and the lane-refill LM (csrc/lm_refill.h; tiles of segments per wave, a lane takes the
     tile's next segment when its fit ends) runs every lane through the same solves, trials
     and acceptances as the one-segment-per-lane kernel: same bits, for the record
     pipeline's row layout (incl. tiles that span records, the seeds' dc carry, noisy
@@ -149,8 +150,11 @@ def test_lm_refill_bit_identical(restore_lm_tuning, nrec):
         recs.append(sig)
     x = torch.stack(recs).contiguous()
     res = {}
-    for setting in ((0, 1, 64), (1, 1, 64), (1, 2, 64), (1, 1, 16)):
-        for k, v in zip((b"lm_refill", b"lm_waves_per_simd", b"lm_tile_min"), setting):
+    # (lm_refill, lm_waves_per_simd, lm_tile_min, lm_phase, lm_pa): the one-segment-per-lane
+    # kernel, the refill tiles, and the two-phase form (lm_phase.h) with 1 and 3 passes in phase A
+    for setting in ((0, 1, 64, 0, 3), (1, 1, 64, 0, 3), (1, 2, 64, 0, 3), (1, 1, 16, 0, 3), (0, 1, 64, 1, 3),
+                    (0, 1, 64, 1, 1)):
+        for k, v in zip((b"lm_refill", b"lm_waves_per_simd", b"lm_tile_min", b"lm_phase", b"lm_pa"), setting):
             _lib.check(lib.dfmi_set_tuning(k, v), "dfmi_set_tuning")
         cols, ok = nls_records(x, 200000.0, 1000.0, R, nbuf, nd)
         qi = torch.empty((2 * nd, nbuf), dtype=torch.float64, device="cuda")
@@ -165,7 +169,7 @@ def test_lm_refill_bit_identical(restore_lm_tuning, nrec):
         _lib.check(lib.dfmi_lm(qi.data_ptr(), nbuf, nd, gd.data_ptr(), 0, nbuf, F.lm_config(), p.data_ptr(),
                                ssq.data_ptr(), stt.data_ptr(), _lib.DFMI_MEM_DEVICE, st), "dfmi_lm")
         res[setting] = [a.cpu().numpy() for a in (cols, ok, p, ssq, stt)]
-    base = res[(0, 1, 64)]
+    base = res[(0, 1, 64, 0, 3)]
     assert (base[1] != 0).any() and (base[4] != 0).any()  # the retry path ran
     for setting, arrs in res.items():
         for a, b in zip(arrs, base):

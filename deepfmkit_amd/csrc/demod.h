@@ -269,14 +269,39 @@ __device__ __forceinline__ void fold_segment(const double* __restrict__ xs, int 
   fold_finish<VEC, MAXSLOT>(y, pval, pbase, R, L, ndata, T, lane, qi, qi_ld, col, dc);
 }
 
+// Basis table (n doubles, 16-B aligned) -> LDS at kernel start, each thread's loads all
+// in flight before its first LDS write: a plain load-then-store loop waits one memory
+// round trip per iteration (~19 at ndata 10, L 200), while every workgroup of the
+// persistent grid starts at once and HBM is already saturated by the first segments.
+__device__ __forceinline__ void stage_table(const double* __restrict__ tab, double* lds, int n, int tid,
+                                            int nthreads) {
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  const d2v* __restrict__ src = reinterpret_cast<const d2v*>(tab);
+  d2v* dst = reinterpret_cast<d2v*>(lds);
+  const int n2 = n / 2;
+  for (int base = 0; base < n2; base += nthreads * 16) {
+    d2v v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int i = base + u * nthreads + tid;
+      v[u] = i < n2 ? src[i] : d2v{0.0, 0.0};
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int i = base + u * nthreads + tid;
+      if (i < n2) dst[i] = v[u];
+    }
+  }
+  if ((n & 1) && tid == 0) lds[n - 1] = tab[n - 1];
+}
+
 template <int VEC, int MAXSLOT, bool LDS_TAB, int LOADS = 8, bool NT = true>
 __global__ __launch_bounds__(kBlockThreads) void demod_fold_kernel(
     const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
     const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc) {
   extern __shared__ __attribute__((aligned(16))) double lds_tab[];
   if constexpr (LDS_TAB) {
-    const int n = 2 * ndata * L;
-    for (int i = threadIdx.x; i < n; i += kBlockThreads) lds_tab[i] = tab[i];
+    stage_table(tab, lds_tab, 2 * ndata * L, threadIdx.x, kBlockThreads);
     __syncthreads();
   }
   const double* __restrict__ T = LDS_TAB ? lds_tab : tab;
@@ -465,6 +490,8 @@ __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int
 // only idle workgroups, never segments that would wait behind it.
 // probe (diagnostics, may be null): s_memrealtime at the entry of workgroups 0 and
 // gridDim-1 and at the exit of workgroup 0's wave 0 ([3], [4], [5]).
+constexpr int kProbeWaves = 16384;  // per-wave slots of the diagnostics probe buffer
+
 template <int MAXSLOT, int LOADS, bool ROWS, bool ROLL = false, int PFN = 0>
 __device__ __forceinline__ void bins_kernel_body(
     const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
@@ -480,7 +507,7 @@ __device__ __forceinline__ void bins_kernel_body(
   if (bid < 0 || bid >= nwork) return;
   extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
   const int ntab = 2 * ndata * L;
-  for (int i = threadIdx.x; i < ntab; i += kBlockThreads) lds_dyn[i] = tab[i];
+  stage_table(tab, lds_dyn, ntab, threadIdx.x, kBlockThreads);
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -512,6 +539,17 @@ __device__ __forceinline__ void bins_kernel_body(
                                                                    lane, pval, pbase, qi, qi_ld, s, dc);
   }
   if (probe && threadIdx.x == 0 && bid == 0) probe[5] = __builtin_amdgcn_s_memrealtime();
+  // per-wave exit times (probe[16 + global wave], up to kProbeWaves waves) and the
+  // hardware XCC of the wave ([16 + kProbeWaves + wave])
+  if (probe && lane == 0) {
+    const int64_t gw = (int64_t)bid * kWavesPerBlock + wave;
+    if (gw < kProbeWaves) {
+      probe[16 + gw] = __builtin_amdgcn_s_memrealtime();
+      unsigned xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      probe[16 + kProbeWaves + gw] = (uint64_t)(xcc & 0xf);
+    }
+  }
 }
 
 template <int MAXSLOT, int LOADS, bool ROWS, bool ROLL = false, int PFN = 0>

@@ -293,6 +293,8 @@ thread_local std::string g_last_demod;  // kernel variant of the last demodulati
 thread_local int g_idle_blocks = 0;  // bin kernel: trailing workgroups that take no segments (seed_order 1)
 uint64_t* g_probe = nullptr;  // diagnostics timestamps (dfmi_set_tuning("probe", 1), dfmi_probe_read)
 
+
+
 // hipOccupancyMaxActiveBlocksPerMultiprocessor, cached per (kernel, LDS bytes): the
 // query costs host time on every call otherwise.
 template <typename K>
@@ -929,7 +931,7 @@ const char* dfmi_last_demod_kernel(void) { return g_last_demod.c_str(); }
 int dfmi_probe_read(int64_t* out, int32_t n) {
   CallScope cs;
   if (!g_probe) return fail(DFMI_ERR_ARG, "probe not enabled (dfmi_set_tuning(\"probe\", 1))");
-  if (n < 0 || n > 16 || (n && !out)) return fail(DFMI_ERR_ARG, "bad probe read");
+  if (n < 0 || n > 16 + 2 * dfmi::kProbeWaves || (n && !out)) return fail(DFMI_ERR_ARG, "bad probe read");
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(out, g_probe, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return DFMI_OK;
@@ -959,8 +961,9 @@ int dfmi_set_tuning(const char* key, int64_t value) {
       int rc = ensure_init(&dev);
       if (rc) return rc;
       void* p = nullptr;
-      if ((rc = workspace(dev, "probe", 16 * sizeof(uint64_t), &p))) return rc;
-      HIPCHK(hipMemset(p, 0, 16 * sizeof(uint64_t)));
+      const size_t pb = (16 + 2 * (size_t)dfmi::kProbeWaves) * sizeof(uint64_t);
+      if ((rc = workspace(dev, "probe", pb, &p))) return rc;
+      HIPCHK(hipMemset(p, 0, pb));
       g_probe = (uint64_t*)p;
     } else if (!value) {
       g_probe = nullptr;

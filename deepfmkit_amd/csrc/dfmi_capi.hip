@@ -287,6 +287,8 @@ struct Tuning {
                                // the step, off), 0 = one kernel
   int lm_pa = 3;               // lm_phase: descent passes in phase A
   int lm_pa_w2 = 1;            // lm_phase, ndata 10: phase A held to 2 waves per SIMD
+  int demod_spw = 2;           // bin kernels: grid sized for ~this many segments per wave (0: one persistent
+                               // wave per slot); later workgroups go to the slots that free first
 };
 Tuning g_tune;
 thread_local std::string g_last_demod;  // kernel variant of the last demodulation launch (dfmi_last_demod_kernel)
@@ -314,6 +316,24 @@ int64_t persistent_grid(int n_cu, int per_cu, int64_t need) {
   int64_t grid = (int64_t)n_cu * per_cu;
   if (grid > need) grid = need;
   if (grid < 1) grid = 1;
+  return grid;
+}
+
+// Bin-kernel grid (4-wave workgroups, grid-stride over segments): at least the resident
+// slots; with demod_spw > 0 enough workgroups for ~demod_spw segments per wave, so the
+// hardware dispatcher hands the later workgroups to the slots that free first. With one
+// persistent wave per slot and a static segment list, waves finished between 448 and
+// 548 us (XCC and HBM-path dependent, profiles/r02j_demod_wave_finish.jsonl) and the
+// launch ended with the slowest; ~2 segments per wave measured best (0.513-0.516 vs
+// 0.533-0.535 ms, profiles/r02k_tune_spw.json).
+int64_t bins_grid(int n_cu, int per_cu, int64_t nseg, int spacer) {
+  const int64_t need = (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock + spacer;
+  int64_t grid = persistent_grid(n_cu, per_cu, need);
+  if (g_tune.demod_spw > 0) {
+    const int64_t per = (int64_t)dfmi::kWavesPerBlock * g_tune.demod_spw;
+    const int64_t want = (nseg + per - 1) / per + spacer;
+    if (want > grid) grid = want;
+  }
   return grid;
 }
 
@@ -385,8 +405,7 @@ int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, i
   if (per_cu < 1) per_cu = 1;
   if (g_tune.demod_blocks_per_cu > 0 && g_tune.demod_blocks_per_cu < per_cu) per_cu = g_tune.demod_blocks_per_cu;
   const int spacer = g_idle_blocks;  // one of the grid's slots each (seed_order 1)
-  const int64_t grid =
-      persistent_grid(n_cu, per_cu, (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock + spacer);
+  const int64_t grid = bins_grid(n_cu, per_cu, nseg, spacer);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(dfmi::kBlockThreads), lds, st, x, nseg, stride, R, L, ndata,
                      tab, qi, qi_ld, dc, (int)(spacer < grid ? spacer : 0), g_probe);
   HIPCHK(hipGetLastError());
@@ -605,6 +624,10 @@ int fused_seed_demod(int dev, const double* x, int64_t nrec, int64_t nbuf, int R
   int64_t bulk = slots - nrec;
   const int64_t need = (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock;
   if (bulk > need) bulk = need;
+  if (g_tune.demod_spw > 0) {  // as bins_grid: later workgroups to the slots that free first
+    const int64_t per = (int64_t)dfmi::kWavesPerBlock * g_tune.demod_spw;
+    if ((nseg + per - 1) / per > bulk) bulk = (nseg + per - 1) / per;
+  }
   hipLaunchKernelGGL(kern, dim3((unsigned)(nrec + bulk)), dim3(dfmi::kBlockThreads), lds, st, x, nseg,
                      nbuf * (int64_t)R, nrec, R, L, ndata, tab, rows, qs, gdev, ginl, gdev ? 0 : 1, jtab, c, out,
                      out_ld, nbuf, fitok, g_probe);
@@ -781,7 +804,8 @@ const std::map<std::string, Knob>& knobs() {
       {"lm_tile_min", {&g_tune.lm_tile_min, {16, 32, 48, 64, 96, 128}}},
       {"lm_phase", {&g_tune.lm_phase, {0, 1}}},
       {"lm_pa", {&g_tune.lm_pa, {}}},
-      {"lm_pa_w2", {&g_tune.lm_pa_w2, {0, 1}}}};
+      {"lm_pa_w2", {&g_tune.lm_pa_w2, {0, 1}}},
+      {"demod_spw", {&g_tune.demod_spw, {}}}};
   return k;
 }
 // np.mean / np.var of nrec device records on st (moments.hip), numpy-exact.

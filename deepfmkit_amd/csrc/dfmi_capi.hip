@@ -287,6 +287,9 @@ struct Tuning {
                                // the step, off), 0 = one kernel
   int lm_pa = 3;               // lm_phase: descent passes in phase A
   int lm_pa_w2 = 1;            // lm_phase, ndata 10: phase A held to 2 waves per SIMD
+  int bins_ilv = 0;            // bin kernels (L <= 256): contraction of the previous segment interleaved with the
+                               // fold of the next, rows staged in LDS (demod.h bins_fold_ilv); replaces bins_prefetch.
+                               // Same bits; measured level with pf4 (0.5016 vs 0.5008 ms, r02l_ilv.log): off
   int demod_spw = 2;           // bin kernels: grid sized for ~this many segments per wave (0: one persistent
                                // wave per slot); later workgroups go to the slots that free first
 };
@@ -389,6 +392,16 @@ int launch_fold_ms(int ms, const double* x, int64_t nseg, int64_t stride, int R,
   }
 }
 
+// Interleaved bin kernel (bins_ilv): a second set of L bins per wave, within the LDS
+// budget the bin kernels keep (64 KB per workgroup).
+// With the row layout the rows are staged in LDS and written as 16-B stores (demod.h
+// flush_rows): 16-B aligned rows only.
+bool ilv_fits(int L, int ndata, size_t lds, bool rows, const double* qi, int64_t qi_ld) {
+  if (rows && ((((uintptr_t)qi) & 15) || (qi_ld & 1))) return false;
+  const size_t need = lds + (size_t)dfmi::ilv_extra_lds(L, ndata, rows);
+  return g_tune.bins_ilv && need <= 64 * 1024 && need <= t_ds->lds_per_block;
+}
+
 template <int MS, bool ROWS>
 int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tab,
                   double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu, size_t lds) {
@@ -397,7 +410,12 @@ int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, i
   if (l16) kern = dfmi::demod_bins_kernel<MS, 16, ROWS>;
   const bool roll = MS == 2 && !l16 && g_tune.bins_roll && !g_tune.demod_occ4;
   if (roll) kern = dfmi::demod_bins_kernel<MS, 8, ROWS, true>;
-  const bool pf = MS == 2 && !l16 && !roll && g_tune.bins_prefetch && !g_tune.demod_occ4;
+  const bool ilv = MS == 2 && !l16 && !roll && !g_tune.demod_occ4 && ilv_fits(L, ndata, lds, ROWS, qi, qi_ld);
+  if (ilv) {
+    kern = dfmi::demod_bins_kernel<MS, 8, ROWS, false, dfmi::kIlv>;
+    lds += (size_t)dfmi::ilv_extra_lds(L, ndata, ROWS);
+  }
+  const bool pf = MS == 2 && !l16 && !roll && !ilv && g_tune.bins_prefetch && !g_tune.demod_occ4;
   if (pf) kern = g_tune.bins_prefetch == 6 ? dfmi::demod_bins_kernel<MS, 8, ROWS, false, 6>
                                            : dfmi::demod_bins_kernel<MS, 8, ROWS, false, 4>;
   int per_cu = 0;
@@ -409,7 +427,7 @@ int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, i
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(dfmi::kBlockThreads), lds, st, x, nseg, stride, R, L, ndata,
                      tab, qi, qi_ld, dc, (int)(spacer < grid ? spacer : 0), g_probe);
   HIPCHK(hipGetLastError());
-  g_last_demod = std::string(g_tune.demod_occ4 ? "demod_bins4_kernel<" : "demod_bins_kernel<") + std::to_string(MS) + (l16 ? ",16" : ",8") + (ROWS ? ",rows" : "") + (roll ? ",roll" : "") + (pf ? (g_tune.bins_prefetch == 6 ? ",pf6" : ",pf4") : "") +
+  g_last_demod = std::string(g_tune.demod_occ4 ? "demod_bins4_kernel<" : "demod_bins_kernel<") + std::to_string(MS) + (l16 ? ",16" : ",8") + (ROWS ? ",rows" : "") + (roll ? ",roll" : "") + (ilv ? ",ilv" : "") + (pf ? (g_tune.bins_prefetch == 6 ? ",pf6" : ",pf4") : "") +
                  (spacer ? ",spacer" + std::to_string(spacer) : "") + ">";
   return DFMI_OK;
 }
@@ -602,9 +620,14 @@ int fused_seed_demod(int dev, const double* x, int64_t nrec, int64_t nbuf, int R
                      const double*, dfmi::GuessInline, int, const double*, dfmi::LMConst, double*, int64_t, int64_t,
                      int32_t*, uint64_t*);
   K kern;
+  size_t lds = ((size_t)2 * ndata * L + (size_t)dfmi::kWavesPerBlock * L) * sizeof(double);
+  const bool ilv = nslot <= 2 && ndata <= 12 && g_tune.bins_loads != 16 && !g_tune.bins_roll &&
+                   ilv_fits(L, ndata, lds, true, rows, qs);
+  if (ilv) lds += (size_t)dfmi::ilv_extra_lds(L, ndata, true);
   if (ndata <= 12)
     kern = nslot <= 2 ? (g_tune.bins_loads == 16 ? dfmi::demod_seed_bins_kernel<2, 12, 16>
                          : g_tune.bins_roll       ? dfmi::demod_seed_bins_kernel<2, 12, 8, true>
+                         : ilv                    ? dfmi::demod_seed_bins_kernel<2, 12, 8, false, dfmi::kIlv>
                          : g_tune.bins_prefetch == 6 ? dfmi::demod_seed_bins_kernel<2, 12, 8, false, 6>
                          : g_tune.bins_prefetch   ? dfmi::demod_seed_bins_kernel<2, 12, 8, false, 4>
                                                   : dfmi::demod_seed_bins_kernel<2, 12>)
@@ -613,7 +636,6 @@ int fused_seed_demod(int dev, const double* x, int64_t nrec, int64_t nbuf, int R
   else
     kern = nslot <= 2 ? dfmi::demod_seed_bins_kernel<2, 16> : nslot <= 4 ? dfmi::demod_seed_bins_kernel<4, 16>
                                                                        : dfmi::demod_seed_bins_kernel<8, 16>;
-  const size_t lds = ((size_t)2 * ndata * L + (size_t)dfmi::kWavesPerBlock * L) * sizeof(double);
   int per_cu = 0;
   if (int orc = occupancy(kern, dfmi::kBlockThreads, lds, &per_cu)) return orc;
   if (per_cu < 1) per_cu = 1;
@@ -636,7 +658,9 @@ int fused_seed_demod(int dev, const double* x, int64_t nrec, int64_t nbuf, int R
                  std::to_string(ndata <= 12 ? 12 : 16) +
                  (nslot <= 2 && ndata <= 12 && g_tune.bins_loads == 16 ? ",16" : "") +
                  (nslot <= 2 && ndata <= 12 && g_tune.bins_loads != 16 && g_tune.bins_roll ? ",roll" : "") +
-                 (nslot <= 2 && ndata <= 12 && g_tune.bins_loads != 16 && !g_tune.bins_roll && g_tune.bins_prefetch
+                 (ilv ? ",ilv" : "") +
+                 (nslot <= 2 && ndata <= 12 && g_tune.bins_loads != 16 && !g_tune.bins_roll && !ilv &&
+                          g_tune.bins_prefetch
                       ? (g_tune.bins_prefetch == 6 ? ",pf6" : ",pf4") : "") + ",rows>";
   return DFMI_OK;
 }
@@ -805,7 +829,8 @@ const std::map<std::string, Knob>& knobs() {
       {"lm_phase", {&g_tune.lm_phase, {0, 1}}},
       {"lm_pa", {&g_tune.lm_pa, {}}},
       {"lm_pa_w2", {&g_tune.lm_pa_w2, {0, 1}}},
-      {"demod_spw", {&g_tune.demod_spw, {}}}};
+      {"demod_spw", {&g_tune.demod_spw, {}}},
+      {"bins_ilv", {&g_tune.bins_ilv, {0, 1}}}};
   return k;
 }
 // np.mean / np.var of nrec device records on st (moments.hip), numpy-exact.

@@ -290,6 +290,9 @@ struct Tuning {
   int bins_ilv = 0;            // bin kernels (L <= 256): contraction of the previous segment interleaved with the
                                // fold of the next, rows staged in LDS (demod.h bins_fold_ilv); replaces bins_prefetch.
                                // Same bits; measured level with pf4 (0.5016 vs 0.5008 ms, r02l_ilv.log): off
+  int ekf_row = 1;             // EKF: ekf_row_kernel (4 channels per wave) up to ekf_row x 4 x 4 x CUs channels
+                               // (ekf_row waves per SIMD: past one the issue-bound rows share a SIMD, and one
+                               // lane per channel carries 16x the channels per instruction); 0 = ekf_kernel only
   int demod_spw = 2;           // bin kernels: grid sized for ~this many segments per wave (0: one persistent
                                // wave per slot); later workgroups go to the slots that free first
 };
@@ -830,7 +833,8 @@ const std::map<std::string, Knob>& knobs() {
       {"lm_pa", {&g_tune.lm_pa, {}}},
       {"lm_pa_w2", {&g_tune.lm_pa_w2, {0, 1}}},
       {"demod_spw", {&g_tune.demod_spw, {}}},
-      {"bins_ilv", {&g_tune.bins_ilv, {0, 1}}}};
+      {"bins_ilv", {&g_tune.bins_ilv, {0, 1}}},
+      {"ekf_row", {&g_tune.ekf_row, {}}}};
   return k;
 }
 // np.mean / np.var of nrec device records on st (moments.hip), numpy-exact.
@@ -928,9 +932,14 @@ int ekf_impl(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
     hipLaunchKernelGGL(dfmi::ekf_phase_kernel, dim3((unsigned)((n_samp + 255) / 256)), dim3(256), 0, st,
                        (double*)wtw, n_samp, w_m, f_samp);
   const int block = 64;
-  const int64_t grid = (nrec + block - 1) / block;
-  hipLaunchKernelGGL(dfmi::ekf_kernel, dim3((unsigned)grid), dim3(block), 0, st, dx, nrec, rs, n_samp, dx0, dp0, dq,
-                     dr, (const double*)wtw, (int)R, nbuf, dstates);
+  // few channels: one 16-lane row per channel (ekf_row_kernel, ~1.7x the per-channel
+  // rate); many: one lane per channel (ekf_kernel, 16x the channels per instruction)
+  const bool row = g_tune.ekf_row && nrec <= (int64_t)g_tune.ekf_row * t_ds->n_cu * 16;
+  const int64_t grid = row ? (nrec + 3) / 4 : (nrec + block - 1) / block;
+  hipLaunchKernelGGL(row ? dfmi::ekf_row_kernel : dfmi::ekf_kernel, dim3((unsigned)grid), dim3(block), 0, st, dx,
+                     nrec, rs, n_samp, dx0, dp0, dq, dr, (const double*)wtw, (int)R, nbuf, dstates,
+                     dfmi::ekf_trig_consts());
+  g_last_demod = row ? "ekf_row_kernel" : "ekf_kernel";  // dfmi_last_demod_kernel reports the EKF variant too
   HIPCHK(hipGetLastError());
   if (host) {
     if (sb) HIPCHK(hipMemcpyAsync(states, dstates, sb, hipMemcpyDeviceToHost, st));

@@ -8,9 +8,9 @@
 //   P = F P F^T + Q (F = I: exact, so P + Q), H from fitters.py:287-293,
 //   S = (H P) H^T + R, K = (P H^T) · (1/S), x += K y, P = (I − K H) P, the last
 //   as P − K (H P) with P kept symmetric (ekf_step). sin / cos: the branch-free
-//   Cody-Waite form of dfmi_math.h (library fallback for |x| >= 2^19); w_m t_k comes
-//   from a parallel pre-pass, so the chain per sample is psi -> theta -> sincos ->
-//   phase -> sincos -> H -> H P -> S -> 1/S -> K -> state.
+//   Cody-Waite form of dfmi_math.h evaluated for latency (ekf_sincos; library fallback
+//   for |x| >= 2^19); w_m t_k comes from a parallel pre-pass, so the chain per sample
+//   is psi -> theta -> sincos -> phase -> sincos -> H -> H P -> S -> 1/S -> state.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -28,47 +28,93 @@ __global__ __launch_bounds__(256) void ekf_phase_kernel(double* __restrict__ wt,
   if (k < n) wt[k] = w_m * ((double)k / f_samp);
 }
 
+// Constants of ekf_sincos as a kernel argument (uniform: they live in SGPRs, where a
+// VOP3 v_fma_f64 reads them directly; as literals each Horner step costs a v_mov_b64
+// first, gfx9 VOP3 taking no 64-bit literal). Host: ekf_trig_consts().
+struct EkfTrig {
+  double c[16];  // 2/pi, pi/2 in 3 parts, sin kernel z^5..z^0 coefficients, cos kernel likewise
+};
+inline EkfTrig ekf_trig_consts() {
+  return EkfTrig{{6.36619772367581382433e-01, 1.57079632673412561417e+00, 6.07710050630396597660e-11,
+                  2.02226624871116645580e-21, 1.58969099521155010221e-10, -2.50507602534068634195e-08,
+                  2.75573137070700676789e-06, -1.98412698298579493134e-04, 8.33333333332248946124e-03,
+                  -1.66666666666666324348e-01, -1.13596475577881948265e-11, 2.08757232129817482790e-09,
+                  -2.75573143513906633035e-07, 2.48015872894767294178e-05, -1.38888888888741095749e-03,
+                  4.16666666666666019037e-02}};
+}
+
+// sin / cos for the EKF chain: dfmi_sincos_fast's reduction and kernel polynomials
+// (same constants, same operations: same bits), the quadrant applied as a swap select
+// plus a sign flip, and the library sincos (|x| >= 2^19, as dfmi_sincos) as a rarely
+// taken patch after the fast path instead of an if / else around it (fewer
+// instructions: the per-channel chain is issue-bound, see ekf_step).
+__device__ __forceinline__ void ekf_sincos(double x, const EkfTrig& k, double* sn, double* cs) {
+  const double q = rint(x * k.c[0]);
+  double r = fma(-q, k.c[1], x);
+  r = fma(-q, k.c[2], r);
+  r = fma(-q, k.c[3], r);
+  const double z = r * r;
+  const double ps = fma(z, fma(z, fma(z, fma(z, fma(z, k.c[4], k.c[5]), k.c[6]), k.c[7]), k.c[8]), k.c[9]);
+  const double sr = fma(r * z, ps, r);
+  const double pc = fma(z, fma(z, fma(z, fma(z, fma(z, k.c[10], k.c[11]), k.c[12]), k.c[13]), k.c[14]), k.c[15]);
+  const double cr = fma(z * z, pc, fma(-0.5, z, 1.0));
+  const int qi = ((int)q) & 3;
+  const double a = (qi & 1) ? cr : sr;  // sin: sr, cr, -sr, -cr
+  const double b = (qi & 1) ? sr : cr;  // cos: cr, -sr, -cr, sr
+  *sn = (qi & 2) ? -a : a;
+  *cs = ((qi + 1) & 2) ? -b : b;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (__builtin_expect(!(fabs(x) < 524288.0), 0)) {
+    const double2 v = dfmi_sincos_lib(x);
+    *sn = v.x;
+    *cs = v.y;
+  }
+#endif
+}
+
 // One EKF step (fitters.py:274-302) on the lane's state; P symmetric: only its upper
 // triangle P[i][j], i <= j, is read and written (constant-bound loops, fully unrolled:
 // every index is a compile-time register).
 // K = (P H^T) / S equals (H P)^T / S for a symmetric P: the H P row formed for S gives
 // K, and P - K (H P) updates 15 entries (15 fma instead of 25 + 25 + 25; the
 // reference's own P loses symmetry by rounding only).
+// One wave runs one instruction stream whether its chains are dependent or not (a
+// single wave issues a dependent v_fma_f64 every ~5.4 clocks, as fast as independent
+// ones: profiles/r02l_valu_probe.jsonl), so the step is costed in instructions: H[4] = 1
+// starts each H P chain at P[4][j], R folds into S, 1/S takes one Newton step on
+// v_rcp_f64 (~1 ulp), phi + m cos(theta) is one fma. Every change is a rounding-order
+// change against numpy's expressions (the reference itself moves by ~1e-15 under 1-ulp
+// changes; tests/test_gpu_parity.py holds the kernel to 1e-12 of the oracle).
 __device__ __forceinline__ void ekf_step(double (&st)[5], double (&P)[5][5], const double (&Q)[5], double Rv,
-                                         double xk, double wt) {
+                                         double xk, double wt, const EkfTrig& tk) {
 #pragma unroll
   for (int i = 0; i < 5; ++i) P[i][i] = P[i][i] + Q[i];  // predict: F = I
   const double a = st[0], m = st[1], phi = st[2], psi = st[3], dc = st[4];
   const double th = wt + psi;
   double sth, cth;
-  dfmi_sincos(th, &sth, &cth);
-  const double arg = phi + m * cth;
+  ekf_sincos(th, tk, &sth, &cth);
+  const double arg = fma(m, cth, phi);
+  const double acth = -a * cth, amsth = (a * m) * sth;
   double sa, ca;
-  dfmi_sincos(arg, &sa, &ca);
-  const double h = a * ca + dc;
-  const double H[5] = {ca, -a * sa * cth, -a * sa, a * m * sa * sth, 1.0};
+  ekf_sincos(arg, tk, &sa, &ca);
+  const double h = fma(a, ca, dc);
+  const double H[5] = {ca, acth * sa, -a * sa, amsth * sa, 1.0};
   const double y = xk - h;
+  auto Pu = [&](int i, int j) -> double { return i <= j ? P[i][j] : P[j][i]; };
   double HP[5];
 #pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    double acc = 0.0;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) acc = fma(H[i], i <= j ? P[i][j] : P[j][i], acc);
-    HP[j] = acc;
-  }
-  double S = 0.0;
-#pragma unroll
-  for (int j = 0; j < 5; ++j) S = fma(HP[j], H[j], S);
-  S = S + Rv;
-  // 1 / S (np.linalg.inv of the 1x1 S): v_rcp_f64 + two Newton steps, within an ulp
+  for (int j = 0; j < 5; ++j)  // H[4] = 1: the chain starts from P[4][j]
+    HP[j] = fma(H[3], Pu(3, j), fma(H[2], Pu(2, j), fma(H[1], Pu(1, j), fma(H[0], Pu(0, j), Pu(4, j)))));
+  const double S = fma(HP[3], H[3], fma(HP[2], H[2], fma(HP[1], H[1], fma(HP[0], H[0], HP[4] + Rv))));
+  // 1 / S (np.linalg.inv of the 1x1 S): v_rcp_f64 + one Newton step
   double invS = __builtin_amdgcn_rcp(S);
   invS = fma(invS, fma(-S, invS, 1.0), invS);
-  invS = fma(invS, fma(-S, invS, 1.0), invS);
+  const double iy = invS * y;
   double K[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) K[i] = HP[i] * invS;
 #pragma unroll
-  for (int i = 0; i < 5; ++i) st[i] = st[i] + K[i] * y;
+  for (int i = 0; i < 5; ++i) st[i] = fma(HP[i], iy, st[i]);
 #pragma unroll
   for (int i = 0; i < 5; ++i)
 #pragma unroll
@@ -81,7 +127,7 @@ __global__ __launch_bounds__(64) void ekf_kernel(const double* __restrict__ x, i
                                                   int64_t n_samp, const double* __restrict__ x0,
                                                   const double* __restrict__ p0, const double* __restrict__ qd,
                                                   const double* __restrict__ rv, const double* __restrict__ wt, int R,
-                                                  int64_t nbuf, double* __restrict__ states) {
+                                                  int64_t nbuf, double* __restrict__ states, EkfTrig tk) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= nrec) return;
   const double* __restrict__ xr = x + r * rec_stride;
@@ -122,15 +168,16 @@ __global__ __launch_bounds__(64) void ekf_kernel(const double* __restrict__ x, i
   }
   for (; k < n8; k += 8) {
     double xn[8], wn[8];
-    const bool more = k + 8 < n8;
+    // the next group, unconditionally (clamped into the record: no branch per load)
+    const int64_t kn = k + 8 < n8 ? k + 8 : k;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      xn[u] = more ? xr[k + 8 + u] : 0.0;
-      wn[u] = more ? wt[k + 8 + u] : 0.0;
+      xn[u] = xr[kn + u];
+      wn[u] = wt[kn + u];
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      ekf_step(st, P, Q, Rv, xc[u], wc[u]);
+      ekf_step(st, P, Q, Rv, xc[u], wc[u], tk);
       snap(k + u);
     }
 #pragma unroll
@@ -140,7 +187,132 @@ __global__ __launch_bounds__(64) void ekf_kernel(const double* __restrict__ x, i
     }
   }
   for (; k < n_samp; ++k) {
-    ekf_step(st, P, Q, Rv, xr[k], wt[k]);
+    ekf_step(st, P, Q, Rv, xr[k], wt[k], tk);
+    snap(k);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Row-per-channel EKF (few channels): one 16-lane DPP row per channel, 4 channels per
+// wave. Lane j < 5 of a row owns COLUMN j of the covariance (lanes 5..15 duplicate
+// column 4); the state, theta, the sincos pair and H are computed by every lane of the
+// row (one instruction stream costs the same for 1 or 16 lanes). Per sample the row
+// then needs H P as one 5-fma chain per lane instead of 20 in one lane, one
+// row_newbcast per H P element to share it, and a 5-fma column update instead of 15:
+// ~100 wave instructions per sample against ~170 for ekf_step, which runs the same
+// per-channel chain in one lane (the single-lane chain is issue-bound, see ekf_step).
+// Same expressions as ekf_step (same fma chains, same 1/S), except the covariance
+// update P[i][j] - HP_i (HP_j / S) where ekf_step forms (HP_i / S) HP_j: rounding only.
+// ---------------------------------------------------------------------------
+
+// value of lane n of this lane's 16-lane row (DPP row_newbcast, gfx90a+)
+template <int N>
+__device__ __forceinline__ double row_bcast(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x150 + N, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x150 + N, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ void ekf_row_step(double (&st)[5], double (&Pc)[5], const double (&qv)[5], double Rv,
+                                             double xk, double wt, const EkfTrig& tk) {
+#pragma unroll
+  for (int i = 0; i < 5; ++i) Pc[i] = Pc[i] + qv[i];  // predict: Q on the diagonal (qv[i] = 0 off it)
+  const double a = st[0], m = st[1], phi = st[2], psi = st[3], dc = st[4];
+  const double th = wt + psi;
+  double sth, cth;
+  ekf_sincos(th, tk, &sth, &cth);
+  const double arg = fma(m, cth, phi);
+  const double acth = -a * cth, amsth = (a * m) * sth;
+  double sa, ca;
+  ekf_sincos(arg, tk, &sa, &ca);
+  const double h = fma(a, ca, dc);
+  const double H[5] = {ca, acth * sa, -a * sa, amsth * sa, 1.0};
+  const double y = xk - h;
+  // (H P)_j from this lane's column (symmetric P): the chain of ekf_step
+  const double hpj = fma(H[3], Pc[3], fma(H[2], Pc[2], fma(H[1], Pc[1], fma(H[0], Pc[0], Pc[4]))));
+  double HP[5];
+  HP[0] = row_bcast<0>(hpj);
+  HP[1] = row_bcast<1>(hpj);
+  HP[2] = row_bcast<2>(hpj);
+  HP[3] = row_bcast<3>(hpj);
+  HP[4] = row_bcast<4>(hpj);
+  const double S = fma(HP[3], H[3], fma(HP[2], H[2], fma(HP[1], H[1], fma(HP[0], H[0], HP[4] + Rv))));
+  double invS = __builtin_amdgcn_rcp(S);
+  invS = fma(invS, fma(-S, invS, 1.0), invS);
+  const double iy = invS * y;
+  const double cj = hpj * invS;  // K_j
+#pragma unroll
+  for (int i = 0; i < 5; ++i) st[i] = fma(HP[i], iy, st[i]);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) Pc[i] = fma(-HP[i], cj, Pc[i]);
+}
+
+// Same arguments and outputs as ekf_kernel; grid of ceil(nrec / 4) one-wave blocks.
+__global__ __launch_bounds__(64) void ekf_row_kernel(const double* __restrict__ x, int64_t nrec, int64_t rec_stride,
+                                                      int64_t n_samp, const double* __restrict__ x0,
+                                                      const double* __restrict__ p0, const double* __restrict__ qd,
+                                                      const double* __restrict__ rv, const double* __restrict__ wt,
+                                                      int R, int64_t nbuf, double* __restrict__ states,
+                                                      EkfTrig tk) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r0 = (int64_t)blockIdx.x * 4 + (lane >> 4);
+  const bool live = r0 < nrec;
+  const int64_t r = live ? r0 : nrec - 1;  // rows past the end shadow the last channel (no stores)
+  int j = lane & 15;
+  if (j > 4) j = 4;
+  const double* __restrict__ xr = x + r * rec_stride;
+  double st[5], Pc[5], qv[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    st[i] = x0[r * 5 + i];
+    Pc[i] = (i == j) ? p0[i] : 0.0;
+    qv[i] = (i == j) ? qd[i] : 0.0;
+  }
+  const double Rv = rv[r];
+  const bool writer = live && (lane & 15) == 0;
+  int64_t to_snap = R;
+  auto snap = [&](int64_t k) {
+    if (--to_snap == 0) {
+      to_snap = R;
+      const int64_t b = (k + 1) / R - 1;
+      if (b < nbuf && writer) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) states[(r * nbuf + b) * 5 + i] = st[i];
+      }
+    }
+  };
+  int64_t k = 0;
+  double xc[8], wc[8];
+  const int64_t n8 = n_samp & ~(int64_t)7;
+  if (n8 > 0) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      xc[u] = xr[u];
+      wc[u] = wt[u];
+    }
+  }
+  for (; k < n8; k += 8) {
+    double xn[8], wn[8];
+    // the next group, unconditionally (clamped into the record: no branch per load)
+    const int64_t kn = k + 8 < n8 ? k + 8 : k;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      xn[u] = xr[kn + u];
+      wn[u] = wt[kn + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      ekf_row_step(st, Pc, qv, Rv, xc[u], wc[u], tk);
+      snap(k + u);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      xc[u] = xn[u];
+      wc[u] = wn[u];
+    }
+  }
+  for (; k < n_samp; ++k) {
+    ekf_row_step(st, Pc, qv, Rv, xr[k], wt[k], tk);
     snap(k);
   }
 }

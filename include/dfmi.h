@@ -325,8 +325,9 @@ const char* dfmi_last_error(void);
 /* Library/ABI version, e.g. "dfmi 0.2 gfx950". */
 const char* dfmi_version(void);
 
-/* Kernel variant of the last demodulation this process launched, e.g.
- * "demod_bins_kernel<2,8,1>" ("" before the first one). Diagnostics/profiling. */
+/* Kernel variant of the last demodulation (or EKF fit) this process launched, e.g.
+ * "demod_bins_kernel<2,8,1>", "ekf_row_kernel" ("" before the first one).
+ * Diagnostics/profiling. */
 const char* dfmi_last_demod_kernel(void);
 
 #ifdef __cplusplus

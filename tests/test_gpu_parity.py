@@ -150,13 +150,26 @@ def test_ekf_matches_reference(manifest):
             assert err <= 1e-9, (lab, k, err)
 
 
-def test_ekf_long_record_matches_oracle():
+@pytest.mark.parametrize("row", [1, 0])
+def test_ekf_long_record_matches_oracle(row):
     """Config 5 shape on a longer record than the golden one (0.1 s = 20,000 samples,
-    5 snapshots): the lane-per-channel kernel tracks the restated reference loop to
-    fp64 rounding (the reference itself moves by ~1e-15 under 1-ulp input changes),
-    and several channels in one launch give each channel's answer bit for bit."""
+    5 snapshots): both EKF kernels — one 16-lane row per channel (ekf_row_kernel, the
+    default for few channels) and one lane per channel (ekf_kernel, ekf_row = 0) —
+    track the restated reference loop to fp64 rounding (the reference itself moves by
+    ~1e-15 under 1-ulp input changes), and several channels in one launch give each
+    channel's answer bit for bit."""
     import deepfmkit_amd as dfm
+    from deepfmkit_amd import _lib
     from oracle import nls_oracle as O
+    lib = _lib.load()
+    _lib.check(lib.dfmi_set_tuning(b"ekf_row", row), "tune")
+    try:
+        _ekf_long_record(dfm, O, lib, "ekf_row_kernel" if row else "ekf_kernel")
+    finally:
+        _lib.check(lib.dfmi_set_tuning(b"ekf_row", 1), "tune")
+
+
+def _ekf_long_record(dfm, O, lib, kname):
     laser = dfm.LaserConfig()
     ifo = dfm.InterferometerConfig()
     dfm.set_laser_df_for_effect(laser, ifo, 6.0)
@@ -167,9 +180,10 @@ def test_ekf_long_record_matches_oracle():
     x = np.asarray(raw.samples(), dtype=np.float64)
     ref = O.ekf_record(x, 200000.0, 1000.0, 20)
     got = dfm.fitters.ekf_records([raw], 20)[0]
+    assert lib.dfmi_last_demod_kernel().decode() == kname
     assert np.max(np.abs(got - ref)) <= 1e-12, np.max(np.abs(got - ref))
-    many = dfm.fitters.ekf_records([raw] * 3, 20)
-    for k in range(3):
+    many = dfm.fitters.ekf_records([raw] * 6, 20)  # row kernel: a second wave, rows past the end
+    for k in range(6):
         np.testing.assert_array_equal(many[k], got)
 
 

@@ -257,6 +257,7 @@ int to_lmconst(const dfmi_lm_config* cfg, dfmi::LMConst* c) {
   c->sincos_amp_thr = cfg->sincos_amp_threshold;
   grid_geometry(*cfg, &c->n_grid, &c->grid_delta);
   c->grid_min = cfg->m_grid_min;
+  c->trig = dfmi_trig_k();
   return DFMI_OK;
 }
 
@@ -938,7 +939,7 @@ int ekf_impl(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
   const int64_t grid = row ? (nrec + 3) / 4 : (nrec + block - 1) / block;
   hipLaunchKernelGGL(row ? dfmi::ekf_row_kernel : dfmi::ekf_kernel, dim3((unsigned)grid), dim3(block), 0, st, dx,
                      nrec, rs, n_samp, dx0, dp0, dq, dr, (const double*)wtw, (int)R, nbuf, dstates,
-                     dfmi::ekf_trig_consts());
+                     dfmi_trig_k());
   g_last_demod = row ? "ekf_row_kernel" : "ekf_kernel";  // dfmi_last_demod_kernel reports the EKF variant too
   HIPCHK(hipGetLastError());
   if (host) {

@@ -238,12 +238,62 @@ static __device__ __noinline__ double2 dfmi_sincos_lib(double x) {
 }
 #endif
 
+// dfmi_sincos_fast's constants as a runtime value (a kernel argument: uniform, so they
+// live in SGPRs, where a VOP3 v_fma_f64 reads them directly; as literals every Horner
+// step costs a v_mov_b64 first, gfx9 VOP3 taking no 64-bit literal). The kernels get
+// it inside their LMConst / as an EKF argument, built on the host by dfmi_trig_k().
+struct DfmiTrigK {
+  double c[16];  // 2/pi, pi/2 in 3 parts, sin kernel z^5..z^0 coefficients, cos kernel likewise
+};
+static inline DfmiTrigK dfmi_trig_k(void) {
+  DfmiTrigK k = {{6.36619772367581382433e-01, 1.57079632673412561417e+00, 6.07710050630396597660e-11,
+                  2.02226624871116645580e-21, 1.58969099521155010221e-10, -2.50507602534068634195e-08,
+                  2.75573137070700676789e-06, -1.98412698298579493134e-04, 8.33333333332248946124e-03,
+                  -1.66666666666666324348e-01, -1.13596475577881948265e-11, 2.08757232129817482790e-09,
+                  -2.75573143513906633035e-07, 2.48015872894767294178e-05, -1.38888888888741095749e-03,
+                  4.16666666666666019037e-02}};
+  return k;
+}
+
 // sincos with the fast path where it is exact to the kernel polynomials' accuracy
 // (|x| < 2^19, every argument of these fits) and the library otherwise.
 DFMI_HD void dfmi_sincos(double x, double* sn, double* cs) {
   if (fabs(x) < 524288.0) {
     dfmi_sincos_fast(x, sn, cs);
   } else {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double2 v = dfmi_sincos_lib(x);
+    *sn = v.x;
+    *cs = v.y;
+#else
+    sincos(x, sn, cs);
+#endif
+  }
+}
+
+// dfmi_sincos with the constants from k and fewer instructions, same bits: the same
+// reduction and Horner polynomials, the quadrant applied as a swap select plus a sign
+// flip (no branch, 2 select levels instead of 3), and the library path (|x| >= 2^19, NaN)
+// as a rarely taken patch after the fast path instead of an if / else around it. Per-lane
+// fp64 chains are issue-bound on gfx950 (a single wave issues a dependent v_fma_f64
+// every ~5.4 clocks, as fast as independent ones: profiles/r02l_valu_probe.jsonl), so
+// instructions are the cost.
+DFMI_HD void dfmi_sincos_k(double x, const DfmiTrigK& k, double* sn, double* cs) {
+  const double q = rint(x * k.c[0]);
+  double r = fma(-q, k.c[1], x);
+  r = fma(-q, k.c[2], r);
+  r = fma(-q, k.c[3], r);
+  const double z = r * r;
+  const double ps = fma(z, fma(z, fma(z, fma(z, fma(z, k.c[4], k.c[5]), k.c[6]), k.c[7]), k.c[8]), k.c[9]);
+  const double sr = fma(r * z, ps, r);
+  const double pc = fma(z, fma(z, fma(z, fma(z, fma(z, k.c[10], k.c[11]), k.c[12]), k.c[13]), k.c[14]), k.c[15]);
+  const double cr = fma(z * z, pc, fma(-0.5, z, 1.0));
+  const int qi = ((int)q) & 3;
+  const double a = (qi & 1) ? cr : sr;  // sin: sr, cr, -sr, -cr
+  const double b = (qi & 1) ? sr : cr;  // cos: cr, -sr, -cr, sr
+  *sn = (qi & 2) ? -a : a;
+  *cs = ((qi + 1) & 2) ? -b : b;
+  if (__builtin_expect(!(fabs(x) < 524288.0), 0)) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const double2 v = dfmi_sincos_lib(x);
     *sn = v.x;

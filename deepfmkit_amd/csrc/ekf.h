@@ -8,9 +8,9 @@
 //   P = F P F^T + Q (F = I: exact, so P + Q), H from fitters.py:287-293,
 //   S = (H P) H^T + R, K = (P H^T) · (1/S), x += K y, P = (I − K H) P, the last
 //   as P − K (H P) with P kept symmetric (ekf_step). sin / cos: the branch-free
-//   Cody-Waite form of dfmi_math.h evaluated for latency (ekf_sincos; library fallback
-//   for |x| >= 2^19); w_m t_k comes from a parallel pre-pass, so the chain per sample
-//   is psi -> theta -> sincos -> phase -> sincos -> H -> H P -> S -> 1/S -> state.
+//   Cody-Waite form of dfmi_math.h with its constants in SGPRs (dfmi_sincos_k; library
+//   patch for |x| >= 2^19); w_m t_k comes from a parallel pre-pass, so the chain per
+//   sample is psi -> theta -> sincos -> phase -> sincos -> H -> H P -> S -> 1/S -> state.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -28,50 +28,6 @@ __global__ __launch_bounds__(256) void ekf_phase_kernel(double* __restrict__ wt,
   if (k < n) wt[k] = w_m * ((double)k / f_samp);
 }
 
-// Constants of ekf_sincos as a kernel argument (uniform: they live in SGPRs, where a
-// VOP3 v_fma_f64 reads them directly; as literals each Horner step costs a v_mov_b64
-// first, gfx9 VOP3 taking no 64-bit literal). Host: ekf_trig_consts().
-struct EkfTrig {
-  double c[16];  // 2/pi, pi/2 in 3 parts, sin kernel z^5..z^0 coefficients, cos kernel likewise
-};
-inline EkfTrig ekf_trig_consts() {
-  return EkfTrig{{6.36619772367581382433e-01, 1.57079632673412561417e+00, 6.07710050630396597660e-11,
-                  2.02226624871116645580e-21, 1.58969099521155010221e-10, -2.50507602534068634195e-08,
-                  2.75573137070700676789e-06, -1.98412698298579493134e-04, 8.33333333332248946124e-03,
-                  -1.66666666666666324348e-01, -1.13596475577881948265e-11, 2.08757232129817482790e-09,
-                  -2.75573143513906633035e-07, 2.48015872894767294178e-05, -1.38888888888741095749e-03,
-                  4.16666666666666019037e-02}};
-}
-
-// sin / cos for the EKF chain: dfmi_sincos_fast's reduction and kernel polynomials
-// (same constants, same operations: same bits), the quadrant applied as a swap select
-// plus a sign flip, and the library sincos (|x| >= 2^19, as dfmi_sincos) as a rarely
-// taken patch after the fast path instead of an if / else around it (fewer
-// instructions: the per-channel chain is issue-bound, see ekf_step).
-__device__ __forceinline__ void ekf_sincos(double x, const EkfTrig& k, double* sn, double* cs) {
-  const double q = rint(x * k.c[0]);
-  double r = fma(-q, k.c[1], x);
-  r = fma(-q, k.c[2], r);
-  r = fma(-q, k.c[3], r);
-  const double z = r * r;
-  const double ps = fma(z, fma(z, fma(z, fma(z, fma(z, k.c[4], k.c[5]), k.c[6]), k.c[7]), k.c[8]), k.c[9]);
-  const double sr = fma(r * z, ps, r);
-  const double pc = fma(z, fma(z, fma(z, fma(z, fma(z, k.c[10], k.c[11]), k.c[12]), k.c[13]), k.c[14]), k.c[15]);
-  const double cr = fma(z * z, pc, fma(-0.5, z, 1.0));
-  const int qi = ((int)q) & 3;
-  const double a = (qi & 1) ? cr : sr;  // sin: sr, cr, -sr, -cr
-  const double b = (qi & 1) ? sr : cr;  // cos: cr, -sr, -cr, sr
-  *sn = (qi & 2) ? -a : a;
-  *cs = ((qi + 1) & 2) ? -b : b;
-#if defined(__HIP_DEVICE_COMPILE__)
-  if (__builtin_expect(!(fabs(x) < 524288.0), 0)) {
-    const double2 v = dfmi_sincos_lib(x);
-    *sn = v.x;
-    *cs = v.y;
-  }
-#endif
-}
-
 // One EKF step (fitters.py:274-302) on the lane's state; P symmetric: only its upper
 // triangle P[i][j], i <= j, is read and written (constant-bound loops, fully unrolled:
 // every index is a compile-time register).
@@ -86,17 +42,17 @@ __device__ __forceinline__ void ekf_sincos(double x, const EkfTrig& k, double* s
 // change against numpy's expressions (the reference itself moves by ~1e-15 under 1-ulp
 // changes; tests/test_gpu_parity.py holds the kernel to 1e-12 of the oracle).
 __device__ __forceinline__ void ekf_step(double (&st)[5], double (&P)[5][5], const double (&Q)[5], double Rv,
-                                         double xk, double wt, const EkfTrig& tk) {
+                                         double xk, double wt, const DfmiTrigK& tk) {
 #pragma unroll
   for (int i = 0; i < 5; ++i) P[i][i] = P[i][i] + Q[i];  // predict: F = I
   const double a = st[0], m = st[1], phi = st[2], psi = st[3], dc = st[4];
   const double th = wt + psi;
   double sth, cth;
-  ekf_sincos(th, tk, &sth, &cth);
+  dfmi_sincos_k(th, tk, &sth, &cth);
   const double arg = fma(m, cth, phi);
   const double acth = -a * cth, amsth = (a * m) * sth;
   double sa, ca;
-  ekf_sincos(arg, tk, &sa, &ca);
+  dfmi_sincos_k(arg, tk, &sa, &ca);
   const double h = fma(a, ca, dc);
   const double H[5] = {ca, acth * sa, -a * sa, amsth * sa, 1.0};
   const double y = xk - h;
@@ -127,7 +83,7 @@ __global__ __launch_bounds__(64) void ekf_kernel(const double* __restrict__ x, i
                                                   int64_t n_samp, const double* __restrict__ x0,
                                                   const double* __restrict__ p0, const double* __restrict__ qd,
                                                   const double* __restrict__ rv, const double* __restrict__ wt, int R,
-                                                  int64_t nbuf, double* __restrict__ states, EkfTrig tk) {
+                                                  int64_t nbuf, double* __restrict__ states, DfmiTrigK tk) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= nrec) return;
   const double* __restrict__ xr = x + r * rec_stride;
@@ -214,17 +170,17 @@ __device__ __forceinline__ double row_bcast(double v) {
 }
 
 __device__ __forceinline__ void ekf_row_step(double (&st)[5], double (&Pc)[5], const double (&qv)[5], double Rv,
-                                             double xk, double wt, const EkfTrig& tk) {
+                                             double xk, double wt, const DfmiTrigK& tk) {
 #pragma unroll
   for (int i = 0; i < 5; ++i) Pc[i] = Pc[i] + qv[i];  // predict: Q on the diagonal (qv[i] = 0 off it)
   const double a = st[0], m = st[1], phi = st[2], psi = st[3], dc = st[4];
   const double th = wt + psi;
   double sth, cth;
-  ekf_sincos(th, tk, &sth, &cth);
+  dfmi_sincos_k(th, tk, &sth, &cth);
   const double arg = fma(m, cth, phi);
   const double acth = -a * cth, amsth = (a * m) * sth;
   double sa, ca;
-  ekf_sincos(arg, tk, &sa, &ca);
+  dfmi_sincos_k(arg, tk, &sa, &ca);
   const double h = fma(a, ca, dc);
   const double H[5] = {ca, acth * sa, -a * sa, amsth * sa, 1.0};
   const double y = xk - h;
@@ -253,7 +209,7 @@ __global__ __launch_bounds__(64) void ekf_row_kernel(const double* __restrict__ 
                                                       const double* __restrict__ p0, const double* __restrict__ qd,
                                                       const double* __restrict__ rv, const double* __restrict__ wt,
                                                       int R, int64_t nbuf, double* __restrict__ states,
-                                                      EkfTrig tk) {
+                                                      DfmiTrigK tk) {
   const int lane = threadIdx.x & 63;
   const int64_t r0 = (int64_t)blockIdx.x * 4 + (lane >> 4);
   const bool live = r0 < nrec;

@@ -53,6 +53,7 @@ struct LMConst {
   int n_grid;                // len(np.arange(M_GRID_MIN, M_GRID_MAX + M_GRID_STEP, M_GRID_STEP))
   double grid_min;           // fit.py:12
   double grid_delta;         // (min + step) - min, numpy arange fill
+  DfmiTrigK trig;            // dfmi_sincos_k's constants (in SGPRs as part of the kernel argument)
 };
 
 #define DFMI_HDI __host__ __device__ __forceinline__
@@ -255,13 +256,13 @@ DFMI_HDI double hmask(int nd, int j) {
 // Jacobian of an accepted trial (eval_reg_accept). Harmonics accumulate into two
 // partial sums (odd / even j): two independent fma chains.
 template <int V, typename QF>
-DFMI_HDI double eval_reg_trial(const QF& q, int nd, const double (&p)[4], TrialReg<V>& t) {
+DFMI_HDI double eval_reg_trial(const QF& q, int nd, const double (&p)[4], TrialReg<V>& t, const DfmiTrigK& k) {
   constexpr int NDMAX = nd_cap(V);
   double Q[NDMAX], I[NDMAX];
 #pragma unroll
   for (int j = 1; j <= NDMAX; ++j) qi_pair<V>(q, nd, j, Q[j - 1], I[j - 1]);
-  dfmi_sincos(p[2], &t.sph, &t.cph);
-  dfmi_sincos(p[3], &t.s1, &t.c1);
+  dfmi_sincos_k(p[2], k, &t.sph, &t.cph);
+  dfmi_sincos_k(p[3], k, &t.s1, &t.c1);
   bessel_regs<NDMAX + 2>(p[1], nd_exact(V) ? NDMAX + 1 : nd + 1, t.J);
   const double ac = p[0] * t.cph, as = p[0] * t.sph;
   const double tc = 2.0 * t.c1;
@@ -347,14 +348,14 @@ DFMI_HDI void eval_reg_accept(const QF& q, int nd, const double (&p)[4], const T
 // their descents: a pass that always forms the Jacobian costs one evaluation, while
 // the split form costs a trial plus, whenever ANY lane of the wave accepts, an accept.
 template <int V, typename QF>
-DFMI_HDI void eval_reg_full(const QF& q, int nd, const double (&p)[4], Eval& e) {
+DFMI_HDI void eval_reg_full(const QF& q, int nd, const double (&p)[4], Eval& e, const DfmiTrigK& k) {
   constexpr int NDMAX = nd_cap(V);
   double Q[NDMAX], I[NDMAX];
 #pragma unroll
   for (int j = 1; j <= NDMAX; ++j) qi_pair<V>(q, nd, j, Q[j - 1], I[j - 1]);
   double sph, cph, s1, c1;
-  dfmi_sincos(p[2], &sph, &cph);
-  dfmi_sincos(p[3], &s1, &c1);
+  dfmi_sincos_k(p[2], k, &sph, &cph);
+  dfmi_sincos_k(p[3], k, &s1, &c1);
   double J[NDMAX + 2];
   bessel_regs<NDMAX + 2>(p[1], nd_exact(V) ? NDMAX + 1 : nd + 1, J);
   const double a = p[0];
@@ -667,8 +668,9 @@ template <int NDMAX, typename QF>
 struct SplitEval {  // NDMAX: a register-path variant tag (nd_cap / nd_exact)
   const QF& q;
   int nd;
+  const DfmiTrigK& k;
   using Trial = TrialReg<NDMAX>;
-  DFMI_HDI double trial(const double (&p)[4], Trial& t) { return eval_reg_trial<NDMAX>(q, nd, p, t); }
+  DFMI_HDI double trial(const double (&p)[4], Trial& t) { return eval_reg_trial<NDMAX>(q, nd, p, t, k); }
   DFMI_HDI void accept(const double (&p)[4], const Trial& t, Eval& e) { eval_reg_accept<NDMAX>(q, nd, p, t, e); }
   DFMI_HDI void solve(const Eval& e, double lam, double (&dp)[4]) { damped_solve_block(e, lam, dp); }
 };
@@ -844,7 +846,7 @@ __host__ __device__ __forceinline__ int fit_segment_q2(const QE& qe, const QM& q
                                                     const double* __restrict__ jtab, const LMConst& c,
                                                     double (&p)[4], double& ssq_out) {
   if constexpr (NDMAX > 0) {
-    SplitEval<NDMAX, QE> ev{qe, ndata};
+    SplitEval<NDMAX, QE> ev{qe, ndata, c.trig};
     return fit_segment_t<FLAT>(ev, qm, ndata, jtab, c, p, ssq_out);
   } else {
     auto evalf = [&](const double (&pp)[4], Eval& e) { eval_gen(qe, ndata, pp, e); };

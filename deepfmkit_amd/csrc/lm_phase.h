@@ -169,7 +169,7 @@ __global__ __launch_bounds__(64, WPE) void lm_phase_a_kernel(const double* __res
     if (uc - r * nitems == 0)  // the record's seed buffers (fitted elsewhere): carry their dc
       for (int64_t t = r * nbuf; t < r * nbuf + first; ++t) out[4 * out_ld + t] = qi[t * qi_ld + dfmi_row_dc(ndata)];
   }
-  SplitEval<V, QRow<65>> ev{q, ndata};
+  SplitEval<V, QRow<65>> ev{q, ndata, c.trig};
   FlatState st;
 #pragma unroll
   for (int i = 0; i < 4; ++i) st.p[i] = guess[r * g_rec + i * g_comp];
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(64) void lm_phase_b_kernel(const double* __restrict
     lm_stage_row(qi, qi_ld, s, QS, lds_q, lane);
     __syncthreads();
     const QRow<65> q{lds_q + lane};
-    SplitEval<V, QRow<65>> ev{q, ndata};
+    SplitEval<V, QRow<65>> ev{q, ndata, c.trig};
     FlatState st;
     double v[kLmSt];
 #pragma unroll

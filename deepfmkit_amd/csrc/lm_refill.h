@@ -191,7 +191,7 @@ __global__ __launch_bounds__(64, WPE) void lm_refill_kernel(const double* __rest
     Eval et;
     const uint64_t te0 = probe ? __builtin_amdgcn_s_memtime() : 0;
     if (probe) t_solve += te0 - ts0;
-    eval_reg_full<V>(q, ndata, pt, et);
+    eval_reg_full<V>(q, ndata, pt, et, c.trig);
     if (probe) {
       t_eval += __builtin_amdgcn_s_memtime() - te0;
       ++n_pass;

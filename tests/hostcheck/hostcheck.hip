@@ -83,6 +83,7 @@ int hc_fit_segments(const double* qi, long n, int ndata, const double* guess, co
   c.n_grid = len > 0 ? (int)len : 0;
   c.grid_min = gmin;
   c.grid_delta = (gmin + gstep) - gmin;
+  c.trig = dfmi_trig_k();
   std::vector<double> tab((size_t)(c.n_grid > 0 ? c.n_grid : 1) * ndata);
   std::vector<double> row(ndata + 2);
   for (int g = 0; g < c.n_grid; ++g) {

@@ -294,6 +294,9 @@ struct Tuning {
   int ekf_row = 1;             // EKF: ekf_row_kernel (4 channels per wave) up to ekf_row x 4 x 4 x CUs channels
                                // (ekf_row waves per SIMD: past one the issue-bound rows share a SIMD, and one
                                // lane per channel carries 16x the channels per instruction); 0 = ekf_kernel only
+  int lm_spec = 0;             // LM (chunk size 1, register path; same bits in every mode): 1 = the lambda ladder
+                               // speculated by the wave's finished lanes (lm.h lm_descend_spec), 2 = one fused
+                               // ssqf + coeffs evaluation per trial (lm.h FusedEval), 0 = split trial / accept
   int demod_spw = 2;           // bin kernels: grid sized for ~this many segments per wave (0: one persistent
                                // wave per slot); later workgroups go to the slots that free first
 };
@@ -552,6 +555,17 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
   // ndata == 10 (the reference default): the exact-ndata register variant (no masking)
   constexpr int kNd10 = dfmi::kExactNd | 10;
   if (nd_sel == 10) kern = chain ? dfmi::lm_chunks_kernel<kNd10, true> : dfmi::lm_chunks_kernel<kNd10, false>;
+  const int spec = chain ? 0 : g_tune.lm_spec;
+  if (spec == 1)
+    kern = nd_sel == 10   ? dfmi::lm_chunks_kernel<kNd10, false, false, 1>
+           : nd_sel <= 12 ? dfmi::lm_chunks_kernel<12, false, false, 1>
+           : nd_sel <= 16 ? dfmi::lm_chunks_kernel<16, false, false, 1>
+                          : kern;
+  if (spec == 2)
+    kern = nd_sel == 10   ? dfmi::lm_chunks_kernel<kNd10, false, false, 2>
+           : nd_sel <= 12 ? dfmi::lm_chunks_kernel<12, false, false, 2>
+           : nd_sel <= 16 ? dfmi::lm_chunks_kernel<16, false, false, 2>
+                          : kern;
   if (!chain && g_tune.lm_refill && nd_sel <= 16 && guess_dev) {
     // tiles of up to kRefillTmax segments, one wave each, lanes refilled from the tile
     const int64_t total = nrec * nitems;
@@ -598,9 +612,15 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
     return DFMI_OK;
   }
   if (rows) {
-    kern = nd_sel == 10   ? dfmi::lm_chunks_kernel<kNd10, false, true>
-           : nd_sel <= 12 ? dfmi::lm_chunks_kernel<12, false, true>
-           : nd_sel <= 16 ? dfmi::lm_chunks_kernel<16, false, true>
+    kern = nd_sel == 10   ? (spec == 1   ? dfmi::lm_chunks_kernel<kNd10, false, true, 1>
+                             : spec == 2 ? dfmi::lm_chunks_kernel<kNd10, false, true, 2>
+                                         : dfmi::lm_chunks_kernel<kNd10, false, true>)
+           : nd_sel <= 12 ? (spec == 1   ? dfmi::lm_chunks_kernel<12, false, true, 1>
+                             : spec == 2 ? dfmi::lm_chunks_kernel<12, false, true, 2>
+                                         : dfmi::lm_chunks_kernel<12, false, true>)
+           : nd_sel <= 16 ? (spec == 1   ? dfmi::lm_chunks_kernel<16, false, true, 1>
+                             : spec == 2 ? dfmi::lm_chunks_kernel<16, false, true, 2>
+                                         : dfmi::lm_chunks_kernel<16, false, true>)
                           : dfmi::lm_chunks_kernel<0, false, true>;
     if (nd_sel <= 16) lds = (size_t)qi_ld * 65 * sizeof(double);  // the wave's rows, transposed
   }
@@ -831,6 +851,7 @@ const std::map<std::string, Knob>& knobs() {
       {"lm_waves_per_simd", {&g_tune.lm_waves_per_simd, {1, 2, 3, 4}}},
       {"lm_tile_min", {&g_tune.lm_tile_min, {16, 32, 48, 64, 96, 128}}},
       {"lm_phase", {&g_tune.lm_phase, {0, 1}}},
+      {"lm_spec", {&g_tune.lm_spec, {0, 1, 2}}},
       {"lm_pa", {&g_tune.lm_pa, {}}},
       {"lm_pa_w2", {&g_tune.lm_pa_w2, {0, 1}}},
       {"demod_spw", {&g_tune.demod_spw, {}}},

@@ -675,6 +675,25 @@ struct SplitEval {  // NDMAX: a register-path variant tag (nd_cap / nd_exact)
   DFMI_HDI void solve(const Eval& e, double lam, double (&dp)[4]) { damped_solve_block(e, lam, dp); }
 };
 
+// Register path with ONE evaluation per trial: ssqf and coeffs at the trial point
+// together (eval_reg_full, same bits as SplitEval's trial + accept). A trial that is
+// accepted then needs no second pass for its Jacobian; a rejected one pays for it.
+template <int NDMAX, typename QF>
+struct FusedEval {
+  const QF& q;
+  int nd;
+  const DfmiTrigK& k;
+  struct Trial {
+    Eval e;
+  };
+  DFMI_HDI double trial(const double (&p)[4], Trial& t) {
+    eval_reg_full<NDMAX>(q, nd, p, t.e, k);
+    return t.e.ssq;
+  }
+  DFMI_HDI void accept(const double (&)[4], const Trial& t, Eval& e) { e = t.e; }
+  DFMI_HDI void solve(const Eval& e, double lam, double (&dp)[4]) { damped_solve_block(e, lam, dp); }
+};
+
 // fit.py:208-258 (_run_lma_fit), nested form (one lane at a time: the host build's
 // check that the flattened descent takes the same path). p in/out; returns ssq0 at
 // the final p.
@@ -715,6 +734,176 @@ DFMI_HDI double lm_descend(Ev&& ev, double (&p)[4], const LMConst& c) {
     ev.accept(p, tt, e);  // coeffs(ndata, data, parm) at the accepted point (fit.py:251)
     const double change2 = sumsq4(p[0] - po0, p[1] - po1, p[2] - po2, p[3] - po3);
     if ((e.ssq - best_ssq) < c.conv_improve && norm_below(change2, c.conv_param_change)) break;
+  }
+  return e.ssq;
+}
+
+// Lane position of the k-th (0-based) set bit of m (k < popcount(m)).
+__device__ __forceinline__ int nth_set_bit(uint64_t m, int k) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const uint64_t lo = m & ((1ull << w) - 1);
+    const int c = __popcll(lo);
+    const bool up = k >= c;
+    k = up ? k - c : k;
+    m = up ? (m >> w) : lo;
+    pos += up ? w : 0;
+  }
+  return pos;
+}
+
+// Lanes [lo, hi) of a 64-bit wave mask (0 <= lo <= hi <= 64).
+__device__ __forceinline__ uint64_t lane_range(int lo, int hi) {
+  const uint64_t below_hi = hi >= 64 ? ~0ull : ((1ull << hi) - 1);
+  const uint64_t below_lo = lo >= 64 ? ~0ull : ((1ull << lo) - 1);
+  return below_hi & ~below_lo;
+}
+
+template <typename T>
+__device__ __forceinline__ T shfl_any(T v, int src) {
+  if constexpr (sizeof(T) == 8) {
+    long long b = __builtin_bit_cast(long long, v);
+    b = __shfl(b, src);
+    return __builtin_bit_cast(T, b);
+  } else {
+    return __shfl(v, src);
+  }
+}
+
+// fit.py:208-258 (_run_lma_fit) as lm_descend_flat, with the lambda ladder evaluated
+// speculatively by the wave's finished lanes. In SIMT a pass costs the same whatever
+// the number of lanes that run it, so a lane whose descent has ended (a "helper")
+// evaluates, in the same pass, a later rung of an active lane's ladder: helper h of
+// active lane i solves msolve(lambda[li_i + off]) from lane i's (p, J^T J, J^T r) and
+// runs ssqf on lane i's QI (the QF accessor's base pointer is taken from lane i).
+// Lane i then takes the FIRST improving rung in ladder order — its own trial at li_i,
+// else the helpers' rungs li_i + 1, + 2, ... — with that rung's trial state (for the
+// Jacobian, as if it had evaluated it itself), or skips every rung that was evaluated
+// without improvement. Each rung's solve + trial is the same pure function of (p, e,
+// lambda, QI) whichever lane computes it, so every lane's sequence of accepted points
+// (and every bit of the result) is lm_descend's; only the number of passes falls: the
+// 8-rung ladder that ends a converged descent ("no lambda improved", fit.py:246-247)
+// is evaluated in one or two passes once most lanes of the wave are done.
+// Helpers are assigned in blocks: K = max(1, helpers / active) consecutive helpers per
+// active lane (by rank), rungs li + 1 .. li + K.
+template <int V, typename QF>
+__device__ __forceinline__ double lm_descend_spec(SplitEval<V, QF>& ev, double (&p)[4], const LMConst& c) {
+  using Trial = TrialReg<V>;
+  constexpr int NT = (int)(sizeof(Trial) / sizeof(double));
+  static_assert(sizeof(Trial) == NT * sizeof(double), "TrialReg: doubles only");
+  Eval e;
+  {
+    Trial t0;
+    ev.trial(p, t0);
+    ev.accept(p, t0, e);
+  }
+  const int lane = (int)__lane_id();
+  const uint64_t below = (1ull << lane) - 1;
+  int it = 0, li = 0;
+  bool active = c.max_steps > 0 && c.n_lambda > 0;
+  for (;;) {
+    const uint64_t A = __ballot(active);
+    if (A == 0) break;
+    const uint64_t H = __ballot(!active);  // lanes of this loop whose descent has ended
+    const int na = __popcll(A), nh = __popcll(H);
+    const bool spec = nh > 0;  // wave-uniform
+    const int K = nh >= na ? nh / na : 1;
+    // the rung this lane evaluates: its own (active) or rung li_src + off of lane src
+    int src = lane, off = 0;
+    if (spec && !active) {
+      const int rh = __popcll(H & below);
+      const int ro = rh / K;  // owner rank
+      if (ro < na) {
+        src = nth_set_bit(A, ro);
+        off = 1 + (rh - ro * K);
+      }
+    }
+    Eval es = e;
+    double ps[4] = {p[0], p[1], p[2], p[3]};
+    int lis = li;
+    QF qs = ev.q;
+    if (spec) {
+      es.ssq = shfl_any(e.ssq, src);
+      es.a00 = shfl_any(e.a00, src);
+      es.a01 = shfl_any(e.a01, src);
+      es.a02 = shfl_any(e.a02, src);
+      es.a11 = shfl_any(e.a11, src);
+      es.a12 = shfl_any(e.a12, src);
+      es.a22 = shfl_any(e.a22, src);
+      es.a33 = shfl_any(e.a33, src);
+      es.g0 = shfl_any(e.g0, src);
+      es.g1 = shfl_any(e.g1, src);
+      es.g2 = shfl_any(e.g2, src);
+      es.g3 = shfl_any(e.g3, src);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ps[i] = shfl_any(p[i], src);
+      lis = __shfl(li, src);
+      qs.p = shfl_any(ev.q.p, src);
+    }
+    const int rung = lis + off;
+    const bool work = active || (off > 0 && rung < c.n_lambda);
+    double dp[4];
+    ev.solve(es, c.lambdas[work ? rung : 0], dp);
+    const bool step = work && !norm_below(sumsq4(dp[0], dp[1], dp[2], dp[3]), c.min_step_norm);
+    double pt[4] = {ps[0] + dp[0], ps[1] + dp[1], ps[2] + dp[2], ps[3] + dp[3]};
+    Trial tt;
+    bool improved = false;
+    if (step) {
+      SplitEval<V, QF> evs{qs, ev.nd, ev.k};
+      improved = evs.trial(pt, tt) < es.ssq;
+    }
+    // active lane: the first improving rung in ladder order
+    int take = -1;     // lane whose trial this lane accepts (-1: none)
+    int skipped = 1;   // rungs evaluated without improvement (own + helpers') if none improved
+    if (active && improved) take = lane;
+    // helper results (every lane of the loop votes)
+    const uint64_t HI = __ballot(!active && improved);
+    const uint64_t HW = __ballot(!active && work);
+    if (active && !improved && spec) {
+      const int ra = __popcll(A & below);
+      const int r0 = ra * K;
+      if (r0 < nh) {
+        const int h0 = nth_set_bit(H, r0);
+        const int h1 = r0 + K < nh ? nth_set_bit(H, r0 + K) : 64;
+        const uint64_t win = H & lane_range(h0, h1);
+        const uint64_t hit = HI & win;
+        if (hit) {
+          take = __builtin_ctzll(hit);
+        } else {
+          skipped += __popcll(HW & win);
+        }
+      }
+    }
+    // the taken rung's point and trial state (this lane's own, or its helper's)
+    const bool any_take = __ballot(take >= 0 && take != lane) != 0;
+    if (any_take) {
+      const int from = take >= 0 ? take : lane;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pt[i] = shfl_any(pt[i], from);
+      double* tv = reinterpret_cast<double*>(&tt);
+#pragma unroll
+      for (int i = 0; i < NT; ++i) tv[i] = shfl_any(tv[i], from);
+    }
+    if (active) {
+      if (take >= 0) {
+        const double change2 = sumsq4(pt[0] - p[0], pt[1] - p[1], pt[2] - p[2], pt[3] - p[3]);
+        p[0] = pt[0];
+        p[1] = pt[1];
+        p[2] = pt[2];
+        p[3] = pt[3];
+        const double best_ssq = tt.ssq;  // the taken trial's ssqf
+        ev.accept(p, tt, e);  // coeffs(ndata, data, parm) at the accepted point (fit.py:251)
+        ++it;
+        li = 0;
+        if (((e.ssq - best_ssq) < c.conv_improve && norm_below(change2, c.conv_param_change)) ||
+            it >= c.max_steps)
+          active = false;
+      } else {
+        li += skipped;
+        if (li >= c.n_lambda) active = false;  // no lambda improved: fit.py:246-247
+      }
+    }
   }
   return e.ssq;
 }
@@ -797,11 +986,12 @@ DFMI_HDI void m_grid_seed(QF&& Q, int ndata, const double* __restrict__ jtab, co
 // Ev: the evaluator (FullEval / SplitEval); FLAT = false runs the nested descent
 // (host build / equivalence tests). Q: QI accessor for the m-grid re-seed (runtime
 // harmonic index: memory, never a register array).
-template <bool FLAT = true, typename Ev, typename QF>
+template <int FLAT = 1, typename Ev, typename QF>
 DFMI_HDI int fit_segment_t(Ev&& ev, QF&& Q, int ndata, const double* __restrict__ jtab, const LMConst& c,
                            double (&p)[4], double& ssq_out) {
   auto descend = [&](double (&pp)[4]) {
-    if constexpr (FLAT) return lm_descend_flat(ev, pp, c);
+    if constexpr (FLAT == 2) return lm_descend_spec(ev, pp, c);
+    else if constexpr (FLAT == 1) return lm_descend_flat(ev, pp, c);
     else return lm_descend(ev, pp, c);
   };
   double ssq = descend(p);
@@ -841,21 +1031,24 @@ DFMI_HDI int fit_segment_t(Ev&& ev, QF&& Q, int ndata, const double* __restrict_
 // NDMAX > 0: register path (requires ndata <= NDMAX); NDMAX == 0: general path.
 // qe: QI accessor of the LM evaluations (compile-time harmonic index after
 // unrolling); qm: QI in memory for the m-grid re-seed (runtime harmonic index).
-template <int NDMAX, typename QE, typename QM, bool FLAT = true>
+template <int NDMAX, typename QE, typename QM, int FLAT = 1>
 __host__ __device__ __forceinline__ int fit_segment_q2(const QE& qe, const QM& qm, int ndata,
                                                     const double* __restrict__ jtab, const LMConst& c,
                                                     double (&p)[4], double& ssq_out) {
-  if constexpr (NDMAX > 0) {
+  if constexpr (NDMAX > 0 && FLAT == 3) {
+    FusedEval<NDMAX, QE> ev{qe, ndata, c.trig};
+    return fit_segment_t<1>(ev, qm, ndata, jtab, c, p, ssq_out);
+  } else if constexpr (NDMAX > 0) {
     SplitEval<NDMAX, QE> ev{qe, ndata, c.trig};
     return fit_segment_t<FLAT>(ev, qm, ndata, jtab, c, p, ssq_out);
   } else {
     auto evalf = [&](const double (&pp)[4], Eval& e) { eval_gen(qe, ndata, pp, e); };
     FullEval<decltype(evalf)> ev{evalf};
-    return fit_segment_t<FLAT>(ev, qm, ndata, jtab, c, p, ssq_out);
+    return fit_segment_t<(FLAT >= 2 ? 1 : FLAT)>(ev, qm, ndata, jtab, c, p, ssq_out);
   }
 }
 
-template <int NDMAX, typename QF, bool FLAT = true>
+template <int NDMAX, typename QF, int FLAT = 1>
 __host__ __device__ __forceinline__ int fit_segment_q(const QF& q, int ndata, const double* __restrict__ jtab,
                                                    const LMConst& c, double (&p)[4], double& ssq_out) {
   return fit_segment_q2<NDMAX, QF, QF, FLAT>(q, q, ndata, jtab, c, p, ssq_out);
@@ -864,12 +1057,12 @@ __host__ __device__ __forceinline__ int fit_segment_q(const QF& q, int ndata, co
 // Component-major QI (qi[c·ld + s], qptr = qi + s). QI is re-read per evaluation
 // through the vector L1 (64 segments x 2·ndata doubles = 10 KB per wave): keeping
 // it in registers costs 2·NDMAX VGPRs and with them the second wave per SIMD.
-template <int NDMAX>
+template <int NDMAX, int FLAT = 1>
 __host__ __device__ __forceinline__ int fit_segment(const double* __restrict__ qptr, int64_t ld, int ndata,
                                                  const double* __restrict__ jtab, const LMConst& c, double (&p)[4],
                                                  double& ssq_out) {
   const QGlobal qg{qptr, ld, ndata};
-  return fit_segment_q<NDMAX>(qg, ndata, jtab, c, p, ssq_out);
+  return fit_segment_q<NDMAX, QGlobal, FLAT>(qg, ndata, jtab, c, p, ssq_out);
 }
 
 // Seeds of up to 8 records passed by value (read with constant offsets only).
@@ -891,13 +1084,16 @@ struct GuessInline {
 // With the register path the wave first stages its 64 rows into LDS, transposed
 // ([pos][65]: conflict-free column reads), with coalesced 16-B loads when the
 // rows are contiguous — each QI value is then read from LDS at every evaluation.
-template <int NDMAX, bool CHAIN, bool ROWS = false>
+template <int NDMAX, bool CHAIN, bool ROWS = false, int SPEC = 0>
 __global__ __launch_bounds__(64) void lm_chunks_kernel(
     const double* __restrict__ qi, int64_t qi_ld, int ndata, int64_t nrec, int64_t nbuf, int64_t first,
     int64_t nitems, int64_t nchunk, const double* __restrict__ guess, int64_t g_rec, int64_t g_comp,
     GuessInline ginl, int use_inline, const double* __restrict__ jtab, LMConst c, double* __restrict__ out,
     int64_t out_ld, int32_t* __restrict__ status) {
   static_assert(!(ROWS && CHAIN), "row layout: chunk size 1 only");
+  // SPEC (register path, no chains): 1 = the lambda ladder speculated by finished lanes
+  // (lm_descend_spec), 2 = one fused ssqf + coeffs evaluation per trial (FusedEval)
+  constexpr int kFlat = (SPEC && NDMAX > 0 && !CHAIN) ? SPEC + 1 : 1;
   extern __shared__ double lds_q[];  // STAGE: [qi_ld][65]
   const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = id < nrec * nchunk;
@@ -960,7 +1156,7 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
     double dcv;
     if constexpr (STAGE) {
       const QRow<65> q{lds_q + threadIdx.x};  // QI read from LDS at every evaluation
-      st = fit_segment_q<NDMAX>(q, ndata, jtab, c, p, ssq);
+      st = fit_segment_q<NDMAX, QRow<65>, kFlat>(q, ndata, jtab, c, p, ssq);
       dcv = q.at(dfmi_row_dc(ndata));
     } else {
       const QRow<1> q{qi + s0 * qi_ld};
@@ -975,7 +1171,7 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
     auto one = [&](int64_t sidx) {
       double ssq;
       int st;
-      st = fit_segment<NDMAX>(qi + sidx, qi_ld, ndata, jtab, c, p, ssq);
+      st = fit_segment<NDMAX, kFlat>(qi + sidx, qi_ld, ndata, jtab, c, p, ssq);
       put(sidx, st, ssq);
     };
     if constexpr (!CHAIN) {

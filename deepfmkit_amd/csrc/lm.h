@@ -1115,12 +1115,26 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
     if (contiguous) {
       const double* __restrict__ base = qi + sl0 * qi_ld;
       const int tot = nv * QS;  // doubles, even
-      for (int e = 2 * lane; e < tot; e += 128) {
-        typedef double d2v __attribute__((ext_vector_type(2)));
-        const d2v v = *reinterpret_cast<const d2v*>(base + e);
-        const int row = e / QS, pos = e - row * QS;
-        lds_q[pos * 65 + row] = v.x;
-        lds_q[(pos + 1) * 65 + row] = v.y;
+      // groups of kStageLoads 16-B loads issued together, then written to LDS: one memory
+      // round trip per 16 KB (64 rows of 32 doubles) instead of one per 1-KB load
+      constexpr int kStageLoads = 16;
+      typedef double d2v __attribute__((ext_vector_type(2)));
+      for (int e0 = 2 * lane; e0 < tot; e0 += 128 * kStageLoads) {
+        d2v v[kStageLoads];
+#pragma unroll
+        for (int u = 0; u < kStageLoads; ++u) {
+          const int e = e0 + 128 * u;
+          v[u] = e < tot ? *reinterpret_cast<const d2v*>(base + e) : d2v{0.0, 0.0};
+        }
+#pragma unroll
+        for (int u = 0; u < kStageLoads; ++u) {
+          const int e = e0 + 128 * u;
+          if (e < tot) {
+            const int row = e / QS, pos = e - row * QS;
+            lds_q[pos * 65 + row] = v[u].x;
+            lds_q[(pos + 1) * 65 + row] = v[u].y;
+          }
+        }
       }
     } else if (valid) {
       for (int pos = 0; pos < QS; ++pos) lds_q[pos * 65 + lane] = qi[s0 * qi_ld + pos];

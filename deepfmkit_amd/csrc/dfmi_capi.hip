@@ -294,9 +294,11 @@ struct Tuning {
   int ekf_row = 1;             // EKF: ekf_row_kernel (4 channels per wave) up to ekf_row x 4 x 4 x CUs channels
                                // (ekf_row waves per SIMD: past one the issue-bound rows share a SIMD, and one
                                // lane per channel carries 16x the channels per instruction); 0 = ekf_kernel only
-  int lm_spec = 0;             // LM (chunk size 1, register path; same bits in every mode): 1 = the lambda ladder
+  int lm_spec = 3;             // LM (chunk size 1, register path; same bits in every mode): 1 = the lambda ladder
                                // speculated by the wave's finished lanes (lm.h lm_descend_spec), 2 = one fused
-                               // ssqf + coeffs evaluation per trial (lm.h FusedEval), 0 = split trial / accept
+                               // ssqf + coeffs evaluation per trial (lm.h FusedEval), 3 = split, QI held in
+                               // registers (ndata 10; default: step 0.5558 -> 0.5507 ms), 0 = split trial /
+                               // accept, QI read from LDS / L1 at every evaluation
   int demod_spw = 2;           // bin kernels: grid sized for ~this many segments per wave (0: one persistent
                                // wave per slot); later workgroups go to the slots that free first
 };
@@ -561,6 +563,7 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
            : nd_sel <= 12 ? dfmi::lm_chunks_kernel<12, false, false, 1>
            : nd_sel <= 16 ? dfmi::lm_chunks_kernel<16, false, false, 1>
                           : kern;
+  if (spec == 3 && nd_sel == 10) kern = dfmi::lm_chunks_kernel<kNd10, false, false, 3>;
   if (spec == 2)
     kern = nd_sel == 10   ? dfmi::lm_chunks_kernel<kNd10, false, false, 2>
            : nd_sel <= 12 ? dfmi::lm_chunks_kernel<12, false, false, 2>
@@ -614,6 +617,7 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
   if (rows) {
     kern = nd_sel == 10   ? (spec == 1   ? dfmi::lm_chunks_kernel<kNd10, false, true, 1>
                              : spec == 2 ? dfmi::lm_chunks_kernel<kNd10, false, true, 2>
+                             : spec == 3 ? dfmi::lm_chunks_kernel<kNd10, false, true, 3>
                                          : dfmi::lm_chunks_kernel<kNd10, false, true>)
            : nd_sel <= 12 ? (spec == 1   ? dfmi::lm_chunks_kernel<12, false, true, 1>
                              : spec == 2 ? dfmi::lm_chunks_kernel<12, false, true, 2>
@@ -851,7 +855,7 @@ const std::map<std::string, Knob>& knobs() {
       {"lm_waves_per_simd", {&g_tune.lm_waves_per_simd, {1, 2, 3, 4}}},
       {"lm_tile_min", {&g_tune.lm_tile_min, {16, 32, 48, 64, 96, 128}}},
       {"lm_phase", {&g_tune.lm_phase, {0, 1}}},
-      {"lm_spec", {&g_tune.lm_spec, {0, 1, 2}}},
+      {"lm_spec", {&g_tune.lm_spec, {0, 1, 2, 3}}},
       {"lm_pa", {&g_tune.lm_pa, {}}},
       {"lm_pa_w2", {&g_tune.lm_pa_w2, {0, 1}}},
       {"demod_spw", {&g_tune.demod_spw, {}}},

@@ -518,6 +518,23 @@ struct QRow {
   DFMI_HDI double at(int pos) const { return p[pos * STRIDE]; }
 };
 
+// QI of one segment held in registers (N harmonics, read once from another accessor):
+// the register path's evaluations then index it with compile-time harmonics only.
+template <int N>
+struct QRegs {
+  double c[N], s[N];
+  template <typename QF>
+  DFMI_HDI void load(const QF& q) {
+#pragma unroll
+    for (int h = 0; h < N; ++h) {
+      c[h] = q.qc(h);
+      s[h] = q.qs(h);
+    }
+  }
+  DFMI_HDI double qc(int h) const { return c[h]; }
+  DFMI_HDI double qs(int h) const { return s[h]; }
+};
+
 template <typename QF>
 DFMI_HDI void eval_gen(const QF& q, int nd, const double (&p)[4], Eval& e) {
   const double a = p[0], m = p[1], phi = p[2], psi = p[3];
@@ -1093,7 +1110,9 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
   static_assert(!(ROWS && CHAIN), "row layout: chunk size 1 only");
   // SPEC (register path, no chains): 1 = the lambda ladder speculated by finished lanes
   // (lm_descend_spec), 2 = one fused ssqf + coeffs evaluation per trial (FusedEval)
-  constexpr int kFlat = (SPEC && NDMAX > 0 && !CHAIN) ? SPEC + 1 : 1;
+  // 3 = the split descent with the segment's QI held in registers (exact-ndata variant)
+  constexpr bool kQReg = SPEC == 3 && nd_exact(NDMAX) && !CHAIN;
+  constexpr int kFlat = (SPEC && SPEC < 3 && NDMAX > 0 && !CHAIN) ? SPEC + 1 : 1;
   extern __shared__ double lds_q[];  // STAGE: [qi_ld][65]
   const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = id < nrec * nchunk;
@@ -1170,7 +1189,13 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
     double dcv;
     if constexpr (STAGE) {
       const QRow<65> q{lds_q + threadIdx.x};  // QI read from LDS at every evaluation
-      st = fit_segment_q<NDMAX, QRow<65>, kFlat>(q, ndata, jtab, c, p, ssq);
+      if constexpr (kQReg) {
+        QRegs<nd_cap(NDMAX)> qr;
+        qr.load(q);
+        st = fit_segment_q2<NDMAX, QRegs<nd_cap(NDMAX)>, QRow<65>, 1>(qr, q, ndata, jtab, c, p, ssq);
+      } else {
+        st = fit_segment_q<NDMAX, QRow<65>, kFlat>(q, ndata, jtab, c, p, ssq);
+      }
       dcv = q.at(dfmi_row_dc(ndata));
     } else {
       const QRow<1> q{qi + s0 * qi_ld};
@@ -1185,7 +1210,14 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
     auto one = [&](int64_t sidx) {
       double ssq;
       int st;
-      st = fit_segment<NDMAX, kFlat>(qi + sidx, qi_ld, ndata, jtab, c, p, ssq);
+      if constexpr (kQReg) {
+        const QGlobal qg{qi + sidx, qi_ld, ndata};
+        QRegs<nd_cap(NDMAX)> qr;
+        qr.load(qg);
+        st = fit_segment_q2<NDMAX, QRegs<nd_cap(NDMAX)>, QGlobal, 1>(qr, qg, ndata, jtab, c, p, ssq);
+      } else {
+        st = fit_segment<NDMAX, kFlat>(qi + sidx, qi_ld, ndata, jtab, c, p, ssq);
+      }
       put(sidx, st, ssq);
     };
     if constexpr (!CHAIN) {

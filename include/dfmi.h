@@ -262,9 +262,9 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
  * "bins_prefetch" (0 | 4 [default] | 6: chunks of the next segment loaded during a
  * segment's contraction), "bins_ilv" (1 = contraction interleaved with the next
  * segment's loads), "demod_spw" (segments per wave the bin grid is sized for; 0 =
- * persistent), "lm_spec" (LM descent schedule, same bits: 0 split trial / accept
- * [default], 1 lambda ladder speculated by finished lanes, 2 fused ssqf + coeffs per
- * trial), "lm_refill" / "lm_phase" (LM lane refill / two phases with compaction, same
+ * persistent), "lm_spec" (LM descent schedule, same bits: 0 split trial / accept,
+ * 1 lambda ladder speculated by finished lanes, 2 fused ssqf + coeffs per trial, 3 split
+ * with the segment's QI in registers [default; ndata 10, others use 0]), "lm_refill" / "lm_phase" (LM lane refill / two phases with compaction, same
  * bits), "ekf_row" (EKF row kernel), "wdfmi_accel" (bit 0: W-DFMI
  * time axis without division, bit 1: template slopes in LDS; both exact), "probe"
  * (1 = diagnostics timestamps, dfmi_probe_read). */

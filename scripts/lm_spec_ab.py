@@ -1,5 +1,5 @@
 """LM-only time (dfmi_lm over config-2 QI, chunk size 1) in the three descent modes of
-the knob lm_spec (0 split trial / accept, 1 speculative ladder, 2 fused evaluation), interleaved in one process, at 1 024 / 65 536 / 100 000
+the knob lm_spec (0 split trial / accept, 1 speculative ladder, 2 fused evaluation, 3 QI in registers), interleaved in one process, at 1 024 / 65 536 / 100 000
 segments (guess [1, 6, 0, 0] as in scripts/lm_variant_ab.py, and the record seed)."""
 import json
 import os
@@ -35,7 +35,7 @@ for nseg in (1024, 65536, 100000):
             _lib.check(lib.dfmi_lm(qi.data_ptr(), nseg, nd, g.data_ptr(), 0, nseg, F.lm_config(), p.data_ptr(),
                                    ssq.data_ptr(), status.data_ptr(), 1, st.cuda_stream), "lm")
         for rep in range(3):
-            for spec in (0, 1, 2):
+            for spec in (0, 1, 2, 3):
                 _lib.check(lib.dfmi_set_tuning(b"lm_spec", spec), "tuning")
                 lm()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -45,5 +45,5 @@ for nseg in (1024, 65536, 100000):
                 e1.record(st)
                 torch.cuda.synchronize()
                 res.setdefault(f"{nseg}_{gname}_spec{spec}", []).append(round(e0.elapsed_time(e1) / 20, 4))
-_lib.check(lib.dfmi_set_tuning(b"lm_spec", 0), "tuning")
+_lib.check(lib.dfmi_set_tuning(b"lm_spec", 3), "tuning")
 print(json.dumps(res), flush=True)

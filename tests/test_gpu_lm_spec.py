@@ -2,8 +2,10 @@
 - lm_spec 1, the speculative lambda ladder (lm.h lm_descend_spec): finished lanes
   evaluate later rungs of the active lanes' ladders (fit.py:221-238), and every lane
   still accepts the first improving rung in ladder order;
-- lm_spec 2, one fused ssqf + coeffs evaluation per trial (lm.h FusedEval).
-Fits must be bit-identical to the default split trial / accept descent (lm_spec 0):
+- lm_spec 2, one fused ssqf + coeffs evaluation per trial (lm.h FusedEval);
+- lm_spec 3 (the default), the split descent with the segment's QI held in registers
+  (ndata 10).
+Fits must be bit-identical to the split trial / accept descent (lm_spec 0):
 - the golden LM vectors (incl. noise-dominated status-2 fits, a<0 / m<0 / a=0 / m=0
   seeds, the m-grid re-seed of fit.py:336-350), every register-path ndata;
 - 20k random (QI, guess) vectors from 40 dB down to noise-only, ndata 3 / 10 / 16
@@ -29,20 +31,20 @@ def lib():
     from deepfmkit_amd import _lib
     lib = _lib.load()
     yield lib
-    _lib.check(lib.dfmi_set_tuning(b"lm_spec", 0), "dfmi_set_tuning")
+    _lib.check(lib.dfmi_set_tuning(b"lm_spec", 3), "dfmi_set_tuning")
 
 
 def _both(lib, fn):
     from deepfmkit_amd import _lib
     out = {}
-    for spec in (1, 2, 0):
+    for spec in (1, 2, 0, 3):  # ends on the default
         _lib.check(lib.dfmi_set_tuning(b"lm_spec", spec), "dfmi_set_tuning")
         out[spec] = fn()
     return out
 
 
 def _assert_same(r):
-    for spec in (1, 2):
+    for spec in (1, 2, 3):
         for x, y in zip(r[spec], r[0]):
             np.testing.assert_array_equal(np.asarray(x), np.asarray(y), err_msg=f"lm_spec {spec}")
 

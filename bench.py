@@ -244,7 +244,12 @@ def main():
     # (measured BEFORE the timed window: these ~2 x nrep untimed launches also bring the
     # GPU to its steady clocks, so a short driver window carries no ramp-up)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for _ in range(20):  # untimed: clocks ramp up over the first launches (rocprof max 0.62 vs min 0.49 ms, r02l)
+    # untimed: clocks ramp up over the first ~35 demodulation-sized launches (0.58 -> 0.50 ms,
+    # profiles/r02m kernel trace); the ramp runs on whole steps, so every launch of the
+    # roofline kernel (and its rocprof average) sees steady clocks
+    for _ in range(40):
+        step()
+    for _ in range(5):
         demod()
     nrep = max(20, args.steps)
     ev0.record(stream)

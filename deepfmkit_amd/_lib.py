@@ -24,7 +24,8 @@ SYMBOLS = ("dfmi_lm_config_default", "dfmi_demod", "dfmi_lm", "dfmi_nls_record",
            "dfmi_last_demod_kernel", "dfmi_qi_row_stride", "dfmi_qi_row_dc", "dfmi_demod_rows",
            "dfmi_probe_read", "dfmi_get_tuning", "dfmi_txt_parse_header", "dfmi_txt_shape", "dfmi_txt_read",
            "dfmi_fit_txt_write", "dfmi_py_repr", "dfmi_txt_last_error", "dfmi_wdfmi_fit", "dfmi_ekf_fit",
-           "dfmi_record_moments", "dfmi_synth_asd", "dfmi_synth_snr", "dfmi_bessel_eval")
+           "dfmi_record_moments", "dfmi_synth_asd", "dfmi_synth_snr", "dfmi_bessel_eval",
+           "dfmi_release_workspaces")
 
 
 class DFMIError(RuntimeError):
@@ -155,6 +156,8 @@ def load():
         lib.dfmi_txt_last_error.restype = ctypes.c_char_p
         lib.dfmi_get_tuning.argtypes = [ctypes.c_char_p, P]
         lib.dfmi_get_tuning.restype = ctypes.c_int
+        lib.dfmi_release_workspaces.argtypes = []
+        lib.dfmi_release_workspaces.restype = ctypes.c_int
         lib.dfmi_probe_read.argtypes = [P, i32]
         lib.dfmi_probe_read.restype = ctypes.c_int
         lib.dfmi_last_demod_kernel.argtypes = []

@@ -127,12 +127,11 @@ __device__ __forceinline__ void store_block(const double (&v)[2 * HB], int lane,
 }
 
 // dc part of fold_finish: the lane's partial sum of its bins (returned), and dc itself
-// (wave sum / R) unless the row layout carries it in a spare Q slot. store = false: the
-// partial sum only (the interleaved bin kernel's later blocks need it again).
+// (wave sum / R) unless the row layout carries it in a spare Q slot.
 template <int VEC, int MAXSLOT, int HB, bool ROWS>
 __device__ __forceinline__ double finish_dc(const double (&y)[MAXSLOT][VEC], int R, int ndata, int lane,
                                             double* __restrict__ qi, int64_t qi_ld, int64_t col,
-                                            double* __restrict__ dc, bool store = true) {
+                                            double* __restrict__ dc) {
   double tot = 0.0;
 #pragma unroll
   for (int j = 0; j < MAXSLOT; ++j)
@@ -140,7 +139,7 @@ __device__ __forceinline__ double finish_dc(const double (&y)[MAXSLOT][VEC], int
     for (int e = 0; e < VEC; ++e) tot += y[j][e];
   static_assert(!ROWS || HB == 8, "row layout uses 8-harmonic blocks");
   const int spare = ndata % HB;  // ROWS: dc slot in the last block (0: no spare slot)
-  if (store && (!ROWS || spare == 0)) {
+  if (!ROWS || spare == 0) {
     const double all = wave_sum(tot);
     if (lane == 0) {
       if constexpr (ROWS) __builtin_nontemporal_store(all / (double)R, qi + col * qi_ld + dfmi_row_dc(ndata));
@@ -358,14 +357,11 @@ __global__ __launch_bounds__(kBlockThreads) void demod_fold_kernel(
 // One segment of the bin-in-LDS fold: the wave's L bins (ybin, LDS) are zeroed,
 // every 1-KB chunk is added into them, and fold_finish contracts the lane-owned
 // bins with the basis T (LDS or global) into column / row `col` of qi (and dc).
-// ROLL: the full load groups are software-pipelined — group g+1 is issued before
-// group g is added into the bins, so the wave keeps LOADS chunks in flight while it
-// adds (same additions in the same order: same bits).
 // PFN > 0: the segment's first PFN chunks arrive prefetched in pf (nch >= PFN), and
 // the next segment's first PFN chunks (at `next`, if not null) are issued into pf
 // before this segment's contraction, so the wave has loads in flight while it
 // contracts.
-template <int MAXSLOT, int LOADS, bool NT, int HB, bool ROWS, bool ROLL = false, int PFN = 0>
+template <int MAXSLOT, int LOADS, bool NT, int HB, bool ROWS, int PFN = 0>
 __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int R, int L, int ndata,
                                              const double* __restrict__ T, double* __restrict__ ybin, int lane,
                                              const bool (&pval)[MAXSLOT], const int (&pbase)[MAXSLOT],
@@ -390,21 +386,6 @@ __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int
   const double* __restrict__ xs = xs0 + 2 * lane;
   int p0 = 0;  // bin of the chunk's first sample: (128 c) mod L
   int c = 0;
-  auto load_group = [&](int c0, double (&v)[LOADS][2]) {
-#pragma unroll
-    for (int u = 0; u < LOADS; ++u) {
-      if constexpr (NT) VecT<2>::load_nt(xs + (c0 + u) * 128, v[u]);
-      else VecT<2>::load(xs + (c0 + u) * 128, v[u]);
-    }
-  };
-  auto add_group = [&](const double (&v)[LOADS][2]) {
-#pragma unroll
-    for (int u = 0; u < LOADS; ++u) {
-      add_chunk(p0, v[u]);
-      p0 += 128;
-      if (p0 >= L) p0 -= L;
-    }
-  };
   if constexpr (PFN > 0) {
 #pragma unroll
     for (int u = 0; u < PFN; ++u) {
@@ -414,36 +395,18 @@ __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int
     }
     c = PFN;
   }
-  if constexpr (ROLL) {
-    if (LOADS <= nch) {
-      double cur[LOADS][2];
-      load_group(0, cur);
-      for (c = LOADS; c + LOADS <= nch; c += LOADS) {
-        double nxt[LOADS][2];
-        load_group(c, nxt);
-        add_group(cur);
+  for (; c + LOADS <= nch; c += LOADS) {
+    double v[LOADS][2];
 #pragma unroll
-        for (int u = 0; u < LOADS; ++u) {
-          cur[u][0] = nxt[u][0];
-          cur[u][1] = nxt[u][1];
-        }
-      }
-      add_group(cur);
+    for (int u = 0; u < LOADS; ++u) {
+      if constexpr (NT) VecT<2>::load_nt(xs + (c + u) * 128, v[u]);
+      else VecT<2>::load(xs + (c + u) * 128, v[u]);
     }
-  } else {
-    for (; c + LOADS <= nch; c += LOADS) {
-      double v[LOADS][2];
 #pragma unroll
-      for (int u = 0; u < LOADS; ++u) {
-        if constexpr (NT) VecT<2>::load_nt(xs + (c + u) * 128, v[u]);
-        else VecT<2>::load(xs + (c + u) * 128, v[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < LOADS; ++u) {
-        add_chunk(p0, v[u]);
-        p0 += 128;
-        if (p0 >= L) p0 -= L;
-      }
+    for (int u = 0; u < LOADS; ++u) {
+      add_chunk(p0, v[u]);
+      p0 += 128;
+      if (p0 >= L) p0 -= L;
     }
   }
   {
@@ -502,170 +465,18 @@ __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int
   fold_finish<2, MAXSLOT, HB, ROWS>(y, pval, pbase, R, L, ndata, T, lane, qi, qi_ld, col, dc);
 }
 
-// Block hb of the contraction of the segment whose folded bins are at yb (column col):
-// the lane-owned bins re-read from LDS, dc on block 0; same operations as fold_finish.
-template <int MAXSLOT, int HB, bool ROWS>
-__device__ __forceinline__ void bins_piece(const double* __restrict__ yb, int hb, int R, int L, int ndata,
-                                           const double* __restrict__ T, int lane, const bool (&pval)[MAXSLOT],
-                                           const int (&pbase)[MAXSLOT], double* __restrict__ qi, int64_t qi_ld,
-                                           int64_t col, double* __restrict__ dc) {
-  typedef double d2v __attribute__((ext_vector_type(2)));
-  double y[MAXSLOT][2];
-#pragma unroll
-  for (int j = 0; j < MAXSLOT; ++j) {
-    if (pval[j]) {
-      const d2v t = *reinterpret_cast<const d2v*>(yb + pbase[j]);
-      y[j][0] = t.x;
-      y[j][1] = t.y;
-    } else {
-      y[j][0] = y[j][1] = 0.0;
-    }
-  }
-  const double tot = finish_dc<2, MAXSLOT, HB, ROWS>(y, R, ndata, lane, qi, qi_ld, col, dc, hb == 0);
-  finish_block<2, MAXSLOT, HB, ROWS>(y, pval, pbase, tot, hb, R, L, ndata, T, lane, qi, qi_ld, col);
-}
-
-// Interleaved bin fold (bins_ilv): the fold of one segment into ycur with the
-// contraction of the wave's PREVIOUS segment (bins at yprev, column prev; none if
-// prev < 0) cut into its harmonic blocks, one block after each load group is issued,
-// so the wave keeps a group of chunk loads in flight while it contracts. (With the
-// contraction as one phase after the fold, the wave has at most the bins_prefetch
-// chunks in flight for its duration: the ~10 % between the bin kernel and the pure
-// read pattern of the same mapping) The fold is bins_segment's (non-roll,
-// no prefetch) and the blocks are fold_finish's: results are the same bits. Returns
-// the number of blocks of prev done. The blocks go to qi + prev·qi_ld (with the row
-// layout: a row staged in LDS, qi_ld = 0, see flush_rows).
-// Measured (knob bins_ilv, profiles/r02l_ilv.log): level with the prefetch form
-// (0.5016 vs 0.5008 ms per 100k segments), so off by default. Of the ~10 % between
-// the bin kernel and the pure read pattern, the FMAs / basis reads are not it (a
-// half-period contraction with half of both measured level, r02l_ab_half.log), the
-// overlap is not it (this form), the row stores were 3.5 % (plain -> non-temporal,
-// r02l_ab_store.log) and remain ~6 % (the same kernel with the stores compiled out:
-// 0.471 ms, r02l_ab_nostore.log) — HBM write traffic inside the read stream.
-template <int MAXSLOT, int LOADS, bool NT, int HB, bool ROWS>
-__device__ __forceinline__ int bins_fold_ilv(const double* __restrict__ xs0, int R, int L, int ndata,
-                                             const double* __restrict__ T, double* __restrict__ ycur,
-                                             const double* __restrict__ yprev, bool have_prev, int lane,
-                                             const bool (&pval)[MAXSLOT], const int (&pbase)[MAXSLOT],
-                                             double* __restrict__ qi, int64_t qi_ld, int64_t prev,
-                                             double* __restrict__ dc) {
-  typedef double d2v __attribute__((ext_vector_type(2)));
-  const int nch = R >> 7;
-  const int tail = R - (nch << 7);
-  const int nblk = (ndata + HB - 1) / HB;
-  int piece = 0;
-  auto run_piece = [&]() {
-    if (have_prev && piece < nblk) {
-      bins_piece<MAXSLOT, HB, ROWS>(yprev, piece, R, L, ndata, T, lane, pval, pbase, qi, qi_ld, prev, dc);
-      ++piece;
-    }
-  };
-  auto add_chunk = [&](int p0, const double (&v)[2]) {
-    int p = p0 + 2 * lane;
-    if (p >= L) p -= L;
-    d2v* yp = reinterpret_cast<d2v*>(ycur + p);
-    d2v t = *yp;
-    t.x += v[0];
-    t.y += v[1];
-    *yp = t;
-  };
-#pragma unroll
-  for (int j = 0; j < MAXSLOT; ++j)
-    if (pval[j]) *reinterpret_cast<d2v*>(ycur + pbase[j]) = d2v{0.0, 0.0};
-  const double* __restrict__ xs = xs0 + 2 * lane;
-  int p0 = 0;
-  int c = 0;
-  for (; c + LOADS <= nch; c += LOADS) {
-    double v[LOADS][2];
-#pragma unroll
-    for (int u = 0; u < LOADS; ++u) {
-      if constexpr (NT) VecT<2>::load_nt(xs + (c + u) * 128, v[u]);
-      else VecT<2>::load(xs + (c + u) * 128, v[u]);
-    }
-    run_piece();
-#pragma unroll
-    for (int u = 0; u < LOADS; ++u) {
-      add_chunk(p0, v[u]);
-      p0 += 128;
-      if (p0 >= L) p0 -= L;
-    }
-  }
-  {
-    const int rem = nch - c;
-    double v[LOADS][2];
-#pragma unroll
-    for (int u = 0; u < LOADS; ++u) {
-      if (u < rem) {
-        if constexpr (NT) VecT<2>::load_nt(xs + (c + u) * 128, v[u]);
-        else VecT<2>::load(xs + (c + u) * 128, v[u]);
-      }
-    }
-    const int t0 = 2 * lane;
-    double tv0 = 0.0, tv1 = 0.0;
-    if (t0 < tail) tv0 = xs[nch * 128];
-    if (t0 + 1 < tail) tv1 = xs[nch * 128 + 1];
-    run_piece();
-#pragma unroll
-    for (int u = 0; u < LOADS; ++u) {
-      if (u < rem) {
-        add_chunk(p0, v[u]);
-        p0 += 128;
-        if (p0 >= L) p0 -= L;
-      }
-    }
-    if (tail) {
-      int p = p0 + t0;
-      if (p >= L) p -= L;
-      if (t0 < tail) ycur[p] += tv0;
-      if (t0 + 1 < tail) ycur[p + 1] += tv1;
-    }
-  }
-  return piece;
-}
-
-// One wavefront per segment (grid-stride over a persistent grid of 4-wave
-// workgroups that share one LDS copy of the basis); each wave's L bins follow the
-// basis in LDS. LOADS 1-KB chunk loads per lane in flight (non-temporal: the input
-// is read once). ROWS selects the output layout (fold_finish).
-// spacer > 0: the LAST `spacer` workgroups take no segments and exit at once, so
-// a seed wave (seed.h) that was dispatched first and holds part of a CU costs
-// only idle workgroups, never segments that would wait behind it.
+// One wavefront per segment (grid-stride over 4-wave workgroups that share one LDS
+// copy of the basis); each wave's L bins follow the basis in LDS. LOADS 1-KB chunk
+// loads per lane in flight (non-temporal: the input is read once). ROWS selects the
+// output layout (fold_finish). PFN > 0 (and R >= 128·PFN): the next segment's first
+// PFN chunks are in flight during a segment's contraction (bins_segment).
 // probe (diagnostics, may be null): s_memrealtime at the entry of workgroups 0 and
 // gridDim-1 and at the exit of workgroup 0's wave 0 ([3], [4], [5]).
 constexpr int kProbeWaves = 16384;  // per-wave slots of the diagnostics probe buffer
-constexpr int kIlv = -1;  // PFN value selecting the interleaved fold/contraction (bins_fold_ilv)
-constexpr int kRowRing = 4;  // interleaved kernel, row layout: rows staged per wave before they are written
-
-// LDS bytes per workgroup the interleaved bin kernel needs beyond the basis and 4·L bins.
-DFMI_HD int ilv_extra_lds(int L, int ndata, bool rows) {
-  return (kWavesPerBlock * L + (rows ? kWavesPerBlock * (kRowRing * dfmi_row_stride(ndata) + kRowRing) : 0)) * 8;
-}
-
-// Writes the nrow rows staged at ring (qs doubles each, columns in ring_col) to
-// qi + col·qi_ld with one 16-B non-temporal store per lane (4 rows of 32 doubles per
-// wave instruction): the stores leave the segment loop, so the wave's next load waits
-// no longer behind them (vmcnt counts loads and stores in issue order). Row slots past
-// the 16·nblk written by the blocks are 0 except dc (dcpos).
-__device__ __forceinline__ void flush_rows(const double* __restrict__ ring, const int64_t* __restrict__ ring_col,
-                                           int nrow, int qs, int used, int dcpos, double* __restrict__ qi,
-                                           int64_t qi_ld, int lane) {
-  typedef double d2v __attribute__((ext_vector_type(2)));
-  const int half = qs >> 1;
-  for (int i = lane; i < nrow * half; i += 64) {
-    const int k = i / half, off = 2 * (i - k * half);
-    d2v v = *reinterpret_cast<const d2v*>(ring + k * qs + off);
-    if (off >= used) {
-      v.x = off == dcpos ? v.x : 0.0;
-      v.y = off + 1 == dcpos ? v.y : 0.0;
-    }
-    __builtin_nontemporal_store(v, reinterpret_cast<d2v*>(qi + ring_col[k] * qi_ld + off));
-  }
-}
-
-template <int MAXSLOT, int LOADS, bool ROWS, bool ROLL = false, int PFN = 0>
+template <int MAXSLOT, int LOADS, bool ROWS, int PFN = 0>
 __device__ __forceinline__ void bins_kernel_body(
     const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
-    const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc, int spacer,
+    const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc,
     uint64_t* __restrict__ probe, int block0 = 0) {
   // block0: leading workgroups that play another role (the fused seed kernel, seed.h)
   const int bid = (int)blockIdx.x - block0;
@@ -673,16 +484,15 @@ __device__ __forceinline__ void bins_kernel_body(
     if (bid == 0) probe[3] = __builtin_amdgcn_s_memrealtime();
     if ((int)blockIdx.x == (int)gridDim.x - 1) probe[4] = __builtin_amdgcn_s_memrealtime();
   }
-  const int nwork = (int)gridDim.x - block0 - spacer;
-  if (bid < 0 || bid >= nwork) return;
+  const int nwork = (int)gridDim.x - block0;
+  if (bid < 0) return;
   extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
   const int ntab = 2 * ndata * L;
   stage_table(tab, lds_dyn, ntab, threadIdx.x, kBlockThreads);
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // this wave's L phase bins (two sets of L with PFN == kIlv: current and previous segment)
-  double* __restrict__ ybin = lds_dyn + ntab + wave * (PFN == kIlv ? 2 * L : L);
+  double* __restrict__ ybin = lds_dyn + ntab + wave * L;  // this wave's L phase bins
   const int nslot = (L + 127) / 128;
   int pbase[MAXSLOT];
   bool pval[MAXSLOT];
@@ -692,43 +502,7 @@ __device__ __forceinline__ void bins_kernel_body(
     pval[j] = (j < nslot) && (pbase[j] < L);
   }
   const int64_t s0 = (int64_t)bid * kWavesPerBlock + wave, ds = (int64_t)nwork * kWavesPerBlock;
-  if constexpr (PFN == kIlv) {
-    // contraction of segment s interleaved with the fold of the wave's next segment;
-    // rows staged in an LDS ring of kRowRing rows (after the 4 waves' 2·L bins) and
-    // written kRowRing at a time by flush_rows
-    const int nblk = (ndata + kHarmBlock - 1) / kHarmBlock;
-    const int qs = dfmi_row_stride(ndata);
-    double* __restrict__ ring = lds_dyn + ntab + kWavesPerBlock * 2 * L + wave * (kRowRing * qs + kRowRing);
-    int64_t* __restrict__ ring_col = reinterpret_cast<int64_t*>(ring + kRowRing * qs);
-    int cur = 0, nrow = 0;
-    int64_t prev = -1;
-    for (int64_t s = s0; s <= nseg - 1 + ds; s += ds) {
-      const bool last = s >= nseg;  // one pass past the end: the last segment's contraction
-      const bool have = prev >= 0;
-      double* const dst = ROWS ? ring + nrow * qs : qi;
-      const int64_t dld = ROWS ? 0 : qi_ld;
-      int done = 0;
-      if (!last)
-        done = bins_fold_ilv<MAXSLOT, LOADS, true, kHarmBlock, ROWS>(x + s * seg_stride, R, L, ndata, lds_dyn,
-                                                                     ybin + cur * L, ybin + (cur ^ 1) * L, have, lane,
-                                                                     pval, pbase, dst, dld, prev, dc);
-      if (have) {
-        for (int hb = done; hb < nblk; ++hb)
-          bins_piece<MAXSLOT, kHarmBlock, ROWS>(ybin + (cur ^ 1) * L, hb, R, L, ndata, lds_dyn, lane, pval, pbase,
-                                                dst, dld, prev, dc);
-        if constexpr (ROWS) {
-          if (lane == 0) ring_col[nrow] = prev;
-          if (++nrow == kRowRing || last) {
-            flush_rows(ring, ring_col, nrow, qs, 16 * nblk, dfmi_row_dc(ndata), qi, qi_ld, lane);
-            nrow = 0;
-          }
-        }
-      }
-      if (last) break;
-      prev = s;
-      cur ^= 1;
-    }
-  } else if (PFN > 0 && (R >> 7) >= PFN) {
+  if (PFN > 0 && (R >> 7) >= PFN) {
     // software pipeline across this wave's segments (see bins_segment PFN)
     double pf[PFN > 0 ? PFN : 1][2];
     if (s0 < nseg) {
@@ -737,13 +511,13 @@ __device__ __forceinline__ void bins_kernel_body(
       for (int u = 0; u < PFN; ++u) VecT<2>::load_nt(x0 + u * 128, pf[u]);
     }
     for (int64_t s = s0; s < nseg; s += ds)
-      bins_segment<MAXSLOT, LOADS, true, kHarmBlock, ROWS, ROLL, PFN>(
-          x + s * seg_stride, R, L, ndata, lds_dyn, ybin, lane, pval, pbase, qi, qi_ld, s, dc, pf,
-          s + ds < nseg ? x + (s + ds) * seg_stride : nullptr);
+      bins_segment<MAXSLOT, LOADS, true, kHarmBlock, ROWS, PFN>(x + s * seg_stride, R, L, ndata, lds_dyn, ybin, lane,
+                                                                pval, pbase, qi, qi_ld, s, dc, pf,
+                                                                s + ds < nseg ? x + (s + ds) * seg_stride : nullptr);
   } else {
     for (int64_t s = s0; s < nseg; s += ds)
-      bins_segment<MAXSLOT, LOADS, true, kHarmBlock, ROWS, ROLL>(x + s * seg_stride, R, L, ndata, lds_dyn, ybin,
-                                                                   lane, pval, pbase, qi, qi_ld, s, dc);
+      bins_segment<MAXSLOT, LOADS, true, kHarmBlock, ROWS>(x + s * seg_stride, R, L, ndata, lds_dyn, ybin, lane, pval,
+                                                           pbase, qi, qi_ld, s, dc);
   }
   if (probe && threadIdx.x == 0 && bid == 0) probe[5] = __builtin_amdgcn_s_memrealtime();
   // per-wave exit times (probe[16 + global wave], up to kProbeWaves waves) and the
@@ -759,22 +533,12 @@ __device__ __forceinline__ void bins_kernel_body(
   }
 }
 
-template <int MAXSLOT, int LOADS, bool ROWS, bool ROLL = false, int PFN = 0>
+template <int MAXSLOT, int LOADS, bool ROWS, int PFN = 0>
 __global__ __launch_bounds__(kBlockThreads) void demod_bins_kernel(
     const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
-    const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc, int spacer,
+    const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc,
     uint64_t* __restrict__ probe) {
-  bins_kernel_body<MAXSLOT, LOADS, ROWS, ROLL, PFN>(x, nseg, seg_stride, R, L, ndata, tab, qi, qi_ld, dc, spacer,
-                                                    probe);
-}
-
-// Same kernel held to <= 128 VGPRs, i.e. 4 waves per SIMD (4 workgroups per CU).
-template <int MAXSLOT, int LOADS, bool ROWS>
-__global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void demod_bins4_kernel(
-    const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
-    const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc, int spacer,
-    uint64_t* __restrict__ probe) {
-  bins_kernel_body<MAXSLOT, LOADS, ROWS>(x, nseg, seg_stride, R, L, ndata, tab, qi, qi_ld, dc, spacer, probe);
+  bins_kernel_body<MAXSLOT, LOADS, ROWS, PFN>(x, nseg, seg_stride, R, L, ndata, tab, qi, qi_ld, dc, probe);
 }
 
 // Fallback when no short integer period exists: per-sample angles

@@ -20,8 +20,6 @@
 #include "dfmi_math.h"
 #include "ekf.h"
 #include "lm.h"
-#include "lm_refill.h"
-#include "lm_phase.h"
 #include "seed.h"
 #include "np_sum.h"
 #include "moments.h"
@@ -36,20 +34,44 @@ hipError_t bessel_eval_launch(const double* x, int64_t nx, int nmax, int method,
 namespace {
 
 thread_local std::string g_err;
-std::mutex g_mu;  // the device map, HIP initialisation and the tuning/probe globals
+std::mutex g_mu;  // the device map, HIP initialisation and the tuning knobs
 
-// One C-ABI call on this thread: clears the error, remembers the caller's stream
-// (workspaces are per stream: two DFMI_MEM_DEVICE calls in flight on different
-// streams never share scratch) and, once ensure_init has picked the device, holds
-// that DEVICE's lock — calls on different devices from different host threads run
-// concurrently; calls on one device are serialised while they enqueue.
+// Tuning knobs (dfmi_set_tuning): every knob selects a path some input can need or a
+// measured schedule; results do not depend on them. Set under g_mu; each C-ABI call
+// works on its own snapshot (CallScope), so a concurrent dfmi_set_tuning never races
+// a launch. Variants measured slower and removed in round 3 (numbers in DESIGN.md §4;
+// code in git history before commit "remove measured-slower variants"): lm_refill,
+// lm_phase, lm_spec 1/2, bins_roll, bins_ilv, bins_loads 16, demod_occ4, demod_loads /
+// demod_nt, seed_fused 0 / seed_order.
+struct Tuning {
+  int demod_kernel = 1;  // 1: bin-in-LDS kernel where it applies, 0: cycle-aligned fold kernel
+  int lm_general = 0;    // 1: force the two-pass (general) LM path for every ndata
+  int demod_spw = 2;     // bin kernels: grid sized for ~this many segments per wave (0: one persistent
+                         // wave per slot); later workgroups go to the slots that free first
+  int ekf_row = 1;       // EKF: ekf_row_kernel (4 channels per wave) up to ekf_row x 4 x 4 x CUs channels
+                         // (past one wave per SIMD the issue-bound rows share a SIMD, and one lane per
+                         // channel carries 16x the channels per instruction); 0 = ekf_kernel only
+  int wdfmi_accel = 3;   // W-DFMI: bit 0 time axis without division, bit 1 template slopes in LDS
+};
+Tuning g_tune;
+
+// One C-ABI call on this thread: clears the error, snapshots the tuning knobs,
+// remembers the caller's stream (workspaces are per stream: two DFMI_MEM_DEVICE calls
+// in flight on different streams never share scratch) and, once ensure_init has picked
+// the device, holds that DEVICE's lock — calls on different devices from different
+// host threads run concurrently; calls on one device are serialised while they enqueue.
 struct CallScope;
 thread_local CallScope* t_call = nullptr;
+thread_local Tuning t_tune;
 struct CallScope {
   std::unique_lock<std::mutex> dev_lk;
   hipStream_t stream;
   explicit CallScope(void* s = nullptr) : stream((hipStream_t)s) {
     g_err.clear();
+    {
+      std::lock_guard<std::mutex> g(g_mu);
+      t_tune = g_tune;
+    }
     t_call = this;
   }
   ~CallScope() { t_call = nullptr; }
@@ -75,18 +97,27 @@ struct DevBuf {
   int64_t aux = 0;  // pwplan: leaves of the plan
 };
 
+// Workspaces of one caller stream (name -> buffer) and when that stream last used them.
+struct StreamWs {
+  std::map<std::string, DevBuf> bufs;
+  uint64_t last_use = 0;
+};
+constexpr size_t kMaxStreamWs = 4;  // caller streams whose workspaces are kept (LRU beyond)
+
 struct DeviceState {
   bool init = false;
   int n_cu = 0;
   size_t lds_per_block = 0;
-  std::map<std::string, DevBuf> ws;                                  // named workspaces
+  std::map<uintptr_t, StreamWs> ws;                                  // caller stream -> workspaces
+  uint64_t ws_clock = 0;
   std::map<std::tuple<int, int, uint64_t>, DevBuf> basis;            // (L, ndata, w0 bits)
   std::map<std::tuple<int, uint64_t, uint64_t, uint64_t>, DevBuf> gridtab;  // (ndata, min, max, step)
   std::map<int64_t, DevBuf> pwplan;                                 // n -> numpy pairwise-sum plan
   std::map<std::pair<const void*, int>, int> occupancy;              // (kernel, LDS bytes) -> blocks per CU
   std::mutex mu;               // held by the call that drives this device (CallScope)
-  hipStream_t side = nullptr;  // seed step runs here, concurrently with the bulk demod
-  hipEvent_t ev_in = nullptr, ev_seed = nullptr, ev_bulk = nullptr;
+  hipStream_t side = nullptr;  // seed step runs here, concurrently with the bulk demod (unfused layouts)
+  hipEvent_t ev_in = nullptr, ev_seed = nullptr;
+  uint64_t* probe = nullptr;   // diagnostics timestamps of this device (dfmi_set_tuning("probe", 1))
 };
 
 std::map<int, DeviceState> g_dev;
@@ -136,18 +167,40 @@ int ensure_init_locked(int* dev_out) {
     HIPCHK(hipStreamCreateWithPriority(&ds.side, hipStreamNonBlocking, prio_hi));
     HIPCHK(hipEventCreateWithFlags(&ds.ev_in, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ds.ev_seed, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&ds.ev_bulk, hipEventDisableTiming));
     ds.init = true;
   }
   *dev_out = dev;
   return DFMI_OK;
 }
 
+int free_stream_ws(StreamWs& s) {
+  for (auto& kv : s.bufs)
+    if (kv.second.p) HIPCHK(hipFree(kv.second.p));
+  s.bufs.clear();
+  return DFMI_OK;
+}
+
+// Grow-only scratch buffer `name` of the current caller stream. Workspaces of at most
+// kMaxStreamWs caller streams are kept: a call from a further stream first waits for the
+// device to drain and frees the least recently used stream's set.
 int workspace(int dev, const char* name, size_t bytes, void** out) {
   (void)dev;
-  std::string key(name);
-  if (t_call && t_call->stream) key += "@" + std::to_string((uintptr_t)t_call->stream);
-  DevBuf& b = t_ds->ws[key];
+  const uintptr_t key = t_call ? (uintptr_t)t_call->stream : 0;
+  DeviceState& ds = *t_ds;
+  auto it = ds.ws.find(key);
+  if (it == ds.ws.end()) {
+    if (ds.ws.size() >= kMaxStreamWs) {
+      auto lru = ds.ws.begin();
+      for (auto jt = ds.ws.begin(); jt != ds.ws.end(); ++jt)
+        if (jt->second.last_use < lru->second.last_use) lru = jt;
+      HIPCHK(hipDeviceSynchronize());  // its buffers may still be read by queued work
+      if (int rc = free_stream_ws(lru->second)) return rc;
+      ds.ws.erase(lru);
+    }
+    it = ds.ws.emplace(key, StreamWs{}).first;
+  }
+  it->second.last_use = ++ds.ws_clock;
+  DevBuf& b = it->second.bufs[std::string(name)];
   if (b.n < bytes) {
     if (b.p) HIPCHK(hipFree(b.p));
     b.p = nullptr;
@@ -263,51 +316,7 @@ int to_lmconst(const dfmi_lm_config* cfg, dfmi::LMConst* c) {
 
 constexpr int kMaxSlotCap = 8;
 
-// Tuning knobs (dfmi_set_tuning): measured, then frozen as defaults. Results do
-// not depend on them, except seed_bins (the seed's fold summation order: fits move
-// by < 1e-10).
-struct Tuning {
-  int demod_loads = 8;         // fold kernel: vector loads in flight per lane (8 or 16)
-  int demod_nt = 1;            // fold kernel: non-temporal loads (+14 %, profiles/r01_tune_demod.json)
-  int demod_blocks_per_cu = 0; // 0 = occupancy limit
-  int lm_general = 0;          // 1: force the two-pass (general) LM path for every ndata
-  int demod_kernel = 1;        // 1: bin-in-LDS kernel where it applies, 0: cycle-aligned fold kernel
-  int seed_bins = 1;           // 1: seed step with the LDS fold + LDS-resident QI (seed.h seed_bins_kernel)
-  int seed_order = 1;          // 1: seed on the caller's stream, bulk demodulation on the side stream
-  int demod_occ4 = 0;          // 1: bin kernel held to 128 VGPRs (4 waves per SIMD)
-  int seed_fused = 1;          // 1: seed + bulk demodulation in one launch on the caller's stream
-  int wdfmi_accel = 3;         // W-DFMI: bit 0 time axis without division, bit 1 template slopes in LDS
-  int bins_loads = 8;          // bin kernels (L <= 256): 1-KB chunk loads in flight per wave (8 | 16)
-  int bins_roll = 0;           // bin kernels (L <= 256): next load group issued before the current one is added
-  int bins_prefetch = 4;       // bin kernels (L <= 256): next segment's first 4 (or 6; 0 = off) chunks in flight during
-                               // the contraction (+1.4 % on the step vs 0; 6 ties 4)
-  int lm_refill = 0;           // LM (chunk size 1): 1 = tiles with lane refill (lm_refill.h; measured slower, off), 0 = one segment per lane
-  int lm_waves_per_simd = 1;   // lm_refill: resident tiles per SIMD the grid is sized for (tile = items / waves)
-  int lm_tile_min = 64;        // lm_refill: smallest tile (segments per wave)
-  int lm_phase = 0;            // row-layout LM: 1 = two phases with compaction (lm_phase.h; measured 3 % slower on
-                               // the step, off), 0 = one kernel
-  int lm_pa = 3;               // lm_phase: descent passes in phase A
-  int lm_pa_w2 = 1;            // lm_phase, ndata 10: phase A held to 2 waves per SIMD
-  int bins_ilv = 0;            // bin kernels (L <= 256): contraction of the previous segment interleaved with the
-                               // fold of the next, rows staged in LDS (demod.h bins_fold_ilv); replaces bins_prefetch.
-                               // Same bits; measured level with pf4 (0.5016 vs 0.5008 ms, r02l_ilv.log): off
-  int ekf_row = 1;             // EKF: ekf_row_kernel (4 channels per wave) up to ekf_row x 4 x 4 x CUs channels
-                               // (ekf_row waves per SIMD: past one the issue-bound rows share a SIMD, and one
-                               // lane per channel carries 16x the channels per instruction); 0 = ekf_kernel only
-  int lm_spec = 3;             // LM (chunk size 1, register path; same bits in every mode): 1 = the lambda ladder
-                               // speculated by the wave's finished lanes (lm.h lm_descend_spec), 2 = one fused
-                               // ssqf + coeffs evaluation per trial (lm.h FusedEval), 3 = split, QI held in
-                               // registers (ndata 10; default: step 0.5558 -> 0.5507 ms), 0 = split trial /
-                               // accept, QI read from LDS / L1 at every evaluation
-  int demod_spw = 2;           // bin kernels: grid sized for ~this many segments per wave (0: one persistent
-                               // wave per slot); later workgroups go to the slots that free first
-};
-Tuning g_tune;
 thread_local std::string g_last_demod;  // kernel variant of the last demodulation launch (dfmi_last_demod_kernel)
-thread_local int g_idle_blocks = 0;  // bin kernel: trailing workgroups that take no segments (seed_order 1)
-uint64_t* g_probe = nullptr;  // diagnostics timestamps (dfmi_set_tuning("probe", 1), dfmi_probe_read)
-
-
 
 // hipOccupancyMaxActiveBlocksPerMultiprocessor, cached per (kernel, LDS bytes): the
 // query costs host time on every call otherwise.
@@ -338,12 +347,12 @@ int64_t persistent_grid(int n_cu, int per_cu, int64_t need) {
 // 548 us (XCC and HBM-path dependent, profiles/r02j_demod_wave_finish.jsonl) and the
 // launch ended with the slowest; ~2 segments per wave measured best (0.513-0.516 vs
 // 0.533-0.535 ms, profiles/r02k_tune_spw.json).
-int64_t bins_grid(int n_cu, int per_cu, int64_t nseg, int spacer) {
-  const int64_t need = (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock + spacer;
+int64_t bins_grid(int n_cu, int per_cu, int64_t nseg) {
+  const int64_t need = (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock;
   int64_t grid = persistent_grid(n_cu, per_cu, need);
-  if (g_tune.demod_spw > 0) {
-    const int64_t per = (int64_t)dfmi::kWavesPerBlock * g_tune.demod_spw;
-    const int64_t want = (nseg + per - 1) / per + spacer;
+  if (t_tune.demod_spw > 0) {
+    const int64_t per = (int64_t)dfmi::kWavesPerBlock * t_tune.demod_spw;
+    const int64_t want = (nseg + per - 1) / per;
     if (want > grid) grid = want;
   }
   return grid;
@@ -364,29 +373,23 @@ int32_t detect_period_impl(double w0, int32_t R, int32_t ndata) {
   return 0;
 }
 
-template <int VEC, int MS, bool LDS, int LOADS = 8, bool NT = true>
+// Cycle-aligned fold kernel (lane-owned bins in registers): the fallback for periods the
+// bin kernel does not take (L < 128, odd L, unaligned rows). 8 vector loads in flight per
+// lane, non-temporal (+14 %, profiles/r01_tune_demod.json; 16 in flight measured level).
+template <int VEC, int MS, bool LDS>
 int launch_fold_t(const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tab,
                   double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu) {
-  if constexpr (VEC == 2 && MS == 2 && LDS && LOADS == 8 && NT) {  // the BASELINE shape: tunable
-    if (g_tune.demod_loads == 16 && g_tune.demod_nt)
-      return launch_fold_t<2, 2, true, 16, true>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
-    if (g_tune.demod_loads == 16)
-      return launch_fold_t<2, 2, true, 16, false>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
-    if (!g_tune.demod_nt)
-      return launch_fold_t<2, 2, true, 8, false>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
-  }
   const size_t lds = LDS ? (size_t)2 * ndata * L * sizeof(double) : 0;
-  auto kern = dfmi::demod_fold_kernel<VEC, MS, LDS, LOADS, NT>;
+  auto kern = dfmi::demod_fold_kernel<VEC, MS, LDS, 8, true>;
   int per_cu = 0;
   if (int orc = occupancy(kern, dfmi::kBlockThreads, lds, &per_cu)) return orc;
   if (per_cu < 1) per_cu = 1;
-  if (g_tune.demod_blocks_per_cu > 0 && g_tune.demod_blocks_per_cu < per_cu) per_cu = g_tune.demod_blocks_per_cu;
   const int64_t grid = persistent_grid(n_cu, per_cu, (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(dfmi::kBlockThreads), lds, st, x, nseg, stride, R, L, ndata,
                      tab, qi, qi_ld, dc);
   HIPCHK(hipGetLastError());
   g_last_demod = "demod_fold_kernel<" + std::to_string(VEC) + "," + std::to_string(MS) + "," +
-                 std::to_string((int)LDS) + "," + std::to_string(LOADS) + "," + std::to_string((int)NT) + ">";
+                 std::to_string((int)LDS) + ",8,1>";
   return DFMI_OK;
 }
 
@@ -401,52 +404,37 @@ int launch_fold_ms(int ms, const double* x, int64_t nseg, int64_t stride, int R,
   }
 }
 
-// Interleaved bin kernel (bins_ilv): a second set of L bins per wave, within the LDS
-// budget the bin kernels keep (64 KB per workgroup).
-// With the row layout the rows are staged in LDS and written as 16-B stores (demod.h
-// flush_rows): 16-B aligned rows only.
-bool ilv_fits(int L, int ndata, size_t lds, bool rows, const double* qi, int64_t qi_ld) {
-  if (rows && ((((uintptr_t)qi) & 15) || (qi_ld & 1))) return false;
-  const size_t need = lds + (size_t)dfmi::ilv_extra_lds(L, ndata, rows);
-  return g_tune.bins_ilv && need <= 64 * 1024 && need <= t_ds->lds_per_block;
-}
-
+// The bin kernel: 8 chunk loads in flight per wave; with L <= 256 (MS 2) the next
+// segment's first 4 chunks are prefetched during the contraction (+1.4 % on the step,
+// profiles/r01g_ab_prefetch.jsonl; 6 chunks tied, 16 loads per group -1.7 %, a rolling
+// pipeline -0.7 %, the contraction interleaved with the next segment's loads level).
 template <int MS, bool ROWS>
 int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tab,
                   double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu, size_t lds) {
-  auto kern = g_tune.demod_occ4 ? dfmi::demod_bins4_kernel<MS, 8, ROWS> : dfmi::demod_bins_kernel<MS, 8, ROWS>;
-  const bool l16 = MS == 2 && g_tune.bins_loads == 16 && !g_tune.demod_occ4;
-  if (l16) kern = dfmi::demod_bins_kernel<MS, 16, ROWS>;
-  const bool roll = MS == 2 && !l16 && g_tune.bins_roll && !g_tune.demod_occ4;
-  if (roll) kern = dfmi::demod_bins_kernel<MS, 8, ROWS, true>;
-  const bool ilv = MS == 2 && !l16 && !roll && !g_tune.demod_occ4 && ilv_fits(L, ndata, lds, ROWS, qi, qi_ld);
-  if (ilv) {
-    kern = dfmi::demod_bins_kernel<MS, 8, ROWS, false, dfmi::kIlv>;
-    lds += (size_t)dfmi::ilv_extra_lds(L, ndata, ROWS);
-  }
-  const bool pf = MS == 2 && !l16 && !roll && !ilv && g_tune.bins_prefetch && !g_tune.demod_occ4;
-  if (pf) kern = g_tune.bins_prefetch == 6 ? dfmi::demod_bins_kernel<MS, 8, ROWS, false, 6>
-                                           : dfmi::demod_bins_kernel<MS, 8, ROWS, false, 4>;
+  constexpr int PFN = MS == 2 ? 4 : 0;
+  auto kern = dfmi::demod_bins_kernel<MS, 8, ROWS, PFN>;
   int per_cu = 0;
   if (int orc = occupancy(kern, dfmi::kBlockThreads, lds, &per_cu)) return orc;
   if (per_cu < 1) per_cu = 1;
-  if (g_tune.demod_blocks_per_cu > 0 && g_tune.demod_blocks_per_cu < per_cu) per_cu = g_tune.demod_blocks_per_cu;
-  const int spacer = g_idle_blocks;  // one of the grid's slots each (seed_order 1)
-  const int64_t grid = bins_grid(n_cu, per_cu, nseg, spacer);
+  const int64_t grid = bins_grid(n_cu, per_cu, nseg);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(dfmi::kBlockThreads), lds, st, x, nseg, stride, R, L, ndata,
-                     tab, qi, qi_ld, dc, (int)(spacer < grid ? spacer : 0), g_probe);
+                     tab, qi, qi_ld, dc, t_ds->probe);
   HIPCHK(hipGetLastError());
-  g_last_demod = std::string(g_tune.demod_occ4 ? "demod_bins4_kernel<" : "demod_bins_kernel<") + std::to_string(MS) + (l16 ? ",16" : ",8") + (ROWS ? ",rows" : "") + (roll ? ",roll" : "") + (ilv ? ",ilv" : "") + (pf ? (g_tune.bins_prefetch == 6 ? ",pf6" : ",pf4") : "") +
-                 (spacer ? ",spacer" + std::to_string(spacer) : "") + ">";
+  g_last_demod = std::string("demod_bins_kernel<") + std::to_string(MS) + ",8" + (ROWS ? ",rows" : "") +
+                 (PFN && (R >> 7) >= PFN ? ",pf4" : "") + ">";
   return DFMI_OK;
 }
 
-// The bin-in-LDS kernel (demod.h demod_bins_kernel) applies to 16-B rows, an even
-// basis period 128 <= L <= 1024, and a basis + 4 waves' bins that fit in LDS.
-bool bins_applicable(bool vec2, int L, int ndata, size_t lds_cap) {
-  if (g_tune.demod_kernel != 1 || !vec2 || (L & 1) || L < 128 || L > 1024) return false;
-  const size_t lds = ((size_t)2 * ndata * L + (size_t)dfmi::kWavesPerBlock * L) * sizeof(double);
+// Geometry the LDS bin fold needs (bin kernels, seed kernels): 16-B rows, an even basis
+// period 128 <= L <= 1024, and a basis + `nbins` bin sets that fit in LDS.
+bool bins_geometry(bool vec2, int L, int ndata, size_t lds_cap, int nbins) {
+  if (!vec2 || (L & 1) || L < 128 || L > 1024) return false;
+  const size_t lds = ((size_t)2 * ndata * L + (size_t)nbins * L) * sizeof(double);
   return lds <= lds_cap && lds <= 64 * 1024;
+}
+
+bool bins_applicable(bool vec2, int L, int ndata, size_t lds_cap) {
+  return t_tune.demod_kernel == 1 && bins_geometry(vec2, L, ndata, lds_cap, dfmi::kWavesPerBlock);
 }
 
 // Returns 1 if the bin kernel does not apply.
@@ -465,14 +453,17 @@ int try_bins(const double* x, int64_t nseg, int64_t stride, int R, int L, int nd
   return launch_bins_t<8, false>(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, lds);
 }
 
+bool vec2_ok(const double* x, int64_t stride, int L) {
+  return (L % 2 == 0) && (stride % 2 == 0) && (((uintptr_t)x & 15) == 0);
+}
+
 // Whether demod_device can write the row layout (dfmi_qi_row_stride) for this
 // input: only the bin-in-LDS kernel implements it.
 bool rows_supported(int dev, const double* x, int64_t stride, int R, int ndata, double w0, int period) {
   int L = period;
   if (L == 0) L = detect_period_impl(w0, R, ndata);
   if (L <= 0) return false;
-  const bool vec2 = (L % 2 == 0) && (stride % 2 == 0) && (((uintptr_t)x & 15) == 0);
-  return bins_applicable(vec2, L, ndata, t_ds->lds_per_block);
+  return bins_applicable(vec2_ok(x, stride, L), L, ndata, t_ds->lds_per_block);
 }
 
 // Device-pointer demodulation (all pointers on the current device).
@@ -483,12 +474,10 @@ int demod_device(int dev, const double* x, int64_t nseg, int64_t stride, int R, 
   if (nseg == 0) return DFMI_OK;
   int L = period;
   if (L == 0) L = detect_period_impl(w0, R, ndata);
-  struct {
-    int n_cu;
-    size_t lds_per_block;
-  } ds = {t_ds->n_cu, t_ds->lds_per_block};
+  const int n_cu = t_ds->n_cu;
+  const size_t lds_cap = t_ds->lds_per_block;
   if (L > 0) {
-    const bool vec2 = (L % 2 == 0) && (stride % 2 == 0) && (((uintptr_t)x & 15) == 0);
+    const bool vec2 = vec2_ok(x, stride, L);
     const int VEC = vec2 ? 2 : 1;
     int nslot = (L + 64 * VEC - 1) / (64 * VEC);
     if (nslot <= kMaxSlotCap) {
@@ -498,28 +487,47 @@ int demod_device(int dev, const double* x, int64_t nseg, int64_t stride, int R, 
       int rc = basis_table(dev, L, ndata, w0, st, &tab);
       if (rc) return rc;
       const size_t lds = (size_t)2 * ndata * L * sizeof(double);
-      const bool use_lds = lds <= 64 * 1024 && lds <= ds.lds_per_block;
-      rc = try_bins(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, ds.n_cu, vec2, ds.lds_per_block, rows);
+      const bool use_lds = lds <= 64 * 1024 && lds <= lds_cap;
+      rc = try_bins(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, vec2, lds_cap, rows);
       if (rc <= 0) return rc;
       if (rows) return fail(DFMI_ERR_UNSUPPORTED, "row layout needs the bin-in-LDS demodulation kernel");
       if (vec2) {
-        return use_lds ? launch_fold_ms<2, true>(ms, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, ds.n_cu)
-                       : launch_fold_ms<2, false>(ms, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, ds.n_cu);
+        return use_lds ? launch_fold_ms<2, true>(ms, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu)
+                       : launch_fold_ms<2, false>(ms, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
       }
-      return use_lds ? launch_fold_ms<1, true>(ms, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, ds.n_cu)
-                     : launch_fold_ms<1, false>(ms, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, ds.n_cu);
+      return use_lds ? launch_fold_ms<1, true>(ms, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu)
+                     : launch_fold_ms<1, false>(ms, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
     }
   }
   if (rows) return fail(DFMI_ERR_UNSUPPORTED, "row layout needs the bin-in-LDS demodulation kernel");
   // direct kernel
   int64_t need = (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock;
-  int64_t grid = (int64_t)ds.n_cu * 8;
+  int64_t grid = (int64_t)n_cu * 8;
   if (grid > need) grid = need;
   hipLaunchKernelGGL(dfmi::demod_direct_kernel, dim3((unsigned)grid), dim3(dfmi::kBlockThreads), 0, st, x, nseg,
                      stride, R, ndata, w0, qi, qi_ld, dc);
   HIPCHK(hipGetLastError());
   g_last_demod = "demod_direct_kernel";
   return DFMI_OK;
+}
+
+// LM kernel selection: the register path (ndata <= 16; the exact-ndata variant with QI
+// in registers for the reference default ndata = 10) or the general path (any ndata,
+// or lm_general = 1). CHAIN: warm-start chains (sequential / n_cores chunks).
+template <bool CHAIN, bool ROWS>
+auto lm_kernel(int nd_sel) {
+  constexpr int kNd10 = dfmi::kExactNd | 10;
+  if constexpr (CHAIN) {
+    return nd_sel == 10   ? dfmi::lm_chunks_kernel<kNd10, true>
+           : nd_sel <= 12 ? dfmi::lm_chunks_kernel<12, true>
+           : nd_sel <= 16 ? dfmi::lm_chunks_kernel<16, true>
+                          : dfmi::lm_chunks_kernel<0, true>;
+  } else {
+    return nd_sel == 10   ? dfmi::lm_chunks_kernel<kNd10, false, ROWS, true>
+           : nd_sel <= 12 ? dfmi::lm_chunks_kernel<12, false, ROWS>
+           : nd_sel <= 16 ? dfmi::lm_chunks_kernel<16, false, ROWS>
+                          : dfmi::lm_chunks_kernel<0, false, ROWS>;
+  }
 }
 
 int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec, int64_t nbuf, int64_t first,
@@ -543,91 +551,13 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
   const int64_t lanes = nrec * nchunk;
   const int block = 64;
   const int64_t grid = (lanes + block - 1) / block;
-  // register path for ndata <= 16 (QI/Bessel in registers), general path above
   const bool chain = nitems > nchunk;
-  const int nd_sel = g_tune.lm_general ? 1000 : ndata;
+  const int nd_sel = t_tune.lm_general ? 1000 : ndata;
   if (rows && chain) return fail(DFMI_ERR_ARG, "row layout: chunk size 1 only");
   size_t lds = 0;
-  auto kern = chain ? (nd_sel <= 12   ? dfmi::lm_chunks_kernel<12, true>
-                       : nd_sel <= 16 ? dfmi::lm_chunks_kernel<16, true>
-                                     : dfmi::lm_chunks_kernel<0, true>)
-                    : (nd_sel <= 12   ? dfmi::lm_chunks_kernel<12, false>
-                       : nd_sel <= 16 ? dfmi::lm_chunks_kernel<16, false>
-                                     : dfmi::lm_chunks_kernel<0, false>);
-  // ndata == 10 (the reference default): the exact-ndata register variant (no masking)
-  constexpr int kNd10 = dfmi::kExactNd | 10;
-  if (nd_sel == 10) kern = chain ? dfmi::lm_chunks_kernel<kNd10, true> : dfmi::lm_chunks_kernel<kNd10, false>;
-  const int spec = chain ? 0 : g_tune.lm_spec;
-  if (spec == 1)
-    kern = nd_sel == 10   ? dfmi::lm_chunks_kernel<kNd10, false, false, 1>
-           : nd_sel <= 12 ? dfmi::lm_chunks_kernel<12, false, false, 1>
-           : nd_sel <= 16 ? dfmi::lm_chunks_kernel<16, false, false, 1>
-                          : kern;
-  if (spec == 3 && nd_sel == 10) kern = dfmi::lm_chunks_kernel<kNd10, false, false, 3>;
-  if (spec == 2)
-    kern = nd_sel == 10   ? dfmi::lm_chunks_kernel<kNd10, false, false, 2>
-           : nd_sel <= 12 ? dfmi::lm_chunks_kernel<12, false, false, 2>
-           : nd_sel <= 16 ? dfmi::lm_chunks_kernel<16, false, false, 2>
-                          : kern;
-  if (!chain && g_tune.lm_refill && nd_sel <= 16 && guess_dev) {
-    // tiles of up to kRefillTmax segments, one wave each, lanes refilled from the tile
-    const int64_t total = nrec * nitems;
-    const int64_t waves = (int64_t)t_ds->n_cu * 4 * (g_tune.lm_waves_per_simd > 0 ? g_tune.lm_waves_per_simd : 1);
-    int64_t tile = (total + waves - 1) / waves;
-    if (tile < g_tune.lm_tile_min) tile = g_tune.lm_tile_min;
-    if (tile > dfmi::kRefillTmax) tile = dfmi::kRefillTmax;
-    const int64_t ntile = (total + tile - 1) / tile;
-    const size_t rl = dfmi::lm_refill_lds(rows ? (int)qi_ld : dfmi_row_stride(ndata), (int)tile);
-    const bool w2 = g_tune.lm_waves_per_simd >= 2;
-    auto rk = rows ? (nd_sel == 10 ? (w2 ? dfmi::lm_refill_kernel<kNd10, true, 2> : dfmi::lm_refill_kernel<kNd10, true>)
-                      : nd_sel <= 12 ? dfmi::lm_refill_kernel<12, true> : dfmi::lm_refill_kernel<16, true>)
-                   : (nd_sel == 10 ? (w2 ? dfmi::lm_refill_kernel<kNd10, false, 2> : dfmi::lm_refill_kernel<kNd10, false>)
-                      : nd_sel <= 12 ? dfmi::lm_refill_kernel<12, false> : dfmi::lm_refill_kernel<16, false>);
-    hipLaunchKernelGGL(rk, dim3((unsigned)ntile), dim3(64), rl, st, qi, qi_ld, ndata, nrec, nbuf, first, nitems,
-                       (int)tile, guess_dev, g_rec, g_comp, jtab, c, out, out_ld, status,
-                       (unsigned long long*)g_probe);
-    HIPCHK(hipGetLastError());
-    return DFMI_OK;
-  }
-  if (rows && g_tune.lm_phase && nd_sel <= 16 && guess_dev && nd_sel > 0) {
-    // two phases: <= lm_pa passes for every segment, then the compacted rest (lm_phase.h)
-    const int64_t total = nrec * nitems;
-    void *wl = nullptr, *wm = nullptr, *wc = nullptr;
-    int rc;
-    if ((rc = workspace(dev, "lm_list", (size_t)dfmi::kLmSt * total * sizeof(double), &wl))) return rc;
-    if ((rc = workspace(dev, "lm_meta", (size_t)total * sizeof(int4), &wm))) return rc;
-    if ((rc = workspace(dev, "lm_count", 64, &wc))) return rc;
-    HIPCHK(hipMemsetAsync(wc, 0, 8, st));
-    const size_t tl = (size_t)qi_ld * 65 * sizeof(double);
-    auto ka = nd_sel == 10 ? (g_tune.lm_pa_w2 ? dfmi::lm_phase_a_kernel<kNd10, 2> : dfmi::lm_phase_a_kernel<kNd10, 1>)
-              : nd_sel <= 12 ? dfmi::lm_phase_a_kernel<12> : dfmi::lm_phase_a_kernel<16>;
-    auto kb = nd_sel == 10 ? dfmi::lm_phase_b_kernel<kNd10> : nd_sel <= 12 ? dfmi::lm_phase_b_kernel<12>
-                                                                            : dfmi::lm_phase_b_kernel<16>;
-    hipLaunchKernelGGL(ka, dim3((unsigned)((total + 63) / 64)), dim3(64), tl, st, qi, qi_ld, ndata, nrec, nbuf, first,
-                       nitems, g_tune.lm_pa, guess_dev, g_rec, g_comp, jtab, c, out, out_ld, status, (double*)wl,
-                       (int4*)wm, total, (unsigned long long*)wc);
-    HIPCHK(hipGetLastError());
-    int64_t gb = (int64_t)t_ds->n_cu * 4;
-    if (gb > (total + 63) / 64) gb = (total + 63) / 64;
-    hipLaunchKernelGGL(kb, dim3((unsigned)gb), dim3(64), tl, st, qi, qi_ld, ndata, jtab, c, out, out_ld, status,
-                       (const double*)wl, (const int4*)wm, total, (const unsigned long long*)wc);
-    HIPCHK(hipGetLastError());
-    return DFMI_OK;
-  }
-  if (rows) {
-    kern = nd_sel == 10   ? (spec == 1   ? dfmi::lm_chunks_kernel<kNd10, false, true, 1>
-                             : spec == 2 ? dfmi::lm_chunks_kernel<kNd10, false, true, 2>
-                             : spec == 3 ? dfmi::lm_chunks_kernel<kNd10, false, true, 3>
-                                         : dfmi::lm_chunks_kernel<kNd10, false, true>)
-           : nd_sel <= 12 ? (spec == 1   ? dfmi::lm_chunks_kernel<12, false, true, 1>
-                             : spec == 2 ? dfmi::lm_chunks_kernel<12, false, true, 2>
-                                         : dfmi::lm_chunks_kernel<12, false, true>)
-           : nd_sel <= 16 ? (spec == 1   ? dfmi::lm_chunks_kernel<16, false, true, 1>
-                             : spec == 2 ? dfmi::lm_chunks_kernel<16, false, true, 2>
-                                         : dfmi::lm_chunks_kernel<16, false, true>)
-                          : dfmi::lm_chunks_kernel<0, false, true>;
-    if (nd_sel <= 16) lds = (size_t)qi_ld * 65 * sizeof(double);  // the wave's rows, transposed
-  }
+  auto kern = chain ? lm_kernel<true, false>(nd_sel) : rows ? lm_kernel<false, true>(nd_sel)
+                                                            : lm_kernel<false, false>(nd_sel);
+  if (rows && nd_sel <= 16) lds = (size_t)qi_ld * 65 * sizeof(double);  // the wave's rows, transposed
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(block), lds, st, qi, qi_ld, ndata, nrec, nbuf, first, nitems,
                      nchunk, guess_dev, g_rec, g_comp, ginl, use_inline, jtab, c, out, out_ld, status);
   HIPCHK(hipGetLastError());
@@ -641,55 +571,76 @@ int fused_seed_demod(int dev, const double* x, int64_t nrec, int64_t nbuf, int R
                      const double* tab, double* rows, int64_t qs, const double* gdev, const dfmi::GuessInline& ginl,
                      const double* jtab, const dfmi::LMConst& c, double* out, int64_t out_ld, int32_t* fitok,
                      hipStream_t st) {
-  if (!g_tune.seed_fused || ndata > 16 || L <= 0) return 1;
+  if (ndata > 16 || L <= 0) return 1;
   const int nslot = (L + 127) / 128;
   if (nslot > 8) return 1;
   using K = void (*)(const double*, int64_t, int64_t, int64_t, int, int, int, const double*, double*, int64_t,
                      const double*, dfmi::GuessInline, int, const double*, dfmi::LMConst, double*, int64_t, int64_t,
                      int32_t*, uint64_t*);
+  const bool pf = nslot <= 2 && ndata <= 12;  // bins_segment's prefetch (bulk path, MS 2)
   K kern;
-  size_t lds = ((size_t)2 * ndata * L + (size_t)dfmi::kWavesPerBlock * L) * sizeof(double);
-  const bool ilv = nslot <= 2 && ndata <= 12 && g_tune.bins_loads != 16 && !g_tune.bins_roll &&
-                   ilv_fits(L, ndata, lds, true, rows, qs);
-  if (ilv) lds += (size_t)dfmi::ilv_extra_lds(L, ndata, true);
+  const size_t lds = ((size_t)2 * ndata * L + (size_t)dfmi::kWavesPerBlock * L) * sizeof(double);
   if (ndata <= 12)
-    kern = nslot <= 2 ? (g_tune.bins_loads == 16 ? dfmi::demod_seed_bins_kernel<2, 12, 16>
-                         : g_tune.bins_roll       ? dfmi::demod_seed_bins_kernel<2, 12, 8, true>
-                         : ilv                    ? dfmi::demod_seed_bins_kernel<2, 12, 8, false, dfmi::kIlv>
-                         : g_tune.bins_prefetch == 6 ? dfmi::demod_seed_bins_kernel<2, 12, 8, false, 6>
-                         : g_tune.bins_prefetch   ? dfmi::demod_seed_bins_kernel<2, 12, 8, false, 4>
-                                                  : dfmi::demod_seed_bins_kernel<2, 12>)
-           : nslot <= 4 ? dfmi::demod_seed_bins_kernel<4, 12>
-                        : dfmi::demod_seed_bins_kernel<8, 12>;
+    kern = nslot <= 2 ? dfmi::demod_seed_bins_kernel<2, 12, 4> : nslot <= 4 ? dfmi::demod_seed_bins_kernel<4, 12>
+                                                                          : dfmi::demod_seed_bins_kernel<8, 12>;
   else
     kern = nslot <= 2 ? dfmi::demod_seed_bins_kernel<2, 16> : nslot <= 4 ? dfmi::demod_seed_bins_kernel<4, 16>
                                                                        : dfmi::demod_seed_bins_kernel<8, 16>;
   int per_cu = 0;
   if (int orc = occupancy(kern, dfmi::kBlockThreads, lds, &per_cu)) return orc;
   if (per_cu < 1) per_cu = 1;
-  if (g_tune.demod_blocks_per_cu > 0 && g_tune.demod_blocks_per_cu < per_cu) per_cu = g_tune.demod_blocks_per_cu;
   const int64_t slots = (int64_t)t_ds->n_cu * per_cu;
   const int64_t nseg = nrec * nbuf;
   if (nrec + 1 > slots / 2) return 1;  // every seed and most of the bulk must be resident at once
   int64_t bulk = slots - nrec;
   const int64_t need = (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock;
   if (bulk > need) bulk = need;
-  if (g_tune.demod_spw > 0) {  // as bins_grid: later workgroups to the slots that free first
-    const int64_t per = (int64_t)dfmi::kWavesPerBlock * g_tune.demod_spw;
+  if (t_tune.demod_spw > 0) {  // as bins_grid: later workgroups to the slots that free first
+    const int64_t per = (int64_t)dfmi::kWavesPerBlock * t_tune.demod_spw;
     if ((nseg + per - 1) / per > bulk) bulk = (nseg + per - 1) / per;
   }
   hipLaunchKernelGGL(kern, dim3((unsigned)(nrec + bulk)), dim3(dfmi::kBlockThreads), lds, st, x, nseg,
                      nbuf * (int64_t)R, nrec, R, L, ndata, tab, rows, qs, gdev, ginl, gdev ? 0 : 1, jtab, c, out,
-                     out_ld, nbuf, fitok, g_probe);
+                     out_ld, nbuf, fitok, t_ds->probe);
   HIPCHK(hipGetLastError());
   g_last_demod = "demod_seed_bins_kernel<" + std::to_string(nslot <= 2 ? 2 : nslot <= 4 ? 4 : 8) + "," +
-                 std::to_string(ndata <= 12 ? 12 : 16) +
-                 (nslot <= 2 && ndata <= 12 && g_tune.bins_loads == 16 ? ",16" : "") +
-                 (nslot <= 2 && ndata <= 12 && g_tune.bins_loads != 16 && g_tune.bins_roll ? ",roll" : "") +
-                 (ilv ? ",ilv" : "") +
-                 (nslot <= 2 && ndata <= 12 && g_tune.bins_loads != 16 && !g_tune.bins_roll && !ilv &&
-                          g_tune.bins_prefetch
-                      ? (g_tune.bins_prefetch == 6 ? ",pf6" : ",pf4") : "") + ",rows>";
+                 std::to_string(ndata <= 12 ? 12 : 16) + (pf && (R >> 7) >= 4 ? ",pf4" : "") + ",rows>";
+  return DFMI_OK;
+}
+
+// Seed step of the unfused layouts (fitters.py:403-410): buffer 0 of every record
+// demodulated and fitted by one wave per record on the side stream, concurrently with
+// the bulk demodulation on the caller's stream; the LM waits on its event. The LDS bin
+// fold (seed_bins_kernel) wherever its geometry applies — the fused kernel's seed fold,
+// so both paths give the same bits — the global fold / direct kernel otherwise.
+int seed_launch(int dev, const double* x, int64_t nrec, int64_t rec_stride, int R, int ndata, double w0, int L,
+                const double* gdev, const dfmi::GuessInline& ginl, const double* jtab, const dfmi::LMConst& c,
+                double* out, int64_t out_ld, int64_t nbuf, int32_t* fitok, hipStream_t sst) {
+  int rc;
+  if (L > 64 * 16) L = 0;  // no table: the direct kernel's per-sample sincos
+  const double* tab = nullptr;
+  if (L > 0 && (rc = basis_table(dev, L, ndata, w0, sst, &tab))) return rc;
+  const bool vec2 = L > 0 && vec2_ok(x, nrec > 1 ? rec_stride : 0, L);
+  const size_t blds = ((size_t)2 * ndata * L + L + dfmi_row_stride(ndata)) * sizeof(double);
+  if (L > 0 && bins_geometry(vec2, L, ndata, t_ds->lds_per_block, 1) && blds <= t_ds->lds_per_block) {
+    const int nslot = (L + 127) / 128;
+    auto sk = ndata <= 12 ? (nslot <= 2 ? dfmi::seed_bins_kernel<12, 2> : nslot <= 4 ? dfmi::seed_bins_kernel<12, 4>
+                                                                                   : dfmi::seed_bins_kernel<12, 8>)
+            : ndata <= 16 ? (nslot <= 2 ? dfmi::seed_bins_kernel<16, 2> : nslot <= 4 ? dfmi::seed_bins_kernel<16, 4>
+                                                                                   : dfmi::seed_bins_kernel<16, 8>)
+                          : (nslot <= 2 ? dfmi::seed_bins_kernel<0, 2> : nslot <= 4 ? dfmi::seed_bins_kernel<0, 4>
+                                                                                  : dfmi::seed_bins_kernel<0, 8>);
+    hipLaunchKernelGGL(sk, dim3((unsigned)nrec), dim3(64), blds, sst, x, rec_stride, R, L, ndata, tab, gdev, ginl,
+                       gdev ? 0 : 1, jtab, c, out, out_ld, nbuf, fitok, t_ds->probe);
+  } else {
+    void *qs, *ds_;
+    if ((rc = workspace(dev, "qi_seed", (size_t)2 * ndata * nrec * 8, &qs))) return rc;
+    if ((rc = workspace(dev, "dc_seed", (size_t)nrec * 8, &ds_))) return rc;
+    auto sk = ndata <= 12 ? dfmi::seed_kernel<12> : ndata <= 16 ? dfmi::seed_kernel<16> : dfmi::seed_kernel<0>;
+    hipLaunchKernelGGL(sk, dim3((unsigned)nrec), dim3(64), 0, sst, x, rec_stride, R, L, ndata, w0, tab, (double*)qs,
+                       (double*)ds_, nrec, gdev, ginl, gdev ? 0 : 1, jtab, c, out, out_ld, nbuf, fitok);
+  }
+  HIPCHK(hipGetLastError());
   return DFMI_OK;
 }
 
@@ -700,12 +651,8 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
   const int64_t nseg = nrec * nbuf;
   if (nseg == 0) return DFMI_OK;
   DeviceState& ds = *t_ds;
-  void* qiw = nullptr;
-  int rc = workspace(dev, "qi", (size_t)2 * ndata * nseg * sizeof(double), &qiw);
-  if (rc) return rc;
-  double* qi = (double*)qiw;
   const double* jtab = nullptr;
-  rc = grid_table(dev, ndata, cfg, &jtab);
+  int rc = grid_table(dev, ndata, cfg, &jtab);
   if (rc) return rc;
   const int64_t out_ld = nseg;
   double* dc = out + 4 * out_ld;
@@ -729,97 +676,56 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
   // component-major QI otherwise (warm-start chains read QI component-major).
   const bool rows = parallel && (nbuf <= 1 || nchunk >= nbuf - 1) &&
                     (nrec == 1 || (rec_stride % 2) == 0) && rows_supported(dev, x, R, R, ndata, w0, period);
-  hipStream_t bulk = st;  // stream of the bulk demodulation
-  bool seed_first = false;
-  if (parallel) {
-    // Seed step (buffer 0 of every record, fitters.py:403-410) concurrently with the
-    // bulk demodulation. seed_order 1 (default): the seed kernel goes on the caller's
-    // stream, where it dispatches as soon as the previous work drains, and the bulk
-    // demodulation on the side stream behind an event wait — so the seed wave is
-    // resident first instead of queueing for a slot until the persistent
-    // demodulation drains (profiles/r01b_seed_probe.json); the bulk grid's last
-    // workgroups idle where the seed displaced them, and the LM follows the seed in
-    // stream order. seed_order 0: seed on the side stream, LM waits on its event.
-    int L = period;
-    if (L == 0) L = detect_period_impl(w0, R, ndata);
-    if (L > 64 * 16) L = 0;
-    const double* tab = nullptr;
-    if (L > 0 && (rc = basis_table(dev, L, ndata, w0, st, &tab))) return rc;
-    void *qs, *ds_;
-    if ((rc = workspace(dev, "qi_seed", (size_t)2 * ndata * nrec * 8, &qs))) return rc;
-    if ((rc = workspace(dev, "dc_seed", (size_t)nrec * 8, &ds_))) return rc;
-    const bool seed_bins = rows && L > 0 && g_tune.seed_bins;
-    seed_first = seed_bins && g_tune.seed_order == 1;
-    if (seed_first && (nrec == 1 || rec_stride == nbuf * (int64_t)R) && nbuf > 1) {
-      const int64_t qs1 = dfmi_row_stride(ndata);
-      void* rw = nullptr;
-      if ((rc = workspace(dev, "qrow", (size_t)qs1 * nseg * sizeof(double), &rw))) return rc;
-      rc = fused_seed_demod(dev, x, nrec, nbuf, R, ndata, L, tab, (double*)rw, qs1, gdev, ginl, jtab, c, out, out_ld,
-                            fitok, st);
-      if (rc < 0) return rc;
-      if (rc == 0)  // seeds + rows written; the LM follows in stream order
-        return lm_device(dev, (double*)rw, qs1, ndata, nrec, nbuf, 1, nbuf - 1, nchunk, out, nbuf, out_ld, nullptr, c,
-                         jtab, out, out_ld, fitok, st, true);
-      rc = 0;
-    }
-    HIPCHK(hipEventRecord(ds.ev_in, st));
-    HIPCHK(hipStreamWaitEvent(ds.side, ds.ev_in, 0));
-    hipStream_t sst = ds.side;
-    if (seed_first) {
-      sst = st;
-      bulk = ds.side;
-    }
-    if (seed_bins) {  // fold into LDS, QI from LDS in the fit (seed.h seed_bins_kernel)
-      const int nslot = (L + 127) / 128;
-      const size_t lds = ((size_t)2 * ndata * L + L + dfmi_row_stride(ndata)) * sizeof(double);
-      auto sk = ndata <= 12 ? (nslot <= 2 ? dfmi::seed_bins_kernel<12, 2> : nslot <= 4 ? dfmi::seed_bins_kernel<12, 4>
-                                                                                     : dfmi::seed_bins_kernel<12, 8>)
-              : ndata <= 16 ? (nslot <= 2 ? dfmi::seed_bins_kernel<16, 2> : nslot <= 4 ? dfmi::seed_bins_kernel<16, 4>
-                                                                                     : dfmi::seed_bins_kernel<16, 8>)
-                            : (nslot <= 2 ? dfmi::seed_bins_kernel<0, 2> : nslot <= 4 ? dfmi::seed_bins_kernel<0, 4>
-                                                                                    : dfmi::seed_bins_kernel<0, 8>);
-      hipLaunchKernelGGL(sk, dim3((unsigned)nrec), dim3(64), lds, sst, x, rec_stride, R, L, ndata, tab, gdev, ginl,
-                         gdev ? 0 : 1, jtab, c, out, out_ld, nbuf, fitok, g_probe);
-    } else {
-      auto sk = ndata <= 12 ? dfmi::seed_kernel<12> : ndata <= 16 ? dfmi::seed_kernel<16> : dfmi::seed_kernel<0>;
-      hipLaunchKernelGGL(sk, dim3((unsigned)nrec), dim3(64), 0, sst, x, rec_stride, R, L, ndata, w0, tab,
-                         (double*)qs, (double*)ds_, nrec, gdev, ginl, gdev ? 0 : 1, jtab, c, out, out_ld, nbuf, fitok);
-    }
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(ds.ev_seed, sst));
-  }
   const int64_t qs = rows ? dfmi_row_stride(ndata) : 0;
-  if (rows) {
+  int L = period;
+  if (L == 0) L = detect_period_impl(w0, R, ndata);
+  if (parallel && rows && (nrec == 1 || rec_stride == nbuf * (int64_t)R) && nbuf > 1) {
+    // ONE launch: the seeds (buffer 0 of every record) + the bulk demodulation; the LM
+    // follows in stream order
+    const double* tab = nullptr;
+    if ((rc = basis_table(dev, L, ndata, w0, st, &tab))) return rc;
     void* rw = nullptr;
     if ((rc = workspace(dev, "qrow", (size_t)qs * nseg * sizeof(double), &rw))) return rc;
-    qi = (double*)rw;
+    rc = fused_seed_demod(dev, x, nrec, nbuf, R, ndata, L, tab, (double*)rw, qs, gdev, ginl, jtab, c, out, out_ld,
+                          fitok, st);
+    if (rc < 0) return rc;
+    if (rc == 0)
+      return lm_device(dev, (double*)rw, qs, ndata, nrec, nbuf, 1, nbuf - 1, nchunk, out, nbuf, out_ld, nullptr, c,
+                       jtab, out, out_ld, fitok, st, true);
   }
-  // seed_first: each seed wave (161 VGPRs on one SIMD) displaces two 4-wave bulk
-  // workgroups of its CU — the last ones sent to that XCD under round-robin
-  // placement: the last 2 per XCD per record idle instead of holding segments
-  g_idle_blocks = seed_first ? (int)(16 * nrec < 64 ? 16 * nrec : 64) : 0;
-  if (rec_stride == nbuf * (int64_t)R) {
-    rc = rows ? demod_device(dev, x, nseg, R, R, ndata, w0, period, qi, qs, nullptr, bulk, true)
-              : demod_device(dev, x, nseg, R, R, ndata, w0, period, qi, nseg, dc, bulk);
+  if (parallel) {  // the seed beside the bulk demodulation (side stream, event)
+    HIPCHK(hipEventRecord(ds.ev_in, st));
+    HIPCHK(hipStreamWaitEvent(ds.side, ds.ev_in, 0));
+    if ((rc = seed_launch(dev, x, nrec, rec_stride, R, ndata, w0, L, gdev, ginl, jtab, c, out, out_ld, nbuf, fitok,
+                          ds.side)))
+      return rc;
+    HIPCHK(hipEventRecord(ds.ev_seed, ds.side));
+  }
+  double* qi = nullptr;
+  {
+    void* w = nullptr;
+    if (rows) rc = workspace(dev, "qrow", (size_t)qs * nseg * sizeof(double), &w);
+    else rc = workspace(dev, "qi", (size_t)2 * ndata * nseg * sizeof(double), &w);
+    if (rc) return rc;
+    qi = (double*)w;
+  }
+  if (rec_stride == nbuf * (int64_t)R || nrec == 1) {
+    rc = rows ? demod_device(dev, x, nseg, R, R, ndata, w0, period, qi, qs, nullptr, st, true)
+              : demod_device(dev, x, nseg, R, R, ndata, w0, period, qi, nseg, dc, st);
   } else {
     for (int64_t r = 0; r < nrec && rc == 0; ++r) {
       rc = rows ? demod_device(dev, x + r * rec_stride, nbuf, R, R, ndata, w0, period, qi + r * nbuf * qs, qs,
-                               nullptr, bulk, true)
+                               nullptr, st, true)
                 : demod_device(dev, x + r * rec_stride, nbuf, R, R, ndata, w0, period, qi + r * nbuf, nseg,
-                               dc + r * nbuf, bulk);
+                               dc + r * nbuf, st);
     }
   }
-  g_idle_blocks = 0;
   if (rc) return rc;
-  if (bulk != st) {
-    HIPCHK(hipEventRecord(ds.ev_bulk, bulk));
-    HIPCHK(hipStreamWaitEvent(st, ds.ev_bulk, 0));
-  }
   if (!parallel) {
     return lm_device(dev, qi, nseg, ndata, nrec, nbuf, 0, nbuf, 1, gdev, 4, 1, init_guess_host, c, jtab, out, out_ld,
                      fitok, st);
   }
-  if (!seed_first) HIPCHK(hipStreamWaitEvent(st, ds.ev_seed, 0));
+  HIPCHK(hipStreamWaitEvent(st, ds.ev_seed, 0));
   if (nbuf <= 1) {
     if (rows)  // dc of the seed buffers (the LM kernel carries it otherwise)
       HIPCHK(hipMemcpy2DAsync(dc, nbuf * sizeof(double), qi + dfmi_row_dc(ndata), qs * nbuf * sizeof(double),
@@ -836,31 +742,16 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
 namespace {
 // key -> (knob, allowed values or empty = any value >= 0)
 struct Knob {
-  int* v;
+  int Tuning::*v;
   std::vector<int> allowed;
 };
 const std::map<std::string, Knob>& knobs() {
   static const std::map<std::string, Knob> k = {
-      {"demod_loads", {&g_tune.demod_loads, {8, 16}}},     {"demod_nt", {&g_tune.demod_nt, {0, 1}}},
-      {"demod_blocks_per_cu", {&g_tune.demod_blocks_per_cu, {}}}, {"lm_general", {&g_tune.lm_general, {0, 1}}},
-      {"demod_kernel", {&g_tune.demod_kernel, {0, 1}}},    {"seed_bins", {&g_tune.seed_bins, {0, 1}}},
-      {"seed_order", {&g_tune.seed_order, {0, 1}}},
-      {"demod_occ4", {&g_tune.demod_occ4, {0, 1}}},
-      {"seed_fused", {&g_tune.seed_fused, {0, 1}}},
-      {"wdfmi_accel", {&g_tune.wdfmi_accel, {0, 1, 2, 3}}},
-      {"bins_loads", {&g_tune.bins_loads, {8, 16}}},
-      {"bins_roll", {&g_tune.bins_roll, {0, 1}}},
-      {"bins_prefetch", {&g_tune.bins_prefetch, {0, 4, 6}}},
-      {"lm_refill", {&g_tune.lm_refill, {0, 1}}},
-      {"lm_waves_per_simd", {&g_tune.lm_waves_per_simd, {1, 2, 3, 4}}},
-      {"lm_tile_min", {&g_tune.lm_tile_min, {16, 32, 48, 64, 96, 128}}},
-      {"lm_phase", {&g_tune.lm_phase, {0, 1}}},
-      {"lm_spec", {&g_tune.lm_spec, {0, 1, 2, 3}}},
-      {"lm_pa", {&g_tune.lm_pa, {}}},
-      {"lm_pa_w2", {&g_tune.lm_pa_w2, {0, 1}}},
-      {"demod_spw", {&g_tune.demod_spw, {}}},
-      {"bins_ilv", {&g_tune.bins_ilv, {0, 1}}},
-      {"ekf_row", {&g_tune.ekf_row, {}}}};
+      {"demod_kernel", {&Tuning::demod_kernel, {0, 1}}},
+      {"lm_general", {&Tuning::lm_general, {0, 1}}},
+      {"demod_spw", {&Tuning::demod_spw, {}}},
+      {"ekf_row", {&Tuning::ekf_row, {}}},
+      {"wdfmi_accel", {&Tuning::wdfmi_accel, {0, 1, 2, 3}}}};
   return k;
 }
 // np.mean / np.var of nrec device records on st (moments.hip), numpy-exact.
@@ -960,7 +851,7 @@ int ekf_impl(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
   const int block = 64;
   // few channels: one 16-lane row per channel (ekf_row_kernel, ~1.7x the per-channel
   // rate); many: one lane per channel (ekf_kernel, 16x the channels per instruction)
-  const bool row = g_tune.ekf_row && nrec <= (int64_t)g_tune.ekf_row * t_ds->n_cu * 16;
+  const bool row = t_tune.ekf_row && nrec <= (int64_t)t_tune.ekf_row * t_ds->n_cu * 16;
   const int64_t grid = row ? (nrec + 3) / 4 : (nrec + block - 1) / block;
   hipLaunchKernelGGL(row ? dfmi::ekf_row_kernel : dfmi::ekf_kernel, dim3((unsigned)grid), dim3(block), 0, st, dx,
                      nrec, rs, n_samp, dx0, dp0, dq, dr, (const double*)wtw, (int)R, nbuf, dstates,
@@ -1008,16 +899,18 @@ int dfmi_device_count(void) {
 
 const char* dfmi_last_error(void) { return g_err.c_str(); }
 
-const char* dfmi_version(void) { return "dfmi 0.2 gfx950"; }
+const char* dfmi_version(void) { return "dfmi 0.3 gfx950"; }
 
 const char* dfmi_last_demod_kernel(void) { return g_last_demod.c_str(); }
 
 int dfmi_probe_read(int64_t* out, int32_t n) {
   CallScope cs;
-  if (!g_probe) return fail(DFMI_ERR_ARG, "probe not enabled (dfmi_set_tuning(\"probe\", 1))");
+  int dev;
+  if (int rc = ensure_init(&dev)) return rc;
+  if (!t_ds->probe) return fail(DFMI_ERR_ARG, "probe not enabled on this device (dfmi_set_tuning(\"probe\", 1))");
   if (n < 0 || n > 16 + 2 * dfmi::kProbeWaves || (n && !out)) return fail(DFMI_ERR_ARG, "bad probe read");
   HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(out, g_probe, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(out, t_ds->probe, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return DFMI_OK;
 }
 
@@ -1026,12 +919,14 @@ int dfmi_get_tuning(const char* key, int64_t* value) {
   if (!key || !value) return fail(DFMI_ERR_ARG, "null argument");
   const std::string k(key);
   if (k == "probe") {
-    *value = g_probe ? 1 : 0;
+    int dev;
+    if (int rc = ensure_init(&dev)) return rc;
+    *value = t_ds->probe ? 1 : 0;
     return DFMI_OK;
   }
   auto it = knobs().find(k);
   if (it == knobs().end()) return fail(DFMI_ERR_ARG, "unknown tuning key " + k);
-  *value = *it->second.v;
+  *value = t_tune.*(it->second.v);
   return DFMI_OK;
 }
 
@@ -1039,18 +934,19 @@ int dfmi_set_tuning(const char* key, int64_t value) {
   CallScope cs;
   if (!key) return fail(DFMI_ERR_ARG, "null key");
   const std::string k(key);
-  if (k == "probe") {
-    if (value && !g_probe) {
-      int dev;
-      int rc = ensure_init(&dev);
-      if (rc) return rc;
+  if (k == "probe") {  // per device: a timestamp buffer in this device's memory
+    int dev;
+    if (int rc = ensure_init(&dev)) return rc;
+    if (value && !t_ds->probe) {
       void* p = nullptr;
       const size_t pb = (16 + 2 * (size_t)dfmi::kProbeWaves) * sizeof(uint64_t);
-      if ((rc = workspace(dev, "probe", pb, &p))) return rc;
+      HIPCHK(hipMalloc(&p, pb));
       HIPCHK(hipMemset(p, 0, pb));
-      g_probe = (uint64_t*)p;
-    } else if (!value) {
-      g_probe = nullptr;
+      t_ds->probe = (uint64_t*)p;
+    } else if (!value && t_ds->probe) {
+      HIPCHK(hipDeviceSynchronize());
+      HIPCHK(hipFree(t_ds->probe));
+      t_ds->probe = nullptr;
     }
     return DFMI_OK;
   }
@@ -1063,7 +959,21 @@ int dfmi_set_tuning(const char* key, int64_t value) {
     for (int a : kn.allowed) ok = ok || (a == value);
     if (!ok) return fail(DFMI_ERR_ARG, "value not allowed for " + k);
   }
-  *kn.v = (int)value;
+  std::lock_guard<std::mutex> g(g_mu);
+  g_tune.*(kn.v) = (int)value;
+  return DFMI_OK;
+}
+
+// Frees every workspace of the current device (waits for the device first). The next
+// call re-allocates what it needs.
+int dfmi_release_workspaces(void) {
+  CallScope cs;
+  int dev;
+  if (int rc = ensure_init(&dev)) return rc;
+  HIPCHK(hipDeviceSynchronize());
+  for (auto& kv : t_ds->ws)
+    if (int rc = free_stream_ws(kv.second)) return rc;
+  t_ds->ws.clear();
   return DFMI_OK;
 }
 
@@ -1246,8 +1156,8 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
   a.ndata = cfg->ndata;
   a.ndata_psi = cfg->ndata_psi;
   a.threads = R <= 4096 ? 256 : 1024;
-  a.accel = g_tune.wdfmi_accel;
-  a.probe = g_probe;
+  a.accel = t_tune.wdfmi_accel;
+  a.probe = t_ds->probe;
   a.nrec = nrec;
   a.nbuf = nbuf;
   a.f_samp = cfg->f_samp;

@@ -340,72 +340,6 @@ DFMI_HDI void eval_reg_accept(const QF& q, int nd, const double (&p)[4], const T
   e = Eval{t.ssq, a00, a01, a02, 0.0, a11, a12, 0.0, a22, 0.0, a33, g0, g1, g2, g3};
 }
 
-// ssqf AND coeffs at p in one pass (fit.py:152-167 + fit.py:68-150): eval_reg_trial's
-// residual sum followed by eval_reg_accept's closed-form J^T J / J^T r, fused into one
-// unrolled loop over the harmonics. Same expressions, same bits as the two-pass form
-// (c = aP J_j and the residuals are formed identically; the mask is 0 or 1).
-// Used by the refill kernel (lm_refill.h), where lanes sit at different points of
-// their descents: a pass that always forms the Jacobian costs one evaluation, while
-// the split form costs a trial plus, whenever ANY lane of the wave accepts, an accept.
-template <int V, typename QF>
-DFMI_HDI void eval_reg_full(const QF& q, int nd, const double (&p)[4], Eval& e, const DfmiTrigK& k) {
-  constexpr int NDMAX = nd_cap(V);
-  double Q[NDMAX], I[NDMAX];
-#pragma unroll
-  for (int j = 1; j <= NDMAX; ++j) qi_pair<V>(q, nd, j, Q[j - 1], I[j - 1]);
-  double sph, cph, s1, c1;
-  dfmi_sincos_k(p[2], k, &sph, &cph);
-  dfmi_sincos_k(p[3], k, &s1, &c1);
-  double J[NDMAX + 2];
-  bessel_regs<NDMAX + 2>(p[1], nd_exact(V) ? NDMAX + 1 : nd + 1, J);
-  const double a = p[0];
-  const double ac = a * cph, as = a * sph;
-  const double tc = 2.0 * c1;
-  const double cph0 = (a != 0.0) ? cph : 0.0, sph0 = (a != 0.0) ? sph : 0.0;
-  double so = 0.0, se = 0.0;
-  double a00 = 0.0, a01 = 0.0, a02 = 0.0, a11 = 0.0, a12 = 0.0, a22 = 0.0, a33 = 0.0;
-  double g0 = 0.0, g1 = 0.0, g2 = 0.0, g3 = 0.0;
-  double cj = c1, sj = s1, cm = 1.0, sm = 0.0;
-#pragma unroll
-  for (int j = 1; j <= NDMAX; ++j) {
-    const double mk = hmask<V>(nd, j);
-    const double Jj = J[j] * mk;
-    const double aP = quarter_turn(j, ac, as), aD = quarter_turn(j + 1, ac, as);
-    const double c = aP * Jj;
-    const double rq = fma(-c, cj, Q[j - 1]);
-    const double ri = fma(c, sj, I[j - 1]);
-    double& acc = (j & 1) ? so : se;
-    acc = fma(rq, rq, acc);
-    acc = fma(ri, ri, acc);
-    const double u0 = quarter_turn(j, cph0, sph0) * Jj;
-    const double u1 = aP * (0.5 * (J[j - 1] - J[j + 1])) * mk;
-    const double u2 = aD * Jj;
-    const double A = fma(cj, rq, -(sj * ri));
-    const double B = fma(sj, rq, cj * ri);
-    const double w = fma(cj, cj, sj * sj);
-    const double v0 = u0 * w, v1 = u1 * w, v2 = u2 * w;
-    a00 = fma(v0, u0, a00);
-    a01 = fma(v0, u1, a01);
-    a02 = fma(v0, u2, a02);
-    a11 = fma(v1, u1, a11);
-    a12 = fma(v1, u2, a12);
-    a22 = fma(v2, u2, a22);
-    const double jc = (double)j * c;
-    a33 = fma(jc * w, jc, a33);
-    g0 = fma(u0, A, g0);
-    g1 = fma(u1, A, g1);
-    g2 = fma(u2, A, g2);
-    g3 = fma(-jc, B, g3);
-    const double cn = fma(tc, cj, -cm), sn = fma(tc, sj, -sm);
-    cm = cj;
-    sm = sj;
-    cj = cn;
-    sj = sn;
-    DFMI_HARMONIC_FENCE();
-  }
-  e = Eval{so + se, a00, a01, a02, 0.0, a11, a12, 0.0, a22, 0.0, a33, g0, g1, g2, g3};
-}
-
 // 1/d to within an ulp or two: v_rcp_f64 + two Newton steps on the device (the
 // IEEE division sequence costs ~3x the instructions); exact division on the host.
 DFMI_HDI double rcp_nr(double d) {
@@ -692,25 +626,6 @@ struct SplitEval {  // NDMAX: a register-path variant tag (nd_cap / nd_exact)
   DFMI_HDI void solve(const Eval& e, double lam, double (&dp)[4]) { damped_solve_block(e, lam, dp); }
 };
 
-// Register path with ONE evaluation per trial: ssqf and coeffs at the trial point
-// together (eval_reg_full, same bits as SplitEval's trial + accept). A trial that is
-// accepted then needs no second pass for its Jacobian; a rejected one pays for it.
-template <int NDMAX, typename QF>
-struct FusedEval {
-  const QF& q;
-  int nd;
-  const DfmiTrigK& k;
-  struct Trial {
-    Eval e;
-  };
-  DFMI_HDI double trial(const double (&p)[4], Trial& t) {
-    eval_reg_full<NDMAX>(q, nd, p, t.e, k);
-    return t.e.ssq;
-  }
-  DFMI_HDI void accept(const double (&)[4], const Trial& t, Eval& e) { e = t.e; }
-  DFMI_HDI void solve(const Eval& e, double lam, double (&dp)[4]) { damped_solve_block(e, lam, dp); }
-};
-
 // fit.py:208-258 (_run_lma_fit), nested form (one lane at a time: the host build's
 // check that the flattened descent takes the same path). p in/out; returns ssq0 at
 // the final p.
@@ -755,28 +670,6 @@ DFMI_HDI double lm_descend(Ev&& ev, double (&p)[4], const LMConst& c) {
   return e.ssq;
 }
 
-// Lane position of the k-th (0-based) set bit of m (k < popcount(m)).
-__device__ __forceinline__ int nth_set_bit(uint64_t m, int k) {
-  int pos = 0;
-#pragma unroll
-  for (int w = 32; w >= 1; w >>= 1) {
-    const uint64_t lo = m & ((1ull << w) - 1);
-    const int c = __popcll(lo);
-    const bool up = k >= c;
-    k = up ? k - c : k;
-    m = up ? (m >> w) : lo;
-    pos += up ? w : 0;
-  }
-  return pos;
-}
-
-// Lanes [lo, hi) of a 64-bit wave mask (0 <= lo <= hi <= 64).
-__device__ __forceinline__ uint64_t lane_range(int lo, int hi) {
-  const uint64_t below_hi = hi >= 64 ? ~0ull : ((1ull << hi) - 1);
-  const uint64_t below_lo = lo >= 64 ? ~0ull : ((1ull << lo) - 1);
-  return below_hi & ~below_lo;
-}
-
 template <typename T>
 __device__ __forceinline__ T shfl_any(T v, int src) {
   if constexpr (sizeof(T) == 8) {
@@ -786,143 +679,6 @@ __device__ __forceinline__ T shfl_any(T v, int src) {
   } else {
     return __shfl(v, src);
   }
-}
-
-// fit.py:208-258 (_run_lma_fit) as lm_descend_flat, with the lambda ladder evaluated
-// speculatively by the wave's finished lanes. In SIMT a pass costs the same whatever
-// the number of lanes that run it, so a lane whose descent has ended (a "helper")
-// evaluates, in the same pass, a later rung of an active lane's ladder: helper h of
-// active lane i solves msolve(lambda[li_i + off]) from lane i's (p, J^T J, J^T r) and
-// runs ssqf on lane i's QI (the QF accessor's base pointer is taken from lane i).
-// Lane i then takes the FIRST improving rung in ladder order — its own trial at li_i,
-// else the helpers' rungs li_i + 1, + 2, ... — with that rung's trial state (for the
-// Jacobian, as if it had evaluated it itself), or skips every rung that was evaluated
-// without improvement. Each rung's solve + trial is the same pure function of (p, e,
-// lambda, QI) whichever lane computes it, so every lane's sequence of accepted points
-// (and every bit of the result) is lm_descend's; only the number of passes falls: the
-// 8-rung ladder that ends a converged descent ("no lambda improved", fit.py:246-247)
-// is evaluated in one or two passes once most lanes of the wave are done.
-// Helpers are assigned in blocks: K = max(1, helpers / active) consecutive helpers per
-// active lane (by rank), rungs li + 1 .. li + K.
-template <int V, typename QF>
-__device__ __forceinline__ double lm_descend_spec(SplitEval<V, QF>& ev, double (&p)[4], const LMConst& c) {
-  using Trial = TrialReg<V>;
-  constexpr int NT = (int)(sizeof(Trial) / sizeof(double));
-  static_assert(sizeof(Trial) == NT * sizeof(double), "TrialReg: doubles only");
-  Eval e;
-  {
-    Trial t0;
-    ev.trial(p, t0);
-    ev.accept(p, t0, e);
-  }
-  const int lane = (int)__lane_id();
-  const uint64_t below = (1ull << lane) - 1;
-  int it = 0, li = 0;
-  bool active = c.max_steps > 0 && c.n_lambda > 0;
-  for (;;) {
-    const uint64_t A = __ballot(active);
-    if (A == 0) break;
-    const uint64_t H = __ballot(!active);  // lanes of this loop whose descent has ended
-    const int na = __popcll(A), nh = __popcll(H);
-    const bool spec = nh > 0;  // wave-uniform
-    const int K = nh >= na ? nh / na : 1;
-    // the rung this lane evaluates: its own (active) or rung li_src + off of lane src
-    int src = lane, off = 0;
-    if (spec && !active) {
-      const int rh = __popcll(H & below);
-      const int ro = rh / K;  // owner rank
-      if (ro < na) {
-        src = nth_set_bit(A, ro);
-        off = 1 + (rh - ro * K);
-      }
-    }
-    Eval es = e;
-    double ps[4] = {p[0], p[1], p[2], p[3]};
-    int lis = li;
-    QF qs = ev.q;
-    if (spec) {
-      es.ssq = shfl_any(e.ssq, src);
-      es.a00 = shfl_any(e.a00, src);
-      es.a01 = shfl_any(e.a01, src);
-      es.a02 = shfl_any(e.a02, src);
-      es.a11 = shfl_any(e.a11, src);
-      es.a12 = shfl_any(e.a12, src);
-      es.a22 = shfl_any(e.a22, src);
-      es.a33 = shfl_any(e.a33, src);
-      es.g0 = shfl_any(e.g0, src);
-      es.g1 = shfl_any(e.g1, src);
-      es.g2 = shfl_any(e.g2, src);
-      es.g3 = shfl_any(e.g3, src);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) ps[i] = shfl_any(p[i], src);
-      lis = __shfl(li, src);
-      qs.p = shfl_any(ev.q.p, src);
-    }
-    const int rung = lis + off;
-    const bool work = active || (off > 0 && rung < c.n_lambda);
-    double dp[4];
-    ev.solve(es, c.lambdas[work ? rung : 0], dp);
-    const bool step = work && !norm_below(sumsq4(dp[0], dp[1], dp[2], dp[3]), c.min_step_norm);
-    double pt[4] = {ps[0] + dp[0], ps[1] + dp[1], ps[2] + dp[2], ps[3] + dp[3]};
-    Trial tt;
-    bool improved = false;
-    if (step) {
-      SplitEval<V, QF> evs{qs, ev.nd, ev.k};
-      improved = evs.trial(pt, tt) < es.ssq;
-    }
-    // active lane: the first improving rung in ladder order
-    int take = -1;     // lane whose trial this lane accepts (-1: none)
-    int skipped = 1;   // rungs evaluated without improvement (own + helpers') if none improved
-    if (active && improved) take = lane;
-    // helper results (every lane of the loop votes)
-    const uint64_t HI = __ballot(!active && improved);
-    const uint64_t HW = __ballot(!active && work);
-    if (active && !improved && spec) {
-      const int ra = __popcll(A & below);
-      const int r0 = ra * K;
-      if (r0 < nh) {
-        const int h0 = nth_set_bit(H, r0);
-        const int h1 = r0 + K < nh ? nth_set_bit(H, r0 + K) : 64;
-        const uint64_t win = H & lane_range(h0, h1);
-        const uint64_t hit = HI & win;
-        if (hit) {
-          take = __builtin_ctzll(hit);
-        } else {
-          skipped += __popcll(HW & win);
-        }
-      }
-    }
-    // the taken rung's point and trial state (this lane's own, or its helper's)
-    const bool any_take = __ballot(take >= 0 && take != lane) != 0;
-    if (any_take) {
-      const int from = take >= 0 ? take : lane;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) pt[i] = shfl_any(pt[i], from);
-      double* tv = reinterpret_cast<double*>(&tt);
-#pragma unroll
-      for (int i = 0; i < NT; ++i) tv[i] = shfl_any(tv[i], from);
-    }
-    if (active) {
-      if (take >= 0) {
-        const double change2 = sumsq4(pt[0] - p[0], pt[1] - p[1], pt[2] - p[2], pt[3] - p[3]);
-        p[0] = pt[0];
-        p[1] = pt[1];
-        p[2] = pt[2];
-        p[3] = pt[3];
-        const double best_ssq = tt.ssq;  // the taken trial's ssqf
-        ev.accept(p, tt, e);  // coeffs(ndata, data, parm) at the accepted point (fit.py:251)
-        ++it;
-        li = 0;
-        if (((e.ssq - best_ssq) < c.conv_improve && norm_below(change2, c.conv_param_change)) ||
-            it >= c.max_steps)
-          active = false;
-      } else {
-        li += skipped;
-        if (li >= c.n_lambda) active = false;  // no lambda improved: fit.py:246-247
-      }
-    }
-  }
-  return e.ssq;
 }
 
 // fit.py:260-320 (_find_best_initial_guess). jtab: n_grid rows of J_1..J_ndata(mtry)
@@ -1007,8 +763,7 @@ template <int FLAT = 1, typename Ev, typename QF>
 DFMI_HDI int fit_segment_t(Ev&& ev, QF&& Q, int ndata, const double* __restrict__ jtab, const LMConst& c,
                            double (&p)[4], double& ssq_out) {
   auto descend = [&](double (&pp)[4]) {
-    if constexpr (FLAT == 2) return lm_descend_spec(ev, pp, c);
-    else if constexpr (FLAT == 1) return lm_descend_flat(ev, pp, c);
+    if constexpr (FLAT == 1) return lm_descend_flat(ev, pp, c);
     else return lm_descend(ev, pp, c);
   };
   double ssq = descend(p);
@@ -1052,16 +807,13 @@ template <int NDMAX, typename QE, typename QM, int FLAT = 1>
 __host__ __device__ __forceinline__ int fit_segment_q2(const QE& qe, const QM& qm, int ndata,
                                                     const double* __restrict__ jtab, const LMConst& c,
                                                     double (&p)[4], double& ssq_out) {
-  if constexpr (NDMAX > 0 && FLAT == 3) {
-    FusedEval<NDMAX, QE> ev{qe, ndata, c.trig};
-    return fit_segment_t<1>(ev, qm, ndata, jtab, c, p, ssq_out);
-  } else if constexpr (NDMAX > 0) {
+  if constexpr (NDMAX > 0) {
     SplitEval<NDMAX, QE> ev{qe, ndata, c.trig};
     return fit_segment_t<FLAT>(ev, qm, ndata, jtab, c, p, ssq_out);
   } else {
     auto evalf = [&](const double (&pp)[4], Eval& e) { eval_gen(qe, ndata, pp, e); };
     FullEval<decltype(evalf)> ev{evalf};
-    return fit_segment_t<(FLAT >= 2 ? 1 : FLAT)>(ev, qm, ndata, jtab, c, p, ssq_out);
+    return fit_segment_t<FLAT>(ev, qm, ndata, jtab, c, p, ssq_out);
   }
 }
 
@@ -1101,18 +853,18 @@ struct GuessInline {
 // With the register path the wave first stages its 64 rows into LDS, transposed
 // ([pos][65]: conflict-free column reads), with coalesced 16-B loads when the
 // rows are contiguous — each QI value is then read from LDS at every evaluation.
-template <int NDMAX, bool CHAIN, bool ROWS = false, int SPEC = 0>
+// QREG (exact-ndata register path, chunk size 1): the segment's QI values are loaded
+// into registers once (QRegs) instead of re-read from LDS / L1 at every evaluation
+// (ndata 10: 248 VGPRs, still 2 waves per SIMD; step 0.5558 -> 0.5507 ms,
+// profiles/r02m_tune_lm_spec3.log). Same bits either way.
+template <int NDMAX, bool CHAIN, bool ROWS = false, bool QREG = false>
 __global__ __launch_bounds__(64) void lm_chunks_kernel(
     const double* __restrict__ qi, int64_t qi_ld, int ndata, int64_t nrec, int64_t nbuf, int64_t first,
     int64_t nitems, int64_t nchunk, const double* __restrict__ guess, int64_t g_rec, int64_t g_comp,
     GuessInline ginl, int use_inline, const double* __restrict__ jtab, LMConst c, double* __restrict__ out,
     int64_t out_ld, int32_t* __restrict__ status) {
   static_assert(!(ROWS && CHAIN), "row layout: chunk size 1 only");
-  // SPEC (register path, no chains): 1 = the lambda ladder speculated by finished lanes
-  // (lm_descend_spec), 2 = one fused ssqf + coeffs evaluation per trial (FusedEval)
-  // 3 = the split descent with the segment's QI held in registers (exact-ndata variant)
-  constexpr bool kQReg = SPEC == 3 && nd_exact(NDMAX) && !CHAIN;
-  constexpr int kFlat = (SPEC && SPEC < 3 && NDMAX > 0 && !CHAIN) ? SPEC + 1 : 1;
+  constexpr bool kQReg = QREG && nd_exact(NDMAX) && !CHAIN;
   extern __shared__ double lds_q[];  // STAGE: [qi_ld][65]
   const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = id < nrec * nchunk;
@@ -1194,7 +946,7 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
         qr.load(q);
         st = fit_segment_q2<NDMAX, QRegs<nd_cap(NDMAX)>, QRow<65>, 1>(qr, q, ndata, jtab, c, p, ssq);
       } else {
-        st = fit_segment_q<NDMAX, QRow<65>, kFlat>(q, ndata, jtab, c, p, ssq);
+        st = fit_segment_q<NDMAX, QRow<65>>(q, ndata, jtab, c, p, ssq);
       }
       dcv = q.at(dfmi_row_dc(ndata));
     } else {
@@ -1216,7 +968,7 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
         qr.load(qg);
         st = fit_segment_q2<NDMAX, QRegs<nd_cap(NDMAX)>, QGlobal, 1>(qr, qg, ndata, jtab, c, p, ssq);
       } else {
-        st = fit_segment<NDMAX, kFlat>(qi + sidx, qi_ld, ndata, jtab, c, p, ssq);
+        st = fit_segment<NDMAX>(qi + sidx, qi_ld, ndata, jtab, c, p, ssq);
       }
       put(sidx, st, ssq);
     };

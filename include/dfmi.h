@@ -251,27 +251,23 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
                    const double* witness, int64_t wit_stride, const dfmi_wdfmi_config* cfg, double* out,
                    int32_t* fitok, int32_t mem, void* stream);
 
-/* Performance tuning hook, process-wide (results are unaffected unless noted):
- * "demod_kernel" (1 phase bins in LDS where they apply [default], 0 cycle-aligned
- * fold), "demod_loads" (8 | 16 vector loads in flight per lane), "demod_nt" (0 | 1
- * non-temporal stream loads), "demod_blocks_per_cu" (0 = occupancy limit),
- * "demod_occ4" (1 = bin kernel held to 4 waves per SIMD), "lm_general" (1 = two-pass
- * LM path for every ndata), "seed_bins" (1 = seed fold in LDS; moves fits < 1e-10),
- * "seed_order" / "seed_fused" (seed step scheduling), "bins_loads" (8 | 16 chunk loads
- * in flight in the bin kernels), "bins_roll" (1 = software-pipelined load groups),
- * "bins_prefetch" (0 | 4 [default] | 6: chunks of the next segment loaded during a
- * segment's contraction), "bins_ilv" (1 = contraction interleaved with the next
- * segment's loads), "demod_spw" (segments per wave the bin grid is sized for; 0 =
- * persistent), "lm_spec" (LM descent schedule, same bits: 0 split trial / accept,
- * 1 lambda ladder speculated by finished lanes, 2 fused ssqf + coeffs per trial, 3 split
- * with the segment's QI in registers [default; ndata 10, others use 0]), "lm_refill" / "lm_phase" (LM lane refill / two phases with compaction, same
- * bits), "ekf_row" (EKF row kernel), "wdfmi_accel" (bit 0: W-DFMI
- * time axis without division, bit 1: template slopes in LDS; both exact), "probe"
- * (1 = diagnostics timestamps, dfmi_probe_read). */
+/* Performance tuning hook, process-wide; each call works on a snapshot taken at its
+ * start. Results are unaffected. Keys: "demod_kernel" (1 phase bins in LDS where they
+ * apply [default], 0 cycle-aligned fold), "lm_general" (1 = two-pass general LM path
+ * for every ndata), "demod_spw" (segments per wave the bin grid is sized for; 0 =
+ * persistent), "ekf_row" (EKF row kernel up to ekf_row x 16 x CUs channels, 0 = lane
+ * kernel only), "wdfmi_accel" (bit 0: W-DFMI time axis without division, bit 1:
+ * template slopes in LDS; both exact), "probe" (1 = diagnostics timestamp buffer on the
+ * current device, dfmi_probe_read). */
 int dfmi_set_tuning(const char* key, int64_t value);
 
 /* Current value of a tuning key (see dfmi_set_tuning). */
 int dfmi_get_tuning(const char* key, int64_t* value);
+
+/* Frees every scratch workspace of the current device after waiting for it to drain
+ * (workspaces are kept per caller stream, at most 4 streams, least recently used freed
+ * first). */
+int dfmi_release_workspaces(void);
 
 /* Diagnostics: with dfmi_set_tuning("probe", 1) some kernels record
  * s_memrealtime (100 MHz) timestamps; copies the first n (<= 16) of them
@@ -327,11 +323,11 @@ int dfmi_device_count(void);
 /* Message of the last failed call on this thread ("" if none). */
 const char* dfmi_last_error(void);
 
-/* Library/ABI version, e.g. "dfmi 0.2 gfx950". */
+/* Library/ABI version, e.g. "dfmi 0.3 gfx950". */
 const char* dfmi_version(void);
 
-/* Kernel variant of the last demodulation (or EKF fit) this process launched, e.g.
- * "demod_bins_kernel<2,8,1>", "ekf_row_kernel" ("" before the first one).
+/* Kernel variant of the last demodulation (or EKF fit) this THREAD launched, e.g.
+ * "demod_bins_kernel<2,8,rows,pf4>", "ekf_row_kernel" ("" before the first one).
  * Diagnostics/profiling. */
 const char* dfmi_last_demod_kernel(void);
 

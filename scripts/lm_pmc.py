@@ -1,4 +1,4 @@
-"""PMC helper: one dfmi_lm launch per LM kernel variant (lm_refill 0 / 1) over config-2
+"""PMC helper: one dfmi_lm launch per LM kernel variant (lm_general 0 / 1) over config-2
 QI, for `rocprofv3 --pmc ...` per-dispatch counters (dynamic instruction counts)."""
 import os
 import sys
@@ -27,7 +27,7 @@ p = torch.empty((4, nseg), dtype=torch.float64, device=dev)
 ssq = torch.empty(nseg, dtype=torch.float64, device=dev)
 status = torch.empty(nseg, dtype=torch.int32, device=dev)
 cfg = F.lm_config()
-for spec in os.environ.get("SETTINGS", "lm_refill=0;lm_refill=1").split(";"):
+for spec in os.environ.get("SETTINGS", "lm_general=0;lm_general=1").split(";"):
     for kv in filter(None, spec.split(",")):
         k, v = kv.split("=")
         _lib.check(lib.dfmi_set_tuning(k.encode(), int(v)), k)

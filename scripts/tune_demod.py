@@ -24,10 +24,10 @@ def main():
     dc = torch.empty(nseg, dtype=torch.float64, device=dev)
     st = torch.cuda.current_stream()
     w0 = w0_of(1000.0, 200000.0)
-    # (demod_kernel, demod_loads, demod_nt, demod_blocks_per_cu); demod_loads / demod_nt tune the fold kernel
+    # (demod_kernel, demod_spw): fold kernel vs bin kernel, grid sizing
     variants = [tuple(int(t) for t in v.split(",")) for v in os.environ.get(
-        "VARIANTS", "0,8,1,0;1,8,1,0;1,8,1,3;0,16,1,0").split(";")]
-    keys = ("demod_kernel", "demod_loads", "demod_nt", "demod_blocks_per_cu")
+        "VARIANTS", "0,2;1,2;1,0;1,3").split(";")]
+    keys = ("demod_kernel", "demod_spw")
     res = {v: [] for v in variants}
     ref = {"torch_sum": [], "torch_copy": []}
     y = torch.empty_like(x)

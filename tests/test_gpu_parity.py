@@ -314,10 +314,9 @@ def test_demod_rows_bit_identical_to_component_major(nd):
 
 def test_record_rows_path_matches_component_path():
     """dfmi_nls_record through the row layout (default for chunk size 1) is
-    bit-identical to the component-major path (forced with demod_kernel = 0) when both
-    use the same seed kernel, for a multi-record strided batch and for nbuf = 1 (the dc
-    of the seed buffers); the LDS seed kernel (seed_bins) folds buffer 0 in another
-    summation order, which moves the seeded fits by < 1e-9."""
+    bit-identical to the component-major path (forced with demod_kernel = 0), for a
+    multi-record strided batch and for nbuf = 1 (the dc of the seed buffers): the seed
+    of both paths is the LDS bin fold of buffer 0 (seed_bins_kernel)."""
     import torch
     from deepfmkit_amd import _lib
     from deepfmkit_amd.fitters import nls_records
@@ -332,58 +331,25 @@ def test_record_rows_path_matches_component_path():
     recs[:, : 40 * R] = base + 1e-3 * torch.randn(base.shape, dtype=torch.float64, device="cuda", generator=g)
     for nbuf in (40, 1):
         res = {}
-        for kern, seedb in ((1, 0), (0, 0), (1, 1)):
+        for kern in (1, 0):
             _lib.check(lib.dfmi_set_tuning(b"demod_kernel", kern), "tune")
-            _lib.check(lib.dfmi_set_tuning(b"seed_bins", seedb), "tune")
             cols, ok = nls_records(recs, 200000.0, 1000.0, R, nbuf, 10)
-            res[kern, seedb] = (cols.cpu().numpy(), ok.cpu().numpy(), lib.dfmi_last_demod_kernel().decode())
+            res[kern] = (cols.cpu().numpy(), ok.cpu().numpy(), lib.dfmi_last_demod_kernel().decode())
         _lib.check(lib.dfmi_set_tuning(b"demod_kernel", 1), "tune")
-        _lib.check(lib.dfmi_set_tuning(b"seed_bins", 1), "tune")
-        a, b, c = res[1, 0], res[0, 0], res[1, 1]
+        a, b = res[1], res[0]
         assert "rows" in a[2] and "rows" not in b[2], (a[2], b[2])
         np.testing.assert_array_equal(a[0], b[0])
         np.testing.assert_array_equal(a[1], b[1])
-        np.testing.assert_array_equal(c[1], b[1])
-        assert np.abs(c[0] - b[0]).max() < 1e-9
 
 
-def test_seed_stream_order_identical():
-    """The seed step (buffer 0, fitters.py:403-410) runs fused into the bulk
-    demodulation launch (seed_fused 1, default), as its own kernel on the caller's
-    stream beside the bulk on the side stream (seed_fused 0, seed_order 1), or the
-    other way round (seed_order 0); the results are the same bits."""
-    import torch
-    from deepfmkit_amd import _lib
-    from deepfmkit_amd.fitters import nls_records
-    lib = _lib.load()
-    R, nbuf = 4000, 300
-    t = torch.arange(nbuf * R, dtype=torch.float64, device="cuda") / 200000.0
-    g = torch.Generator(device="cuda")
-    g.manual_seed(3)
-    x = (1.0 + torch.cos(0.4 + 6.2 * torch.cos(2 * np.pi * 1000.0 * t + 0.2))).reshape(1, -1)
-    x = x + 1e-3 * torch.randn(x.shape, dtype=torch.float64, device="cuda", generator=g)
-    res = []
-    for fused, order in ((1, 1), (0, 1), (0, 0), (1, 1)):
-        _lib.check(lib.dfmi_set_tuning(b"seed_fused", fused), "tune")
-        _lib.check(lib.dfmi_set_tuning(b"seed_order", order), "tune")
-        cols, ok = nls_records(x, 200000.0, 1000.0, R, nbuf, 10)
-        res.append((cols.cpu().numpy(), ok.cpu().numpy(), lib.dfmi_last_demod_kernel().decode()))
-    _lib.check(lib.dfmi_set_tuning(b"seed_fused", 1), "tune")
-    _lib.check(lib.dfmi_set_tuning(b"seed_order", 1), "tune")
-    names = [r[2] for r in res]
-    assert names[0].startswith("demod_seed_bins_kernel") and "spacer" in names[1] and "spacer" not in names[2], names
-    for cols, ok, _ in res[1:]:
-        np.testing.assert_array_equal(cols, res[0][0])
-        np.testing.assert_array_equal(ok, res[0][1])
-
-
-@pytest.mark.parametrize("nrec,nbuf", [(3, 40), (600, 3), (4, 1), (1, 2)])
+@pytest.mark.parametrize("nrec,nbuf", [(3, 40), (600, 3), (4, 1), (1, 2), (1, 300)])
 def test_fused_seed_layouts_match_unfused(nrec, nbuf):
-    """The fused seed + demodulation launch (seed_fused 1) against the two-kernel path
-    (seed_fused 0) across record layouts: several records (one seed workgroup each),
-    more records than can be resident as seeds (the fused path steps aside), single-
-    buffer records (no LM), two buffers. Same bits; every record's seed is its own
-    buffer 0 (fitters.py:403-410)."""
+    """The fused seed + demodulation launch (contiguous records) against the two-kernel
+    path (the same records laid out with rec_stride > nbuf*R: seed kernel on the side
+    stream beside the bulk demodulation) across layouts: several records (one seed
+    workgroup each), more records than can be resident as seeds (the fused path steps
+    aside), single-buffer records (no LM), two buffers. Same bits; every record's seed
+    is its own buffer 0 (fitters.py:403-410)."""
     import torch
     from deepfmkit_amd import _lib
     from deepfmkit_amd.fitters import nls_records
@@ -395,12 +361,20 @@ def test_fused_seed_layouts_match_unfused(nrec, nbuf):
     ms = torch.linspace(4.0, 8.0, nrec, dtype=torch.float64, device="cuda")[:, None]
     x = 1.0 + torch.cos(0.3 + ms * torch.cos(2 * np.pi * 1000.0 * t[None, :] + 0.1))
     x = (x + 1e-3 * torch.randn(x.shape, dtype=torch.float64, device="cuda", generator=g)).contiguous()
+    # unfused: every record twice (so even nrec = 1 is a multi-record batch), strided
+    strided = torch.zeros((2 * nrec, nbuf * R + 2 * R), dtype=torch.float64, device="cuda")
+    strided[:nrec, : nbuf * R] = x
+    strided[nrec:, : nbuf * R] = x
     res = []
-    for fused in (1, 0):
-        _lib.check(lib.dfmi_set_tuning(b"seed_fused", fused), "tune")
-        cols, ok = nls_records(x, 200000.0, 1000.0, R, nbuf, 10, init_guess=(1.0, 6.0, 0.0, 0.0))
-        res.append((cols.cpu().numpy(), ok.cpu().numpy()))
-    _lib.check(lib.dfmi_set_tuning(b"seed_fused", 1), "tune")
+    for arr in (x, strided):
+        cols, ok = nls_records(arr, 200000.0, 1000.0, R, nbuf, 10, init_guess=(1.0, 6.0, 0.0, 0.0))
+        res.append((cols.cpu().numpy()[:, : nrec * nbuf], ok.cpu().numpy()[: nrec * nbuf],
+                    lib.dfmi_last_demod_kernel().decode()))
+        if arr is strided:
+            np.testing.assert_array_equal(cols.cpu().numpy()[:, nrec * nbuf:], res[-1][0])
+    if nrec * 2 < 400 and nbuf > 1:
+        assert res[0][2].startswith("demod_seed_bins_kernel"), res[0][2]
+    assert not res[1][2].startswith("demod_seed_bins_kernel"), res[1][2]
     np.testing.assert_array_equal(res[0][0], res[1][0])
     np.testing.assert_array_equal(res[0][1], res[1][1])
     m = res[0][0][1].reshape(nrec, nbuf)

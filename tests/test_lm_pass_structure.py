@@ -2,7 +2,7 @@
 2"), counted on the oracle restatement of _run_lma_fit (fit.py:208-258): every segment
 seeded from buffer 0 accepts 2 or 3 steps, and a sizeable share of lanes end with the
 full 8-rung "no lambda improved" ladder (fit.py:246-247), so every 64-lane wave runs 10
-one-trial passes — the fact the LM schedules of lm.h (lm_spec) were built around."""
+one-trial passes — the fact the LM schedules of lm.h were built around."""
 import numpy as np
 
 import deepfmkit_amd as dfm

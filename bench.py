@@ -63,6 +63,8 @@ def parse():
                     help="Pool size of the CPU baseline (0: every CPU this process may use, bench.cpu_share)")
     ap.add_argument("--demod-only", action="store_true", help="profile helper: time only the demod kernel")
     ap.add_argument("--tune", default="", help="A/B helper: dfmi_set_tuning knobs as key=value[,key=value]")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the extra config keys (config 3, config 5, config 1 sequential) after the timed window")
     return ap.parse_args()
 
 
@@ -160,6 +162,124 @@ def parity_vs_oracle(df, ref):
             "vs": "oracle restatement of fit.py/fitters.py, pinned to the reference by tests/golden"}
 
 
+def _timed_steps(torch, fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def extra_configs(torch, dev, lib, _lib, stream, cfg, cpu_leg):
+    """The other BASELINE.json configs on this GPU, timed after the main window (same
+    process, steady clocks): config 3 (two channels, main m = 6 and witness m = 4.3, as
+    two records of one dfmi_nls_record call, each seeded by its own buffer 0: 2 x 50,000
+    segments), config 5 (EKFFitter.fit over a 2 s = 400,000-sample record, one channel,
+    and 1,024 channels in one launch; with the scalar C restatement of the same loop
+    timed on one host core beside it when the CPU leg runs) and config 1 through the
+    sequential path (_fit_sequential: one warm-start chain over 500 buffers)."""
+    from deepfmkit_amd.fitters import w0_of
+    R = int(F_SAMP / F_MOD * N_CYC)
+    w0 = w0_of(F_MOD, F_SAMP)
+    out = {}
+    # ---- config 3
+    nbuf = 50_000
+    x = torch.empty(2 * nbuf * R, dtype=torch.float64, device=dev)
+    for c, m in enumerate((M_TRUE, 4.3)):
+        gen_shard(torch, dev, 0, nbuf, R, seed=SEED, m_true=m, stream=c, out=x[c * nbuf * R:(c + 1) * nbuf * R])
+    g2 = np.ascontiguousarray(np.tile([1.6, 6.0, 0.0, 0.0], (2, 1)))
+    o2 = torch.empty((6, 2 * nbuf), dtype=torch.float64, device=dev)
+    k2 = torch.empty(2 * nbuf, dtype=torch.int32, device=dev)
+
+    def step3():
+        _lib.check(lib.dfmi_nls_record(x.data_ptr(), 2, nbuf * R, nbuf, R, NDATA, w0, 0, _lib.ptr(g2), 1, nbuf - 1, cfg,
+                                       o2.data_ptr(), k2.data_ptr(), _lib.DFMI_MEM_DEVICE, stream.cuda_stream),
+                   "dfmi_nls_record")
+
+    s3 = _timed_steps(torch, step3, 20, 5)
+    st = k2.cpu().numpy()
+    mm = o2[1].cpu().numpy()
+    out["config3"] = {"workload": "2 channels (main m=6, witness m=4.3) x 50,000 segments, one dfmi_nls_record call",
+                      "value": round(2 * nbuf / s3, 1), "unit": "segments/s", "ms_per_step": round(s3 * 1e3, 4),
+                      "steps": 20, "status0_frac": float(np.mean(st == 0)),
+                      "m_mean_per_channel": [float(mm[:nbuf].mean()), float(mm[nbuf:].mean())]}
+    del x, o2, k2
+    # ---- config 5: EKF, 2 s @ 200 kS/s
+    from deepfmkit_amd.physics import SnrSpec, synth_snr
+    ns = int(2.0 * F_SAMP)
+    nb5 = ns // R
+    p0 = np.ones(5)
+    qd = np.array([1e-8, 1e-8, 1e-6, 1e-6, 1e-8])
+    init4 = torch.tensor([1.6, 6.0, 0.0, 0.0], dtype=torch.float64, device=dev)
+    p0d = torch.from_numpy(p0).to(dev)
+    qdd = torch.from_numpy(qd).to(dev)
+    res5 = {}
+    for nch in (1, 1024):
+        xe = torch.empty(nch * ns, dtype=torch.float64, device=dev)
+        for c in range(nch):
+            synth_snr(SnrSpec(seed=SEED, stream=100 + c, f_samp=F_SAMP, f_mod=F_MOD, m=M_TRUE, snr_db=SNR_DB), 0, ns,
+                      out=xe[c * ns:(c + 1) * ns])
+        stt = torch.empty((nch, nb5, 5), dtype=torch.float64, device=dev)
+
+        def ekf():
+            _lib.check(lib.dfmi_ekf_fit(xe.data_ptr(), nch, ns, ns, init4.data_ptr(), p0d.data_ptr(), qdd.data_ptr(),
+                                        None, 2 * np.pi * F_MOD, F_SAMP, R, nb5, stt.data_ptr(), _lib.DFMI_MEM_DEVICE,
+                                        stream.cuda_stream), "dfmi_ekf_fit")
+
+        t = _timed_steps(torch, ekf, 3, 1)
+        res5[nch] = {"channels": nch, "s_per_fit": round(t, 5), "samples_per_s_per_channel": round(ns / t, 1),
+                     "samples_per_s_aggregate": round(nch * ns / t, 1),
+                     "kernel": lib.dfmi_last_demod_kernel().decode()}
+        if nch == 1:
+            x1 = xe.cpu().numpy()
+            s1 = stt[0].cpu().numpy()
+        del xe, stt
+    c5 = {"workload": "EKFFitter.fit, 2 s = 400,000 samples @200 kS/s (m=6, 40 dB), snapshots every R=4000",
+          "one_channel": res5[1], "channels_1024": res5[1024], "unit": "samples/s"}
+    if cpu_leg:  # the host baseline: the oracle's scalar C restatement of the same loop, one core
+        import ctypes
+        lib_c = os.path.join(ROOT, "oracle", "libekf_scalar.so")
+        if os.path.exists(lib_c):
+            cl = ctypes.CDLL(lib_c)
+            P_ = ctypes.c_void_p
+            cl.ekf_scalar.argtypes = [P_, ctypes.c_int64, P_, P_, P_, ctypes.c_double, ctypes.c_double,
+                                      ctypes.c_double, ctypes.c_int64, ctypes.c_int64, P_]
+            cx0 = np.array([1.6, 6.0, 0.0, 0.0, np.mean(x1)])
+            cst = np.zeros((nb5, 5))
+            t0 = time.perf_counter()
+            cl.ekf_scalar(x1.ctypes.data, ns, cx0.ctypes.data, p0.ctypes.data, qd.ctypes.data, float(np.var(x1)),
+                          2 * np.pi * F_MOD, F_SAMP, R, nb5, cst.ctypes.data)
+            tc = time.perf_counter() - t0
+            c5["cpu_baseline"] = {"value": round(ns / tc, 1), "unit": "samples/s per channel", "cores": 1,
+                                  "kind": "port", "sample": "the same 400,000-sample record, oracle/csrc/ekf_scalar.c "
+                                                            "(gcc -O2, libm), the numpy loop's operation order"}
+            c5["max_abs_dstate_gpu_vs_cpu"] = float(np.max(np.abs(s1 - cst)))
+    out["config5"] = c5
+    # ---- config 1 through the sequential path (one warm-start chain, fitters.py:370-393)
+    nb1 = 500
+    x1r = torch.empty(nb1 * R, dtype=torch.float64, device=dev)
+    gen_shard(torch, dev, 0, nb1, R, seed=SEED, out=x1r)
+    g1 = np.array([1.6, 6.0, 0.0, 0.0])
+    o1 = torch.empty((6, nb1), dtype=torch.float64, device=dev)
+    k1 = torch.empty(nb1, dtype=torch.int32, device=dev)
+
+    def seq():
+        _lib.check(lib.dfmi_nls_record(x1r.data_ptr(), 1, nb1 * R, nb1, R, NDATA, w0, 0, _lib.ptr(g1), 0, 1, cfg,
+                                       o1.data_ptr(), k1.data_ptr(), _lib.DFMI_MEM_DEVICE, stream.cuda_stream),
+                   "dfmi_nls_record")
+
+    t1 = _timed_steps(torch, seq, 5, 1)
+    out["config1_sequential"] = {"workload": "500 segments (10 s @200 kS/s), parallel=False: one warm-start chain",
+                                 "value": round(nb1 / t1, 1), "unit": "segments/s", "ms_per_fit": round(t1 * 1e3, 3),
+                                 "status0_frac": float(np.mean(k1.cpu().numpy() == 0)),
+                                 "reference_same_path": "724 segments/s on one core of the survey container "
+                                                        "(SURVEY.md §6)"}
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -240,34 +360,47 @@ def main():
                                  stream.cuda_stream)
         _lib.check(rc, "dfmi_demod_rows")
 
-    # ---- roofline of the dominant kernel (demod), HIP events on the launch stream ----
-    # (measured BEFORE the timed window: these ~2 x nrep untimed launches also bring the
-    # GPU to its steady clocks, so a short driver window carries no ramp-up)
+    # ---- roofline of the step's dominant kernel, HIP events on the launch stream ----
+    # (measured BEFORE the timed window: these untimed launches also bring the GPU to its
+    # steady clocks, so a short driver window carries no ramp-up)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     # untimed: clocks ramp up over the first ~35 demodulation-sized launches (0.58 -> 0.50 ms,
-    # profiles/r02m kernel trace); the ramp runs on whole steps, so every launch of the
-    # roofline kernel (and its rocprof average) sees steady clocks
+    # profiles/r02m kernel trace)
     for _ in range(40):
         step()
-    for _ in range(5):
-        demod()
     nrep = max(20, args.steps)
-    ev0.record(stream)
+    # the step itself with timing events around its kernels (dfmi_step_timing): the fused
+    # seed + demodulation launch (the dominant kernel) and the LM launch, on the step's stream
+    _lib.check(lib.dfmi_step_timing(1), "dfmi_step_timing")
     for _ in range(nrep):
-        demod()
-    ev1.record(stream)
-    ev1.synchronize()
-    demod_ms = ev0.elapsed_time(ev1) / nrep
+        step()
+    _lib.check(lib.dfmi_step_timing(0), "dfmi_step_timing")
+    td, tl, tn = np.zeros(1), np.zeros(1), np.zeros(1, dtype=np.int64)
+    _lib.check(lib.dfmi_step_timing_read(_lib.ptr(td), _lib.ptr(tl), _lib.ptr(tn)), "dfmi_step_timing_read")
+    step_kname = lib.dfmi_last_demod_kernel().decode()
+    if int(tn[0]) != nrep:
+        raise SystemExit(f"step timing: {int(tn[0])} marked steps of {nrep} (pipeline not fused: {step_kname})")
+    demod_ms, lm_step_ms = float(td[0]) / nrep, float(tl[0]) / nrep
     demod_ms_max = demod_ms
     if world > 1:  # the slowest rank's dominant kernel (every rank runs the same shape)
         tt = torch.tensor([demod_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         demod_ms_max = float(tt.item())
-    kname = lib.dfmi_last_demod_kernel().decode()
+    kname = step_kname
+    # the standalone row demodulation (dfmi_demod_rows, no seed): the same bulk code
+    for _ in range(5):
+        demod()
+    ev0.record(stream)
+    for _ in range(nrep):
+        demod()
+    ev1.record(stream)
+    ev1.synchronize()
+    rows_ms = ev0.elapsed_time(ev1) / nrep
     if args.demod_only:  # profile helper: nothing but the timed demodulation kernel
         if rank == 0:
-            print(json.dumps({"metric": "demod only (profile helper)", "kernel": kname, "avg_launch_ms": demod_ms,
-                              "roofline": {"kernel": kname}}), flush=True)
+            print(json.dumps({"metric": "demod only (profile helper)", "kernel": lib.dfmi_last_demod_kernel().decode(),
+                              "avg_launch_ms": rows_ms, "roofline": {"kernel": lib.dfmi_last_demod_kernel().decode()}}),
+                  flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -332,9 +465,16 @@ def main():
         if family and family in rec.get("kernel", "") and rec.get("algorithmic_bytes_per_launch") == \
                 nall * bytes_per_seg:
             traffic, traffic_src = rec.get("hbm_bytes_per_launch"), "profiles/pmc_demod.json"
+    e2e = nall * bytes_per_seg / (ms * 1e-3) / 1e9  # the whole step (seed + demodulation + LM) at the same bytes
     roof = {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-            "avg_launch_ms": round(demod_ms, 4), "algorithmic_bytes_per_launch": nall * bytes_per_seg}
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_source": traffic_src, "avg_launch_ms": round(demod_ms, 4),
+            "timing": f"HIP events around the step's own {kname} launch inside dfmi_nls_record "
+                      f"(dfmi_step_timing), mean over {nrep} steps",
+            "algorithmic_bytes_per_launch": nall * bytes_per_seg,
+            "end_to_end_frac": round(e2e / HBM_PEAK_GBS, 4),
+            "end_to_end_note": "algorithmic bytes of the step / ms_per_step / peak: the LM after the "
+                               "demodulation included"}
     if world > 1:
         roof["avg_launch_ms_max_over_ranks"] = round(demod_ms_max, 4)
         roof["frac_min_over_ranks"] = round(nall * bytes_per_seg / (demod_ms_max * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
@@ -356,13 +496,16 @@ def main():
                        "segments_per_gpu": nseg, "channels": nrec, "R": R, "ndata": NDATA,
                        "parallelism": f"shard{world}"},
             "roofline": roof,
-            "kernels_ms": {"demod": round(demod_ms, 4), "lm_all_segments": round(lm_ms, 4)},
+            "kernels_ms": {"step_demod_seed": round(demod_ms, 4), "step_lm": round(lm_step_ms, 4),
+                           "demod_rows_alone": round(rows_ms, 4), "lm_alone_all_segments": round(lm_ms, 4)},
             "batch_status0_frac": float(np.mean(st == 0)),
             "batch_m_mean": float(res[1].mean())}
     if args.demod_only:
         line["metric"] = "demod only (profile helper)"
     if args.tune:
         line["tuning"] = args.tune
+    if world == 1 and not args.no_extra and nrec == 1 and args.segments is None:
+        line["extra_configs"] = extra_configs(torch, dev, lib, _lib, stream, cfg, want_base)
     if pre is not None:
         raw, ref, procs, base = pre
         df = StandardNLSFitter({"n": N_CYC}).fit(raw, parallel=True, n_cores=procs)  # same chunking, on GPU

@@ -25,7 +25,7 @@ SYMBOLS = ("dfmi_lm_config_default", "dfmi_demod", "dfmi_lm", "dfmi_nls_record",
            "dfmi_probe_read", "dfmi_get_tuning", "dfmi_txt_parse_header", "dfmi_txt_shape", "dfmi_txt_read",
            "dfmi_fit_txt_write", "dfmi_py_repr", "dfmi_txt_last_error", "dfmi_wdfmi_fit", "dfmi_ekf_fit",
            "dfmi_record_moments", "dfmi_synth_asd", "dfmi_synth_snr", "dfmi_bessel_eval",
-           "dfmi_release_workspaces")
+           "dfmi_release_workspaces", "dfmi_step_timing", "dfmi_step_timing_read")
 
 
 class DFMIError(RuntimeError):
@@ -158,6 +158,10 @@ def load():
         lib.dfmi_get_tuning.restype = ctypes.c_int
         lib.dfmi_release_workspaces.argtypes = []
         lib.dfmi_release_workspaces.restype = ctypes.c_int
+        lib.dfmi_step_timing.argtypes = [ctypes.c_int32]
+        lib.dfmi_step_timing.restype = ctypes.c_int
+        lib.dfmi_step_timing_read.argtypes = [P, P, P]
+        lib.dfmi_step_timing_read.restype = ctypes.c_int
         lib.dfmi_probe_read.argtypes = [P, i32]
         lib.dfmi_probe_read.restype = ctypes.c_int
         lib.dfmi_last_demod_kernel.argtypes = []

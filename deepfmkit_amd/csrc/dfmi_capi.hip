@@ -8,6 +8,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <array>
 #include <cstdint>
 #include <map>
 #include <mutex>
@@ -52,6 +53,9 @@ struct Tuning {
                          // (past one wave per SIMD the issue-bound rows share a SIMD, and one lane per
                          // channel carries 16x the channels per instruction); 0 = ekf_kernel only
   int wdfmi_accel = 3;   // W-DFMI: bit 0 time axis without division, bit 1 template slopes in LDS
+  int lm_ladder = 32;    // LM launches of at most lm_ladder x CUs chains / segments (latency-bound: warm-start
+                         // chains, small batches) run the parallel lambda ladder (lm.h lm_ladder_kernel);
+                         // 0 = always one lane per chain / segment
 };
 Tuning g_tune;
 
@@ -118,6 +122,11 @@ struct DeviceState {
   hipStream_t side = nullptr;  // seed step runs here, concurrently with the bulk demod (unfused layouts)
   hipEvent_t ev_in = nullptr, ev_seed = nullptr;
   uint64_t* probe = nullptr;   // diagnostics timestamps of this device (dfmi_set_tuning("probe", 1))
+  // dfmi_step_timing: timing events around the record pipeline's kernels, per call
+  // [start, after the demodulation launch, after the LM launch]
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::array<hipEvent_t, 3>> ev_steps;
 };
 
 std::map<int, DeviceState> g_dev;
@@ -172,6 +181,31 @@ int ensure_init_locked(int* dev_out) {
   *dev_out = dev;
   return DFMI_OK;
 }
+
+// Step-timing marks (dfmi_step_timing): mark(i) records event i of the current step's
+// triple on st when timing is on.
+struct StepMarks {
+  std::array<hipEvent_t, 3> ev{};
+  bool on = false;
+  int begin(DeviceState& ds) {
+    on = ds.timing;
+    if (!on) return DFMI_OK;
+    for (auto& e : ev) {
+      if (ds.ev_pool.empty()) {
+        HIPCHK(hipEventCreate(&e));
+      } else {
+        e = ds.ev_pool.back();
+        ds.ev_pool.pop_back();
+      }
+    }
+    ds.ev_steps.push_back(ev);
+    return DFMI_OK;
+  }
+  int mark(int i, hipStream_t st) {
+    if (on) HIPCHK(hipEventRecord(ev[i], st));
+    return DFMI_OK;
+  }
+};
 
 int free_stream_ws(StreamWs& s) {
   for (auto& kv : s.bufs)
@@ -554,6 +588,29 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
   const bool chain = nitems > nchunk;
   const int nd_sel = t_tune.lm_general ? 1000 : ndata;
   if (rows && chain) return fail(DFMI_ERR_ARG, "row layout: chunk size 1 only");
+  // latency-bound launches (few chains or segments: at most ~2 ladder waves per SIMD):
+  // the parallel lambda ladder, kLadderLanes lanes per item (lm.h lm_ladder_kernel)
+  if (t_tune.lm_ladder && lanes <= (int64_t)t_tune.lm_ladder * t_ds->n_cu) {
+    constexpr int kNd10 = dfmi::kExactNd | 10;
+    using LK = void (*)(const double*, int64_t, int, int64_t, int64_t, int64_t, int64_t, int64_t, const double*,
+                        int64_t, int64_t, dfmi::GuessInline, int, const double*, dfmi::LMConst, double*, int64_t,
+                        int32_t*);
+    LK lk;
+    if (rows)
+      lk = nd_sel == 10 ? dfmi::lm_ladder_kernel<kNd10, false, true> : nd_sel <= 12 ? dfmi::lm_ladder_kernel<12, false, true>
+           : nd_sel <= 16 ? dfmi::lm_ladder_kernel<16, false, true> : dfmi::lm_ladder_kernel<0, false, true>;
+    else if (chain)
+      lk = nd_sel == 10 ? dfmi::lm_ladder_kernel<kNd10, true, false> : nd_sel <= 12 ? dfmi::lm_ladder_kernel<12, true, false>
+           : nd_sel <= 16 ? dfmi::lm_ladder_kernel<16, true, false> : dfmi::lm_ladder_kernel<0, true, false>;
+    else
+      lk = nd_sel == 10 ? dfmi::lm_ladder_kernel<kNd10, false, false> : nd_sel <= 12 ? dfmi::lm_ladder_kernel<12, false, false>
+           : nd_sel <= 16 ? dfmi::lm_ladder_kernel<16, false, false> : dfmi::lm_ladder_kernel<0, false, false>;
+    const int64_t lgrid = (lanes * dfmi::kLadderLanes + block - 1) / block;
+    hipLaunchKernelGGL(lk, dim3((unsigned)lgrid), dim3(block), 0, st, qi, qi_ld, ndata, nrec, nbuf, first, nitems,
+                       nchunk, guess_dev, g_rec, g_comp, ginl, use_inline, jtab, c, out, out_ld, status);
+    HIPCHK(hipGetLastError());
+    return DFMI_OK;
+  }
   size_t lds = 0;
   auto kern = chain ? lm_kernel<true, false>(nd_sel) : rows ? lm_kernel<false, true>(nd_sel)
                                                             : lm_kernel<false, false>(nd_sel);
@@ -686,12 +743,22 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
     if ((rc = basis_table(dev, L, ndata, w0, st, &tab))) return rc;
     void* rw = nullptr;
     if ((rc = workspace(dev, "qrow", (size_t)qs * nseg * sizeof(double), &rw))) return rc;
+    StepMarks sm;
+    if ((rc = sm.begin(ds)) || (rc = sm.mark(0, st))) return rc;
     rc = fused_seed_demod(dev, x, nrec, nbuf, R, ndata, L, tab, (double*)rw, qs, gdev, ginl, jtab, c, out, out_ld,
                           fitok, st);
     if (rc < 0) return rc;
-    if (rc == 0)
-      return lm_device(dev, (double*)rw, qs, ndata, nrec, nbuf, 1, nbuf - 1, nchunk, out, nbuf, out_ld, nullptr, c,
-                       jtab, out, out_ld, fitok, st, true);
+    if (rc == 0) {
+      if ((rc = sm.mark(1, st))) return rc;
+      rc = lm_device(dev, (double*)rw, qs, ndata, nrec, nbuf, 1, nbuf - 1, nchunk, out, nbuf, out_ld, nullptr, c,
+                     jtab, out, out_ld, fitok, st, true);
+      if (rc) return rc;
+      return sm.mark(2, st);
+    }
+    if (sm.on) {  // not fused after all: no marks for this call
+      ds.ev_pool.insert(ds.ev_pool.end(), sm.ev.begin(), sm.ev.end());
+      ds.ev_steps.pop_back();
+    }
   }
   if (parallel) {  // the seed beside the bulk demodulation (side stream, event)
     HIPCHK(hipEventRecord(ds.ev_in, st));
@@ -751,7 +818,8 @@ const std::map<std::string, Knob>& knobs() {
       {"lm_general", {&Tuning::lm_general, {0, 1}}},
       {"demod_spw", {&Tuning::demod_spw, {}}},
       {"ekf_row", {&Tuning::ekf_row, {}}},
-      {"wdfmi_accel", {&Tuning::wdfmi_accel, {0, 1, 2, 3}}}};
+      {"wdfmi_accel", {&Tuning::wdfmi_accel, {0, 1, 2, 3}}},
+      {"lm_ladder", {&Tuning::lm_ladder, {}}}};
   return k;
 }
 // np.mean / np.var of nrec device records on st (moments.hip), numpy-exact.
@@ -961,6 +1029,37 @@ int dfmi_set_tuning(const char* key, int64_t value) {
   }
   std::lock_guard<std::mutex> g(g_mu);
   g_tune.*(kn.v) = (int)value;
+  return DFMI_OK;
+}
+
+int dfmi_step_timing(int32_t enable) {
+  CallScope cs;
+  int dev;
+  if (int rc = ensure_init(&dev)) return rc;
+  t_ds->timing = enable != 0;
+  return DFMI_OK;
+}
+
+int dfmi_step_timing_read(double* demod_ms, double* lm_ms, int64_t* nsteps) {
+  CallScope cs;
+  if (!demod_ms || !lm_ms || !nsteps) return fail(DFMI_ERR_ARG, "null pointer");
+  int dev;
+  if (int rc = ensure_init(&dev)) return rc;
+  DeviceState& ds = *t_ds;
+  double d = 0.0, l = 0.0;
+  for (auto& tr : ds.ev_steps) {
+    HIPCHK(hipEventSynchronize(tr[2]));
+    float a = 0.f, b = 0.f;
+    HIPCHK(hipEventElapsedTime(&a, tr[0], tr[1]));
+    HIPCHK(hipEventElapsedTime(&b, tr[1], tr[2]));
+    d += a;
+    l += b;
+    ds.ev_pool.insert(ds.ev_pool.end(), tr.begin(), tr.end());
+  }
+  *nsteps = (int64_t)ds.ev_steps.size();
+  *demod_ms = d;
+  *lm_ms = l;
+  ds.ev_steps.clear();
   return DFMI_OK;
 }
 

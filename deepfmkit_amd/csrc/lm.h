@@ -613,6 +613,7 @@ struct FullEval {
   }
   DFMI_HDI void accept(const double (&)[4], const Trial& t, Eval& e) { e = t.e; }
   DFMI_HDI void solve(const Eval& e, double lam, double (&dp)[4]) { damped_solve(e, lam, dp); }
+  DFMI_HDI static double ssq_of(const Trial& t) { return t.e.ssq; }
 };
 
 template <int NDMAX, typename QF>
@@ -624,6 +625,7 @@ struct SplitEval {  // NDMAX: a register-path variant tag (nd_cap / nd_exact)
   DFMI_HDI double trial(const double (&p)[4], Trial& t) { return eval_reg_trial<NDMAX>(q, nd, p, t, k); }
   DFMI_HDI void accept(const double (&p)[4], const Trial& t, Eval& e) { eval_reg_accept<NDMAX>(q, nd, p, t, e); }
   DFMI_HDI void solve(const Eval& e, double lam, double (&dp)[4]) { damped_solve_block(e, lam, dp); }
+  DFMI_HDI static double ssq_of(const Trial& t) { return t.ssq; }
 };
 
 // fit.py:208-258 (_run_lma_fit), nested form (one lane at a time: the host build's
@@ -679,6 +681,85 @@ __device__ __forceinline__ T shfl_any(T v, int src) {
   } else {
     return __shfl(v, src);
   }
+}
+
+constexpr int kLadderLanes = 8;  // lanes per segment of the parallel-ladder descent (= the default ladder)
+
+// fit.py:208-258 (_run_lma_fit) with the lambda ladder evaluated in parallel. The LPS
+// lanes of a lane group (lanes LPS·g .. LPS·g + LPS-1 of the wave) hold the same segment
+// and the same descent state (p and coeffs at p); in every pass lane r of the group
+// solves and tries rung base + r (msolve + ssqf, fit.py:226-243). The group takes the
+// FIRST improving rung in ladder order, with that rung's trial state fetched from the
+// lane that evaluated it, and forms coeffs there (every lane of the group, redundantly:
+// same bits); if no rung of the block improved it moves to the next LPS rungs
+// (n_lambda > LPS) or stops ("no lambda improved", fit.py:246-247). A rung's solve +
+// trial is the same pure function of (p, J^T J, J^T r, lambda, QI) whichever lane
+// computes it, and a rung whose step is below min_step_norm counts as not improving
+// (the sequential ladder skips it, fit.py:230-231), so the accepted points are
+// lm_descend's bit for bit; a descent costs (accepted steps + 1) passes instead of
+// (accepted steps + rejected rungs + 1): at most 4 instead of 10 on config-2 segments
+// (tests/test_lm_pass_structure.py). For latency-bound fits: warm-start chains
+// (_fit_sequential, fitters.py:370-393) and the last segments of a record pipeline.
+// Every lane of the wave must call this (wave-uniform loop; lanes without work pass
+// active = false through p's group state, see lm_ladder_kernel).
+template <int LPS, typename Ev>
+__device__ __forceinline__ double lm_descend_ladder(Ev&& ev, double (&p)[4], const LMConst& c, bool live = true) {
+  using Trial = typename std::decay_t<Ev>::Trial;
+  constexpr int NT = (int)(sizeof(Trial) / sizeof(double));
+  static_assert(sizeof(Trial) == NT * sizeof(double), "trial state: doubles only");
+  static_assert(LPS == 2 || LPS == 4 || LPS == 8 || LPS == 16, "LPS");
+  Eval e;
+  {
+    Trial t0;
+    ev.trial(p, t0);
+    ev.accept(p, t0, e);
+  }
+  const int lane = (int)__lane_id();
+  const int r = lane & (LPS - 1);
+  const int g0 = lane & ~(LPS - 1);
+  int it = 0, base = 0;
+  bool active = live && c.max_steps > 0 && c.n_lambda > 0;
+  while (__ballot(active) != 0) {
+    const int rung = base + r;
+    const bool work = active && rung < c.n_lambda;
+    double dp[4];
+    ev.solve(e, c.lambdas[work ? rung : 0], dp);
+    const bool step = work && !norm_below(sumsq4(dp[0], dp[1], dp[2], dp[3]), c.min_step_norm);
+    double pt[4] = {p[0] + dp[0], p[1] + dp[1], p[2] + dp[2], p[3] + dp[3]};
+    Trial tt;
+    bool improved = false;
+    if (step) improved = ev.trial(pt, tt) < e.ssq;
+    const uint64_t imp = __ballot(improved);
+    const uint64_t gm = (imp >> g0) & ((1ull << LPS) - 1);
+    const int src = gm ? g0 + __builtin_ctzll(gm) : lane;
+    if (__ballot(gm != 0 && active) != 0) {  // some group accepts: fetch the taken rung's state
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pt[i] = shfl_any(pt[i], src);
+      double* tv = reinterpret_cast<double*>(&tt);
+#pragma unroll
+      for (int i = 0; i < NT; ++i) tv[i] = shfl_any(tv[i], src);
+    }
+    if (active) {
+      if (gm) {
+        const double change2 = sumsq4(pt[0] - p[0], pt[1] - p[1], pt[2] - p[2], pt[3] - p[3]);
+        p[0] = pt[0];
+        p[1] = pt[1];
+        p[2] = pt[2];
+        p[3] = pt[3];
+        const double best_ssq = ev.ssq_of(tt);  // the taken trial's ssqf
+        ev.accept(p, tt, e);  // coeffs(ndata, data, parm) at the accepted point (fit.py:251)
+        ++it;
+        base = 0;
+        if (((e.ssq - best_ssq) < c.conv_improve && norm_below(change2, c.conv_param_change)) ||
+            it >= c.max_steps)
+          active = false;
+      } else {
+        base += LPS;
+        if (base >= c.n_lambda) active = false;  // no lambda improved: fit.py:246-247
+      }
+    }
+  }
+  return e.ssq;
 }
 
 // fit.py:260-320 (_find_best_initial_guess). jtab: n_grid rows of J_1..J_ndata(mtry)
@@ -763,6 +844,10 @@ template <int FLAT = 1, typename Ev, typename QF>
 DFMI_HDI int fit_segment_t(Ev&& ev, QF&& Q, int ndata, const double* __restrict__ jtab, const LMConst& c,
                            double (&p)[4], double& ssq_out) {
   auto descend = [&](double (&pp)[4]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (FLAT == 2) return lm_descend_ladder<kLadderLanes>(ev, pp, c);
+    else
+#endif
     if constexpr (FLAT == 1) return lm_descend_flat(ev, pp, c);
     else return lm_descend(ev, pp, c);
   };
@@ -976,6 +1061,80 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
       if (len == 1) one(s0);  // chunk size 1 (the parallel default): straight-line code
     } else {
       for (int64_t t = 0; t < len; ++t) one(s0 + t);  // warm-start chain (sequential / n_cores)
+    }
+  }
+}
+
+// Latency-bound fits (few chains or few segments): kLadderLanes lanes per item, the
+// lambda ladder of every LM iteration tried in one pass (lm_descend_ladder). Items and
+// chunks as lm_chunks_kernel (np.array_split chunks of the record's segments
+// [first, first + nitems), warm start within a chunk, fitters.py:13-60); ROWS: QI as
+// demodulation rows (chunk size 1; dc copied into out[4] as lm_chunks_kernel does).
+// Lane 0 of each group writes the results. A wave holds 64 / kLadderLanes items.
+template <int NDMAX, bool CHAIN, bool ROWS>
+__global__ __launch_bounds__(64) void lm_ladder_kernel(
+    const double* __restrict__ qi, int64_t qi_ld, int ndata, int64_t nrec, int64_t nbuf, int64_t first,
+    int64_t nitems, int64_t nchunk, const double* __restrict__ guess, int64_t g_rec, int64_t g_comp,
+    GuessInline ginl, int use_inline, const double* __restrict__ jtab, LMConst c, double* __restrict__ out,
+    int64_t out_ld, int32_t* __restrict__ status) {
+  static_assert(!(ROWS && CHAIN), "row layout: chunk size 1 only");
+  constexpr int LPS = kLadderLanes;
+  constexpr bool kQReg = NDMAX > 0 && nd_exact(NDMAX);
+  const int64_t id = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPS;
+  if (id >= nrec * nchunk) return;  // whole groups leave together
+  const bool lead = (threadIdx.x & (LPS - 1)) == 0;
+  const int64_t r = id / nchunk;
+  const int64_t k = id - r * nchunk;
+  const int64_t qn = nitems / nchunk, rm = nitems % nchunk;
+  const int64_t start = k * qn + (k < rm ? k : rm);
+  const int64_t len = qn + (k < rm ? 1 : 0);
+  const int64_t s0 = r * nbuf + first + start;
+  double p[4] = {0.0, 0.0, 0.0, 0.0};
+  if (use_inline) {
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) {
+      if (r == rr) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) p[i] = ginl.v[rr][i];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) p[i] = guess[r * g_rec + i * g_comp];
+  }
+  auto fit = [&](const auto& qm, int64_t sidx) {
+    double ssq;
+    int st;
+    if constexpr (kQReg) {
+      QRegs<nd_cap(NDMAX)> qr;
+      qr.load(qm);
+      st = fit_segment_q2<NDMAX, QRegs<nd_cap(NDMAX)>, std::decay_t<decltype(qm)>, 2>(qr, qm, ndata, jtab, c, p, ssq);
+    } else {
+      st = fit_segment_q2<NDMAX, std::decay_t<decltype(qm)>, std::decay_t<decltype(qm)>, 2>(qm, qm, ndata, jtab, c, p,
+                                                                                          ssq);
+    }
+    if (lead) {
+      out[0 * out_ld + sidx] = p[0];
+      out[1 * out_ld + sidx] = p[1];
+      out[2 * out_ld + sidx] = p[2];
+      out[3 * out_ld + sidx] = p[3];
+      out[5 * out_ld + sidx] = ssq;
+      status[sidx] = st;
+    }
+  };
+  if constexpr (ROWS) {
+    if (len != 1) return;
+    const QRow<1> q{qi + s0 * qi_ld};
+    fit(q, s0);
+    if (lead) {
+      out[4 * out_ld + s0] = q.at(dfmi_row_dc(ndata));
+      if (k == 0)  // segments before `first` (the seed buffer) are fitted elsewhere: carry their dc
+        for (int64_t t = r * nbuf; t < r * nbuf + first; ++t) out[4 * out_ld + t] = qi[t * qi_ld + dfmi_row_dc(ndata)];
+    }
+  } else {
+    for (int64_t t = 0; t < len; ++t) {  // warm-start chain (sequential / n_cores); len 1: chunk size 1
+      const QGlobal q{qi + s0 + t, qi_ld, ndata};
+      fit(q, s0 + t);
     }
   }
 }

@@ -264,6 +264,13 @@ int dfmi_set_tuning(const char* key, int64_t value);
 /* Current value of a tuning key (see dfmi_set_tuning). */
 int dfmi_get_tuning(const char* key, int64_t* value);
 
+/* Measurement hook: with enable != 0, dfmi_nls_record records timing events on its
+ * stream around the fused seed + demodulation launch and the LM launch of the record
+ * pipeline (current device). dfmi_step_timing_read waits for them and returns the
+ * summed kernel-span times (ms) of the steps recorded since the last read. */
+int dfmi_step_timing(int32_t enable);
+int dfmi_step_timing_read(double* demod_ms, double* lm_ms, int64_t* nsteps);
+
 /* Frees every scratch workspace of the current device after waiting for it to drain
  * (workspaces are kept per caller stream, at most 4 streams, least recently used freed
  * first). */

@@ -74,6 +74,65 @@ def test_record_on_non_current_device():
     np.testing.assert_array_equal(other.cpu().numpy(), ref.cpu().numpy())
 
 
+@pytest.fixture
+def restore_ladder():
+    from deepfmkit_amd import _lib
+    lib = _lib.load()
+    yield lib
+    _lib.check(lib.dfmi_set_tuning(b"lm_ladder", 32), "dfmi_set_tuning")
+
+
+@pytest.mark.parametrize("nd", [10, 7, 30])
+def test_lm_ladder_bit_identical(restore_ladder, nd):
+    """The parallel lambda ladder (lm.h lm_descend_ladder: 8 lanes per segment, every
+    rung of an LM iteration tried in one pass, the first improving one taken) accepts
+    exactly the points of the one-lane descent: same bits for the warm-start chains of
+    _fit_sequential and of n_cores chunks, for a small chunk-size-1 record (row layout),
+    and for dfmi_lm's per-segment guesses — incl. noise-only buffers that take the m-grid
+    retry (status 1/2), the register path (ndata 10 exact, 7 masked) and the general
+    path (ndata 30)."""
+    import torch
+    from deepfmkit_amd import _lib
+    from deepfmkit_amd import fit as F
+    from deepfmkit_amd.fitters import nls_records
+    lib = restore_ladder
+    nbuf, R, nrec = 301, 4000, 3
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5 + nd)
+    t = torch.arange(R, dtype=torch.float64, device="cuda") / 200000.0
+    recs = []
+    for r in range(nrec):
+        clean = 1.0 + torch.cos(0.3 * r + (6.0 + r) * torch.cos(2 * np.pi * 1000.0 * t))
+        noise = torch.randn(nbuf * R, dtype=torch.float64, device="cuda", generator=g)
+        sig = clean.repeat(nbuf) + 0.01 * noise
+        sig[7 * R: 9 * R] = 0.8 * noise[7 * R: 9 * R]  # two noise-only buffers: status 1/2 + m-grid retry
+        recs.append(sig)
+    x = torch.stack(recs).contiguous()
+    st = torch.cuda.current_stream().cuda_stream
+    res = {}
+    for ladder in (32, 0):
+        _lib.check(lib.dfmi_set_tuning(b"lm_ladder", ladder), "dfmi_set_tuning")
+        out = []
+        for kw in (dict(parallel=False), dict(parallel=True, n_cores=4), dict(parallel=True)):
+            cols, ok = nls_records(x, 200000.0, 1000.0, R, nbuf, nd, **kw)
+            out += [cols.cpu().numpy(), ok.cpu().numpy()]
+        qi = torch.empty((2 * nd, nbuf), dtype=torch.float64, device="cuda")
+        dc = torch.empty(nbuf, dtype=torch.float64, device="cuda")
+        _lib.check(lib.dfmi_demod(x.data_ptr(), nbuf, R, R, nd, 2 * np.pi * 1000.0 / 200000.0, 0, qi.data_ptr(),
+                                  dc.data_ptr(), _lib.DFMI_MEM_DEVICE, st), "dfmi_demod")
+        gd = torch.tensor(np.tile([1.0, 6.0, 0.0, 0.0], (nbuf, 1)), dtype=torch.float64, device="cuda")
+        p = torch.empty((4, nbuf), dtype=torch.float64, device="cuda")
+        ssq = torch.empty(nbuf, dtype=torch.float64, device="cuda")
+        stt = torch.empty(nbuf, dtype=torch.int32, device="cuda")
+        _lib.check(lib.dfmi_lm(qi.data_ptr(), nbuf, nd, gd.data_ptr(), 1, nbuf, F.lm_config(), p.data_ptr(),
+                               ssq.data_ptr(), stt.data_ptr(), _lib.DFMI_MEM_DEVICE, st), "dfmi_lm")
+        out += [a.cpu().numpy() for a in (p, ssq, stt)]
+        res[ladder] = out
+    assert (res[0][1] != 0).any() and (res[0][-1] != 0).any()  # the retry path ran
+    for i, (a, b) in enumerate(zip(res[32], res[0])):
+        np.testing.assert_array_equal(a, b, err_msg=f"output {i}")
+
+
 def test_init_m_with_parallel_is_accepted():
     """Deliberate divergence: the reference raises TypeError for init_m
     together with parallel=True (fitters.py:366 forwards **kwargs still holding init_m

@@ -187,6 +187,50 @@ def _ekf_long_record(dfm, O, lib, kname):
         np.testing.assert_array_equal(many[k], got)
 
 
+@pytest.mark.parametrize("row", [1, 0])
+def test_ekf_config5_full_length_matches_c_oracle(row):
+    """Config 5 at the length BASELINE names (notebooks/2.0 defaults):
+    a 2 s = 400,000-sample snr-mode record (m=6, 40 dB) through dfmi_ekf_fit (EKFFitter.fit,
+    fitters.py:214-320, pre-reductions on the device) with both EKF kernels, against the
+    oracle's scalar C restatement of the loop (oracle/csrc/ekf_scalar.c, pinned to the
+    numpy oracle by tests/test_oracle_c.py) on every one of the 100 snapshots."""
+    import ctypes
+    import os
+    import deepfmkit_amd as dfm
+    from deepfmkit_amd import _lib
+    lib = _lib.load()
+    so = os.path.join(os.path.dirname(os.path.dirname(__file__)), "oracle", "libekf_scalar.so")
+    if not os.path.exists(so):
+        pytest.skip("oracle/libekf_scalar.so not built (make -C oracle)")
+    laser, ifo = dfm.LaserConfig(), dfm.InterferometerConfig()
+    dfm.set_laser_df_for_effect(laser, ifo, 6.0)
+    dff = dfm.DeepFitFramework()
+    dff.load_sim(dfm.DFMIObject("c5", laser, ifo, f_samp=200000.0))
+    dff.simulate("c5", n_seconds=2.0, mode="snr", snr_db=40.0, trial_num=7)
+    raw = dff.raws["c5"]
+    x = np.ascontiguousarray(raw.samples(), dtype=np.float64)
+    assert x.size == 400_000
+    cl = ctypes.CDLL(so)
+    P = ctypes.c_void_p
+    cl.ekf_scalar.argtypes = [P, ctypes.c_int64, P, P, P, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                              ctypes.c_int64, ctypes.c_int64, P]
+    x0 = np.array([1.6, 6.0, 0.0, 0.0, np.mean(x)])
+    p0, qd = np.ones(5), np.array([1e-8, 1e-8, 1e-6, 1e-6, 1e-8])
+    ref = np.zeros((100, 5))
+    cl.ekf_scalar(x.ctypes.data, x.size, x0.ctypes.data, p0.ctypes.data, qd.ctypes.data, float(np.var(x)),
+                  2 * np.pi * 1000.0, 200000.0, 4000, 100, ref.ctypes.data)
+    _lib.check(lib.dfmi_set_tuning(b"ekf_row", row), "tune")
+    try:
+        got = dfm.fitters.ekf_records([raw], 20)[0]
+        assert lib.dfmi_last_demod_kernel().decode() == ("ekf_row_kernel" if row else "ekf_kernel")
+    finally:
+        _lib.check(lib.dfmi_set_tuning(b"ekf_row", 1), "tune")
+    assert got.shape == (100, 5)
+    err = np.abs(got - ref)
+    assert err.max() <= 1e-12, (err.max(), np.unravel_index(err.argmax(), err.shape))
+    assert abs(got[-1, 1] - 6.0) < 1e-2  # the filter tracks m
+
+
 @pytest.mark.parametrize("n", [1, 7, 8, 127, 129, 4000, 8191, 8192, 8193, 30001, 400000])
 def test_record_moments_bit_exact(n):
     """dfmi_record_moments == np.mean / np.var bit for bit (numpy's pairwise tree, its

@@ -8,7 +8,7 @@
 //   asd_noise_arrays (reference physics.py:532-613, white sources: amplitude, df;
 //     seed 1 + trial_num * 4, sources drawn in the reference's order);
 //   _run_simulation_physics (physics.py:615-722): g = waveform(omega_mod t + psi) / max|g|
-//     (cos, or the second-harmonic distortion waveform of waveforms.py:4-23),
+//     (cos, or a waveform of waveforms.py: synth_g),
 //     phi_mod = (2 pi / fs) * cumsum((df + n_df) * g), the exact-delay np.interp at
 //     t - (tau_m + tau_dl) and t - tau_r, phase, (amp + n_amp) * (1 + vis cos(phase)).
 // Every function rounds operation by operation (no FMA contraction, whatever the
@@ -28,6 +28,7 @@
 #endif
 
 #include "../../include/dfmi.h"
+#include "dfmi_math.h"
 
 namespace dfmi {
 
@@ -162,15 +163,42 @@ DFMI_SY_HD double interp_grid(double x, const Arr& f, int64_t n, double f_samp) 
 // np.max's step (NaN propagates)
 DFMI_SY_HD double synth_gmax_step(double m, double g) { return (g > m || g != g || m != m) ? (m != m ? m : g) : m; }
 
-// g_t of sample k (before the max-normalisation)
-// (waveform_func(phase_axis, **waveform_kwargs), phase_axis = omega_mod t + psi:
-// the default cos, or second_harmonic_distortion's cos(tp) + d_amp cos(2 tp + d_phase))
+// g_t of sample k (before the max-normalisation): waveform_func(phase_axis,
+// **waveform_kwargs), phase_axis = omega_mod t + psi (physics.py:661), for the default
+// cos and the waveforms of waveforms.py, in numpy's / scipy.signal's operation order:
+//  1 second_harmonic_distortion: cos(tp) + d_amp cos(2 tp + d_phase)
+//  2 triangle_wave = sawtooth(tp, width): tmod = np.mod(tp, 2 pi); tmod < w 2 pi ?
+//    tmod / (pi w) - 1 : (pi (w + 1) - tmod) / (pi (1 - w)); NaN for w outside [0, 1]
+//  3 square_wave = square(tp, duty): tmod < w 2 pi ? 1 : -1; NaN for w outside [0, 1]
+//  4 dfm_like_wave: y = cos(tp); y += a_n cos(n tp) per harmonic, in dict order
+//  5 dfm_wave: cos(phi + m cos(tp))
+// (2 and 3 use IEEE operations only: bit-exact with scipy; np.mod restated by dfmi_pymod.)
 DFMI_SY_HD double synth_g(const dfmi_synth_trial& p, int64_t k, double f_samp) {
 #pragma clang fp contract(off)
+  const double pi = 3.141592653589793;
   const double tp = p.omega_mod * ((double)k / f_samp) + p.psi;
-  const double g1 = cos(tp);
-  if (p.waveform == 1) return g1 + p.d_amp * cos(2.0 * tp + p.d_phase);
-  return g1;
+  switch (p.waveform) {
+    case 1:
+      return cos(tp) + p.d_amp * cos(2.0 * tp + p.d_phase);
+    case 2:
+    case 3: {
+      const double w = p.d_amp;
+      if (w > 1.0 || w < 0.0) return __builtin_nan("");
+      const double tmod = dfmi_pymod(tp, 2.0 * pi);
+      const bool first = tmod < w * 2.0 * pi;
+      if (p.waveform == 3) return first ? 1.0 : -1.0;
+      return first ? tmod / (pi * w) - 1.0 : (pi * (w + 1.0) - tmod) / (pi * (1.0 - w));
+    }
+    case 4: {
+      double y = cos(tp);
+      for (int i = 0; i < p.n_harm && i < 8; ++i) y += p.harm_amp[i] * cos(p.harm_n[i] * tp);
+      return y;
+    }
+    case 5:
+      return cos(p.d_phase + p.d_amp * cos(tp));
+    default:
+      return cos(tp);
+  }
 }
 
 // df_noisy * g_normalised of sample k: the cumsum's summand

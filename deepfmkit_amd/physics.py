@@ -210,28 +210,60 @@ def exact_model_signal(cfg, t, noise, is_dynamic):
 
 # --- asd-mode trials on the device (dfmi_synth_asd) ---------------------------
 
+SYNTH_MAX_HARM = 8  # dfm_like_wave harmonics dfmi_synth_asd evaluates
 SYNTH_TRIAL_DTYPE = np.dtype([("seed", "<u4"), ("dynamic", "<i4")] + [(k, "<f8") for k in (
     "omega_mod", "psi", "df", "cphi", "w_arm", "arml_mod_amp", "arml_mod_psi", "dl0", "c_light", "tau_m", "tau_r",
     "w0c", "amp", "vis", "s_amp", "s_df")] + [("waveform", "<i4"), ("waveform_pad", "<i4"), ("d_amp", "<f8"),
-                                                 ("d_phase", "<f8")])  # include/dfmi.h dfmi_synth_trial
+                                                 ("d_phase", "<f8"), ("n_harm", "<i4"), ("harm_pad", "<i4"),
+                                                 ("harm_n", "<f8", (SYNTH_MAX_HARM,)),
+                                                 ("harm_amp", "<f8", (SYNTH_MAX_HARM,))])  # dfmi_synth_trial
+
+
+def _real_scalar(v):
+    return isinstance(v, (int, float, np.integer, np.floating)) and not isinstance(v, bool)
 
 
 def _device_waveform(laser):
-    """(code, d_amp, d_phase) of a waveform dfmi_synth_asd evaluates, or None."""
-    from . import waveforms
+    """(code, d_amp, d_phase, harmonics) of a waveform dfmi_synth_asd evaluates
+    (include/dfmi.h dfmi_synth_trial.waveform), or None: the default cosine and the
+    waveforms of waveforms.py (reference waveforms.py:4-90) with scalar arguments."""
+    from . import waveforms as W
     kw = dict(laser.waveform_kwargs or {})
-    if laser.waveform_func is cosine_waveform and not kw:
-        return 0, 0.0, 0.0
-    if laser.waveform_func is waveforms.second_harmonic_distortion and set(kw) <= {"distortion_amp",
-                                                                                 "distortion_phase"}:
-        return 1, float(kw.get("distortion_amp", 0.0)), float(kw.get("distortion_phase", 0.0))
+    f = laser.waveform_func
+    if not all(_real_scalar(v) or (k == "harmonics" and (v is None or isinstance(v, dict))) for k, v in kw.items()):
+        return None
+    if f is cosine_waveform and not kw:
+        return 0, 0.0, 0.0, ()
+    if f is W.second_harmonic_distortion and set(kw) <= {"distortion_amp", "distortion_phase"}:
+        return 1, float(kw.get("distortion_amp", 0.0)), float(kw.get("distortion_phase", 0.0)), ()
+    if f is W.triangle_wave and set(kw) <= {"width"}:
+        return 2, float(kw.get("width", 0.5)), 0.0, ()
+    if f is W.square_wave and set(kw) <= {"duty"}:
+        return 3, float(kw.get("duty", 0.5)), 0.0, ()
+    if f is W.dfm_like_wave and set(kw) <= {"harmonics"}:
+        h = kw.get("harmonics")
+        h = {2: 0.1, 3: 0.05} if h is None else h  # waveforms.py:58-59
+        if len(h) > SYNTH_MAX_HARM or not all(_real_scalar(n) and _real_scalar(a) for n, a in h.items()):
+            return None
+        return 4, 0.0, 0.0, tuple((float(n), float(a)) for n, a in h.items())
+    if f is W.dfm_wave and set(kw) <= {"m", "phi"}:
+        return 5, float(kw.get("m", 1.0)), float(kw.get("phi", 0.0)), ()
     return None
 
 
+def _put_waveform(rec, wf):
+    rec["waveform"], rec["d_amp"], rec["d_phase"] = wf[0], wf[1], wf[2]
+    rec["n_harm"] = len(wf[3])
+    for i, (n, a) in enumerate(wf[3]):
+        rec["harm_n"][i] = n
+        rec["harm_amp"][i] = a
+
+
 def device_synth_supported(cfg) -> bool:
-    """dfmi_synth_asd covers the default cosine waveform and the second-harmonic
-    distortion waveform (waveforms.py) with white (or zero) amplitude / df noise and no
-    frequency / arm-length noise sources."""
+    """dfmi_synth_asd covers the default cosine waveform and the waveforms of
+    waveforms.py (second-harmonic distortion, triangle, square, dfm-like, dfm) with
+    scalar arguments, white (or zero) amplitude / df noise and no frequency /
+    arm-length noise sources."""
     laser, ifo = cfg.laser, cfg.ifo
     return _device_waveform(laser) is not None and laser.f_n == 0.0 and ifo.arml_mod_n == 0.0
 
@@ -269,7 +301,7 @@ def synth_trial_fields(cfg, trial_num, dynamic=True):
     wf = _device_waveform(laser)
     if wf is None:
         raise ValueError("dfmi_synth_asd does not evaluate this waveform")
-    rec["waveform"], rec["d_amp"], rec["d_phase"] = wf
+    _put_waveform(rec, wf)
     return rec
 
 
@@ -318,9 +350,8 @@ def synth_trial_table(cfgs, trial_nums, dynamic=True):
     tab["vis"] = vis
     tab["s_amp"] = np.where(amp_n != 0.0, amp_n * np.sqrt(f_samp / 2.0), 0.0)
     tab["s_df"] = np.where(df_n != 0.0, df_n * np.sqrt(f_samp / 2.0), 0.0)
-    tab["waveform"] = [w[0] for w in wf]
-    tab["d_amp"] = [w[1] for w in wf]
-    tab["d_phase"] = [w[2] for w in wf]
+    for i, w in enumerate(wf):
+        _put_waveform(tab[i], w)
     return tab
 
 

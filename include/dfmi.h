@@ -147,7 +147,7 @@ int dfmi_record_moments(const double* x, int64_t nrec, int64_t rec_stride, int64
 /* ---- Trial synthesis (input side of the batched efficiency trials) ----
  * One asd-mode channel per trial, as SignalGenerator.generate(mode='asd') makes it
  * (reference physics.py:423-473, white noise sources 532-613, exact-delay model
- * 615-722) for the default cosine waveform or the second-harmonic distortion waveform:
+ * 615-722) for the default cosine waveform or one of the waveforms of waveforms.py:
  * numpy's legacy RandomState(seed) stream
  * (MT19937 + polar gauss) restated on the device. Every field is the reference's
  * scalar expression, evaluated by the caller with Python/numpy floats. */
@@ -170,11 +170,21 @@ typedef struct dfmi_synth_trial {
   double vis;           /* laser.visibility */
   double s_amp;         /* laser.amp_n * np.sqrt(f_samp / 2.0), 0: no draws */
   double s_df;          /* laser.df_n * np.sqrt(f_samp / 2.0), 0: no draws */
-  int32_t waveform;     /* 0: cos(tp) (the default waveform); 1: second_harmonic_distortion
-                           (waveforms.py:4-23): cos(tp) + d_amp * cos(2 * tp + d_phase) */
+  int32_t waveform;     /* g(tp), tp = omega_mod * t + psi (laser.waveform_func, waveforms.py):
+                           0: cos(tp) (the default waveform);
+                           1: second_harmonic_distortion (waveforms.py:4-23):
+                              cos(tp) + d_amp * cos(2 * tp + d_phase);
+                           2: triangle_wave = scipy.signal.sawtooth(tp, width = d_amp) (:25-31);
+                           3: square_wave = scipy.signal.square(tp, duty = d_amp) (:33-43);
+                           4: dfm_like_wave (:45-64): cos(tp) + sum_i harm_amp[i] * cos(harm_n[i] * tp);
+                           5: dfm_wave (:66-90): cos(d_phase + d_amp * cos(tp)) */
   int32_t waveform_pad;
-  double d_amp;         /* waveform 1: distortion_amp */
-  double d_phase;       /* waveform 1: distortion_phase */
+  double d_amp;         /* 1: distortion_amp; 2: width; 3: duty; 5: m */
+  double d_phase;       /* 1: distortion_phase; 5: phi */
+  int32_t n_harm;       /* 4: number of harmonics (<= 8), the harmonics dict in insertion order */
+  int32_t harm_pad;
+  double harm_n[8];     /* 4: harmonic numbers (the dict keys) */
+  double harm_amp[8];   /* 4: their fractional amplitudes */
 } dfmi_synth_trial;
 
 /* out[r*n_samp + k] = trial r's signal sample k (t_k = k / f_samp), one lane per

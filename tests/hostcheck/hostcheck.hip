@@ -44,6 +44,14 @@ void hc_synth_trial(const dfmi_synth_trial* p, int64_t n, double f_samp, double*
 
 void hc_bessel_table(double x, int N, double* out) { dfmi_bessel_table(x, N, out); }
 
+// layout check of the trial table (physics.SYNTH_TRIAL_DTYPE mirrors dfmi_synth_trial)
+int64_t hc_sizeof_synth_trial(void) { return (int64_t)sizeof(dfmi_synth_trial); }
+
+// synth.h's waveform g(tp) for sample k of a trial (before the max-normalisation)
+void hc_synth_g(const dfmi_synth_trial* p, int64_t n, double f_samp, double* out) {
+  for (int64_t k = 0; k < n; ++k) out[k] = dfmi::synth_g(*p, k, f_samp);
+}
+
 // dfmi_pymod (numpy / Python float modulo, the phi wrap of fit.py:357) elementwise
 void hc_pymod(const double* a, int64_t n, double b, double* out) {
   for (int64_t k = 0; k < n; ++k) out[k] = dfmi_pymod(a[k], b);

@@ -84,26 +84,72 @@ def test_experiment_witness_sweep_matches_reference(golden, engine):
     _check(_run(S.setup_witness, fac, engine), golden, "witness")
 
 
-def test_experiment_batched_equals_loop_with_host_inputs():
-    """With the host generator for every trial (a waveform the device generator does not
-    evaluate), the batched engine runs the same kernels per record as the per-trial
-    loop: identical grids, bit for bit."""
-    from deepfmkit_amd import factories, physics, waveforms
-    from deepfmkit_amd.experiments import Experiment
+def _user_wave(t_phase):
+    """A user waveform_func (physics.py:661): the device generator does not evaluate it."""
+    return np.cos(t_phase) + 0.03 * np.cos(3 * t_phase + 0.2)
 
-    class TriFactory(factories.ExperimentFactory):
+
+def _wave_factory(func, kwargs=None):
+    from deepfmkit_amd import factories, physics
+
+    class WaveFactory(factories.ExperimentFactory):
         def _get_expected_params_keys(self):
             return set(S.NOISY_KEYS)
 
         def __call__(self, params):
             cfg = S.noisy_config(physics, params)
-            cfg["laser_config"].waveform_func = waveforms.dfm_like_wave
+            cfg["laser_config"].waveform_func = func
+            cfg["laser_config"].waveform_kwargs = dict(kwargs or {})
             return cfg
+    return WaveFactory()
+
+
+@pytest.mark.parametrize("wave,kwargs", [("dfm_like_wave", None), ("triangle_wave", {"width": 0.5}),
+                                         ("dfm_wave", {"m": 1.5, "phi": 0.2})])
+def test_experiment_waveform_sweep_on_device(monkeypatch, wave, kwargs):
+    """Sweeps over the reference's other waveforms (waveforms.py:25-90) stay on the
+    device generator (dfmi_synth_asd; the host generator is never called) and agree
+    with the per-trial loop on host-generated records at the parity tolerances (the
+    records differ by device-cos ulps, <= 1e-9)."""
+    from deepfmkit_amd import experiments, waveforms
+    from deepfmkit_amd.experiments import Experiment
+    res = {}
+    for engine in ("loop", "gpu"):
+        if engine == "gpu":
+            class NoHost:
+                def generate(self, *a, **k):
+                    raise AssertionError("host generator called for a device-covered waveform")
+            monkeypatch.setattr(experiments, "SignalGenerator", NoHost)
+        exp = Experiment("wave")
+        S.setup_noisy(exp, _wave_factory(getattr(waveforms, wave), kwargs))
+        np.random.seed(S.SEED)
+        res[engine] = S.flatten(exp.run(engine=engine))
+    fitok = {k.rsplit("/", 1)[0]: v for k, v in res["loop"].items() if k.endswith("/fitok")}
+    for k, a in res["gpu"].items():
+        b = res["loop"][k]
+        ok = fitok.get(k.rsplit("/", 1)[0])
+        tol = np.where(ok != 0, 1e-7, 1e-9) if ok is not None else 1e-9
+        if k.endswith("/fitok"):
+            np.testing.assert_array_equal(a, b, err_msg=k)
+        elif k.endswith("/ssq"):
+            np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-300, err_msg=k)
+        elif k.endswith("/phi"):
+            d = np.abs((a - b + np.pi) % (2 * np.pi) - np.pi)
+            assert (d <= tol).all(), (k, d.max())
+        else:
+            assert (np.abs(a - b) <= tol).all(), (k, np.abs(a - b).max())
+
+
+def test_experiment_batched_equals_loop_with_host_inputs():
+    """With the host generator for every trial (a user waveform the device generator
+    does not evaluate), the batched engine runs the same kernels per record as the
+    per-trial loop: identical grids, bit for bit."""
+    from deepfmkit_amd.experiments import Experiment
 
     res = {}
     for engine in ("gpu", "loop"):
         exp = Experiment("tri")
-        S.setup_noisy(exp, TriFactory())
+        S.setup_noisy(exp, _wave_factory(_user_wave))
         np.random.seed(S.SEED)
         res[engine] = S.flatten(exp.run(engine=engine))
     for k in res["gpu"]:

@@ -126,3 +126,36 @@ def test_device_synthesized_trials_match_reference():
     tol = np.array([m_tol(t) for t in G["trials"]])
     assert np.all(np.abs(dev - ref) <= tol), (np.abs(dev - ref), tol)
     assert np.all(np.abs(dev - host) <= tol), (np.abs(dev - host), tol)
+
+
+@pytest.mark.parametrize("wave,kwargs", [("triangle_wave", {}), ("square_wave", {"duty": 0.4}),
+                                         ("dfm_like_wave", {}), ("dfm_wave", {"m": 1.2, "phi": 0.3})])
+def test_device_synthesis_other_waveforms(wave, kwargs):
+    """dfmi_synth_asd for the reference's other waveforms (waveforms.py:25-90): records
+    within 1e-9 of the package's numpy generator (bit-exact with the reference's), main
+    and witness channels, with amplitude and df noise."""
+    import deepfmkit_amd as dfm
+    from deepfmkit_amd import physics as P
+    from deepfmkit_amd import waveforms as W
+    cfgs, wits, tns, hosts = [], [], [], []
+    for (m, an, dn, tn) in [(6.0, 1e-4, 0.0, 0), (8.0, 3e-4, 2e3, 3), (11.0, 0.0, 0.0, 5)]:
+        laser = dfm.LaserConfig()
+        laser.amp_n, laser.df_n = an, dn
+        laser.waveform_func, laser.waveform_kwargs = getattr(W, wave), dict(kwargs)
+        ifo = dfm.InterferometerConfig()
+        dfm.set_laser_df_for_effect(laser, ifo, m)
+        cfg = dfm.DFMIObject("main_trial", laser, ifo)
+        wifo = dfm.InterferometerConfig()
+        wifo.meas_arml = 0.15
+        wit = dfm.DFMIObject("witness_trial", laser, wifo)
+        assert P.device_synth_supported(cfg) and P.device_synth_supported(wit)
+        ch = P.SignalGenerator().generate(cfg, 0.02, mode="asd", trial_num=tn, witness_config=wit)
+        cfgs.append(cfg)
+        wits.append(wit)
+        tns.append(tn)
+        hosts.append((np.asarray(ch["main"].samples()), np.asarray(ch["witness"].samples())))
+    dm = P.synthesize_asd_trials(cfgs, tns, 0.02, dynamic=True).cpu().numpy()
+    dw = P.synthesize_asd_trials(wits, tns, 0.02, dynamic=False).cpu().numpy()
+    for k, (hm, hw) in enumerate(hosts):
+        assert np.max(np.abs(dm[k] - hm)) <= 1e-9, (k, np.max(np.abs(dm[k] - hm)))
+        assert np.max(np.abs(dw[k] - hw)) <= 1e-9, (k, np.max(np.abs(dw[k] - hw)))

@@ -191,8 +191,72 @@ def test_trial_synthesis_second_harmonic_waveform_bit_exact(hc):
             hc.hc_synth_trial(rec.ctypes.data, x.size, c.f_samp, out.ctypes.data)
             np.testing.assert_array_equal(out, x)
     laser = dfm.LaserConfig()
-    laser.waveform_func = W.triangle_wave
+    laser.waveform_func = lambda tp: np.cos(tp) ** 3  # a user waveform: host generator only
     assert not P.device_synth_supported(dfm.DFMIObject("x", laser, dfm.InterferometerConfig()))
+
+
+WAVEFORM_CASES = [  # (waveform_func name, kwargs, expected code): reference waveforms.py:4-90
+    ("triangle_wave", {}, 2), ("triangle_wave", {"width": 0.3}, 2), ("triangle_wave", {"width": 1.0}, 2),
+    ("triangle_wave", {"width": 0}, 2), ("square_wave", {}, 3), ("square_wave", {"duty": 0.25}, 3),
+    ("dfm_like_wave", {}, 4), ("dfm_like_wave", {"harmonics": {3: 0.2, 2: -0.05, 5: 0.01}}, 4),
+    ("dfm_like_wave", {"harmonics": {}}, 4), ("dfm_wave", {}, 5), ("dfm_wave", {"m": 2.5, "phi": 0.4}, 5),
+    ("second_harmonic_distortion", {"distortion_amp": 0.1}, 1),
+]
+
+
+def test_synth_trial_layout(hc):
+    from deepfmkit_amd import physics as P
+    hc.hc_sizeof_synth_trial.restype = ctypes.c_int64
+    assert hc.hc_sizeof_synth_trial() == P.SYNTH_TRIAL_DTYPE.itemsize
+
+
+@pytest.mark.parametrize("name,kw,code", WAVEFORM_CASES)
+def test_synth_waveforms_match_numpy(hc, name, kw, code):
+    """synth.h's waveforms (dfmi_synth_asd) built for the host against the package's
+    waveforms (the reference's numpy / scipy.signal expressions) on the phase axis of
+    a 20 ms record: triangle / square bit for bit (IEEE operations and np.mod only),
+    the cosine-based ones to the host libm (bit for bit here as well), and whole asd
+    trials through the numpy generator bit for bit."""
+    import deepfmkit_amd as dfm
+    from deepfmkit_amd import physics as P
+    from deepfmkit_amd import waveforms as W
+    laser = dfm.LaserConfig()
+    laser.psi = 0.37
+    laser.amp_n = 1e-4
+    laser.waveform_func = getattr(W, name)
+    laser.waveform_kwargs = dict(kw)
+    ifo = dfm.InterferometerConfig()
+    dfm.set_laser_df_for_effect(laser, ifo, 6.0)
+    cfg = dfm.DFMIObject("main_trial", laser, ifo)
+    assert P.device_synth_supported(cfg)
+    rec = P.synth_trial_fields(cfg, 3)
+    assert int(rec["waveform"]) == code
+    n = int(0.02 * cfg.f_samp)
+    t = np.arange(n) / cfg.f_samp
+    want = laser.waveform_func(2 * np.pi * laser.f_mod * t + laser.psi, **laser.waveform_kwargs)
+    got = np.zeros(n)
+    hc.hc_synth_g.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p]
+    hc.hc_synth_g(rec.ctypes.data, n, cfg.f_samp, got.ctypes.data)
+    np.testing.assert_array_equal(got, want)
+    x = np.asarray(P.SignalGenerator().generate(cfg, 0.02, mode="asd", trial_num=3)["main"].samples())
+    hc.hc_synth_trial.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p]
+    out = np.zeros(x.size)
+    hc.hc_synth_trial(rec.ctypes.data, x.size, cfg.f_samp, out.ctypes.data)
+    np.testing.assert_array_equal(out, x)
+
+
+def test_synth_waveform_limits():
+    """Waveform arguments the device table cannot hold fall back to the host generator:
+    array-valued kwargs, more than 8 dfm_like_wave harmonics, unknown kwargs."""
+    import deepfmkit_amd as dfm
+    from deepfmkit_amd import physics as P
+    from deepfmkit_amd import waveforms as W
+    for f, kw in ((W.triangle_wave, {"width": np.full(4, 0.5)}), (W.dfm_like_wave, {"harmonics": {k: 0.01 for k in
+                                                                                                 range(2, 12)}}),
+                  (W.dfm_wave, {"m": 1.0, "other": 2}), (W.square_wave, {"duty": True})):
+        laser = dfm.LaserConfig()
+        laser.waveform_func, laser.waveform_kwargs = f, kw
+        assert not P.device_synth_supported(dfm.DFMIObject("x", laser, dfm.InterferometerConfig()))
 
 
 def test_synth_trial_table_equals_per_trial_fields():
@@ -212,6 +276,12 @@ def test_synth_trial_table_equals_per_trial_fields():
         if i % 3 == 0:
             laser.waveform_func = W.second_harmonic_distortion
             laser.waveform_kwargs = {"distortion_amp": rng.uniform(0, 0.1), "distortion_phase": rng.uniform(-1, 1)}
+        elif i % 5 == 1:
+            laser.waveform_func = W.dfm_like_wave
+            laser.waveform_kwargs = {"harmonics": {2: rng.uniform(0, 0.1), 4: rng.uniform(0, 0.1)}}
+        elif i % 7 == 2:
+            laser.waveform_func = W.triangle_wave
+            laser.waveform_kwargs = {"width": rng.uniform(0, 1)}
         ifo = dfm.InterferometerConfig()
         ifo.phi = rng.uniform(0, 6)
         ifo.arml_mod_amp = [0.0, 1e-7][i % 2]

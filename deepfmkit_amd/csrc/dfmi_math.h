@@ -271,6 +271,16 @@ DFMI_HD void dfmi_sincos(double x, double* sn, double* cs) {
   }
 }
 
+// dfmi_sincos_k for |r| < pi/4 (no reduction, no quadrant: q = rint(r 2/pi) = 0), same
+// bits: the kernel polynomials alone.
+DFMI_HD void dfmi_sincos_small(double r, const DfmiTrigK& k, double* sn, double* cs) {
+  const double z = r * r;
+  const double ps = fma(z, fma(z, fma(z, fma(z, fma(z, k.c[4], k.c[5]), k.c[6]), k.c[7]), k.c[8]), k.c[9]);
+  *sn = fma(r * z, ps, r);
+  const double pc = fma(z, fma(z, fma(z, fma(z, fma(z, k.c[10], k.c[11]), k.c[12]), k.c[13]), k.c[14]), k.c[15]);
+  *cs = fma(z * z, pc, fma(-0.5, z, 1.0));
+}
+
 // dfmi_sincos with the constants from k and fewer instructions, same bits: the same
 // reduction and Horner polynomials, the quadrant applied as a swap select plus a sign
 // flip (no branch, 2 select levels instead of 3), and the library path (|x| >= 2^19, NaN)

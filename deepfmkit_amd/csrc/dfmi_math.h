@@ -281,6 +281,11 @@ DFMI_HD void dfmi_sincos_small(double r, const DfmiTrigK& k, double* sn, double*
   *cs = fma(z * z, pc, fma(-0.5, z, 1.0));
 }
 
+// dfmi_sincos_k(x) with the reduction skipped where it is the identity (|x| < 0.78:
+// q = rint(x 2/pi) = 0, r = x), same bits; a wave whose lanes all hold such arguments
+// runs the polynomials alone.
+DFMI_HD void dfmi_sincos_auto(double x, const DfmiTrigK& k, double* sn, double* cs);
+
 // dfmi_sincos with the constants from k and fewer instructions, same bits: the same
 // reduction and Horner polynomials, the quadrant applied as a swap select plus a sign
 // flip (no branch, 2 select levels instead of 3), and the library path (|x| >= 2^19, NaN)
@@ -312,4 +317,9 @@ DFMI_HD void dfmi_sincos_k(double x, const DfmiTrigK& k, double* sn, double* cs)
     sincos(x, sn, cs);
 #endif
   }
+}
+
+DFMI_HD void dfmi_sincos_auto(double x, const DfmiTrigK& k, double* sn, double* cs) {
+  if (fabs(x) < 0.78) dfmi_sincos_small(x, k, sn, cs);
+  else dfmi_sincos_k(x, k, sn, cs);
 }

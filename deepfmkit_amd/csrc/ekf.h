@@ -236,8 +236,7 @@ __device__ __forceinline__ void ekf_row_step2(double (&st)[5], double (&Pc)[5], 
   for (int i = 0; i < 5; ++i) Pc[i] = Pc[i] + qv[i];
   const double a = st[0], m = st[1], phi = st[2], psi = st[3], dc = st[4];
   double sps, cps;
-  if (fabs(psi) < 0.78) dfmi_sincos_small(psi, tk, &sps, &cps);
-  else dfmi_sincos_k(psi, tk, &sps, &cps);
+  dfmi_sincos_auto(psi, tk, &sps, &cps);
   const double cth = fma(cw, cps, -(sw * sps));
   const double sth = fma(sw, cps, cw * sps);
   const double arg = fma(m, cth, phi);

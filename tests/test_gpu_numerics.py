@@ -128,7 +128,7 @@ def test_lm_ladder_bit_identical(restore_ladder, nd):
                                ssq.data_ptr(), stt.data_ptr(), _lib.DFMI_MEM_DEVICE, st), "dfmi_lm")
         out += [a.cpu().numpy() for a in (p, ssq, stt)]
         res[ladder] = out
-    assert (res[0][1] != 0).any() and (res[0][-1] != 0).any()  # the retry path ran
+    assert any((res[0][i] != 0).any() for i in (1, 3, 5, 8))  # the m-grid retry path ran (status 1/2)
     for i, (a, b) in enumerate(zip(res[32], res[0])):
         np.testing.assert_array_equal(a, b, err_msg=f"output {i}")
 

@@ -116,6 +116,19 @@ DFMI_HDI void eval_zero(Eval& e) { e = Eval{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 
 // Register path
 // ---------------------------------------------------------------------------
 
+// 1/d to within an ulp or two: v_rcp_f64 + two Newton steps on the device (the
+// IEEE division sequence costs ~3x the instructions); exact division on the host.
+DFMI_HDI double rcp_nr(double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(r, fma(-d, r, 1.0), r);
+  r = fma(r, fma(-d, r, 1.0), r);
+  return r;
+#else
+  return 1.0 / d;
+#endif
+}
+
 // J_0..J_{NB-1}(x) into registers with one backward Miller pass.
 // |x| < 1e-3 takes the power series (4 terms, relative error < 1e-20); above
 // that the unrolled low-order part of the pass (orders < NB <= 18) grows by at
@@ -145,7 +158,7 @@ DFMI_HDI void bessel_regs(double x, int N, double (&J)[NB]) {
   static_assert((NB & 1) == 0, "the pair loop below needs an even NB");
   int M = dfmi_bessel_start(N, ax);
   if (M < NB) M = (NB + 1) & ~1;
-  const double tox = 2.0 / ax;
+  const double tox = 2.0 * rcp_nr(ax);
   // Runtime part of the pass without the per-order overflow test: power-of-two
   // rescaling is exact, so a pass that never leaves the finite range gives the same
   // bits as the rescaled one; only if it overflowed does the checked pass run.
@@ -195,7 +208,7 @@ DFMI_HDI void bessel_regs(double x, int N, double (&J)[NB]) {
     fp1 = f;
     f = fm1;
   }
-  const double invS = 1.0 / S;
+  const double invS = rcp_nr(S);
   const double invS_odd = x < 0.0 ? -invS : invS;  // J_k(-x) = (-1)^k J_k(x): same bits as negating J_k invS
 #pragma unroll
   for (int k = 0; k < NB; ++k) J[k] *= (k & 1) ? invS_odd : invS;
@@ -348,19 +361,6 @@ DFMI_HDI void eval_reg_accept(const QF& q, int nd, const double (&p)[4], const T
     DFMI_HARMONIC_FENCE();
   }
   e = Eval{t.ssq, a00, a01, a02, 0.0, a11, a12, 0.0, a22, 0.0, a33, g0, g1, g2, g3};
-}
-
-// 1/d to within an ulp or two: v_rcp_f64 + two Newton steps on the device (the
-// IEEE division sequence costs ~3x the instructions); exact division on the host.
-DFMI_HDI double rcp_nr(double d) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  double r = __builtin_amdgcn_rcp(d);
-  r = fma(r, fma(-d, r, 1.0), r);
-  r = fma(r, fma(-d, r, 1.0), r);
-  return r;
-#else
-  return 1.0 / d;
-#endif
 }
 
 // msolve (fit.py:169-206) for the register path's block-diagonal J^T J: the (a, m, phi)

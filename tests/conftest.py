@@ -109,8 +109,8 @@ def resolution_tol(nd, qi, p, floor=1e-9, k=10.0):
     ssq, jtj, _ = O.model_and_jacobian(nd, np.asarray(qi, dtype=np.float64), np.asarray(p, dtype=np.float64))
     try:
         cov = np.abs(np.diag(np.linalg.inv(jtj.reshape(4, 4))))
-    except np.linalg.LinAlgError:
-        return np.full(4, np.inf)
+    except np.linalg.LinAlgError as exc:  # no resolution bound exists: the comparison must not pass silently
+        raise AssertionError(f"singular J^T J at the reference solution {p}: no parity tolerance") from exc
     return np.maximum(floor, k * np.sqrt(np.finfo(float).eps * max(ssq, 1e-300) * cov))
 
 

@@ -6,10 +6,12 @@ record of one GPU call, each with its own seed): with the host generator it give
 the same bits; with the device generator (dfmi_synth_asd) the records agree with
 numpy's to ~1e-15 and the fits with the reference's within the tolerance.
 
-Tolerance: |m - m_ref| <= max(1e-9, the reference's own resolution of m) per trial
-(status-0 fits; conftest.resolution_tol at the oracle's fit of the
-trial's record: the 1e-9 floor for 4 of the 10 trials, 1.3e-9 .. 8.4e-9 for the
-others, whose amplitude noise leaves ssq at 6e-6 .. 2.5e-4)."""
+Tolerance: the flat BASELINE.md gate, |m - m_ref| <= 1e-9 per trial (status-0 fits,
+SURVEY.md §8d), for the host-generated and the device-generated records. (The
+reference's own resolution of m at these trials, conftest.resolution_tol, is 1e-9 ..
+8.4e-9: the flat gate is the stricter one. The host build of the LM, both the
+register path and the literal general path, lands within 8.1e-10 of the reference on
+every trial, tests/test_host_numerics.py::test_worker_trials_within_flat_gate.)"""
 import json
 import os
 
@@ -33,6 +35,11 @@ _TOL = {}
 
 
 def m_tol(t):
+    """The flat parity gate of BASELINE.md (1e-9, status-0 fits)."""
+    return 1e-9
+
+
+def m_resolution(t):
     """max(1e-9, resolution of m): the reference's acceptance test ssq_try < ssq0
     (fit.py:240) cannot resolve changes of m below sqrt(eps * ssq * cov_mm)."""
     key = json.dumps(t, sort_keys=True)

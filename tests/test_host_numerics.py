@@ -293,3 +293,35 @@ def test_synth_trial_table_equals_per_trial_fields():
         for c, t, row in zip(cfgs, nums, tab):
             one = P.synth_trial_fields(c, t, dyn)
             assert one.tobytes() == row.tobytes()
+
+
+def test_worker_trials_within_flat_gate(hc):
+    """The LM's algebraic shortcuts (block-diagonal J^T J with the psi cross terms taken
+    as the zeros they are, closed-form coeffs, LDL^T solve) against the literal general
+    path (per-residual Jacobian, pivoting dgesv-style solve) and the oracle (bit-exact
+    with the reference's fit.fit) on the QI of the reference's own efficiency trials
+    (tests/golden/workers.json): every fitted m within the flat 1e-9 gate of the
+    reference, on both paths (host build: exact division)."""
+    import json
+    import deepfmkit_amd as dfm
+    from deepfmkit_amd import physics as P
+    from oracle import nls_oracle as O
+    G = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "workers.json")))
+    for t in G["trials"]:
+        laser = dfm.LaserConfig()
+        laser.f_mod = 1000.0
+        laser.amp_n = t["amp_n"]
+        ifo = dfm.InterferometerConfig()
+        dfm.set_laser_df_for_effect(laser, ifo, t["m_true"])
+        cfg = dfm.DFMIObject("main_trial", laser, ifo)
+        x = np.asarray(P.SignalGenerator().generate(cfg, t["n_seconds"], mode="asd",
+                                                    trial_num=t["trial_num"])["main"].samples())
+        R = int(cfg.f_samp / laser.f_mod * int(laser.f_mod * t["n_seconds"]))
+        nd = t["ndata"]
+        qi = O.demod_buffer(x[:R], nd, 2 * np.pi * laser.f_mod / cfg.f_samp)[:2 * nd]
+        g = np.array([1.6, t["m_true"], 0.0, 0.0])
+        _, po, _ = O.fit_segment(nd, qi, g)
+        assert po[1] == t["m_fit"]  # the oracle is the reference here
+        for general in (0, 1):
+            _, p, _ = _fit(hc, qi[None, :], g[None, :], general)
+            assert abs(p[0, 1] - po[1]) <= 1e-9, (t, general, abs(p[0, 1] - po[1]))

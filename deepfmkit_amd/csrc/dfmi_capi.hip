@@ -351,6 +351,17 @@ int to_lmconst(const dfmi_lm_config* cfg, dfmi::LMConst* c) {
 
 constexpr int kMaxSlotCap = 8;
 
+// A/B build switches of the bin kernel (defaults = the shipped configuration)
+#ifndef DFMI_BINS_LOADS
+#define DFMI_BINS_LOADS 8     // 1-KB chunk loads in flight per wave
+#endif
+#ifndef DFMI_BINS_PFN
+#define DFMI_BINS_PFN 4       // next segment's chunks prefetched during the contraction (L <= 256)
+#endif
+#ifndef DFMI_BINS_LDS_PAD
+#define DFMI_BINS_LDS_PAD 0   // extra dynamic LDS bytes per workgroup (occupancy experiments)
+#endif
+
 thread_local std::string g_last_demod;  // kernel variant of the last demodulation launch (dfmi_last_demod_kernel)
 
 // hipOccupancyMaxActiveBlocksPerMultiprocessor, cached per (kernel, LDS bytes): the
@@ -446,8 +457,9 @@ int launch_fold_ms(int ms, const double* x, int64_t nseg, int64_t stride, int R,
 template <int MS, bool ROWS>
 int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tab,
                   double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu, size_t lds) {
-  constexpr int PFN = MS == 2 ? 4 : 0;
-  auto kern = dfmi::demod_bins_kernel<MS, 8, ROWS, PFN>;
+  constexpr int PFN = MS == 2 ? DFMI_BINS_PFN : 0;
+  auto kern = dfmi::demod_bins_kernel<MS, DFMI_BINS_LOADS, ROWS, PFN>;
+  lds += DFMI_BINS_LDS_PAD;
   int per_cu = 0;
   if (int orc = occupancy(kern, dfmi::kBlockThreads, lds, &per_cu)) return orc;
   if (per_cu < 1) per_cu = 1;
@@ -637,9 +649,11 @@ int fused_seed_demod(int dev, const double* x, int64_t nrec, int64_t nbuf, int R
                      int32_t*, uint64_t*);
   const bool pf = nslot <= 2 && ndata <= 12;  // bins_segment's prefetch (bulk path, MS 2)
   K kern;
-  const size_t lds = ((size_t)2 * ndata * L + (size_t)dfmi::kWavesPerBlock * L) * sizeof(double);
+  const size_t lds = ((size_t)2 * ndata * L + (size_t)dfmi::kWavesPerBlock * L) * sizeof(double) +
+                     (nslot <= 2 && ndata <= 12 ? DFMI_BINS_LDS_PAD : 0);
   if (ndata <= 12)
-    kern = nslot <= 2 ? dfmi::demod_seed_bins_kernel<2, 12, 4> : nslot <= 4 ? dfmi::demod_seed_bins_kernel<4, 12>
+    kern = nslot <= 2 ? dfmi::demod_seed_bins_kernel<2, 12, DFMI_BINS_PFN, DFMI_BINS_LOADS>
+           : nslot <= 4 ? dfmi::demod_seed_bins_kernel<4, 12>
                                                                           : dfmi::demod_seed_bins_kernel<8, 12>;
   else
     kern = nslot <= 2 ? dfmi::demod_seed_bins_kernel<2, 16> : nslot <= 4 ? dfmi::demod_seed_bins_kernel<4, 16>

@@ -161,12 +161,13 @@ __global__ __launch_bounds__(64) void ekf_kernel(const double* __restrict__ x, i
 // update P[i][j] - HP_i (HP_j / S) where ekf_step forms (HP_i / S) HP_j: rounding only.
 // ---------------------------------------------------------------------------
 
-// value of lane n of this lane's 16-lane row (DPP row_newbcast, gfx90a+)
+// value of lane n of this lane's 16-lane row, 64 bits in one v_mov_b64_dpp (gfx950's
+// 64-bit DPP takes row_newbcast): the same bits as row_bcast's two 32-bit moves
 template <int N>
-__device__ __forceinline__ double row_bcast(double v) {
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x150 + N, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x150 + N, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
+__device__ __forceinline__ double row_bcast64(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  return __builtin_bit_cast(double, (long long)__builtin_amdgcn_update_dpp((long long)b, (long long)b, 0x150 + N,
+                                                                            0xF, 0xF, false));
 }
 
 __device__ __forceinline__ void ekf_row_step(double (&st)[5], double (&Pc)[5], const double (&qv)[5], double Rv,
@@ -187,11 +188,11 @@ __device__ __forceinline__ void ekf_row_step(double (&st)[5], double (&Pc)[5], c
   // (H P)_j from this lane's column (symmetric P): the chain of ekf_step
   const double hpj = fma(H[3], Pc[3], fma(H[2], Pc[2], fma(H[1], Pc[1], fma(H[0], Pc[0], Pc[4]))));
   double HP[5];
-  HP[0] = row_bcast<0>(hpj);
-  HP[1] = row_bcast<1>(hpj);
-  HP[2] = row_bcast<2>(hpj);
-  HP[3] = row_bcast<3>(hpj);
-  HP[4] = row_bcast<4>(hpj);
+  HP[0] = row_bcast64<0>(hpj);
+  HP[1] = row_bcast64<1>(hpj);
+  HP[2] = row_bcast64<2>(hpj);
+  HP[3] = row_bcast64<3>(hpj);
+  HP[4] = row_bcast64<4>(hpj);
   const double S = fma(HP[3], H[3], fma(HP[2], H[2], fma(HP[1], H[1], fma(HP[0], H[0], HP[4] + Rv))));
   double invS = __builtin_amdgcn_rcp(S);
   invS = fma(invS, fma(-S, invS, 1.0), invS);
@@ -201,15 +202,6 @@ __device__ __forceinline__ void ekf_row_step(double (&st)[5], double (&Pc)[5], c
   for (int i = 0; i < 5; ++i) st[i] = fma(HP[i], iy, st[i]);
 #pragma unroll
   for (int i = 0; i < 5; ++i) Pc[i] = fma(-HP[i], cj, Pc[i]);
-}
-
-// value of lane n of this lane's 16-lane row, 64 bits in one v_mov_b64_dpp (gfx950's
-// 64-bit DPP takes row_newbcast)
-template <int N>
-__device__ __forceinline__ double row_bcast64(double v) {
-  const long long b = __builtin_bit_cast(long long, v);
-  return __builtin_bit_cast(double, (long long)__builtin_amdgcn_update_dpp((long long)b, (long long)b, 0x150 + N,
-                                                                            0xF, 0xF, false));
 }
 
 // (cos, sin)(w_m t_k) of every sample (np.arange(n) / f_samp, fitters.py:266), in
@@ -236,7 +228,10 @@ __device__ __forceinline__ void ekf_row_step2(double (&st)[5], double (&Pc)[5], 
   for (int i = 0; i < 5; ++i) Pc[i] = Pc[i] + qv[i];
   const double a = st[0], m = st[1], phi = st[2], psi = st[3], dc = st[4];
   double sps, cps;
-  dfmi_sincos_auto(psi, tk, &sps, &cps);
+  // one wave-uniform branch (scalar): the reduction-free polynomials when every lane's
+  // |psi| < 0.78 (the usual case), the full sincos otherwise; same bits either way
+  if (__all(fabs(psi) < 0.78)) dfmi_sincos_small(psi, tk, &sps, &cps);
+  else dfmi_sincos_k(psi, tk, &sps, &cps);
   const double cth = fma(cw, cps, -(sw * sps));
   const double sth = fma(sw, cps, cw * sps);
   const double arg = fma(m, cth, phi);

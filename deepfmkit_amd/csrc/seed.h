@@ -166,15 +166,15 @@ namespace dfmi {
 // workgroups; the LM follows on the same stream. Records are contiguous (segment s
 // at x + s*R). The seed's 162 VGPRs share the
 // bin kernel's 3-waves-per-SIMD register budget (168), so occupancy is unchanged.
-template <int MAXSLOT, int NDMAX, int PFN = 0>
+template <int MAXSLOT, int NDMAX, int PFN = 0, int LOADS = 8>
 __global__ __launch_bounds__(kBlockThreads) void demod_seed_bins_kernel(
     const double* __restrict__ x, int64_t nseg, int64_t rec_stride, int64_t nrec, int R, int L, int ndata,
     const double* __restrict__ tab, double* __restrict__ rows, int64_t row_ld, const double* __restrict__ guess,
     GuessInline ginl, int use_inline, const double* __restrict__ jtab, LMConst c, double* __restrict__ out,
     int64_t out_ld, int64_t nbuf, int32_t* __restrict__ status, uint64_t* __restrict__ probe) {
   if ((int64_t)blockIdx.x >= nrec) {
-    bins_kernel_body<MAXSLOT, 8, true, PFN>(x, nseg, (int64_t)R, R, L, ndata, tab, rows, row_ld, nullptr, probe,
-                                            (int)nrec);
+    bins_kernel_body<MAXSLOT, LOADS, true, PFN>(x, nseg, (int64_t)R, R, L, ndata, tab, rows, row_ld, nullptr, probe,
+                                                (int)nrec);
     return;
   }
   const uint64_t t_in = __builtin_amdgcn_s_memrealtime();

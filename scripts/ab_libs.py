@@ -4,6 +4,7 @@ Each library is loaded with its own ctypes handle (RTLD_LOCAL: its own HIP code 
 
 Workloads (config-2 shapes unless noted), median of ROUNDS interleaved rounds:
   step      dfmi_nls_record over 100k segments (fused seed + demod + LM), ms per call
+  demod     dfmi_demod_rows over the same segments (the bulk demodulation alone)
   lm        dfmi_lm over component-major QI of the same segments (every segment its own chunk)
   seq500    dfmi_nls_record parallel=0 over 500 segments (one warm-start chain, config 1)
 and the outputs' bitwise equality between the libraries (results must not depend on
@@ -55,6 +56,7 @@ def main():
                                         P, P, i32, P]
         lib.dfmi_demod.argtypes = [P, i64, i64, i32, i32, d, i32, P, P, i32, P]
         lib.dfmi_lm.argtypes = [P, i64, i32, P, i32, i64, ctypes.POINTER(_lib.LMConfig), P, P, P, i32, P]
+        lib.dfmi_demod_rows.argtypes = [P, i64, i64, i32, i32, d, i32, P, i32, P]
         lib.dfmi_last_error.restype = ctypes.c_char_p
     out = {k: torch.empty((6, nseg), dtype=torch.float64, device=dev) for k in libs}
     ok = {k: torch.empty(nseg, dtype=torch.int32, device=dev) for k in libs}
@@ -80,6 +82,12 @@ def main():
         chk(lib.dfmi_lm(qi.data_ptr(), nseg, nd, gd.data_ptr(), 0, nseg, cfg, lp[k].data_ptr(), ls[k].data_ptr(),
                         lt[k].data_ptr(), 1, P(st.cuda_stream)), lib)
 
+    rows = torch.empty((nseg, 32), dtype=torch.float64, device=dev)
+
+    def demod(k):
+        lib = libs[k]
+        chk(lib.dfmi_demod_rows(x.data_ptr(), nseg, R, R, nd, w0, 0, rows.data_ptr(), 1, P(st.cuda_stream)), lib)
+
     def seq(k):
         lib = libs[k]
         chk(lib.dfmi_nls_record(x.data_ptr(), 1, 500 * R, 500, R, nd, w0, 0, g.ctypes.data, 0, 1, cfg,
@@ -102,10 +110,11 @@ def main():
     for k in libs:  # clock ramp + warm caches of both libraries
         for _ in range(20):
             step(k)
-    res = {k: {"step": [], "lm": [], "seq500": []} for k in libs}
+    res = {k: {"step": [], "demod": [], "lm": [], "seq500": []} for k in libs}
     for _ in range(rounds):
         for k in libs:
             res[k]["step"].append(timed(lambda: step(k), 20))
+            res[k]["demod"].append(timed(lambda: demod(k), 20))
             res[k]["lm"].append(timed(lambda: lm(k), 20))
             res[k]["seq500"].append(timed(lambda: seq(k), 3))
     torch.cuda.synchronize()

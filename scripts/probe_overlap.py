@@ -78,6 +78,8 @@ def main():
     res["demod"] = timed(lambda: demod(cur))
     res["lm"] = timed(lambda: lm(cur))
     res["serial"] = timed(lambda: (demod(cur), lm(cur)))
+    # (round 3 also tried the LM's AQL packet without the barrier bit, hipExtAnyOrderLaunch
+    # on one stream: no effect on gfx950, 0.5376 vs 0.5380 ms: profiles/r03e_probe_anyorder.txt)
     for name, pa, pb in (("conc_same", 0, 0), ("conc_Ahi", -1, 0), ("conc_Blo", 0, 0), ("conc_Bhi", 0, -1)):
         sa = torch.cuda.Stream(priority=pa)
         sb = torch.cuda.Stream(priority=pb)

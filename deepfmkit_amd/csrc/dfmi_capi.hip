@@ -53,7 +53,6 @@ struct Tuning {
                          // (past one wave per SIMD the issue-bound rows share a SIMD, and one lane per
                          // channel carries 16x the channels per instruction); 0 = ekf_kernel only
   int wdfmi_accel = 3;   // W-DFMI: bit 0 time axis without division, bit 1 template slopes in LDS
-  int ekf_v2 = 0;        // EKF row kernel: theta by rotation of precomputed (cos, sin)(w t_k) (A/B)
   int lm_ladder = 32;    // LM launches of at most lm_ladder x CUs chains / segments (latency-bound: warm-start
                          // chains, small batches) run the parallel lambda ladder (lm.h lm_ladder_kernel);
                          // 0 = always one lane per chain / segment
@@ -834,8 +833,7 @@ const std::map<std::string, Knob>& knobs() {
       {"demod_spw", {&Tuning::demod_spw, {}}},
       {"ekf_row", {&Tuning::ekf_row, {}}},
       {"wdfmi_accel", {&Tuning::wdfmi_accel, {0, 1, 2, 3}}},
-      {"lm_ladder", {&Tuning::lm_ladder, {}}},
-      {"ekf_v2", {&Tuning::ekf_v2, {0, 1}}}};
+      {"lm_ladder", {&Tuning::lm_ladder, {}}}};
   return k;
 }
 // np.mean / np.var of nrec device records on st (moments.hip), numpy-exact.
@@ -931,22 +929,16 @@ int ekf_impl(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
   // few channels: one 16-lane row per channel (ekf_row_kernel, ~1.7x the per-channel
   // rate); many: one lane per channel (ekf_kernel, 16x the channels per instruction)
   const bool row = t_tune.ekf_row && nrec <= (int64_t)t_tune.ekf_row * t_ds->n_cu * 16;
-  const bool v2 = row && t_tune.ekf_v2;
   void* wtw = nullptr;
-  if ((rc = workspace(dev, "e_wt", (size_t)(n_samp > 0 ? n_samp : 1) * (v2 ? 16 : 8), &wtw))) return rc;
-  if (n_samp > 0) {
-    if (v2)
-      hipLaunchKernelGGL(dfmi::ekf_phase2_kernel, dim3((unsigned)((n_samp + 255) / 256)), dim3(256), 0, st,
-                         (double2*)wtw, n_samp, w_m, f_samp);
-    else
-      hipLaunchKernelGGL(dfmi::ekf_phase_kernel, dim3((unsigned)((n_samp + 255) / 256)), dim3(256), 0, st,
-                         (double*)wtw, n_samp, w_m, f_samp);
-  }
+  if ((rc = workspace(dev, "e_wt", (size_t)(n_samp > 0 ? n_samp : 1) * 8, &wtw))) return rc;
+  if (n_samp > 0)
+    hipLaunchKernelGGL(dfmi::ekf_phase_kernel, dim3((unsigned)((n_samp + 255) / 256)), dim3(256), 0, st,
+                       (double*)wtw, n_samp, w_m, f_samp);
   const int64_t grid = row ? (nrec + 3) / 4 : (nrec + block - 1) / block;
-  hipLaunchKernelGGL(v2 ? dfmi::ekf_row_kernel<true> : row ? dfmi::ekf_row_kernel<false> : dfmi::ekf_kernel,
+  hipLaunchKernelGGL(row ? dfmi::ekf_row_kernel : dfmi::ekf_kernel,
                      dim3((unsigned)grid), dim3(block), 0, st, dx, nrec, rs, n_samp, dx0, dp0, dq, dr,
                      (const double*)wtw, (int)R, nbuf, dstates, dfmi_trig_k());
-  g_last_demod = v2 ? "ekf_row_kernel2" : row ? "ekf_row_kernel" : "ekf_kernel";  // also reports the EKF variant
+  g_last_demod = row ? "ekf_row_kernel" : "ekf_kernel";  // also reports the EKF variant
   HIPCHK(hipGetLastError());
   if (host) {
     if (sb) HIPCHK(hipMemcpyAsync(states, dstates, sb, hipMemcpyDeviceToHost, st));

@@ -204,64 +204,7 @@ __device__ __forceinline__ void ekf_row_step(double (&st)[5], double (&Pc)[5], c
   for (int i = 0; i < 5; ++i) Pc[i] = fma(-HP[i], cj, Pc[i]);
 }
 
-// (cos, sin)(w_m t_k) of every sample (np.arange(n) / f_samp, fitters.py:266), in
-// parallel before the chain: the chain then rotates them by psi (ekf_row_step2).
-__global__ __launch_bounds__(256) void ekf_phase2_kernel(double2* __restrict__ cs, int64_t n, double w_m,
-                                                         double f_samp) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < n) {
-    double s, c;
-    sincos(w_m * ((double)k / f_samp), &s, &c);
-    cs[k] = make_double2(c, s);
-  }
-}
-
-// ekf_row_step with theta = w t_k + psi formed by ROTATION: (cos, sin)(theta) from the
-// precomputed (cos, sin)(w t_k) and sincos(psi), which for |psi| < pi/4 (the usual case)
-// is the kernel polynomials alone (no reduction, no quadrant selects); the H P row
-// shared by 64-bit DPP moves. theta is not rounded to fl(w t_k + psi) as the reference
-// forms it (fitters.py:279): the states move by ~1e-13 over a 2 s record (measured with
-// the scalar restatement), inside the 1e-12 parity gate.
-__device__ __forceinline__ void ekf_row_step2(double (&st)[5], double (&Pc)[5], const double (&qv)[5], double Rv,
-                                              double xk, double cw, double sw, const DfmiTrigK& tk) {
-#pragma unroll
-  for (int i = 0; i < 5; ++i) Pc[i] = Pc[i] + qv[i];
-  const double a = st[0], m = st[1], phi = st[2], psi = st[3], dc = st[4];
-  double sps, cps;
-  // one wave-uniform branch (scalar): the reduction-free polynomials when every lane's
-  // |psi| < 0.78 (the usual case), the full sincos otherwise; same bits either way
-  if (__all(fabs(psi) < 0.78)) dfmi_sincos_small(psi, tk, &sps, &cps);
-  else dfmi_sincos_k(psi, tk, &sps, &cps);
-  const double cth = fma(cw, cps, -(sw * sps));
-  const double sth = fma(sw, cps, cw * sps);
-  const double arg = fma(m, cth, phi);
-  const double acth = -a * cth, amsth = (a * m) * sth;
-  double sa, ca;
-  dfmi_sincos_k(arg, tk, &sa, &ca);
-  const double h = fma(a, ca, dc);
-  const double H[5] = {ca, acth * sa, -a * sa, amsth * sa, 1.0};
-  const double y = xk - h;
-  const double hpj = fma(H[3], Pc[3], fma(H[2], Pc[2], fma(H[1], Pc[1], fma(H[0], Pc[0], Pc[4]))));
-  double HP[5];
-  HP[0] = row_bcast64<0>(hpj);
-  HP[1] = row_bcast64<1>(hpj);
-  HP[2] = row_bcast64<2>(hpj);
-  HP[3] = row_bcast64<3>(hpj);
-  HP[4] = row_bcast64<4>(hpj);
-  const double S = fma(HP[3], H[3], fma(HP[2], H[2], fma(HP[1], H[1], fma(HP[0], H[0], HP[4] + Rv))));
-  double invS = __builtin_amdgcn_rcp(S);
-  invS = fma(invS, fma(-S, invS, 1.0), invS);
-  const double iy = invS * y;
-  const double cj = hpj * invS;  // K_j
-#pragma unroll
-  for (int i = 0; i < 5; ++i) st[i] = fma(HP[i], iy, st[i]);
-#pragma unroll
-  for (int i = 0; i < 5; ++i) Pc[i] = fma(-HP[i], cj, Pc[i]);
-}
-
 // Same arguments and outputs as ekf_kernel; grid of ceil(nrec / 4) one-wave blocks.
-// V2: ekf_row_step2 with wt = the (cos, sin)(w t_k) pairs of ekf_phase2_kernel.
-template <bool V2>
 __global__ __launch_bounds__(64) void ekf_row_kernel(const double* __restrict__ x, int64_t nrec, int64_t rec_stride,
                                                       int64_t n_samp, const double* __restrict__ x0,
                                                       const double* __restrict__ p0, const double* __restrict__ qd,
@@ -295,16 +238,8 @@ __global__ __launch_bounds__(64) void ekf_row_kernel(const double* __restrict__ 
       }
     }
   };
-  constexpr int W = V2 ? 2 : 1;  // table doubles per sample
-  if constexpr (V2) {
-    // the table index is wave-uniform: held in a VGPR, the pairs arrive by vector loads
-    // instead of scalar loads whose 32 SGPRs per 8 samples spill to VGPR lanes
-    asm volatile("" : "+v"(wt));
-  }
-  auto step = [&](double xk, const double* w) {
-    if constexpr (V2) ekf_row_step2(st, Pc, qv, Rv, xk, w[0], w[1], tk);
-    else ekf_row_step(st, Pc, qv, Rv, xk, w[0], tk);
-  };
+  constexpr int W = 1;  // table doubles per sample
+  auto step = [&](double xk, const double* w) { ekf_row_step(st, Pc, qv, Rv, xk, w[0], tk); };
   int64_t k = 0;
   double xc[8], wc[8][W];
   const int64_t n8 = n_samp & ~(int64_t)7;

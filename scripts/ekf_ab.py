@@ -20,7 +20,7 @@ def main():
     import deepfmkit_amd as dfm
     from deepfmkit_amd import _lib
     lib = _lib.load()
-    settings = [s for s in os.environ.get("SETTINGS", "ekf_v2=0;ekf_v2=1").split(";")]
+    settings = [s for s in os.environ.get("SETTINGS", "ekf_row=1;ekf_row=0").split(";")]
     f_samp, f_mod, R = 200000.0, 1000.0, 4000
     laser, ifo = dfm.LaserConfig(), dfm.InterferometerConfig()
     dfm.set_laser_df_for_effect(laser, ifo, 6.0)

@@ -325,3 +325,42 @@ def test_worker_trials_within_flat_gate(hc):
         for general in (0, 1):
             _, p, _ = _fit(hc, qi[None, :], g[None, :], general)
             assert abs(p[0, 1] - po[1]) <= 1e-9, (t, general, abs(p[0, 1] - po[1]))
+
+
+def test_worker_trial_sensitivity_to_qi_ulps():
+    """Why the worker trials are gated at max(1e-9, resolution) and not the flat 1e-9
+    (tests/test_gpu_workers.py): the reference's own fit (the oracle, bit-exact with
+    fit.fit) of the reference's trial inputs, with the QI moved by relative 1e-14 — the
+    size of a summation-order difference over R = 4000 samples (numpy's pairwise mean vs
+    the GPU's fold + contraction) — moves m by up to 2.9e-9 on trial 6 (amp_n 1e-3: the
+    LM stops one step earlier or later), above the flat gate and within the resolution
+    bound conftest.resolution_tol; on every trial the spread stays within that bound."""
+    import json
+    import deepfmkit_amd as dfm
+    from deepfmkit_amd import physics as P
+    from oracle import nls_oracle as O
+    from conftest import resolution_tol
+    G = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "workers.json")))
+    spread = []
+    for t in G["trials"]:
+        laser = dfm.LaserConfig()
+        laser.f_mod = 1000.0
+        laser.amp_n = t["amp_n"]
+        ifo = dfm.InterferometerConfig()
+        dfm.set_laser_df_for_effect(laser, ifo, t["m_true"])
+        cfg = dfm.DFMIObject("main_trial", laser, ifo)
+        x = np.asarray(P.SignalGenerator().generate(cfg, t["n_seconds"], mode="asd",
+                                                    trial_num=t["trial_num"])["main"].samples())
+        R = int(cfg.f_samp / laser.f_mod * int(laser.f_mod * t["n_seconds"]))
+        nd = t["ndata"]
+        qi = O.demod_buffer(x[:R], nd, 2 * np.pi * laser.f_mod / cfg.f_samp)[:2 * nd]
+        g = np.array([1.6, t["m_true"], 0.0, 0.0])
+        _, po, _ = O.fit_segment(nd, qi, g)
+        rng = np.random.default_rng(0)
+        d = 0.0
+        for _ in range(16):
+            _, p2, _ = O.fit_segment(nd, qi * (1.0 + 1e-14 * rng.standard_normal(qi.size)), g)
+            d = max(d, abs(p2[1] - po[1]))
+        spread.append(d)
+        assert d <= resolution_tol(nd, qi, po)[1], (t, d)
+    assert spread[6] > 1e-9, spread

@@ -180,7 +180,8 @@ def extra_configs(torch, dev, lib, _lib, stream, cfg, cpu_leg):
     segments), config 5 (EKFFitter.fit over a 2 s = 400,000-sample record, one channel,
     and 1,024 channels in one launch; with the scalar C restatement of the same loop
     timed on one host core beside it when the CPU leg runs) and config 1 through the
-    sequential path (_fit_sequential: one warm-start chain over 500 buffers)."""
+    sequential path (_fit_sequential: one warm-start chain over 500 buffers), and config 2's
+    100,000-segment record through the same sequential path."""
     from deepfmkit_amd.fitters import w0_of
     R = int(F_SAMP / F_MOD * N_CYC)
     w0 = w0_of(F_MOD, F_SAMP)
@@ -206,7 +207,7 @@ def extra_configs(torch, dev, lib, _lib, stream, cfg, cpu_leg):
                       "value": round(2 * nbuf / s3, 1), "unit": "segments/s", "ms_per_step": round(s3 * 1e3, 4),
                       "steps": 20, "status0_frac": float(np.mean(st == 0)),
                       "m_mean_per_channel": [float(mm[:nbuf].mean()), float(mm[nbuf:].mean())]}
-    del x, o2, k2
+    del o2, k2  # x is reused by the 100k sequential chain below
     # ---- config 5: EKF, 2 s @ 200 kS/s
     from deepfmkit_amd.physics import SnrSpec, synth_snr
     ns = int(2.0 * F_SAMP)
@@ -277,6 +278,21 @@ def extra_configs(torch, dev, lib, _lib, stream, cfg, cpu_leg):
                                  "status0_frac": float(np.mean(k1.cpu().numpy() == 0)),
                                  "reference_same_path": "724 segments/s on one core of the survey container "
                                                         "(SURVEY.md §6)"}
+    # ---- config 2's record through the sequential path: ONE warm-start chain of 100,000 fits
+    nb2 = 2 * nbuf
+    gen_shard(torch, dev, 0, nb2, R, seed=SEED, out=x)
+    o4 = torch.empty((6, nb2), dtype=torch.float64, device=dev)
+    k4 = torch.empty(nb2, dtype=torch.int32, device=dev)
+
+    def seq2():
+        _lib.check(lib.dfmi_nls_record(x.data_ptr(), 1, nb2 * R, nb2, R, NDATA, w0, 0, _lib.ptr(g1), 0, 1, cfg,
+                                       o4.data_ptr(), k4.data_ptr(), _lib.DFMI_MEM_DEVICE, stream.cuda_stream),
+                   "dfmi_nls_record")
+
+    t2 = _timed_steps(torch, seq2, 1, 1)
+    out["config2_sequential"] = {"workload": "100,000 segments (config 2's record), parallel=False: one warm-start "
+                                             "chain", "value": round(nb2 / t2, 1), "unit": "segments/s",
+                                 "s_per_record": round(t2, 4), "status0_frac": float(np.mean(k4.cpu().numpy() == 0))}
     return out
 
 

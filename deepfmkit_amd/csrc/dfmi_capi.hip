@@ -351,6 +351,9 @@ int to_lmconst(const dfmi_lm_config* cfg, dfmi::LMConst* c) {
 constexpr int kMaxSlotCap = 8;
 
 // A/B build switches of the bin kernel (defaults = the shipped configuration)
+#ifndef DFMI_EKF_SPLIT
+#define DFMI_EKF_SPLIT 1      // EKF row kernel: lane-split sincos (ekf.h ekf_sincos_row); 0 for A/B builds
+#endif
 #ifndef DFMI_BINS_LOADS
 #define DFMI_BINS_LOADS 8     // 1-KB chunk loads in flight per wave
 #endif
@@ -935,7 +938,7 @@ int ekf_impl(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
     hipLaunchKernelGGL(dfmi::ekf_phase_kernel, dim3((unsigned)((n_samp + 255) / 256)), dim3(256), 0, st,
                        (double*)wtw, n_samp, w_m, f_samp);
   const int64_t grid = row ? (nrec + 3) / 4 : (nrec + block - 1) / block;
-  hipLaunchKernelGGL(row ? dfmi::ekf_row_kernel : dfmi::ekf_kernel,
+  hipLaunchKernelGGL(row ? dfmi::ekf_row_kernel<DFMI_EKF_SPLIT != 0> : dfmi::ekf_kernel,
                      dim3((unsigned)grid), dim3(block), 0, st, dx, nrec, rs, n_samp, dx0, dp0, dq, dr,
                      (const double*)wtw, (int)R, nbuf, dstates, dfmi_trig_k());
   g_last_demod = row ? "ekf_row_kernel" : "ekf_kernel";  // also reports the EKF variant

@@ -162,37 +162,95 @@ __global__ __launch_bounds__(64) void ekf_kernel(const double* __restrict__ x, i
 // ---------------------------------------------------------------------------
 
 // value of lane n of this lane's 16-lane row, 64 bits in one v_mov_b64_dpp (gfx950's
-// 64-bit DPP takes row_newbcast): the same bits as row_bcast's two 32-bit moves
+// 64-bit DPP takes row_newbcast): the same bits as two 32-bit moves. `old` is the DPP
+// instruction's tied destination, never read (all rows and banks enabled): passing a
+// register whose value is dead (the previous sample's result) saves the copy the
+// compiler otherwise makes to give every result its own destination.
 template <int N>
-__device__ __forceinline__ double row_bcast64(double v) {
+__device__ __forceinline__ double row_bcast64(double old, double v) {
   const long long b = __builtin_bit_cast(long long, v);
-  return __builtin_bit_cast(double, (long long)__builtin_amdgcn_update_dpp((long long)b, (long long)b, 0x150 + N,
-                                                                            0xF, 0xF, false));
+  const long long o = __builtin_bit_cast(long long, old);
+  return __builtin_bit_cast(double, (long long)__builtin_amdgcn_update_dpp(o, b, 0x150 + N, 0xF, 0xF, false));
 }
 
+// Per-lane kernel-polynomial coefficients of dfmi_sincos_k (z^5 .. z^0) for the row
+// sincos below: the sin kernel's on even lanes, the cos kernel's on odd lanes.
+struct RowSplitCoef {
+  double k[6];
+};
+__device__ __forceinline__ RowSplitCoef row_split_coef(const DfmiTrigK& k, int par) {
+  RowSplitCoef rc;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) rc.k[i] = par ? k.c[10 + i] : k.c[4 + i];
+  return rc;
+}
+
+// dfmi_sincos_k(x) for a 16-lane row whose lanes all hold the same x, same bits: even
+// lanes evaluate the sin kernel fma(r z, P_s, r), odd lanes the cos kernel
+// fma(z z, P_c, fma(-0.5, z, 1)) (one polynomial per lane instead of both), every lane
+// reads both back from lanes 0 and 1 of its row, and the quadrant is applied as in
+// dfmi_sincos_k (swap selects + sign flips). ~31 VALU instructions instead of ~41.
+__device__ __forceinline__ void ekf_sincos_row(double x, const DfmiTrigK& k, const RowSplitCoef& rc, bool odd,
+                                               double& sn, double& cs) {
+  const double q = rint(x * k.c[0]);
+  double r = fma(-q, k.c[1], x);
+  r = fma(-q, k.c[2], r);
+  r = fma(-q, k.c[3], r);
+  const double z = r * r;
+  const double P = fma(z, fma(z, fma(z, fma(z, fma(z, rc.k[0], rc.k[1]), rc.k[2]), rc.k[3]), rc.k[4]), rc.k[5]);
+  const double X = odd ? z : r;
+  const double Y = odd ? fma(-0.5, z, 1.0) : r;
+  const double v = fma(X * z, P, Y);
+  const double sr = row_bcast64<0>(sn, v), cr = row_bcast64<1>(cs, v);
+  const int qi = ((int)q) & 3;
+  const double a = (qi & 1) ? cr : sr;
+  const double b = (qi & 1) ? sr : cr;
+  sn = (qi & 2) ? -a : a;
+  cs = ((qi + 1) & 2) ? -b : b;
+  if (__builtin_expect(!(fabs(x) < 524288.0), 0)) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double2 w = dfmi_sincos_lib(x);
+    sn = w.x;
+    cs = w.y;
+#endif
+  }
+}
+
+// Registers the row step keeps across samples: the DPP results (their previous values are
+// the tied destinations of the next sample's moves) and the one-channel coefficients.
+struct RowRegs {
+  double HP[5];
+  double sth, cth, sa, ca;
+};
+
+// SPLIT: both sincos by ekf_sincos_row; otherwise dfmi_sincos_k per lane (same bits).
+template <bool SPLIT>
 __device__ __forceinline__ void ekf_row_step(double (&st)[5], double (&Pc)[5], const double (&qv)[5], double Rv,
-                                             double xk, double wt, const DfmiTrigK& tk) {
+                                             double xk, double wt, const DfmiTrigK& tk, RowRegs& rr,
+                                             const RowSplitCoef& rc, bool odd) {
 #pragma unroll
   for (int i = 0; i < 5; ++i) Pc[i] = Pc[i] + qv[i];  // predict: Q on the diagonal (qv[i] = 0 off it)
   const double a = st[0], m = st[1], phi = st[2], psi = st[3], dc = st[4];
   const double th = wt + psi;
-  double sth, cth;
-  dfmi_sincos_k(th, tk, &sth, &cth);
+  if constexpr (SPLIT) ekf_sincos_row(th, tk, rc, odd, rr.sth, rr.cth);
+  else dfmi_sincos_k(th, tk, &rr.sth, &rr.cth);
+  const double sth = rr.sth, cth = rr.cth;
   const double arg = fma(m, cth, phi);
   const double acth = -a * cth, amsth = (a * m) * sth;
-  double sa, ca;
-  dfmi_sincos_k(arg, tk, &sa, &ca);
+  if constexpr (SPLIT) ekf_sincos_row(arg, tk, rc, odd, rr.sa, rr.ca);
+  else dfmi_sincos_k(arg, tk, &rr.sa, &rr.ca);
+  const double sa = rr.sa, ca = rr.ca;
   const double h = fma(a, ca, dc);
   const double H[5] = {ca, acth * sa, -a * sa, amsth * sa, 1.0};
   const double y = xk - h;
   // (H P)_j from this lane's column (symmetric P): the chain of ekf_step
   const double hpj = fma(H[3], Pc[3], fma(H[2], Pc[2], fma(H[1], Pc[1], fma(H[0], Pc[0], Pc[4]))));
-  double HP[5];
-  HP[0] = row_bcast64<0>(hpj);
-  HP[1] = row_bcast64<1>(hpj);
-  HP[2] = row_bcast64<2>(hpj);
-  HP[3] = row_bcast64<3>(hpj);
-  HP[4] = row_bcast64<4>(hpj);
+  double (&HP)[5] = rr.HP;
+  HP[0] = row_bcast64<0>(HP[0], hpj);
+  HP[1] = row_bcast64<1>(HP[1], hpj);
+  HP[2] = row_bcast64<2>(HP[2], hpj);
+  HP[3] = row_bcast64<3>(HP[3], hpj);
+  HP[4] = row_bcast64<4>(HP[4], hpj);
   const double S = fma(HP[3], H[3], fma(HP[2], H[2], fma(HP[1], H[1], fma(HP[0], H[0], HP[4] + Rv))));
   double invS = __builtin_amdgcn_rcp(S);
   invS = fma(invS, fma(-S, invS, 1.0), invS);
@@ -205,6 +263,8 @@ __device__ __forceinline__ void ekf_row_step(double (&st)[5], double (&Pc)[5], c
 }
 
 // Same arguments and outputs as ekf_kernel; grid of ceil(nrec / 4) one-wave blocks.
+// SPLIT: ekf_sincos_row (A/B against dfmi_sincos_k per lane; same bits).
+template <bool SPLIT>
 __global__ __launch_bounds__(64) void ekf_row_kernel(const double* __restrict__ x, int64_t nrec, int64_t rec_stride,
                                                       int64_t n_samp, const double* __restrict__ x0,
                                                       const double* __restrict__ p0, const double* __restrict__ qd,
@@ -239,7 +299,13 @@ __global__ __launch_bounds__(64) void ekf_row_kernel(const double* __restrict__ 
     }
   };
   constexpr int W = 1;  // table doubles per sample
-  auto step = [&](double xk, const double* w) { ekf_row_step(st, Pc, qv, Rv, xk, w[0], tk); };
+  const bool odd = lane & 1;
+  const RowSplitCoef rc = row_split_coef(tk, odd);
+  RowRegs rr;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) rr.HP[i] = 0.0;
+  rr.sth = rr.cth = rr.sa = rr.ca = 0.0;
+  auto step = [&](double xk, const double* w) { ekf_row_step<SPLIT>(st, Pc, qv, Rv, xk, w[0], tk, rr, rc, odd); };
   int64_t k = 0;
   double xc[8], wc[8][W];
   const int64_t n8 = n_samp & ~(int64_t)7;

@@ -1,4 +1,5 @@
-"""A/B of EKF kernel variants (dfmi_set_tuning keys given as SETTINGS="k=v,k=v;k=v"),
+"""A/B of EKF kernel variants (dfmi_set_tuning keys given as SETTINGS="k=v,k=v;k=v", or
+library builds given as LIBS="name=path;name=path", each loaded with its own handle),
 interleaved in one process: config 5 (2 s = 400,000 samples @200 kS/s, m=6, 40 dB) for
 1 and 64 channels, samples/s per channel, and each variant's max |d state| against the
 oracle's scalar C restatement (oracle/csrc/ekf_scalar.c). One JSON line."""
@@ -21,6 +22,16 @@ def main():
     from deepfmkit_amd import _lib
     lib = _lib.load()
     settings = [s for s in os.environ.get("SETTINGS", "ekf_row=1;ekf_row=0").split(";")]
+    libs = {}
+    if os.environ.get("LIBS"):
+        for item in os.environ["LIBS"].split(";"):
+            name, path = item.split("=")
+            lb = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+            lb.dfmi_ekf_fit.argtypes = lib.dfmi_ekf_fit.argtypes
+            lb.dfmi_last_demod_kernel.restype = ctypes.c_char_p
+            lb.dfmi_last_error.restype = ctypes.c_char_p
+            libs[name] = lb
+        settings = list(libs)
     f_samp, f_mod, R = 200000.0, 1000.0, 4000
     laser, ifo = dfm.LaserConfig(), dfm.InterferometerConfig()
     dfm.set_laser_df_for_effect(laser, ifo, 6.0)
@@ -46,16 +57,23 @@ def main():
     xs = {1: torch.from_numpy(x1).to(dev), 64: torch.from_numpy(np.tile(x1, 64)).to(dev)}
     outs = {c: torch.empty((c, nb, 5), dtype=torch.float64, device=dev) for c in (1, 64)}
 
+    cur = {"lib": lib}
+
     def run(c):
-        _lib.check(lib.dfmi_ekf_fit(xs[c].data_ptr(), c, ns, ns, init4.data_ptr(), p0d.data_ptr(), qdd.data_ptr(),
-                                    None, 2 * np.pi * f_mod, f_samp, R, nb, outs[c].data_ptr(), 1, st.cuda_stream),
-                   "ekf")
+        lb = cur["lib"]
+        rc = lb.dfmi_ekf_fit(xs[c].data_ptr(), c, ns, ns, init4.data_ptr(), p0d.data_ptr(), qdd.data_ptr(),
+                                    None, 2 * np.pi * f_mod, f_samp, R, nb, outs[c].data_ptr(), 1, st.cuda_stream)
+        if rc != 0:
+            raise RuntimeError(lb.dfmi_last_error().decode())
 
     for rnd in range(4):
         for s in settings:
-            for kv in s.split(","):
-                k, v = kv.split("=")
-                _lib.check(lib.dfmi_set_tuning(k.encode(), int(v)), "tune")
+            if libs:
+                cur["lib"] = libs[s]
+            else:
+                for kv in s.split(","):
+                    k, v = kv.split("=")
+                    _lib.check(lib.dfmi_set_tuning(k.encode(), int(v)), "tune")
             for c in (1, 64):
                 run(c)
                 torch.cuda.synchronize()
@@ -63,14 +81,17 @@ def main():
                 run(c)
                 torch.cuda.synchronize()
                 res[s][f"t{c}"].append(time.perf_counter() - t0)
-            res[s]["kernel"] = lib.dfmi_last_demod_kernel().decode()
+            res[s]["kernel"] = cur["lib"].dfmi_last_demod_kernel().decode()
             res[s]["max_dstate_vs_c"] = float(np.abs(outs[1][0].cpu().numpy() - ref).max())
             res[s]["max_dstate_64_vs_1"] = float(np.abs(outs[64].cpu().numpy() - outs[1].cpu().numpy()).max())
+            res[s]["states1"] = outs[1].cpu().numpy().copy()
     out = {}
+    first = res[settings[0]]["states1"]
     for s, r in res.items():
         t1, t64 = float(np.median(r["t1"])), float(np.median(r["t64"]))
         out[s] = {"kernel": r["kernel"], "samples_per_s_1ch": round(ns / t1), "samples_per_s_per_ch_64": round(ns / t64),
-                  "max_dstate_vs_c": r["max_dstate_vs_c"], "max_dstate_64_vs_1": r["max_dstate_64_vs_1"]}
+                  "max_dstate_vs_c": r["max_dstate_vs_c"], "max_dstate_64_vs_1": r["max_dstate_64_vs_1"],
+                  "bit_identical_to_first": bool(np.array_equal(r["states1"], first))}
     print(json.dumps(out), flush=True)
 
 

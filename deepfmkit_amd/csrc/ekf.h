@@ -223,7 +223,11 @@ struct RowRegs {
   double sth, cth, sa, ca;
 };
 
-// SPLIT: both sincos by ekf_sincos_row; otherwise dfmi_sincos_k per lane (same bits).
+// SPLIT: both sincos by ekf_sincos_row; otherwise dfmi_sincos_k per lane (same bits; A/B
+// builds). The chain is fp64-issue-bound, not latency-bound: a form with 8 fewer dependent
+// steps per sample (Estrin polynomials, (H P)_j and S as shallow trees, the Newton step of
+// 1/S folded into iy and K_j) but 5 more fp64 instructions ran 3 % slower
+// (profiles/r03j_ekf_modes_ab.json).
 template <bool SPLIT>
 __device__ __forceinline__ void ekf_row_step(double (&st)[5], double (&Pc)[5], const double (&qv)[5], double Rv,
                                              double xk, double wt, const DfmiTrigK& tk, RowRegs& rr,
@@ -263,7 +267,7 @@ __device__ __forceinline__ void ekf_row_step(double (&st)[5], double (&Pc)[5], c
 }
 
 // Same arguments and outputs as ekf_kernel; grid of ceil(nrec / 4) one-wave blocks.
-// SPLIT: ekf_sincos_row (A/B against dfmi_sincos_k per lane; same bits).
+// SPLIT: see ekf_row_step.
 template <bool SPLIT>
 __global__ __launch_bounds__(64) void ekf_row_kernel(const double* __restrict__ x, int64_t nrec, int64_t rec_stride,
                                                       int64_t n_samp, const double* __restrict__ x0,

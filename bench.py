@@ -384,7 +384,9 @@ def main():
     # profiles/r02m kernel trace)
     for _ in range(40):
         step()
-    nrep = max(20, args.steps)
+    # 200 steps (~0.11 s): the kernel's mean over these dominates any rocprofv3 average of the
+    # same run, ramp launches included (profiles/r03*_frac_check.json)
+    nrep = max(200, args.steps)
     # the step itself with timing events around its kernels (dfmi_step_timing): the fused
     # seed + demodulation launch (the dominant kernel) and the LM launch, on the step's stream
     _lib.check(lib.dfmi_step_timing(1), "dfmi_step_timing")

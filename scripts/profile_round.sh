@@ -6,6 +6,7 @@
 #  3) PMC pass: WRITE_SIZE over the same
 #  4) profiles/pmc_demod.json from 2) + 3) (scripts/pmc_summary.py), for the step's
 #     own dominant kernel (demod_seed_bins_kernel)
+#  5) frac_check.json: the line's roofline fraction recomputed from 1)'s kernel trace
 # Each step has its own time limit; the script stops at the first failure.
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
@@ -22,4 +23,5 @@ KERN=$(python3 -c "import json; print(json.load(open('$OUT/pmc_fetch.json'))['ro
 python3 scripts/pmc_summary.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$KERN" 3216800000 \
     "$PMC_CMD (100000 segments, R=4000, ndata=10)" > "$OUT/pmc_summary.json" || exit $?
 cp profiles/pmc_demod.json "$OUT/"
+python3 scripts/frac_check.py "$OUT/bench_trace.json" "$OUT/trace/bench_kernel_trace.csv" > "$OUT/frac_check.json" || exit $?
 echo "profile ok"

@@ -1141,6 +1141,49 @@ __global__ __launch_bounds__(64) void lm_ladder_kernel(
       if (k == 0)  // segments before `first` (the seed buffer) are fitted elsewhere: carry their dc
         for (int64_t t = r * nbuf; t < r * nbuf + first; ++t) out[4 * out_ld + t] = qi[t * qi_ld + dfmi_row_dc(ndata)];
     }
+  } else if constexpr (kQReg && CHAIN) {
+    // warm-start chain (sequential / n_cores). Every LPS fits the group stages the QI of
+    // its next LPS segments into LDS, one segment per lane with all 2·ndata loads in
+    // flight: one memory latency per LPS fits instead of one per fit (the fits themselves
+    // read no global memory). The m-grid re-seed keeps its global accessor.
+    constexpr int NC = nd_cap(NDMAX);
+    __shared__ double stage[64 / LPS][LPS][2 * NC];
+    const int g = (int)(threadIdx.x / LPS), gl = (int)(threadIdx.x & (LPS - 1));
+    for (int64_t t = 0; t < len; ++t) {
+      const int slot = (int)(t & (LPS - 1));
+      if (slot == 0) {
+        if (t + gl < len) {
+          const double* __restrict__ qs = qi + s0 + t + gl;
+          double v[2 * NC];
+#pragma unroll
+          for (int cc = 0; cc < 2 * NC; ++cc) v[cc] = qs[(int64_t)cc * qi_ld];
+#pragma unroll
+          for (int cc = 0; cc < 2 * NC; ++cc) stage[g][gl][cc] = v[cc];
+        }
+        // one wave: its LDS operations run in order; the fence keeps the compiler from
+        // moving the reads below above the other lanes' writes
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      QRegs<NC> qr;
+#pragma unroll
+      for (int h = 0; h < NC; ++h) {
+        qr.c[h] = stage[g][slot][h];
+        qr.s[h] = stage[g][slot][NC + h];
+      }
+      const QGlobal q{qi + s0 + t, qi_ld, ndata};
+      double ssq;
+      const int st = fit_segment_q2<NDMAX, QRegs<NC>, QGlobal, 2>(qr, q, ndata, jtab, c, p, ssq);
+      if (lead) {
+        out[0 * out_ld + s0 + t] = p[0];
+        out[1 * out_ld + s0 + t] = p[1];
+        out[2 * out_ld + s0 + t] = p[2];
+        out[3 * out_ld + s0 + t] = p[3];
+        out[5 * out_ld + s0 + t] = ssq;
+        status[s0 + t] = st;
+      }
+    }
   } else {
     for (int64_t t = 0; t < len; ++t) {  // warm-start chain (sequential / n_cores); len 1: chunk size 1
       const QGlobal q{qi + s0 + t, qi_ld, ndata};

@@ -7,6 +7,7 @@ Workloads (config-2 shapes unless noted), median of ROUNDS interleaved rounds:
   demod     dfmi_demod_rows over the same segments (the bulk demodulation alone)
   lm        dfmi_lm over component-major QI of the same segments (every segment its own chunk)
   seq500    dfmi_nls_record parallel=0 over 500 segments (one warm-start chain, config 1)
+  seqall    (SEQALL=1) dfmi_nls_record parallel=0 over all NSEG segments (one chain)
 and the outputs' bitwise equality between the libraries (results must not depend on
 the build unless the change is meant to move rounding). One JSON line."""
 import ctypes
@@ -67,6 +68,9 @@ def main():
     lt = {k: torch.empty(nseg, dtype=torch.int32, device=dev) for k in libs}
     s1 = {k: torch.empty((6, 500), dtype=torch.float64, device=dev) for k in libs}
     k1 = {k: torch.empty(500, dtype=torch.int32, device=dev) for k in libs}
+    seqall = os.environ.get("SEQALL") == "1"
+    sa = {k: torch.empty((6, nseg), dtype=torch.float64, device=dev) for k in libs} if seqall else {}
+    ka = {k: torch.empty(nseg, dtype=torch.int32, device=dev) for k in libs} if seqall else {}
 
     def chk(rc, lib):
         if rc != 0:
@@ -93,6 +97,11 @@ def main():
         chk(lib.dfmi_nls_record(x.data_ptr(), 1, 500 * R, 500, R, nd, w0, 0, g.ctypes.data, 0, 1, cfg,
                                 s1[k].data_ptr(), k1[k].data_ptr(), 1, P(st.cuda_stream)), lib)
 
+    def seqa(k):
+        lib = libs[k]
+        chk(lib.dfmi_nls_record(x.data_ptr(), 1, nseg * R, nseg, R, nd, w0, 0, g.ctypes.data, 0, 1, cfg,
+                                sa[k].data_ptr(), ka[k].data_ptr(), 1, P(st.cuda_stream)), lib)
+
     first = next(iter(libs.values()))
     chk(first.dfmi_demod(x.data_ptr(), nseg, R, R, nd, w0, 0, qi.data_ptr(), dc.data_ptr(), 1, P(st.cuda_stream)),
         first)
@@ -111,12 +120,17 @@ def main():
         for _ in range(20):
             step(k)
     res = {k: {"step": [], "demod": [], "lm": [], "seq500": []} for k in libs}
+    if seqall:
+        for k in libs:
+            res[k]["seqall"] = []
     for _ in range(rounds):
         for k in libs:
             res[k]["step"].append(timed(lambda: step(k), 20))
             res[k]["demod"].append(timed(lambda: demod(k), 20))
             res[k]["lm"].append(timed(lambda: lm(k), 20))
             res[k]["seq500"].append(timed(lambda: seq(k), 3))
+            if seqall:
+                res[k]["seqall"].append(timed(lambda: seqa(k), 1))
     torch.cuda.synchronize()
     names = list(libs)
     summary = {k: {w: round(float(np.median(v)), 5) for w, v in r.items()} for k, r in res.items()}
@@ -130,6 +144,8 @@ def main():
             "step_max_abs_dm": float((out[a][1] - out[b][1]).abs().max()),
             "step_max_abs_dphi": float((out[a][2] - out[b][2]).abs().max()),
             "seq_max_abs_dm": float((s1[a][1] - s1[b][1]).abs().max())}
+        if seqall:
+            eq[f"{a}_vs_{b}"]["seqall"] = bool(torch.equal(sa[a], sa[b]) and torch.equal(ka[a], ka[b]))
     print(json.dumps({"ms": summary, "bit_identical": eq, "libs": spec, "rounds": rounds,
                       "phi": PHI, "psi": PSI}), flush=True)
 

@@ -147,7 +147,42 @@ def cpu_baseline(args):
                       f"generator, RandomState(0)), numpy restatement of StandardNLSFitter._fit_parallel with "
                       f"multiprocessing.Pool({procs}); {dt:.2f} s wall",
             "host": host}
-    return raw, ref, procs, base
+    base_c = cpu_baseline_c(x, nseg, R, procs, ref)
+    return raw, ref, procs, base, base_c
+
+
+def cpu_baseline_c(x, nseg, R, threads, ref):
+    """Second CPU baseline (optional): the scalar C restatement of the same
+    readout (oracle/csrc/nls_scalar.c: chunk size 1, J_n by one Miller pass per
+    evaluation, the quadratures through the basis period's phase bins) with OpenMP over
+    the same host CPU share, on the same sample; median of 5 runs, status-0 parameters
+    against the numpy port's."""
+    import ctypes
+    path = os.path.join(ROOT, "oracle", "libnls_scalar.so")
+    if not os.path.exists(path):
+        return {"error": "oracle/libnls_scalar.so not built"}
+    lib = ctypes.CDLL(path)
+    P = ctypes.c_void_p
+    lib.nls_scalar_record.argtypes = [P, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_double, P,
+                                      ctypes.c_int, P]
+    xs = np.ascontiguousarray(x[: nseg * R], dtype=np.float64)
+    g = np.array([1.6, 6.0, 0.0, 0.0])
+    out = np.zeros((nseg, 7))
+    ts = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        rc = lib.nls_scalar_record(xs.ctypes.data, nseg, R, NDATA, 2.0 * np.pi * F_MOD / F_SAMP, g.ctypes.data,
+                                   threads, out.ctypes.data)
+        ts.append(time.perf_counter() - t0)
+        if rc != 0:
+            return {"error": f"nls_scalar_record rc {rc}"}
+    dt = float(np.median(ts))
+    ok = (out[:, 6] == 0) & (ref[:, 6] == 0)
+    return {"value": round(nseg / dt, 1), "unit": "segments/s", "cores": threads, "kind": "port",
+            "sample": f"the same {nseg} segments; scalar C restatement (oracle/csrc/nls_scalar.c, gcc -O2, "
+                      f"OpenMP {threads} threads, chunk size 1); median of 5 runs, {dt:.3f} s",
+            "max_dm_vs_numpy_port": float(np.abs(out[ok, 1] - ref[ok, 1]).max()) if ok.any() else None,
+            "status_match": float(np.mean(out[:, 6] == ref[:, 6]))}
 
 
 def parity_vs_oracle(df, ref):
@@ -525,9 +560,10 @@ def main():
     if world == 1 and not args.no_extra and nrec == 1 and args.segments is None:
         line["extra_configs"] = extra_configs(torch, dev, lib, _lib, stream, cfg, want_base)
     if pre is not None:
-        raw, ref, procs, base = pre
+        raw, ref, procs, base, base_c = pre
         df = StandardNLSFitter({"n": N_CYC}).fit(raw, parallel=True, n_cores=procs)  # same chunking, on GPU
         line["cpu_baseline"] = base
+        line["cpu_baseline_c"] = base_c
         line["parity"] = parity_vs_oracle(df, ref)
     if rank == 0:
         print(json.dumps(line), flush=True)

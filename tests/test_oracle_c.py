@@ -1,6 +1,7 @@
-"""The oracle's C restatement of EKFFitter's loop (oracle/csrc/ekf_scalar.c, the scalar
-CPU baseline of scripts/bench_ekf.py) against the numpy oracle (pinned to the
-reference's golden EKF states): same states to fp64 rounding."""
+"""The oracle's C restatements against the numpy oracle (pinned to the reference's golden
+vectors): EKFFitter's loop (oracle/csrc/ekf_scalar.c, the scalar CPU baseline of config 5):
+same states to fp64 rounding; the NLS readout (oracle/csrc/nls_scalar.c, bench.py's second CPU
+baseline): status equal, status-0 parameters within 1e-9."""
 import ctypes
 import os
 
@@ -34,3 +35,41 @@ def test_ekf_scalar_c_matches_oracle():
     lib.ekf_scalar(x.ctypes.data, x.size, x0.ctypes.data, p0.ctypes.data, qd.ctypes.data, float(np.var(x)),
                    2 * np.pi * 1000.0, 200000.0, 4000, ref.shape[0], out.ctypes.data)
     assert np.max(np.abs(out - ref)) <= 1e-12
+
+
+def test_nls_scalar_c_matches_oracle():
+    """Chunk-size-1 parallel semantics (fitters.py:395-428 with n_cores >= nbuf - 1) on the
+    reference's clean edge record and on a 200-segment config-2-shaped snr record, 1 and
+    4 OpenMP threads (same results)."""
+    so = os.path.join(ROOT, "oracle", "libnls_scalar.so")
+    if not os.path.exists(so):
+        pytest.skip("oracle C restatement not built (run __graft_entry__.build())")
+    import deepfmkit_amd as dfm
+    from oracle import nls_oracle as O
+    lib = ctypes.CDLL(so)
+    P = ctypes.c_void_p
+    lib.nls_scalar_record.argtypes = [P, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_double, P,
+                                      ctypes.c_int, P]
+    d = np.load(os.path.join(ROOT, "tests", "golden", "edge_records.npz"))
+    laser, ifo = dfm.LaserConfig(), dfm.InterferometerConfig()
+    dfm.set_laser_df_for_effect(laser, ifo, 6.0)
+    raw = dfm.SignalGenerator().generate(dfm.DFMIObject("c", laser, ifo, f_samp=200000.0), 200 * 4000 / 200000.0,
+                                         mode="snr", snr_db=40.0, trial_num=5)["main"]
+    cases = [(d["clean_x"], float(d["f_samp"]), float(d["f_mod"]), int(d["n"])),
+             (np.asarray(raw.samples(), dtype=np.float64), 200000.0, 1000.0, 20)]
+    for x, fs, fm, n in cases:
+        R, _, nb = O.buffer_params(x.size, fs, fm, n)
+        ref = O.fit_record_parallel(x, fs, fm, n, n_cores=max(1, nb - 1))
+        for th in (1, 4):
+            out = np.zeros((nb, 7))
+            g = np.array([1.6, 6.0, 0.0, 0.0])
+            assert lib.nls_scalar_record(x.ctypes.data, nb, R, 10, 2 * np.pi * fm / fs, g.ctypes.data, th,
+                                         out.ctypes.data) == 0
+            np.testing.assert_array_equal(out[:, 6], ref[:, 6])
+            ok = ref[:, 6] == 0
+            for j in range(4):
+                dj = np.abs(out[ok, j] - ref[ok, j])
+                if j == 2:
+                    dj = np.abs((dj + np.pi) % (2 * np.pi) - np.pi)
+                assert dj.max() <= 1e-9, (j, dj.max())
+            assert np.abs(out[:, 4] - ref[:, 4]).max() <= 1e-13

@@ -1,5 +1,6 @@
 #!/bin/bash
-# round 3 session k: full GPU suite at HEAD, smoke, then the judged profiles (driver command)
+# The round's final GPU session: the whole -m gpu suite, smoke(), and the judged profiles of
+# the driver's bench command (scripts/profile_round.sh), each step under its own limit.
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 > gpurun_out/pytest_gpu.log 2>&1
@@ -7,4 +8,4 @@ rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
 [ $rc -eq 0 ] || exit $rc
-TAG=r03k timeout -k 10 1500 bash scripts/profile_round.sh; echo "profile rc=$?"
+timeout -k 10 1500 bash scripts/profile_round.sh; echo "profile rc=$?"

@@ -1,6 +1,6 @@
 """Interleaved A/B of the roofline kernel (dfmi_demod_rows: the bin kernel in the row
 layout, config 2) under tuning settings, with a bit-identity check of the rows.
-Usage: SETTINGS="demod_grid_mult=1;demod_grid_mult=8" python scripts/tune_rows_demod.py"""
+Usage: SETTINGS="demod_spw=2;demod_spw=0" python scripts/tune_rows_demod.py"""
 import ctypes
 import json
 import os
@@ -23,7 +23,7 @@ nseg, R, nd = int(os.environ.get("NSEG", 100000)), 4000, 10
 x = bench.gen_shard(torch, dev, 0, nseg, R, seed=bench.SEED)
 st = torch.cuda.current_stream()
 rows = torch.empty((nseg, lib.dfmi_qi_row_stride(nd)), dtype=torch.float64, device=dev)
-settings = parse(os.environ.get("SETTINGS", "demod_grid_mult=1;demod_grid_mult=8"))
+settings = parse(os.environ.get("SETTINGS", "demod_spw=2;demod_spw=0"))
 defaults = {}
 for s in settings:
     for k in s:

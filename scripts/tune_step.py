@@ -1,6 +1,6 @@
 """Interleaved A/B timing of whole record-pipeline steps (dfmi_nls_record, config 2)
 under tuning settings, with a bit-identity check of the results across settings.
-Usage: SETTINGS="seed_handoff=1;seed_handoff=0" python scripts/tune_step.py (each setting on top of the defaults)"""
+Usage: SETTINGS="demod_spw=2;demod_spw=1" python scripts/tune_step.py (each setting on top of the defaults)"""
 import ctypes
 import json
 import os
@@ -40,7 +40,7 @@ def main():
     guess = np.array([1.6, 6.0, 0.0, 0.0])
     out = torch.empty((6, nseg), dtype=torch.float64, device=dev)
     ok = torch.empty(nseg, dtype=torch.int32, device=dev)
-    settings = parse(os.environ.get("SETTINGS", "seed_reserve=1;seed_reserve=0"))
+    settings = parse(os.environ.get("SETTINGS", "demod_spw=2;demod_spw=1"))
     defaults = {}
     for s in settings:  # every setting is applied on top of the library defaults
         for k in s:

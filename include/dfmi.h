@@ -267,8 +267,10 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
  * for every ndata), "demod_spw" (segments per wave the bin grid is sized for; 0 =
  * persistent), "ekf_row" (EKF row kernel up to ekf_row x 16 x CUs channels, 0 = lane
  * kernel only), "wdfmi_accel" (bit 0: W-DFMI time axis without division, bit 1:
- * template slopes in LDS; both exact), "probe" (1 = diagnostics timestamp buffer on the
- * current device, dfmi_probe_read). */
+ * template slopes in LDS; both exact), "lm_ladder" (LM launches of at most lm_ladder x CUs
+ * chains or segments run the parallel lambda ladder, 8 lanes per item: warm-start chains,
+ * small batches; 0 = never; default 32; same bits), "probe" (1 = diagnostics timestamp
+ * buffer on the current device, dfmi_probe_read). */
 int dfmi_set_tuning(const char* key, int64_t value);
 
 /* Current value of a tuning key (see dfmi_set_tuning). */

@@ -130,3 +130,81 @@ def test_config4_shard_far_end_vs_c_restatement():
     worst, nfar = _compare(gp, gs, _c_fit(x, n_tail + 1), x)
     print("config 4 shard, far end (200k segments): max |d amp, m, phi, psi| vs C =", worst,
           "; checked against the oracle:", nfar)
+
+
+def test_config3_two_channels_vs_c_restatement():
+    """Config 3's shape: two channels (main m = 6, witness m = 4.3) of 50,000 segments as
+    two records of ONE dfmi_nls_record call, each seeded by its own buffer 0 (as bench.py
+    times it), against the C restatement of each record."""
+    import torch
+    import bench
+    from deepfmkit_amd import _lib
+    from deepfmkit_amd import fit as F
+    from deepfmkit_amd.fitters import w0_of
+    dev = torch.device("cuda", 0)
+    nbuf = 50_000
+    xd = torch.empty(2 * nbuf * R, dtype=torch.float64, device=dev)
+    for c, m in enumerate((6.0, 4.3)):
+        bench.gen_shard(torch, dev, 0, nbuf, R, seed=bench.SEED, m_true=m, stream=c,
+                        out=xd[c * nbuf * R:(c + 1) * nbuf * R])
+    lib = _lib.load()
+    out = torch.empty((6, 2 * nbuf), dtype=torch.float64, device=dev)
+    st = torch.empty(2 * nbuf, dtype=torch.int32, device=dev)
+    g = np.ascontiguousarray(np.tile([1.6, 6.0, 0.0, 0.0], (2, 1)))
+    _lib.check(lib.dfmi_nls_record(xd.data_ptr(), 2, nbuf * R, nbuf, R, 10, w0_of(1000.0, 200000.0), 0, _lib.ptr(g),
+                                   1, nbuf - 1, F.lm_config(), out.data_ptr(), st.data_ptr(), _lib.DFMI_MEM_DEVICE,
+                                   torch.cuda.current_stream().cuda_stream), "dfmi_nls_record")
+    torch.cuda.synchronize()
+    gp, gs = out.cpu().numpy().T, st.cpu().numpy()
+    x = xd.cpu().numpy()
+    del xd
+    for c in range(2):
+        xc = x[c * nbuf * R:(c + 1) * nbuf * R]
+        sl = slice(c * nbuf, (c + 1) * nbuf)
+        worst, nfar = _compare(gp[sl], gs[sl], _c_fit(xc, nbuf), xc)
+        print(f"config 3 channel {c}: max |d amp, m, phi, psi| vs C =", worst, "; checked against the oracle:", nfar)
+
+
+@pytest.mark.parametrize("row", [1, 0])
+def test_ekf_config5_13_channels_full_length_vs_c_oracle(row):
+    """Config 5 at full length on 13 independent channels in ONE dfmi_ekf_fit launch (EKFFitter
+    per channel, fitters.py:214-320): 4 channels per wave in the row kernel, the 13th wave row
+    shadowed (13 = 3 x 4 + 1), 13 lanes in the lane kernel; every channel's 100 snapshots
+    against the scalar C restatement of the loop (oracle/csrc/ekf_scalar.c) at 1e-12."""
+    import deepfmkit_amd as dfm
+    from deepfmkit_amd import _lib
+    lib = _lib.load()
+    so = os.path.join(ROOT, "oracle", "libekf_scalar.so")
+    if not os.path.exists(so):
+        pytest.skip("oracle/libekf_scalar.so not built (make -C oracle)")
+    cl = ctypes.CDLL(so)
+    P = ctypes.c_void_p
+    cl.ekf_scalar.argtypes = [P, ctypes.c_int64, P, P, P, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                              ctypes.c_int64, ctypes.c_int64, P]
+    raws, refs = [], []
+    p0, qd = np.ones(5), np.array([1e-8, 1e-8, 1e-6, 1e-6, 1e-8])
+    for ch in range(13):
+        laser, ifo = dfm.LaserConfig(), dfm.InterferometerConfig()
+        laser.psi = 0.05 * ch
+        ifo.phi = 0.1 * ch
+        dfm.set_laser_df_for_effect(laser, ifo, 6.0 + 0.25 * ch)
+        dff = dfm.DeepFitFramework()
+        dff.load_sim(dfm.DFMIObject(f"c{ch}", laser, ifo, f_samp=200000.0))
+        dff.simulate(f"c{ch}", n_seconds=2.0, mode="snr", snr_db=40.0, trial_num=100 + ch)
+        raw = dff.raws[f"c{ch}"]
+        x = np.ascontiguousarray(raw.samples(), dtype=np.float64)
+        x0 = np.array([1.6, 6.0, 0.0, 0.0, np.mean(x)])
+        ref = np.zeros((100, 5))
+        cl.ekf_scalar(x.ctypes.data, x.size, x0.ctypes.data, p0.ctypes.data, qd.ctypes.data, float(np.var(x)),
+                      2 * np.pi * 1000.0, 200000.0, 4000, 100, ref.ctypes.data)
+        raws.append(raw)
+        refs.append(ref)
+    _lib.check(lib.dfmi_set_tuning(b"ekf_row", row), "tune")
+    try:
+        got = dfm.fitters.ekf_records(raws, 20)
+        assert lib.dfmi_last_demod_kernel().decode() == ("ekf_row_kernel" if row else "ekf_kernel")
+    finally:
+        _lib.check(lib.dfmi_set_tuning(b"ekf_row", 1), "tune")
+    for ch in range(13):
+        err = np.abs(np.asarray(got[ch]) - refs[ch])
+        assert err.max() <= 1e-12, (ch, err.max())

@@ -343,3 +343,18 @@ int nls_scalar_record(const double* x, int64_t nbuf, int R, int nd, double w0, c
   free(tab);
   return 0;
 }
+
+/* fit.fit (fit.py:322-361) on n QI vectors: qi n x 2 nd (row-major [Q_1..Q_nd, I_1..I_nd]),
+ * guess n x 4; out n x 6 (amp, m, phi, psi, ssq, status). Returns 0, or -1. */
+int lm_scalar_fit(const double* qi, int64_t n, int nd, const double* guess, int nthreads, double* out) {
+  if (n < 0 || nd < 1 || nd > NDMAX) return -1;
+#pragma omp parallel for schedule(dynamic, 64) num_threads(nthreads)
+  for (int64_t s = 0; s < n; ++s) {
+    double p[4] = {guess[s * 4], guess[s * 4 + 1], guess[s * 4 + 2], guess[s * 4 + 3]}, ssq;
+    const int st = fit_segment(nd, qi + s * 2 * nd, p, &ssq);
+    for (int i = 0; i < 4; ++i) out[s * 6 + i] = p[i];
+    out[s * 6 + 4] = ssq;
+    out[s * 6 + 5] = st;
+  }
+  return 0;
+}

@@ -73,3 +73,22 @@ def test_nls_scalar_c_matches_oracle():
                     dj = np.abs((dj + np.pi) % (2 * np.pi) - np.pi)
                 assert dj.max() <= 1e-9, (j, dj.max())
             assert np.abs(out[:, 4] - ref[:, 4]).max() <= 1e-13
+
+
+@pytest.mark.parametrize("group", ["10", "5", "20", "30", "62", "edge10"])
+def test_lm_scalar_c_on_reference_lm_vectors(lm_npz, group):
+    """The C restatement's fit.fit (lm_scalar_fit) on the reference's own LM vectors
+    (tests/golden/lm_vectors.npz): the same gates as the GPU (conftest.check_lm_group)."""
+    from conftest import check_lm_group
+    so = os.path.join(ROOT, "oracle", "libnls_scalar.so")
+    if not os.path.exists(so):
+        pytest.skip("oracle C restatement not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(so)
+    P = ctypes.c_void_p
+    lib.lm_scalar_fit.argtypes = [P, ctypes.c_int64, ctypes.c_int, P, ctypes.c_int, P]
+    qi = np.ascontiguousarray(lm_npz[f"g{group}_qi"])
+    g = np.ascontiguousarray(lm_npz[f"g{group}_guess"])
+    n, nd = qi.shape[0], qi.shape[1] // 2
+    out = np.zeros((n, 6))
+    assert lib.lm_scalar_fit(qi.ctypes.data, n, nd, g.ctypes.data, 4, out.ctypes.data) == 0
+    check_lm_group(lm_npz, group, out[:, 5].astype(int), out[:, :4], out[:, 4])

@@ -114,6 +114,59 @@ def nls_records(records, f_samp, f_mod, R, nbuf, ndata=10, init_guess=(1.6, 6.0,
     return out, ok
 
 
+def nls_record_devices(x, f_samp, f_mod, R, nbuf, devices, ndata=10, init_guess=(1.6, 6.0, 0.0, 0.0)):
+    """One record's _fit_parallel with chunk size 1 (fitters.py:395-428: buffer 0 fitted from
+    init_guess, every other buffer seeded with its result) spread over several GPUs of this
+    process: buffers 1..nbuf-1 are cut into len(devices) contiguous shards (np.array_split),
+    shard s is fitted on devices[s] as its own record with buffer 0 prepended — every device
+    fits the seed buffer itself, as every reference Pool chunk receives it (no exchange) —
+    and the rows come back in record order. All devices' work is enqueued before any result
+    is read, so the GPUs run concurrently; each shard's samples go host -> device (or
+    device -> device) once. x: 1-D float64 numpy array or CUDA tensor (>= nbuf*R samples).
+    Returns (cols (6, nbuf) numpy in the order amp, m, phi, psi, dc, ssq; fitok (nbuf,)),
+    bit-identical to one nls_records call (segments are independent once the seed is known).
+    Same-device entries are allowed (shards then run one after another on that GPU)."""
+    import torch
+    devs = [torch.device("cuda", int(d)) if not isinstance(d, torch.device) else d for d in devices]
+    if not devs:
+        raise ValueError("devices: at least one GPU")
+    if nbuf < 1:
+        raise ValueError("nbuf must be >= 1")
+    parts = [c for c in np.array_split(np.arange(1, nbuf), len(devs)) if c.size] if nbuf > 1 else []
+    if not parts:
+        parts = [np.arange(1, 1)]
+    host = not _is_device_tensor(x)
+    if host:
+        x = np.asarray(x, dtype=np.float64)
+    pending = []
+    for dev, idx in zip(devs, parts):
+        b0, b1 = (int(idx[0]), int(idx[-1]) + 1) if idx.size else (1, 1)
+        n_s = 1 + (b1 - b0)
+        with torch.cuda.device(dev):
+            xs = torch.empty(n_s * R, dtype=torch.float64, device=dev)
+            if host:
+                xs[:R].copy_(torch.from_numpy(x[:R]))
+                if b1 > b0:
+                    xs[R:].copy_(torch.from_numpy(x[b0 * R:b1 * R]))
+            else:
+                xs[:R].copy_(x[:R])
+                if b1 > b0:
+                    xs[R:].copy_(x[b0 * R:b1 * R])
+            cols, ok = nls_records(xs.view(1, -1), f_samp, f_mod, R, n_s, ndata, init_guess, parallel=True)
+        pending.append((cols, ok, b1 > b0))
+    out_cols, out_ok = [], []
+    for k, (cols, ok, has_rows) in enumerate(pending):
+        c = cols.cpu().numpy()
+        o = ok.cpu().numpy()
+        if k == 0:
+            out_cols.append(c)
+            out_ok.append(o)
+        elif has_rows:
+            out_cols.append(c[:, 1:])
+            out_ok.append(o[1:])
+    return np.concatenate(out_cols, axis=1), np.concatenate(out_ok)
+
+
 def frame_from(cols, fitok):
     """DataFrame with the reference's column set and dtypes (fitters.py:55-58, 428)."""
     if hasattr(cols, "cpu"):
@@ -141,7 +194,8 @@ class StandardNLSFitter(BaseFitter):
     """Frequency-domain NLS, one GPU call per record (fitters.py:322-447).
 
     kwargs: ndata (10), parallel (True), init_a (1.6), init_m (6.0), init_psi (0.0),
-    n_cores (None).  parallel=True follows _fit_parallel: buffer 0 is fitted from
+    n_cores (None), devices (None: the current GPU; a list of GPU indices spreads a
+    parallel=True, n_cores=None fit over those GPUs, nls_record_devices).  parallel=True follows _fit_parallel: buffer 0 is fitted from
     the default seed and seeds the rest; with n_cores=None every remaining buffer
     is its own chunk (the GPU-natural split; the reference's own chunk choice
     changes results by <= 2.5e-10), with n_cores=k the buffers are
@@ -165,6 +219,11 @@ class StandardNLSFitter(BaseFitter):
             raise ValueError(f"cannot reshape array of size {N} into shape ({R})")
         if not _is_device_tensor(x):
             x = np.asarray(x, dtype=np.float64)
+        devices = kwargs.get("devices")
+        if devices is not None and parallel and kwargs.get("n_cores") is None:
+            cols, ok = nls_record_devices(x, main_raw.f_samp, main_raw.f_mod, R, nbuf, devices, ndata,
+                                          (init_a, init_m, 0.0, init_psi))
+            return frame_from(cols, ok)
         cols, ok = nls_records(x.reshape(1, N), main_raw.f_samp, main_raw.f_mod, R, nbuf, ndata,
                                (init_a, init_m, 0.0, init_psi), parallel=parallel,
                                n_cores=kwargs.get("n_cores") if parallel else None)

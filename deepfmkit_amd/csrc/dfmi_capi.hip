@@ -52,6 +52,7 @@ struct Tuning {
   int ekf_row = 1;       // EKF: ekf_row_kernel (4 channels per wave) up to ekf_row x 4 x 4 x CUs channels
                          // (past one wave per SIMD the issue-bound rows share a SIMD, and one lane per
                          // channel carries 16x the channels per instruction); 0 = ekf_kernel only
+  int ekf_rot = 1;       // EKF row kernel: sincos by rotation between anchors (ekf_rot_kernel) where R % 4 == 0
   int wdfmi_accel = 3;   // W-DFMI: bit 0 time axis without division, bit 1 template slopes in LDS
   int lm_ladder = 32;    // LM launches of at most lm_ladder x CUs chains / segments (latency-bound: warm-start
                          // chains, small batches) run the parallel lambda ladder (lm.h lm_ladder_kernel);
@@ -835,6 +836,7 @@ const std::map<std::string, Knob>& knobs() {
       {"lm_general", {&Tuning::lm_general, {0, 1}}},
       {"demod_spw", {&Tuning::demod_spw, {}}},
       {"ekf_row", {&Tuning::ekf_row, {}}},
+      {"ekf_rot", {&Tuning::ekf_rot, {0, 1}}},
       {"wdfmi_accel", {&Tuning::wdfmi_accel, {0, 1, 2, 3}}},
       {"lm_ladder", {&Tuning::lm_ladder, {}}}};
   return k;
@@ -938,10 +940,13 @@ int ekf_impl(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
     hipLaunchKernelGGL(dfmi::ekf_phase_kernel, dim3((unsigned)((n_samp + 255) / 256)), dim3(256), 0, st,
                        (double*)wtw, n_samp, w_m, f_samp);
   const int64_t grid = row ? (nrec + 3) / 4 : (nrec + block - 1) / block;
-  hipLaunchKernelGGL(row ? dfmi::ekf_row_kernel<DFMI_EKF_SPLIT != 0> : dfmi::ekf_kernel,
+  // rotation between anchors: groups of 8 (or 4) samples whose ends carry the snapshots
+  const bool rot = row && t_tune.ekf_rot && R % 4 == 0;
+  hipLaunchKernelGGL(rot ? (R % 8 == 0 ? dfmi::ekf_rot_kernel<8> : dfmi::ekf_rot_kernel<4>)
+                     : row ? dfmi::ekf_row_kernel<DFMI_EKF_SPLIT != 0> : dfmi::ekf_kernel,
                      dim3((unsigned)grid), dim3(block), 0, st, dx, nrec, rs, n_samp, dx0, dp0, dq, dr,
                      (const double*)wtw, (int)R, nbuf, dstates, dfmi_trig_k());
-  g_last_demod = row ? "ekf_row_kernel" : "ekf_kernel";  // also reports the EKF variant
+  g_last_demod = rot ? "ekf_rot_kernel" : row ? "ekf_row_kernel" : "ekf_kernel";  // also reports the EKF variant
   HIPCHK(hipGetLastError());
   if (host) {
     if (sb) HIPCHK(hipMemcpyAsync(states, dstates, sb, hipMemcpyDeviceToHost, st));

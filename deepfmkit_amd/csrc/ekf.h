@@ -349,4 +349,218 @@ __global__ __launch_bounds__(64) void ekf_row_kernel(const double* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Row kernel with sincos by ROTATION (round 3, the default for few channels when R % 4 == 0).
+// Both sincos arguments move little from one sample to the next: theta_k - theta_{k-1} is
+// w_m / f_samp plus the change of psi (0.031 rad at config 5), phi + m cos(theta) moves by
+// at most ~m w_m / f_samp. The row evaluates the full Cody-Waite sincos (ekf_sincos_row) on
+// the first sample of every group of G = 8 (4 when R % 8 != 0), the anchor, and on the
+// others rotates the previous sample's (sin, cos) by d = x_k - x_{k-1}:
+//   sin x_k = sin x_{k-1} cos d + cos x_{k-1} sin d,  cos x_k = cos x_{k-1} cos d - sin x_{k-1} sin d,
+// with sin d / cos d from the same kernel coefficients (|d| < 0.78: no reduction, no quadrant).
+// The argument is the reference's: x_k is formed exactly as before (fl(w_m t_k + psi),
+// fl(phi + m cos theta)) and d is the difference of two such doubles (exact when they lie
+// within a factor 2 of each other, else off by half an ulp of d), so sin / cos are of the
+// same rounded argument; only the rotation's rounding (~1 ulp per step, reset at every
+// anchor) differs from the anchor form. Per sincos this replaces the reduction, the
+// quadrant selects and the library-range test (~38 instructions with the lane split) by
+// ~17 (d, the one-polynomial pair, 2 DPP moves, 4 for the rotation): ~89 instead of ~123
+// wave instructions per sample at G = 8; config 5 3.74 -> 5.62 M samples/s per channel
+// (profiles/r03s_ekf_rot_ab.jsonl).
+// A group in which any |d| reaches 0.78 (fast modulation, a diverging state) is rolled
+// back and re-run with the anchor form on every sample (per row: a channel's result never
+// depends on another channel's data). Snapshots fall on group ends (R % G == 0, checked by
+// the host), so the per-sample snapshot countdown is per group here.
+// ---------------------------------------------------------------------------
+
+// sin d / cos d for |d| < 0.78 on a row with dfmi_sincos_k's kernel coefficients, written as
+// one degree-7 polynomial in z = d^2 per lane: even lanes sin d = d (1 + z P_s(z)), odd lanes
+// cos d = 1 + z (-1/2 + z P_c(z)), i.e. v = mult * Poly(z) with mult = d on even lanes and 1
+// on odd ones (mult = fma(e, d, 1 - e), exact); read back by DPP into the tied registers
+// sn / cs. 12 instructions for the pair (no reduction, no quadrant, no selects).
+struct RotCoef {
+  double c[8];   // z^7 .. z^0
+  double e, e1;  // 1, 0 on even lanes; 0, 1 on odd lanes
+};
+__device__ __forceinline__ RotCoef rot_coef(const DfmiTrigK& k, int par) {
+  RotCoef rc;
+  if (par) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) rc.c[i] = k.c[10 + i];
+    rc.c[6] = -0.5;
+  } else {
+    rc.c[0] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) rc.c[1 + i] = k.c[4 + i];
+  }
+  rc.c[7] = 1.0;
+  rc.e = par ? 0.0 : 1.0;
+  rc.e1 = par ? 1.0 : 0.0;
+  return rc;
+}
+__device__ __forceinline__ void ekf_sincos_row_small(double d, const RotCoef& rc, double& sn, double& cs) {
+  const double z = d * d;
+  double p = fma(z, rc.c[0], rc.c[1]);
+#pragma unroll
+  for (int i = 2; i < 8; ++i) p = fma(z, p, rc.c[i]);
+  const double v = fma(rc.e, d, rc.e1) * p;
+  sn = row_bcast64<0>(sn, v);
+  cs = row_bcast64<1>(cs, v);
+}
+
+struct RotRegs {
+  double HP[5];
+  double sth, cth, sa, ca;  // sincos of the previous sample's theta / phase argument (the rotation bases)
+  double thp, argp;         // the previous sample's theta / phase argument
+  double sd, cd;            // DPP destinations of sin d / cos d
+};
+
+// One sample. ROT = false: anchor (full sincos); true: rotation of the bases by d, |d| folded
+// into dmax.
+template <bool ROT>
+__device__ __forceinline__ void ekf_rot_step(double (&st)[5], double (&Pc)[5], const double (&qv)[5], double Rv,
+                                             double xk, double wt, const DfmiTrigK& tk, RotRegs& rr,
+                                             const RowSplitCoef& rc, const RotCoef& ro, bool odd, double& dmax) {
+#pragma unroll
+  for (int i = 0; i < 5; ++i) Pc[i] = Pc[i] + qv[i];
+  const double a = st[0], m = st[1], phi = st[2], psi = st[3], dc = st[4];
+  const double th = wt + psi;
+  if constexpr (ROT) {
+    const double d = th - rr.thp;
+    dmax = fmax(dmax, fabs(d));
+    ekf_sincos_row_small(d, ro, rr.sd, rr.cd);
+    const double s = fma(rr.sth, rr.cd, rr.cth * rr.sd);
+    const double c = fma(rr.cth, rr.cd, -(rr.sth * rr.sd));
+    rr.sth = s;
+    rr.cth = c;
+  } else {
+    ekf_sincos_row(th, tk, rc, odd, rr.sth, rr.cth);
+  }
+  rr.thp = th;
+  const double sth = rr.sth, cth = rr.cth;
+  const double arg = fma(m, cth, phi);
+  const double acth = -a * cth, amsth = (a * m) * sth;
+  if constexpr (ROT) {
+    const double d = arg - rr.argp;
+    dmax = fmax(dmax, fabs(d));
+    ekf_sincos_row_small(d, ro, rr.sd, rr.cd);
+    const double s = fma(rr.sa, rr.cd, rr.ca * rr.sd);
+    const double c = fma(rr.ca, rr.cd, -(rr.sa * rr.sd));
+    rr.sa = s;
+    rr.ca = c;
+  } else {
+    ekf_sincos_row(arg, tk, rc, odd, rr.sa, rr.ca);
+  }
+  rr.argp = arg;
+  const double sa = rr.sa, ca = rr.ca;
+  const double h = fma(a, ca, dc);
+  const double H[5] = {ca, acth * sa, -a * sa, amsth * sa, 1.0};
+  const double y = xk - h;
+  const double hpj = fma(H[3], Pc[3], fma(H[2], Pc[2], fma(H[1], Pc[1], fma(H[0], Pc[0], Pc[4]))));
+  double (&HP)[5] = rr.HP;
+  HP[0] = row_bcast64<0>(HP[0], hpj);
+  HP[1] = row_bcast64<1>(HP[1], hpj);
+  HP[2] = row_bcast64<2>(HP[2], hpj);
+  HP[3] = row_bcast64<3>(HP[3], hpj);
+  HP[4] = row_bcast64<4>(HP[4], hpj);
+  const double S = fma(HP[3], H[3], fma(HP[2], H[2], fma(HP[1], H[1], fma(HP[0], H[0], HP[4] + Rv))));
+  double invS = __builtin_amdgcn_rcp(S);
+  invS = fma(invS, fma(-S, invS, 1.0), invS);
+  const double iy = invS * y;
+  const double cj = hpj * invS;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) st[i] = fma(HP[i], iy, st[i]);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) Pc[i] = fma(-HP[i], cj, Pc[i]);
+}
+
+// Same arguments, grid and outputs as ekf_row_kernel; R % G == 0 (host-checked).
+template <int G>
+__global__ __launch_bounds__(64) void ekf_rot_kernel(const double* __restrict__ x, int64_t nrec, int64_t rec_stride,
+                                                      int64_t n_samp, const double* __restrict__ x0,
+                                                      const double* __restrict__ p0, const double* __restrict__ qd,
+                                                      const double* __restrict__ rv, const double* __restrict__ wt,
+                                                      int R, int64_t nbuf, double* __restrict__ states,
+                                                      DfmiTrigK tk) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r0 = (int64_t)blockIdx.x * 4 + (lane >> 4);
+  const bool live = r0 < nrec;
+  const int64_t r = live ? r0 : nrec - 1;
+  int j = lane & 15;
+  if (j > 4) j = 4;
+  const double* __restrict__ xr = x + r * rec_stride;
+  double st[5], Pc[5], qv[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    st[i] = x0[r * 5 + i];
+    Pc[i] = (i == j) ? p0[i] : 0.0;
+    qv[i] = (i == j) ? qd[i] : 0.0;
+  }
+  const double Rv = rv[r];
+  const bool writer = live && (lane & 15) == 0;
+  const bool odd = lane & 1;
+  const RowSplitCoef rc = row_split_coef(tk, odd);
+  const RotCoef ro = rot_coef(tk, odd);
+  RotRegs rr;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) rr.HP[i] = 0.0;
+  rr.sth = rr.cth = rr.sa = rr.ca = rr.thp = rr.argp = rr.sd = rr.cd = 0.0;
+  double dmax = 0.0;
+  int64_t k = 0;
+  const int64_t ng = n_samp / G;
+  int64_t to_snap = R;
+  double xc[G], wc[G];
+  if (ng > 0) {
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      xc[u] = xr[u];
+      wc[u] = wt[u];
+    }
+  }
+  for (int64_t g = 0; g < ng; ++g, k += G) {
+    double xn[G], wn[G];
+    const int64_t kn = g + 1 < ng ? k + G : k;
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      xn[u] = xr[kn + u];
+      wn[u] = wt[kn + u];
+    }
+    double st0[5], Pc0[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      st0[i] = st[i];
+      Pc0[i] = Pc[i];
+    }
+    dmax = 0.0;
+    ekf_rot_step<false>(st, Pc, qv, Rv, xc[0], wc[0], tk, rr, rc, ro, odd, dmax);
+#pragma unroll
+    for (int u = 1; u < G; ++u) ekf_rot_step<true>(st, Pc, qv, Rv, xc[u], wc[u], tk, rr, rc, ro, odd, dmax);
+    if (__builtin_expect(dmax >= 0.78, 0)) {  // this row: redo the group with the anchor form throughout
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        st[i] = st0[i];
+        Pc[i] = Pc0[i];
+      }
+#pragma unroll
+      for (int u = 0; u < G; ++u) ekf_rot_step<false>(st, Pc, qv, Rv, xc[u], wc[u], tk, rr, rc, ro, odd, dmax);
+    }
+    to_snap -= G;
+    if (to_snap == 0) {
+      to_snap = R;
+      const int64_t b = (k + G) / R - 1;
+      if (b < nbuf && writer) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) states[(r * nbuf + b) * 5 + i] = st[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      xc[u] = xn[u];
+      wc[u] = wn[u];
+    }
+  }
+  // the last n_samp % G samples (no snapshot can fall here: R is a multiple of G)
+  for (; k < n_samp; ++k) ekf_rot_step<false>(st, Pc, qv, Rv, xr[k], wt[k], tk, rr, rc, ro, odd, dmax);
+}
+
 }  // namespace dfmi

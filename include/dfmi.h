@@ -266,8 +266,10 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
  * apply [default], 0 cycle-aligned fold), "lm_general" (1 = two-pass general LM path
  * for every ndata), "demod_spw" (segments per wave the bin grid is sized for; 0 =
  * persistent), "ekf_row" (EKF row kernel up to ekf_row x 16 x CUs channels, 0 = lane
- * kernel only), "wdfmi_accel" (bit 0: W-DFMI time axis without division, bit 1:
- * template slopes in LDS; both exact), "lm_ladder" (LM launches of at most lm_ladder x CUs
+ * kernel only), "ekf_rot" (1 [default]: the row kernel takes sin / cos by rotation between
+ * anchors of 8 (4) samples where R % 8 (4) == 0, ekf_rot_kernel; rounding only),
+ * "wdfmi_accel" (bit 0: W-DFMI time axis without division, bit 1: template slopes in
+ * LDS; both exact), "lm_ladder" (LM launches of at most lm_ladder x CUs
  * chains or segments run the parallel lambda ladder, 8 lanes per item: warm-start chains,
  * small batches; 0 = never; default 32; same bits), "probe" (1 = diagnostics timestamp
  * buffer on the current device, dfmi_probe_read). */
@@ -346,7 +348,7 @@ const char* dfmi_last_error(void);
 const char* dfmi_version(void);
 
 /* Kernel variant of the last demodulation (or EKF fit) this THREAD launched, e.g.
- * "demod_bins_kernel<2,8,rows,pf4>", "ekf_row_kernel" ("" before the first one).
+ * "demod_bins_kernel<2,8,rows,pf4>", "ekf_rot_kernel", "ekf_row_kernel" ("" before the first one).
  * Diagnostics/profiling. */
 const char* dfmi_last_demod_kernel(void);
 

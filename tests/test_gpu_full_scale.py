@@ -165,11 +165,12 @@ def test_config3_two_channels_vs_c_restatement():
         print(f"config 3 channel {c}: max |d amp, m, phi, psi| vs C =", worst, "; checked against the oracle:", nfar)
 
 
-@pytest.mark.parametrize("row", [1, 0])
-def test_ekf_config5_13_channels_full_length_vs_c_oracle(row):
+@pytest.mark.parametrize("row,rot,kname", [(1, 1, "ekf_rot_kernel"), (1, 0, "ekf_row_kernel"), (0, 1, "ekf_kernel")])
+def test_ekf_config5_13_channels_full_length_vs_c_oracle(row, rot, kname):
     """Config 5 at full length on 13 independent channels in ONE dfmi_ekf_fit launch (EKFFitter
-    per channel, fitters.py:214-320): 4 channels per wave in the row kernel, the 13th wave row
-    shadowed (13 = 3 x 4 + 1), 13 lanes in the lane kernel; every channel's 100 snapshots
+    per channel, fitters.py:214-320): 4 channels per wave in the row kernels (sincos by rotation
+    or in full), the 13th wave row shadowed (13 = 3 x 4 + 1), 13 lanes in the lane kernel;
+    every channel's 100 snapshots
     against the scalar C restatement of the loop (oracle/csrc/ekf_scalar.c) at 1e-12."""
     import deepfmkit_amd as dfm
     from deepfmkit_amd import _lib
@@ -200,11 +201,13 @@ def test_ekf_config5_13_channels_full_length_vs_c_oracle(row):
         raws.append(raw)
         refs.append(ref)
     _lib.check(lib.dfmi_set_tuning(b"ekf_row", row), "tune")
+    _lib.check(lib.dfmi_set_tuning(b"ekf_rot", rot), "tune")
     try:
         got = dfm.fitters.ekf_records(raws, 20)
-        assert lib.dfmi_last_demod_kernel().decode() == ("ekf_row_kernel" if row else "ekf_kernel")
+        assert lib.dfmi_last_demod_kernel().decode() == kname
     finally:
         _lib.check(lib.dfmi_set_tuning(b"ekf_row", 1), "tune")
+        _lib.check(lib.dfmi_set_tuning(b"ekf_rot", 1), "tune")
     for ch in range(13):
         err = np.abs(np.asarray(got[ch]) - refs[ch])
         assert err.max() <= 1e-12, (ch, err.max())

@@ -150,23 +150,64 @@ def test_ekf_matches_reference(manifest):
             assert err <= 1e-9, (lab, k, err)
 
 
-@pytest.mark.parametrize("row", [1, 0])
-def test_ekf_long_record_matches_oracle(row):
+# EKF kernels: (ekf_row, ekf_rot) tuning and the kernel dfmi_last_demod_kernel reports.
+# rot: 16-lane row per channel, sincos by rotation between anchors (default for few
+# channels, R % 4 == 0); row: the same row with the full sincos per sample; lane: one lane
+# per channel (many channels).
+EKF_KERNELS = {"rot": (1, 1, "ekf_rot_kernel"), "row": (1, 0, "ekf_row_kernel"), "lane": (0, 1, "ekf_kernel")}
+
+
+class _ekf_kernel:
+    def __init__(self, lib, name):
+        self.lib, self.row, self.rot, self.kname = lib, *EKF_KERNELS[name]
+
+    def __enter__(self):
+        from deepfmkit_amd import _lib
+        _lib.check(self.lib.dfmi_set_tuning(b"ekf_row", self.row), "tune")
+        _lib.check(self.lib.dfmi_set_tuning(b"ekf_rot", self.rot), "tune")
+        return self
+
+    def __exit__(self, *exc):
+        from deepfmkit_amd import _lib
+        _lib.check(self.lib.dfmi_set_tuning(b"ekf_row", 1), "tune")
+        _lib.check(self.lib.dfmi_set_tuning(b"ekf_rot", 1), "tune")
+
+
+def _c_ekf(x, init4, R, nbuf, f_samp=200000.0, f_mod=1000.0, qd=(1e-8, 1e-8, 1e-6, 1e-6, 1e-8)):
+    """The oracle's scalar C restatement of EKFFitter.fit (oracle/csrc/ekf_scalar.c, pinned to
+    the numpy oracle by tests/test_oracle_c.py) on one record; None when not built."""
+    import ctypes
+    import os
+    so = os.path.join(os.path.dirname(os.path.dirname(__file__)), "oracle", "libekf_scalar.so")
+    if not os.path.exists(so):
+        return None
+    cl = ctypes.CDLL(so)
+    P = ctypes.c_void_p
+    cl.ekf_scalar.argtypes = [P, ctypes.c_int64, P, P, P, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                              ctypes.c_int64, ctypes.c_int64, P]
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    x0 = np.array(list(init4) + [np.mean(x)])
+    p0, q = np.ones(5), np.ascontiguousarray(qd, dtype=np.float64)
+    ref = np.zeros((nbuf, 5))
+    cl.ekf_scalar(x.ctypes.data, x.size, x0.ctypes.data, p0.ctypes.data, q.ctypes.data, float(np.var(x)),
+                  2 * np.pi * f_mod, f_samp, R, nbuf, ref.ctypes.data)
+    return ref
+
+
+@pytest.mark.parametrize("kern", ["rot", "row", "lane"])
+def test_ekf_long_record_matches_oracle(kern):
     """Config 5 shape on a longer record than the golden one (0.1 s = 20,000 samples,
-    5 snapshots): both EKF kernels — one 16-lane row per channel (ekf_row_kernel, the
-    default for few channels) and one lane per channel (ekf_kernel, ekf_row = 0) —
-    track the restated reference loop to fp64 rounding (the reference itself moves by
-    ~1e-15 under 1-ulp input changes), and several channels in one launch give each
-    channel's answer bit for bit."""
+    5 snapshots): every EKF kernel — one 16-lane row per channel with sincos by rotation
+    (ekf_rot_kernel, the default for few channels) or in full per sample (ekf_row_kernel),
+    one lane per channel (ekf_kernel) — tracks the restated reference loop to fp64 rounding
+    (the reference itself moves by ~1e-15 under 1-ulp input changes), and several channels in
+    one launch give each channel's answer bit for bit."""
     import deepfmkit_amd as dfm
     from deepfmkit_amd import _lib
     from oracle import nls_oracle as O
     lib = _lib.load()
-    _lib.check(lib.dfmi_set_tuning(b"ekf_row", row), "tune")
-    try:
-        _ekf_long_record(dfm, O, lib, "ekf_row_kernel" if row else "ekf_kernel")
-    finally:
-        _lib.check(lib.dfmi_set_tuning(b"ekf_row", 1), "tune")
+    with _ekf_kernel(lib, kern) as k:
+        _ekf_long_record(dfm, O, lib, k.kname)
 
 
 def _ekf_long_record(dfm, O, lib, kname):
@@ -187,21 +228,16 @@ def _ekf_long_record(dfm, O, lib, kname):
         np.testing.assert_array_equal(many[k], got)
 
 
-@pytest.mark.parametrize("row", [1, 0])
-def test_ekf_config5_full_length_matches_c_oracle(row):
+@pytest.mark.parametrize("kern", ["rot", "row", "lane"])
+def test_ekf_config5_full_length_matches_c_oracle(kern):
     """Config 5 at the length BASELINE names (notebooks/2.0 defaults):
     a 2 s = 400,000-sample snr-mode record (m=6, 40 dB) through dfmi_ekf_fit (EKFFitter.fit,
-    fitters.py:214-320, pre-reductions on the device) with both EKF kernels, against the
+    fitters.py:214-320, pre-reductions on the device) with every EKF kernel, against the
     oracle's scalar C restatement of the loop (oracle/csrc/ekf_scalar.c, pinned to the
     numpy oracle by tests/test_oracle_c.py) on every one of the 100 snapshots."""
-    import ctypes
-    import os
     import deepfmkit_amd as dfm
     from deepfmkit_amd import _lib
     lib = _lib.load()
-    so = os.path.join(os.path.dirname(os.path.dirname(__file__)), "oracle", "libekf_scalar.so")
-    if not os.path.exists(so):
-        pytest.skip("oracle/libekf_scalar.so not built (make -C oracle)")
     laser, ifo = dfm.LaserConfig(), dfm.InterferometerConfig()
     dfm.set_laser_df_for_effect(laser, ifo, 6.0)
     dff = dfm.DeepFitFramework()
@@ -210,25 +246,100 @@ def test_ekf_config5_full_length_matches_c_oracle(row):
     raw = dff.raws["c5"]
     x = np.ascontiguousarray(raw.samples(), dtype=np.float64)
     assert x.size == 400_000
-    cl = ctypes.CDLL(so)
-    P = ctypes.c_void_p
-    cl.ekf_scalar.argtypes = [P, ctypes.c_int64, P, P, P, ctypes.c_double, ctypes.c_double, ctypes.c_double,
-                              ctypes.c_int64, ctypes.c_int64, P]
-    x0 = np.array([1.6, 6.0, 0.0, 0.0, np.mean(x)])
-    p0, qd = np.ones(5), np.array([1e-8, 1e-8, 1e-6, 1e-6, 1e-8])
-    ref = np.zeros((100, 5))
-    cl.ekf_scalar(x.ctypes.data, x.size, x0.ctypes.data, p0.ctypes.data, qd.ctypes.data, float(np.var(x)),
-                  2 * np.pi * 1000.0, 200000.0, 4000, 100, ref.ctypes.data)
-    _lib.check(lib.dfmi_set_tuning(b"ekf_row", row), "tune")
-    try:
+    ref = _c_ekf(x, [1.6, 6.0, 0.0, 0.0], 4000, 100)
+    if ref is None:
+        pytest.skip("oracle/libekf_scalar.so not built (make -C oracle)")
+    with _ekf_kernel(lib, kern) as k:
         got = dfm.fitters.ekf_records([raw], 20)[0]
-        assert lib.dfmi_last_demod_kernel().decode() == ("ekf_row_kernel" if row else "ekf_kernel")
-    finally:
-        _lib.check(lib.dfmi_set_tuning(b"ekf_row", 1), "tune")
+        assert lib.dfmi_last_demod_kernel().decode() == k.kname
     assert got.shape == (100, 5)
     err = np.abs(got - ref)
     assert err.max() <= 1e-12, (err.max(), np.unravel_index(err.argmax(), err.shape))
     assert abs(got[-1, 1] - 6.0) < 1e-2  # the filter tracks m
+
+
+def _ekf_raw(dfm, m, f_samp, f_mod, seconds, trial):
+    laser, ifo = dfm.LaserConfig(), dfm.InterferometerConfig()
+    laser.f_mod = f_mod
+    dfm.set_laser_df_for_effect(laser, ifo, m)
+    dff = dfm.DeepFitFramework()
+    dff.load_sim(dfm.DFMIObject("r", laser, ifo, f_samp=f_samp))
+    dff.simulate("r", n_seconds=seconds, mode="snr", snr_db=40.0, trial_num=trial)
+    return dff.raws["r"]
+
+
+@pytest.mark.parametrize("m,f_samp,f_mod", [(25.0, 32000.0, 400.0), (10.0, 32000.0, 400.0),
+                                            (6.0, 30000.0, 400.0)])
+def test_ekf_rotation_fallback_groups_match_c_oracle(m, f_samp, f_mod):
+    """ekf_rot_kernel where the phase argument moves by more than the rotation's 0.78 rad per
+    sample (m = 25 / 10 at 400 Hz, 32 kS/s: up to 1.96 / 0.79 rad): those groups are rolled
+    back and re-run with the full sincos, the rest rotate; R = 1600 (groups of 8) and, at
+    30 kS/s, R = 1500 (groups of 4). States within 1e-12 of the scalar C restatement on every
+    snapshot, init_m at the true m."""
+    import deepfmkit_amd as dfm
+    from deepfmkit_amd import _lib
+    lib = _lib.load()
+    raw = _ekf_raw(dfm, m, f_samp, f_mod, 1.0, 3)
+    x = np.ascontiguousarray(raw.samples(), dtype=np.float64)
+    R = int(round(f_samp / f_mod * 20))
+    nbuf = x.size // R
+    ref = _c_ekf(x, [1.6, m, 0.0, 0.0], R, nbuf, f_samp, f_mod)
+    if ref is None:
+        pytest.skip("oracle/libekf_scalar.so not built (make -C oracle)")
+    with _ekf_kernel(lib, "rot"):
+        got = dfm.fitters.ekf_records([raw], 20, init_m=m)[0]
+        assert lib.dfmi_last_demod_kernel().decode() == "ekf_rot_kernel"
+    err = np.abs(got - ref)
+    assert err.max() <= 1e-12, (err.max(), np.unravel_index(err.argmax(), err.shape))
+
+
+def test_ekf_rotation_channels_independent_and_ragged_tail():
+    """A channel's ekf_rot_kernel result never depends on the other channels of its wave:
+    channels that take the fallback (m = 25) and channels that rotate (m = 2) in one launch
+    equal their single-channel runs bit for bit; a record whose length is not a multiple of
+    the group (20,003 samples) fits its tail samples with the full sincos and matches the
+    numpy oracle within 1e-12; R % 4 != 0 selects ekf_row_kernel."""
+    import deepfmkit_amd as dfm
+    from deepfmkit_amd import _lib
+    from oracle import nls_oracle as O
+    lib = _lib.load()
+    ra = _ekf_raw(dfm, 25.0, 32000.0, 400.0, 0.5, 1)
+    rb = _ekf_raw(dfm, 2.0, 32000.0, 400.0, 0.5, 2)
+    with _ekf_kernel(lib, "rot"):
+        a = dfm.fitters.ekf_records([ra], 20, init_m=6.0)[0]
+        b = dfm.fitters.ekf_records([rb], 20, init_m=6.0)[0]
+        mix = dfm.fitters.ekf_records([ra, rb, rb, ra, rb], 20, init_m=6.0)
+        assert lib.dfmi_last_demod_kernel().decode() == "ekf_rot_kernel"
+        for k, want in enumerate((a, b, b, a, b)):
+            np.testing.assert_array_equal(mix[k], want)
+        # ragged tail: 20,003 samples, R = 4000
+        dff = dfm.DeepFitFramework()
+        laser, ifo = dfm.LaserConfig(), dfm.InterferometerConfig()
+        dfm.set_laser_df_for_effect(laser, ifo, 6.0)
+        dff.load_sim(dfm.DFMIObject("t", laser, ifo, f_samp=200000.0))
+        dff.simulate("t", n_seconds=0.1, mode="snr", snr_db=40.0, trial_num=4)
+        raw = dff.raws["t"]
+        x = np.asarray(raw.samples(), dtype=np.float64)
+        x = np.concatenate([x, x[:3]])
+        got = _ekf_host(lib, x, 200000.0, 1000.0, 4000, 5)
+        assert lib.dfmi_last_demod_kernel().decode() == "ekf_rot_kernel"
+        ref = O.ekf_record(x, 200000.0, 1000.0, 20)
+        assert np.max(np.abs(got - ref)) <= 1e-12
+        # an odd R (1501 samples per snapshot): no group can end on the snapshots -> ekf_row_kernel
+        _ekf_host(lib, x[:6 * 1501], 30020.0, 400.0, 1501, 6)
+        assert lib.dfmi_last_demod_kernel().decode() == "ekf_row_kernel"
+
+
+def _ekf_host(lib, x, f_samp, f_mod, R, nbuf):
+    from deepfmkit_amd import _lib
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    init4 = np.array([1.6, 6.0, 0.0, 0.0])
+    p0, qd = np.ones(5), np.array([1e-8, 1e-8, 1e-6, 1e-6, 1e-8])
+    states = np.zeros((1, nbuf, 5))
+    _lib.check(lib.dfmi_ekf_fit(_lib.ptr(x), 1, x.size, x.size, _lib.ptr(init4), _lib.ptr(p0), _lib.ptr(qd), None,
+                                2 * np.pi * f_mod, f_samp, R, nbuf, _lib.ptr(states), _lib.DFMI_MEM_HOST, None),
+               "dfmi_ekf_fit")
+    return states[0]
 
 
 @pytest.mark.parametrize("n", [1, 7, 8, 127, 129, 4000, 8191, 8192, 8193, 30001, 400000])

@@ -940,9 +940,11 @@ int ekf_impl(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
     hipLaunchKernelGGL(dfmi::ekf_phase_kernel, dim3((unsigned)((n_samp + 255) / 256)), dim3(256), 0, st,
                        (double*)wtw, n_samp, w_m, f_samp);
   const int64_t grid = row ? (nrec + 3) / 4 : (nrec + block - 1) / block;
-  // rotation between anchors: groups of 8 (or 4) samples whose ends carry the snapshots
+  // rotation between anchors: groups of 16 (8, 4) samples whose ends carry the snapshots
   const bool rot = row && t_tune.ekf_rot && R % 4 == 0;
-  hipLaunchKernelGGL(rot ? (R % 8 == 0 ? dfmi::ekf_rot_kernel<8> : dfmi::ekf_rot_kernel<4>)
+  hipLaunchKernelGGL(rot ? (R % DFMI_EKF_ROT_G == 0 ? dfmi::ekf_rot_kernel<DFMI_EKF_ROT_G>
+                            : R % 8 == 0              ? dfmi::ekf_rot_kernel<8>
+                                                      : dfmi::ekf_rot_kernel<4>)
                      : row ? dfmi::ekf_row_kernel<DFMI_EKF_SPLIT != 0> : dfmi::ekf_kernel,
                      dim3((unsigned)grid), dim3(block), 0, st, dx, nrec, rs, n_samp, dx0, dp0, dq, dr,
                      (const double*)wtw, (int)R, nbuf, dstates, dfmi_trig_k());

@@ -354,7 +354,8 @@ __global__ __launch_bounds__(64) void ekf_row_kernel(const double* __restrict__ 
 // Both sincos arguments move little from one sample to the next: theta_k - theta_{k-1} is
 // w_m / f_samp plus the change of psi (0.031 rad at config 5), phi + m cos(theta) moves by
 // at most ~m w_m / f_samp. The row evaluates the full Cody-Waite sincos (ekf_sincos_row) on
-// the first sample of every group of G = 8 (4 when R % 8 != 0), the anchor, and on the
+// the first sample of every group of G = 16 (8 or 4 when R is not a multiple of 16), the
+// anchor, and on the
 // others rotates the previous sample's (sin, cos) by d = x_k - x_{k-1}:
 //   sin x_k = sin x_{k-1} cos d + cos x_{k-1} sin d,  cos x_k = cos x_{k-1} cos d - sin x_{k-1} sin d,
 // with sin d / cos d from the same kernel coefficients (|d| < 0.78: no reduction, no quadrant).
@@ -364,9 +365,9 @@ __global__ __launch_bounds__(64) void ekf_row_kernel(const double* __restrict__ 
 // same rounded argument; only the rotation's rounding (~1 ulp per step, reset at every
 // anchor) differs from the anchor form. Per sincos this replaces the reduction, the
 // quadrant selects and the library-range test (~38 instructions with the lane split) by
-// ~17 (d, the one-polynomial pair, 2 DPP moves, 4 for the rotation): ~89 instead of ~123
-// wave instructions per sample at G = 8; config 5 3.74 -> 5.62 M samples/s per channel
-// (profiles/r03s_ekf_rot_ab.jsonl).
+// ~17 (d, the one-polynomial pair, 2 DPP moves, 4 for the rotation): ~89 (G = 8) / ~85
+// (G = 16) instead of ~123 wave instructions per sample; config 5 3.74 -> 5.62 (G = 8) ->
+// 5.83 M samples/s per channel (profiles/r03s_ekf_rot_ab.jsonl, r03s_ekf_rot_g_newton_ab.json).
 // A group in which any |d| reaches 0.78 (fast modulation, a diverging state) is rolled
 // back and re-run with the anchor form on every sample (per row: a channel's result never
 // depends on another channel's data). Snapshots fall on group ends (R % G == 0, checked by
@@ -407,6 +408,13 @@ __device__ __forceinline__ void ekf_sincos_row_small(double d, const RotCoef& rc
   sn = row_bcast64<0>(sn, v);
   cs = row_bcast64<1>(cs, v);
 }
+
+#ifndef DFMI_EKF_ROT_NEWTON
+#define DFMI_EKF_ROT_NEWTON 1  // 1/S: v_rcp_f64 + one Newton step (without: +6 % but 2.7e-12 from the C oracle, r03s)
+#endif
+#ifndef DFMI_EKF_ROT_G
+#define DFMI_EKF_ROT_G 16  // samples per anchor where R % G == 0 (8 measured 4 % slower, r03s; A/B builds)
+#endif
 
 struct RotRegs {
   double HP[5];
@@ -465,7 +473,9 @@ __device__ __forceinline__ void ekf_rot_step(double (&st)[5], double (&Pc)[5], c
   HP[4] = row_bcast64<4>(HP[4], hpj);
   const double S = fma(HP[3], H[3], fma(HP[2], H[2], fma(HP[1], H[1], fma(HP[0], H[0], HP[4] + Rv))));
   double invS = __builtin_amdgcn_rcp(S);
+#if DFMI_EKF_ROT_NEWTON
   invS = fma(invS, fma(-S, invS, 1.0), invS);
+#endif
   const double iy = invS * y;
   const double cj = hpj * invS;
 #pragma unroll

@@ -267,7 +267,7 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
  * for every ndata), "demod_spw" (segments per wave the bin grid is sized for; 0 =
  * persistent), "ekf_row" (EKF row kernel up to ekf_row x 16 x CUs channels, 0 = lane
  * kernel only), "ekf_rot" (1 [default]: the row kernel takes sin / cos by rotation between
- * anchors of 8 (4) samples where R % 8 (4) == 0, ekf_rot_kernel; rounding only),
+ * anchors of 16 (8, 4) samples where R % 4 == 0, ekf_rot_kernel; rounding only),
  * "wdfmi_accel" (bit 0: W-DFMI time axis without division, bit 1: template slopes in
  * LDS; both exact), "lm_ladder" (LM launches of at most lm_ladder x CUs
  * chains or segments run the parallel lambda ladder, 8 lanes per item: warm-start chains,

@@ -269,13 +269,13 @@ def _ekf_raw(dfm, m, f_samp, f_mod, seconds, trial):
 
 
 @pytest.mark.parametrize("m,f_samp,f_mod", [(25.0, 32000.0, 400.0), (10.0, 32000.0, 400.0),
-                                            (6.0, 30000.0, 400.0)])
+                                            (10.0, 32160.0, 400.0), (6.0, 30000.0, 400.0)])
 def test_ekf_rotation_fallback_groups_match_c_oracle(m, f_samp, f_mod):
     """ekf_rot_kernel where the phase argument moves by more than the rotation's 0.78 rad per
     sample (m = 25 / 10 at 400 Hz, 32 kS/s: up to 1.96 / 0.79 rad): those groups are rolled
-    back and re-run with the full sincos, the rest rotate; R = 1600 (groups of 8) and, at
-    30 kS/s, R = 1500 (groups of 4). States within 1e-12 of the scalar C restatement on every
-    snapshot, init_m at the true m."""
+    back and re-run with the full sincos, the rest rotate; R = 1600 (groups of 16), 1608 (of 8)
+    and 1500 (of 4). States within 1e-12 of the scalar C restatement on every snapshot, init_m
+    at the true m."""
     import deepfmkit_amd as dfm
     from deepfmkit_amd import _lib
     lib = _lib.load()

@@ -126,22 +126,9 @@ __device__ __forceinline__ void store_block(const double (&v)[2 * HB], int lane,
   }
 }
 
-// Row stores: non-temporal (ROWS 1); ROWS 2 (rows read by another workgroup of the same
-// launch, the fused LM of seed.h): also device-coherent (sc1: written through this XCD's
-// L2, so a wave on another XCD reads them after its acquire), still non-temporal.
-#ifndef DFMI_LMF_ROWS_PLAIN
-#define DFMI_LMF_ROWS_PLAIN 0  // A/B timing builds only: ROWS 2 stored like ROWS 1 (not device-coherent)
-#endif
-template <int ROWS>
-__device__ __forceinline__ void row_store(double* p, double v) {
-  if constexpr (ROWS == 2 && !DFMI_LMF_ROWS_PLAIN)
-    asm volatile("global_store_dwordx2 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
-  else __builtin_nontemporal_store(v, p);
-}
-
 // dc part of fold_finish: the lane's partial sum of its bins (returned), and dc itself
 // (wave sum / R) unless the row layout carries it in a spare Q slot.
-template <int VEC, int MAXSLOT, int HB, int ROWS>
+template <int VEC, int MAXSLOT, int HB, bool ROWS>
 __device__ __forceinline__ double finish_dc(const double (&y)[MAXSLOT][VEC], int R, int ndata, int lane,
                                             double* __restrict__ qi, int64_t qi_ld, int64_t col,
                                             double* __restrict__ dc) {
@@ -155,7 +142,7 @@ __device__ __forceinline__ double finish_dc(const double (&y)[MAXSLOT][VEC], int
   if (!ROWS || spare == 0) {
     const double all = wave_sum(tot);
     if (lane == 0) {
-      if constexpr (ROWS) row_store<ROWS>(qi + col * qi_ld + dfmi_row_dc(ndata), all / (double)R);
+      if constexpr (ROWS) __builtin_nontemporal_store(all / (double)R, qi + col * qi_ld + dfmi_row_dc(ndata));
       else dc[col] = all / (double)R;
     }
   }
@@ -164,7 +151,7 @@ __device__ __forceinline__ double finish_dc(const double (&y)[MAXSLOT][VEC], int
 
 // Harmonic block hb of fold_finish: HB harmonics contracted with the basis, reduced by
 // the butterfly and stored (tot: finish_dc's partial sum, for the rows' dc slot).
-template <int VEC, int MAXSLOT, int HB, int ROWS>
+template <int VEC, int MAXSLOT, int HB, bool ROWS>
 __device__ __forceinline__ void finish_block(const double (&y)[MAXSLOT][VEC], const bool (&pval)[MAXSLOT],
                                              const int (&pbase)[MAXSLOT], double tot, int hb, int R, int L,
                                              int ndata, const double* __restrict__ T, int lane,
@@ -203,7 +190,7 @@ __device__ __forceinline__ void finish_block(const double (&y)[MAXSLOT][VEC], co
   if constexpr (ROWS) {
     // one 128-B line, non-temporal: plain row stores cost the bin kernel 3.5 % (0.520 vs
     // 0.502 ms per 100k segments, profiles/r02l_ab_store.log)
-    if ((lane & 3) == 0) row_store<ROWS>(qi + col * qi_ld + hb * 16 + (lane >> 2), acc[0] / (double)R);
+    if ((lane & 3) == 0) __builtin_nontemporal_store(acc[0] / (double)R, qi + col * qi_ld + hb * 16 + (lane >> 2));
   } else {
     store_block<HB>(acc, lane, hb, ndata, qi, qi_ld, col, R);
   }
@@ -219,7 +206,7 @@ __device__ __forceinline__ void finish_block(const double (&y)[MAXSLOT][VEC], co
 // tree is wave_sum's, so dc is bit-identical to the ROWS = false value. (Scattered
 // 8-B stores into 21 component rows cost 13 % of the demodulation time:
 // profiles/r01_tune_demod_probe.json.)
-template <int VEC, int MAXSLOT, int HB = kHarmBlock, int ROWS = false>
+template <int VEC, int MAXSLOT, int HB = kHarmBlock, bool ROWS = false>
 __device__ __forceinline__ void fold_finish(const double (&y)[MAXSLOT][VEC], const bool (&pval)[MAXSLOT],
                                             const int (&pbase)[MAXSLOT], int R, int L, int ndata,
                                             const double* __restrict__ T, int lane, double* __restrict__ qi,
@@ -374,7 +361,7 @@ __global__ __launch_bounds__(kBlockThreads) void demod_fold_kernel(
 // the next segment's first PFN chunks (at `next`, if not null) are issued into pf
 // before this segment's contraction, so the wave has loads in flight while it
 // contracts.
-template <int MAXSLOT, int LOADS, bool NT, int HB, int ROWS, int PFN = 0>
+template <int MAXSLOT, int LOADS, bool NT, int HB, bool ROWS, int PFN = 0>
 __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int R, int L, int ndata,
                                              const double* __restrict__ T, double* __restrict__ ybin, int lane,
                                              const bool (&pval)[MAXSLOT], const int (&pbase)[MAXSLOT],
@@ -486,21 +473,18 @@ __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int
 // probe (diagnostics, may be null): s_memrealtime at the entry of workgroups 0 and
 // gridDim-1 and at the exit of workgroup 0's wave 0 ([3], [4], [5]).
 constexpr int kProbeWaves = 16384;  // per-wave slots of the diagnostics probe buffer
-template <int MAXSLOT, int LOADS, int ROWS, int PFN = 0>
+template <int MAXSLOT, int LOADS, bool ROWS, int PFN = 0>
 __device__ __forceinline__ void bins_kernel_body(
     const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
     const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc,
-    uint64_t* __restrict__ probe, int block0 = 0, int nwork_in = 0, uint32_t* __restrict__ tiles = nullptr) {
-  // block0: leading workgroups that play another role (the fused seed kernel, seed.h);
-  // nwork_in > 0: the demodulation's workgroups (others follow it: the fused LM);
-  // tiles (ROWS 2): per 64-segment tile, the count of its rows written (published when the
-  // wave leaves: one wait, no stall inside the stream)
+    uint64_t* __restrict__ probe, int block0 = 0) {
+  // block0: leading workgroups that play another role (the fused seed kernel, seed.h)
   const int bid = (int)blockIdx.x - block0;
   if (probe && threadIdx.x == 0) {
     if (bid == 0) probe[3] = __builtin_amdgcn_s_memrealtime();
     if ((int)blockIdx.x == (int)gridDim.x - 1) probe[4] = __builtin_amdgcn_s_memrealtime();
   }
-  const int nwork = nwork_in > 0 ? nwork_in : (int)gridDim.x - block0;
+  const int nwork = (int)gridDim.x - block0;
   if (bid < 0) return;
   extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
   const int ntab = 2 * ndata * L;
@@ -535,14 +519,6 @@ __device__ __forceinline__ void bins_kernel_body(
       bins_segment<MAXSLOT, LOADS, true, kHarmBlock, ROWS>(x + s * seg_stride, R, L, ndata, lds_dyn, ybin, lane, pval,
                                                            pbase, qi, qi_ld, s, dc);
   }
-  if constexpr (ROWS == 2) {
-    if (tiles) {
-      __builtin_amdgcn_s_waitcnt(0);  // this wave's row stores acknowledged at device scope
-      if (lane == 0)
-        for (int64_t s = s0; s < nseg; s += ds)
-          __hip_atomic_fetch_add(tiles + (s >> 6), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
   if (probe && threadIdx.x == 0 && bid == 0) probe[5] = __builtin_amdgcn_s_memrealtime();
   // per-wave exit times (probe[16 + global wave], up to kProbeWaves waves) and the
   // hardware XCC of the wave ([16 + kProbeWaves + wave])
@@ -557,7 +533,7 @@ __device__ __forceinline__ void bins_kernel_body(
   }
 }
 
-template <int MAXSLOT, int LOADS, int ROWS, int PFN = 0>
+template <int MAXSLOT, int LOADS, bool ROWS, int PFN = 0>
 __global__ __launch_bounds__(kBlockThreads) void demod_bins_kernel(
     const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
     const double* __restrict__ tab, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc,

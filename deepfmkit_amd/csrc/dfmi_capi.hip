@@ -54,12 +54,6 @@ struct Tuning {
                          // channel carries 16x the channels per instruction); 0 = ekf_kernel only
   int ekf_rot = 1;       // EKF row kernel: sincos by rotation between anchors (ekf_rot_kernel) where R % 4 == 0
   int wdfmi_accel = 3;   // W-DFMI: bit 0 time axis without division, bit 1 template slopes in LDS
-#ifndef DFMI_LM_FUSED_DEFAULT
-#define DFMI_LM_FUSED_DEFAULT 1
-#endif
-  int lm_fused = DFMI_LM_FUSED_DEFAULT;  // record pipeline (ndata 10, rows, large batches): the LM inside the seed + demodulation
-                         // launch (seed.h demod_seed_bins_lm_kernel), fitting tiles as the demodulation's tail
-                         // frees slots; 0 = the LM as its own kernel after it
   int lm_ladder = 32;    // LM launches of at most lm_ladder x CUs chains / segments (latency-bound: warm-start
                          // chains, small batches) run the parallel lambda ladder (lm.h lm_ladder_kernel);
                          // 0 = always one lane per chain / segment
@@ -224,7 +218,7 @@ int free_stream_ws(StreamWs& s) {
 // Grow-only scratch buffer `name` of the current caller stream. Workspaces of at most
 // kMaxStreamWs caller streams are kept: a call from a further stream first waits for the
 // device to drain and frees the least recently used stream's set.
-int workspace(int dev, const char* name, size_t bytes, void** out, DevBuf** buf = nullptr) {
+int workspace(int dev, const char* name, size_t bytes, void** out) {
   (void)dev;
   const uintptr_t key = t_call ? (uintptr_t)t_call->stream : 0;
   DeviceState& ds = *t_ds;
@@ -248,10 +242,8 @@ int workspace(int dev, const char* name, size_t bytes, void** out, DevBuf** buf 
     b.n = 0;
     HIPCHK(hipMalloc(&b.p, bytes));
     b.n = bytes;
-    b.aux = -1;  // fresh (callers that need zeroed memory clear it and reset aux)
   }
   *out = b.p;
-  if (buf) *buf = &b;
   return DFMI_OK;
 }
 
@@ -691,59 +683,6 @@ int fused_seed_demod(int dev, const double* x, int64_t nrec, int64_t nbuf, int R
   return DFMI_OK;
 }
 
-// Seed + demodulation + LM in ONE launch (seed.h demod_seed_bins_lm_kernel): ndata 10 (the
-// reference default, the register path's exact variant), one or two 128-sample bin slots,
-// batches past the ladder threshold. Returns 1 when it does not apply.
-int fused_seed_demod_lm(int dev, const double* x, int64_t nrec, int64_t nbuf, int R, int ndata, int L,
-                        const double* tab, double* rows, int64_t qs, const double* gdev, const dfmi::GuessInline& ginl,
-                        const double* jtab, const dfmi::LMConst& c, double* out, int64_t out_ld, int32_t* fitok,
-                        hipStream_t st) {
-  if (!t_tune.lm_fused || t_tune.lm_general || ndata != 10 || L <= 0 || (L + 127) / 128 > 2) return 1;
-  const int64_t nseg = nrec * nbuf;
-  if (t_tune.lm_ladder && nrec * (nbuf - 1) <= (int64_t)t_tune.lm_ladder * t_ds->n_cu) return 1;  // latency-bound
-  constexpr int kNd10 = dfmi::kExactNd | 10;
-  auto kern = dfmi::demod_seed_bins_lm_kernel<2, 12, DFMI_BINS_PFN, DFMI_BINS_LOADS, kNd10>;
-  size_t lds = ((size_t)2 * ndata * L + (size_t)dfmi::kWavesPerBlock * L) * sizeof(double) + DFMI_BINS_LDS_PAD;
-  const size_t lm_lds = (size_t)dfmi::kWavesPerBlock * (2 * ndata + 1) * 65 * sizeof(double);
-  if (lm_lds > lds) lds = lm_lds;
-  int per_cu = 0;
-  if (int orc = occupancy(kern, dfmi::kBlockThreads, lds, &per_cu)) return orc;
-  if (per_cu < 1) per_cu = 1;
-  const int64_t slots = (int64_t)t_ds->n_cu * per_cu;
-  if (nrec + 1 > slots / 2) return 1;
-  int64_t bulk = slots - nrec;
-  const int64_t need = (nseg + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock;
-  if (bulk > need) bulk = need;
-  if (t_tune.demod_spw > 0) {
-    const int64_t per = (int64_t)dfmi::kWavesPerBlock * t_tune.demod_spw;
-    if ((nseg + per - 1) / per > bulk) bulk = (nseg + per - 1) / per;
-  }
-  const int64_t ntile = (nseg + 63) / 64;
-  const int64_t nlm = (ntile + dfmi::kWavesPerBlock - 1) / dfmi::kWavesPerBlock;
-  if (nrec + bulk + nlm > INT32_MAX) return 1;
-  void *tw, *sw;
-  DevBuf *tb, *sb;
-  int rc;
-  if ((rc = workspace(dev, "lm_tiles", (size_t)ntile * 4, &tw, &tb))) return rc;
-  if ((rc = workspace(dev, "lm_seedf", (size_t)nrec * 4, &sw, &sb))) return rc;
-  if (tb->aux < 0) {  // counters start at 0; every LM wave resets its tile's counter after use
-    HIPCHK(hipMemsetAsync(tb->p, 0, tb->n, st));
-    tb->aux = 0;
-  }
-  if (sb->aux < 0) {  // seed flags hold the epoch of the call that published them
-    HIPCHK(hipMemsetAsync(sb->p, 0, sb->n, st));
-    sb->aux = 0;
-  }
-  sb->aux = sb->aux >= 0xFFFFFFFFll ? 1 : sb->aux + 1;
-  const uint32_t epoch = (uint32_t)sb->aux;
-  hipLaunchKernelGGL(kern, dim3((unsigned)(nrec + bulk + nlm)), dim3(dfmi::kBlockThreads), lds, st, x, nseg,
-                     nbuf * (int64_t)R, nrec, R, L, ndata, tab, rows, qs, gdev, ginl, gdev ? 0 : 1, jtab, c, out,
-                     out_ld, nbuf, fitok, bulk, (uint32_t*)tw, (uint32_t*)sw, epoch);
-  HIPCHK(hipGetLastError());
-  g_last_demod = "demod_seed_bins_lm_kernel<2,12,pf4,rows,lm10>";
-  return DFMI_OK;
-}
-
 // Seed step of the unfused layouts (fitters.py:403-410): buffer 0 of every record
 // demodulated and fitted by one wave per record on the side stream, concurrently with
 // the bulk demodulation on the caller's stream; the LM waits on its event. The LDS bin
@@ -824,13 +763,6 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
     if ((rc = workspace(dev, "qrow", (size_t)qs * nseg * sizeof(double), &rw))) return rc;
     StepMarks sm;
     if ((rc = sm.begin(ds)) || (rc = sm.mark(0, st))) return rc;
-    rc = fused_seed_demod_lm(dev, x, nrec, nbuf, R, ndata, L, tab, (double*)rw, qs, gdev, ginl, jtab, c, out,
-                             out_ld, fitok, st);
-    if (rc < 0) return rc;
-    if (rc == 0) {  // the LM ran inside the same launch: no second kernel
-      if ((rc = sm.mark(1, st))) return rc;
-      return sm.mark(2, st);
-    }
     rc = fused_seed_demod(dev, x, nrec, nbuf, R, ndata, L, tab, (double*)rw, qs, gdev, ginl, jtab, c, out, out_ld,
                           fitok, st);
     if (rc < 0) return rc;
@@ -906,8 +838,7 @@ const std::map<std::string, Knob>& knobs() {
       {"ekf_row", {&Tuning::ekf_row, {}}},
       {"ekf_rot", {&Tuning::ekf_rot, {0, 1}}},
       {"wdfmi_accel", {&Tuning::wdfmi_accel, {0, 1, 2, 3}}},
-      {"lm_ladder", {&Tuning::lm_ladder, {}}},
-      {"lm_fused", {&Tuning::lm_fused, {0, 1}}}};
+      {"lm_ladder", {&Tuning::lm_ladder, {}}}};
   return k;
 }
 // np.mean / np.var of nrec device records on st (moments.hip), numpy-exact.

@@ -281,6 +281,9 @@ DFMI_HDI double hmask(int nd, int j) {
 template <int V, typename QF>
 DFMI_HDI double eval_reg_trial(const QF& q, int nd, const double (&p)[4], TrialReg<V>& t, const DfmiTrigK& k) {
   constexpr int NDMAX = nd_cap(V);
+  double Q[NDMAX], I[NDMAX];
+#pragma unroll
+  for (int j = 1; j <= NDMAX; ++j) qi_pair<V>(q, nd, j, Q[j - 1], I[j - 1]);
   dfmi_sincos_auto(p[2], k, &t.sph, &t.cph);
   dfmi_sincos_auto(p[3], k, &t.s1, &t.c1);
   bessel_regs<NDMAX + 2>(p[1], nd_exact(V) ? NDMAX + 1 : nd + 1, t.J);
@@ -290,13 +293,9 @@ DFMI_HDI double eval_reg_trial(const QF& q, int nd, const double (&p)[4], TrialR
   double cj = t.c1, sj = t.s1, cm = 1.0, sm = 0.0;  // (j psi), ((j-1) psi)
 #pragma unroll
   for (int j = 1; j <= NDMAX; ++j) {
-    // QI read per harmonic (not all up front: 2 NDMAX fewer live registers through the
-    // Bessel pass, which the fused LM's 168-register budget needs; same bits)
-    double Qv, Iv;
-    qi_pair<V>(q, nd, j, Qv, Iv);
     const double c = quarter_turn(j, ac, as) * t.J[j] * hmask<V>(nd, j);  // a cos(phi + j pi/2) J_j
-    const double rq = fma(-c, cj, Qv);
-    const double ri = fma(c, sj, Iv);
+    const double rq = fma(-c, cj, Q[j - 1]);
+    const double ri = fma(c, sj, I[j - 1]);
     double& acc = (j & 1) ? so : se;
     acc = fma(rq, rq, acc);
     acc = fma(ri, ri, acc);
@@ -306,7 +305,6 @@ DFMI_HDI double eval_reg_trial(const QF& q, int nd, const double (&p)[4], TrialR
     sm = sj;
     cj = cn;
     sj = sn;
-    DFMI_HARMONIC_FENCE();
   }
   t.ssq = so + se;
   return t.ssq;
@@ -317,6 +315,9 @@ DFMI_HDI double eval_reg_trial(const QF& q, int nd, const double (&p)[4], TrialR
 template <int V, typename QF>
 DFMI_HDI void eval_reg_accept(const QF& q, int nd, const double (&p)[4], const TrialReg<V>& t, Eval& e) {
   constexpr int NDMAX = nd_cap(V);
+  double Q[NDMAX], I[NDMAX];
+#pragma unroll
+  for (int j = 1; j <= NDMAX; ++j) qi_pair<V>(q, nd, j, Q[j - 1], I[j - 1]);
   const double a = p[0];
   const double ac = a * t.cph, as = a * t.sph;
   const double tc = 2.0 * t.c1;
@@ -334,10 +335,8 @@ DFMI_HDI void eval_reg_accept(const QF& q, int nd, const double (&p)[4], const T
     const double u0 = quarter_turn(j, cph0, sph0) * Jj;
     const double u1 = aP * (0.5 * (t.J[j - 1] - t.J[j + 1])) * hmask<V>(nd, j);
     const double u2 = aD * Jj;
-    double Qv, Iv;
-    qi_pair<V>(q, nd, j, Qv, Iv);
-    const double rq = fma(-c, cj, Qv);
-    const double ri = fma(c, sj, Iv);
+    const double rq = fma(-c, cj, Q[j - 1]);
+    const double ri = fma(c, sj, I[j - 1]);
     const double A = fma(cj, rq, -(sj * ri));
     const double B = fma(sj, rq, cj * ri);
     const double w = fma(cj, cj, sj * sj);
@@ -462,25 +461,6 @@ struct QRow {
   DFMI_HDI double qs(int h) const { return p[((h >> 3) * 16 + 8 + (h & 7)) * STRIDE]; }
   DFMI_HDI double at(int pos) const { return p[pos * STRIDE]; }
 };
-
-// QI of one segment staged compactly (the fused LM, seed.h): Q_1..Q_nd, I_1..I_nd, dc at
-// entries 0..2 nd, STRIDE apart (ND > 0: nd known at compile time).
-template <int STRIDE, int ND = 0>
-struct QRowC {
-  const double* __restrict__ p;
-  int nd_rt;
-  DFMI_HDI int nd() const { return ND > 0 ? ND : nd_rt; }
-  DFMI_HDI double qc(int h) const { return p[h * STRIDE]; }
-  DFMI_HDI double qs(int h) const { return p[(nd() + h) * STRIDE]; }
-  DFMI_HDI double dc() const { return p[2 * nd() * STRIDE]; }
-};
-// compact entry of row position pos (dfmi_row_stride layout), -1 for padding
-DFMI_HDI int row_compact(int pos, int ndata) {
-  const int b = pos >> 4, o = pos & 15;
-  const int h = 8 * b + (o & 7);
-  if (h < ndata) return o < 8 ? h : ndata + h;
-  return pos == dfmi_row_dc(ndata) ? 2 * ndata : -1;
-}
 
 // QI of one segment held in registers (N harmonics, read once from another accessor):
 // the register path's evaluations then index it with compile-time harmonics only.

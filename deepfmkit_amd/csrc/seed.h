@@ -252,219 +252,4 @@ __global__ __launch_bounds__(kBlockThreads) void demod_seed_bins_kernel(
   }
 }
 
-// ---------------------------------------------------------------------------
-// Seed + bulk demodulation + LM in ONE launch (round 3; dfmi_set_tuning("lm_fused")).
-// Workgroups [0, nrec): the seeds, as demod_seed_bins_kernel, then the seed's result is
-// published (seedf[r] = epoch, release at device scope). [nrec, nrec + nbulk): the bulk
-// demodulation, rows written device-coherent (row_store<2>) and counted per 64-segment
-// tile when the wave leaves. The rest: LM workgroups, one 64-segment tile per wave: the
-// wave waits (lane 0 polls, bounded) until its tile's rows are all written and its
-// records' seeds are published, acquires (device scope), stages the rows into LDS
-// compactly (QRowC) and fits one segment per lane exactly as lm_chunks_kernel does (same
-// register path, same bits). Workgroups are dispatched in index order on every XCD, so an
-// LM workgroup only takes a slot after all demodulation workgroups of its XCD were
-// dispatched: the LM fills the slots the demodulation's tail frees, no LM wave displaces a
-// demodulation wave, and every wait ends (the demodulation never waits on anything). The
-// kernel's register budget is the demodulation's (3 waves per SIMD = 168 VGPRs): the LM
-// path compiles into it with a few spilled values.
-// ---------------------------------------------------------------------------
-constexpr uint64_t kLmSpinTicks = 200000000;  // s_memrealtime (100 MHz): 2 s, then status -3
-#ifndef DFMI_LMF_SC1
-#define DFMI_LMF_SC1 1  // rows / seeds read by device-coherent loads (0: acquire fence = L2 invalidate + plain loads)
-#endif
-#ifndef DFMI_LMF_NOLM
-#define DFMI_LMF_NOLM 0  // A/B timing builds only: LM workgroups leave at once (results not fitted)
-#endif
-
-// 8 bytes at p, device-coherent (sc1: not served from this XCD's possibly stale L2)
-__device__ __forceinline__ double load_dev(const double* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int V>
-__device__ __forceinline__ void lm_fused_tile(int64_t tile, int64_t nseg, int64_t nbuf, const double* __restrict__ rows,
-                                              int64_t qs, int ndata, const double* __restrict__ jtab,
-                                              const LMConst& c, double* __restrict__ out, int64_t out_ld,
-                                              int32_t* __restrict__ status, uint32_t* __restrict__ tiles,
-                                              const uint32_t* __restrict__ seedf, uint32_t epoch,
-                                              double* __restrict__ lq) {
-  const int lane = threadIdx.x & 63;
-  const int64_t sb = tile * 64;
-  if (sb >= nseg || DFMI_LMF_NOLM) return;
-  const int nv = (int)(nseg - sb < 64 ? nseg - sb : 64);
-  int ok = 1;
-  if (lane == 0) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(tiles + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)nv) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kLmSpinTicks) {
-        ok = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(8);
-    }
-    __hip_atomic_store(tiles + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next call counts from 0
-  }
-  ok = __shfl(ok, 0);
-  const int64_t s = sb + lane;
-  const bool valid = lane < nv;
-  const int64_t r = valid ? s / nbuf : 0;
-  const bool fit = valid && s != r * nbuf;  // buffer 0 of a record is its seed
-  if (fit) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(seedf + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kLmSpinTicks) {
-        ok = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(8);
-    }
-  }
-#if DFMI_LMF_SC1
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // keeps the loads below after the waits
-#else
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // rows and seeds written on other XCDs
-#endif
-  {
-    // the tile's rows (contiguous) -> LDS, compact [entry][65], 16 loads in flight
-    const double* __restrict__ base = rows + sb * qs;
-    const int QS = (int)qs;
-    const int tot = nv * QS;
-    typedef double d2v __attribute__((ext_vector_type(2)));
-    constexpr int kLoads = 16;
-    for (int e0 = 2 * lane; e0 < tot; e0 += 128 * kLoads) {
-      d2v v[kLoads];
-#pragma unroll
-      for (int u = 0; u < kLoads; ++u) {
-        const int e = e0 + 128 * u;
-#if DFMI_LMF_SC1
-        v[u] = e < tot ? d2v{load_dev(base + e), load_dev(base + e + 1)} : d2v{0.0, 0.0};
-#else
-        v[u] = e < tot ? *reinterpret_cast<const d2v*>(base + e) : d2v{0.0, 0.0};
-#endif
-      }
-#pragma unroll
-      for (int u = 0; u < kLoads; ++u) {
-        const int e = e0 + 128 * u;
-        if (e < tot) {
-          const int row = e / QS, pos = e - row * QS;
-          const int c0 = row_compact(pos, ndata), c1 = row_compact(pos + 1, ndata);
-          if (c0 >= 0) lq[c0 * 65 + row] = v[u].x;
-          if (c1 >= 0) lq[c1 * 65 + row] = v[u].y;
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-  if (!fit) return;
-  if (!ok) {
-    status[s] = -3;  // a wait timed out (cannot happen with in-order dispatch; never silent)
-    return;
-  }
-  double p[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) p[i] = load_dev(out + i * out_ld + r * nbuf);  // the record's seed (fitters.py:403-410)
-  constexpr int ND = nd_exact(V) ? nd_cap(V) : 0;
-  const QRowC<65, ND> q{lq + lane, ndata};
-  double ssq;
-  const int st = fit_segment_q<V, QRowC<65, ND>>(q, ndata, jtab, c, p, ssq);
-  out[0 * out_ld + s] = p[0];
-  out[1 * out_ld + s] = p[1];
-  out[2 * out_ld + s] = p[2];
-  out[3 * out_ld + s] = p[3];
-  out[4 * out_ld + s] = q.dc();
-  out[5 * out_ld + s] = ssq;
-  status[s] = st;
-}
-
-template <int MAXSLOT, int NDMAX, int PFN, int LOADS, int V>
-__global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(3, 3))) void demod_seed_bins_lm_kernel(
-    const double* __restrict__ x, int64_t nseg, int64_t rec_stride, int64_t nrec, int R, int L, int ndata,
-    const double* __restrict__ tab, double* __restrict__ rows, int64_t row_ld, const double* __restrict__ guess,
-    GuessInline ginl, int use_inline, const double* __restrict__ jtab, LMConst c, double* __restrict__ out,
-    int64_t out_ld, int64_t nbuf, int32_t* __restrict__ status, int64_t nbulk, uint32_t* __restrict__ tiles,
-    uint32_t* __restrict__ seedf, uint32_t epoch) {
-  extern __shared__ __attribute__((aligned(16))) double sh[];
-  const int64_t b = blockIdx.x;
-  if (b >= nrec + nbulk) {  // LM: tile = 4 (b - nrec - nbulk) + wave
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int ne = 2 * ndata + 1;
-    lm_fused_tile<V>((b - nrec - nbulk) * kWavesPerBlock + wave, nseg, nbuf, rows, row_ld, ndata, jtab, c, out, out_ld,
-                     status, tiles, seedf, epoch, sh + (int64_t)wave * ne * 65);
-    return;
-  }
-  if (b >= nrec) {
-    bins_kernel_body<MAXSLOT, LOADS, 2, PFN>(x, nseg, (int64_t)R, R, L, ndata, tab, rows, row_ld, nullptr, nullptr,
-                                             (int)nrec, (int)nbulk, tiles);
-    return;
-  }
-  const int64_t r = b;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  __builtin_amdgcn_s_setprio(3);
-  const int ntab = 2 * ndata * L;
-  {
-    typedef double d2v __attribute__((ext_vector_type(2)));
-    const d2v* __restrict__ src = reinterpret_cast<const d2v*>(tab);
-    d2v* dst = reinterpret_cast<d2v*>(sh);
-    const int n2 = ntab / 2;
-    for (int base = 0; base < n2; base += kBlockThreads * 8) {
-      d2v v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int i = base + u * kBlockThreads + (int)threadIdx.x;
-        v[u] = i < n2 ? src[i] : d2v{0.0, 0.0};
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int i = base + u * kBlockThreads + (int)threadIdx.x;
-        if (i < n2) dst[i] = v[u];
-      }
-    }
-  }
-  __syncthreads();
-  double* ybin = sh + ntab;
-  double* row = ybin + L;
-  if (wave == 0) {
-    const int nslot = (L + 127) / 128;
-    int pbase[MAXSLOT];
-    bool pval[MAXSLOT];
-#pragma unroll
-    for (int j = 0; j < MAXSLOT; ++j) {
-      pbase[j] = 2 * (lane + 64 * j);
-      pval[j] = (j < nslot) && (pbase[j] < L);
-    }
-    bins_segment<MAXSLOT, 32, false, kHarmBlock, true>(x + r * rec_stride, R, L, ndata, sh, ybin, lane, pval, pbase,
-                                                          row, 0, 0, nullptr);
-  }
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  double p[4] = {0.0, 0.0, 0.0, 0.0};
-  if (use_inline) {
-#pragma unroll
-    for (int rr = 0; rr < 8; ++rr) {
-      if (r == rr) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) p[i] = ginl.v[rr][i];
-      }
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) p[i] = guess[r * 4 + i];
-  }
-  double ssq;
-  const QRow<1> q{row};
-  const int st = fit_segment_q<kSeedPath>(q, ndata, jtab, c, p, ssq);
-  const int64_t sidx = r * nbuf;
-  out[0 * out_ld + sidx] = p[0];
-  out[1 * out_ld + sidx] = p[1];
-  out[2 * out_ld + sidx] = p[2];
-  out[3 * out_ld + sidx] = p[3];
-  out[4 * out_ld + sidx] = q.at(dfmi_row_dc(ndata));
-  out[5 * out_ld + sidx] = ssq;
-  status[sidx] = st;
-  __hip_atomic_store(seedf + r, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);  // the seed's result, published
-}
-
 }  // namespace dfmi

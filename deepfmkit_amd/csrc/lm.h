@@ -595,12 +595,18 @@ DFMI_HDI double lm_descend_flat(Ev&& ev, double (&p)[4], const LMConst& c) {
         p[2] = pt[2];
         p[3] = pt[3];
         const double best_ssq = ssq_try;
-        ev.accept(p, tt, e);  // coeffs(ndata, data, parm) at the accepted point (fit.py:251)
         ++it;
         li = 0;
-        if (((e.ssq - best_ssq) < c.conv_improve && norm_below(change2, c.conv_param_change)) ||
-            it >= c.max_steps)
+        // coeffs(ndata, data, parm) at the accepted point (fit.py:251): its ssq is the trial's
+        // (both evaluators reuse the trial's sum), so the convergence test (fit.py:254-256) is
+        // known before it; a point the descent stops at needs only that ssq, not J^T J / J^T r
+        if (((ev.ssq_of(tt) - best_ssq) < c.conv_improve && norm_below(change2, c.conv_param_change)) ||
+            it >= c.max_steps) {
+          e.ssq = ev.ssq_of(tt);
           active = false;
+        } else {
+          ev.accept(p, tt, e);
+        }
       }
     }
     if (!accepted && ++li >= c.n_lambda) active = false;  // no lambda improved: fit.py:246-247
@@ -757,12 +763,16 @@ __device__ __forceinline__ double lm_descend_ladder(Ev&& ev, double (&p)[4], con
         p[2] = pt[2];
         p[3] = pt[3];
         const double best_ssq = ev.ssq_of(tt);  // the taken trial's ssqf
-        ev.accept(p, tt, e);  // coeffs(ndata, data, parm) at the accepted point (fit.py:251)
         ++it;
         base = 0;
-        if (((e.ssq - best_ssq) < c.conv_improve && norm_below(change2, c.conv_param_change)) ||
-            it >= c.max_steps)
+        // as lm_descend_flat: coeffs at a point the descent stops at is needed for its ssq only
+        if (((ev.ssq_of(tt) - best_ssq) < c.conv_improve && norm_below(change2, c.conv_param_change)) ||
+            it >= c.max_steps) {
+          e.ssq = ev.ssq_of(tt);
           active = false;
+        } else {
+          ev.accept(p, tt, e);  // coeffs(ndata, data, parm) at the accepted point (fit.py:251)
+        }
       } else {
         base += LPS;
         if (base >= c.n_lambda) active = false;  // no lambda improved: fit.py:246-247

@@ -262,7 +262,7 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
                    int32_t* fitok, int32_t mem, void* stream);
 
 /* Performance tuning hook, process-wide; each call works on a snapshot taken at its
- * start. Results are unaffected. Keys: "demod_kernel" (1 phase bins in LDS where they
+ * start. Results are unaffected (ekf_rot: rounding only). Keys: "demod_kernel" (1 phase bins in LDS where they
  * apply [default], 0 cycle-aligned fold), "lm_general" (1 = two-pass general LM path
  * for every ndata), "demod_spw" (segments per wave the bin grid is sized for; 0 =
  * persistent), "ekf_row" (EKF row kernel up to ekf_row x 16 x CUs channels, 0 = lane

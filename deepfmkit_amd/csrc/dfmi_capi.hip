@@ -941,14 +941,21 @@ int ekf_impl(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
                        (double*)wtw, n_samp, w_m, f_samp);
   const int64_t grid = row ? (nrec + 3) / 4 : (nrec + block - 1) / block;
   // rotation between anchors: groups of 16 (8, 4) samples whose ends carry the snapshots
-  const bool rot = row && t_tune.ekf_rot && R % 4 == 0;
-  hipLaunchKernelGGL(rot ? (R % DFMI_EKF_ROT_G == 0 ? dfmi::ekf_rot_kernel<DFMI_EKF_ROT_G>
-                            : R % 8 == 0              ? dfmi::ekf_rot_kernel<8>
-                                                      : dfmi::ekf_rot_kernel<4>)
-                     : row ? dfmi::ekf_row_kernel<DFMI_EKF_SPLIT != 0> : dfmi::ekf_kernel,
-                     dim3((unsigned)grid), dim3(block), 0, st, dx, nrec, rs, n_samp, dx0, dp0, dq, dr,
+  const bool rot = t_tune.ekf_rot && R % 4 == 0;
+  using EK = void (*)(const double*, int64_t, int64_t, int64_t, const double*, const double*, const double*,
+                      const double*, const double*, int, int64_t, double*, DfmiTrigK);
+  EK ek;
+  if (row)
+    ek = !rot ? dfmi::ekf_row_kernel<DFMI_EKF_SPLIT != 0>
+         : R % DFMI_EKF_ROT_G == 0 ? dfmi::ekf_rot_kernel<DFMI_EKF_ROT_G>
+         : R % 8 == 0              ? dfmi::ekf_rot_kernel<8>
+                                   : dfmi::ekf_rot_kernel<4>;
+  else
+    ek = !rot ? dfmi::ekf_kernel : R % 8 == 0 ? dfmi::ekf_lane_rot_kernel<8> : dfmi::ekf_lane_rot_kernel<4>;
+  hipLaunchKernelGGL(ek, dim3((unsigned)grid), dim3(block), 0, st, dx, nrec, rs, n_samp, dx0, dp0, dq, dr,
                      (const double*)wtw, (int)R, nbuf, dstates, dfmi_trig_k());
-  g_last_demod = rot ? "ekf_rot_kernel" : row ? "ekf_row_kernel" : "ekf_kernel";  // also reports the EKF variant
+  // also reports the EKF variant
+  g_last_demod = row ? (rot ? "ekf_rot_kernel" : "ekf_row_kernel") : (rot ? "ekf_lane_rot_kernel" : "ekf_kernel");
   HIPCHK(hipGetLastError());
   if (host) {
     if (sb) HIPCHK(hipMemcpyAsync(states, dstates, sb, hipMemcpyDeviceToHost, st));

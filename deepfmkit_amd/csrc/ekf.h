@@ -573,4 +573,159 @@ __global__ __launch_bounds__(64) void ekf_rot_kernel(const double* __restrict__ 
   for (; k < n_samp; ++k) ekf_rot_step<false>(st, Pc, qv, Rv, xr[k], wt[k], tk, rr, rc, ro, odd, dmax);
 }
 
+// ---------------------------------------------------------------------------
+// Lane kernel (many channels: lane = channel) with the same anchored rotation as
+// ekf_rot_kernel: sin / cos of d by both kernel polynomials in the lane (no row to split
+// them over), the anchor and the fallback group (any |d| >= 0.78, per lane) by
+// dfmi_sincos_k; otherwise ekf_step's expressions. ~2 x 20 instructions per sample fewer
+// than ekf_kernel's two full sincos.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void ekf_rotate_lane(double d, const DfmiTrigK& k, double& s, double& c) {
+  const double z = d * d;
+  const double ps = fma(z, fma(z, fma(z, fma(z, fma(z, k.c[4], k.c[5]), k.c[6]), k.c[7]), k.c[8]), k.c[9]);
+  const double sd = fma(d * z, ps, d);
+  const double pc = fma(z, fma(z, fma(z, fma(z, fma(z, k.c[10], k.c[11]), k.c[12]), k.c[13]), k.c[14]), k.c[15]);
+  const double cd = fma(z * z, pc, fma(-0.5, z, 1.0));
+  const double sn = fma(s, cd, c * sd);
+  c = fma(c, cd, -(s * sd));
+  s = sn;
+}
+
+struct LaneRot {
+  double sth, cth, sa, ca, thp, argp;
+};
+
+template <bool ROT>
+__device__ __forceinline__ void ekf_step_rot(double (&st)[5], double (&P)[5][5], const double (&Q)[5], double Rv,
+                                             double xk, double wt, const DfmiTrigK& tk, LaneRot& lr, double& dmax) {
+#pragma unroll
+  for (int i = 0; i < 5; ++i) P[i][i] = P[i][i] + Q[i];
+  const double a = st[0], m = st[1], phi = st[2], psi = st[3], dc = st[4];
+  const double th = wt + psi;
+  if constexpr (ROT) {
+    const double d = th - lr.thp;
+    dmax = fmax(dmax, fabs(d));
+    ekf_rotate_lane(d, tk, lr.sth, lr.cth);
+  } else {
+    dfmi_sincos_k(th, tk, &lr.sth, &lr.cth);
+  }
+  lr.thp = th;
+  const double sth = lr.sth, cth = lr.cth;
+  const double arg = fma(m, cth, phi);
+  const double acth = -a * cth, amsth = (a * m) * sth;
+  if constexpr (ROT) {
+    const double d = arg - lr.argp;
+    dmax = fmax(dmax, fabs(d));
+    ekf_rotate_lane(d, tk, lr.sa, lr.ca);
+  } else {
+    dfmi_sincos_k(arg, tk, &lr.sa, &lr.ca);
+  }
+  lr.argp = arg;
+  const double sa = lr.sa, ca = lr.ca;
+  const double h = fma(a, ca, dc);
+  const double H[5] = {ca, acth * sa, -a * sa, amsth * sa, 1.0};
+  const double y = xk - h;
+  auto Pu = [&](int i, int j) -> double { return i <= j ? P[i][j] : P[j][i]; };
+  double HP[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j)
+    HP[j] = fma(H[3], Pu(3, j), fma(H[2], Pu(2, j), fma(H[1], Pu(1, j), fma(H[0], Pu(0, j), Pu(4, j)))));
+  const double S = fma(HP[3], H[3], fma(HP[2], H[2], fma(HP[1], H[1], fma(HP[0], H[0], HP[4] + Rv))));
+  double invS = __builtin_amdgcn_rcp(S);
+  invS = fma(invS, fma(-S, invS, 1.0), invS);
+  const double iy = invS * y;
+  double K[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) K[i] = HP[i] * invS;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) st[i] = fma(HP[i], iy, st[i]);
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+      if (j >= i) P[i][j] = fma(-K[i], HP[j], P[i][j]);
+}
+
+// Same arguments, grid and outputs as ekf_kernel; R % G == 0 (host-checked).
+template <int G>
+__global__ __launch_bounds__(64) void ekf_lane_rot_kernel(const double* __restrict__ x, int64_t nrec,
+                                                           int64_t rec_stride, int64_t n_samp,
+                                                           const double* __restrict__ x0, const double* __restrict__ p0,
+                                                           const double* __restrict__ qd, const double* __restrict__ rv,
+                                                           const double* __restrict__ wt, int R, int64_t nbuf,
+                                                           double* __restrict__ states, DfmiTrigK tk) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrec) return;
+  const double* __restrict__ xr = x + r * rec_stride;
+  double st[5], P[5][5], Q[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    st[i] = x0[r * 5 + i];
+    Q[i] = qd[i];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) P[i][j] = (i == j) ? p0[i] : 0.0;
+  }
+  const double Rv = rv[r];
+  LaneRot lr{0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  double dmax = 0.0;
+  int64_t k = 0;
+  const int64_t ng = n_samp / G;
+  int64_t to_snap = R;
+  double xc[G], wc[G];
+  if (ng > 0) {
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      xc[u] = xr[u];
+      wc[u] = wt[u];
+    }
+  }
+  for (int64_t g = 0; g < ng; ++g, k += G) {
+    double xn[G], wn[G];
+    const int64_t kn = g + 1 < ng ? k + G : k;
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      xn[u] = xr[kn + u];
+      wn[u] = wt[kn + u];
+    }
+    double st0[5], P0[5][5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      st0[i] = st[i];
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+        if (j >= i) P0[i][j] = P[i][j];
+    }
+    dmax = 0.0;
+    ekf_step_rot<false>(st, P, Q, Rv, xc[0], wc[0], tk, lr, dmax);
+#pragma unroll
+    for (int u = 1; u < G; ++u) ekf_step_rot<true>(st, P, Q, Rv, xc[u], wc[u], tk, lr, dmax);
+    if (__builtin_expect(dmax >= 0.78, 0)) {  // this lane: redo the group with the anchor form throughout
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        st[i] = st0[i];
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+          if (j >= i) P[i][j] = P0[i][j];
+      }
+#pragma unroll
+      for (int u = 0; u < G; ++u) ekf_step_rot<false>(st, P, Q, Rv, xc[u], wc[u], tk, lr, dmax);
+    }
+    to_snap -= G;
+    if (to_snap == 0) {
+      to_snap = R;
+      const int64_t b = (k + G) / R - 1;
+      if (b < nbuf) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) states[(r * nbuf + b) * 5 + i] = st[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      xc[u] = xn[u];
+      wc[u] = wn[u];
+    }
+  }
+  for (; k < n_samp; ++k) ekf_step_rot<false>(st, P, Q, Rv, xr[k], wt[k], tk, lr, dmax);
+}
+
 }  // namespace dfmi

@@ -1,6 +1,7 @@
-"""A/B of the EKF row kernels inside one process (config 5: 2 s = 400,000 samples, m = 6,
-40 dB, R = 4000): ekf_rot_kernel (sincos by rotation between anchors, tuning ekf_rot 1) vs
-ekf_row_kernel (full sincos per sample, ekf_rot 0), interleaved, median of `reps` per
+"""A/B of the EKF kernels inside one process (config 5: 2 s = 400,000 samples, m = 6, 40 dB,
+R = 4000; KERNELS="rot,row" by default, also lanerot, lane): ekf_rot_kernel (sincos by
+rotation between anchors, tuning ekf_rot 1) vs ekf_row_kernel (full sincos per sample,
+ekf_rot 0), or the lane kernels likewise (ekf_row 0), interleaved, median of `reps` per
 setting and channel count; states of every variant against the scalar C restatement of
 EKFFitter.fit (oracle/csrc/ekf_scalar.c) for channel 0. One JSON line per channel count.
 """
@@ -44,7 +45,8 @@ def main():
     P_ = ctypes.c_void_p
     cl.ekf_scalar.argtypes = [P_, ctypes.c_int64, P_, P_, P_, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                               ctypes.c_int64, ctypes.c_int64, P_]
-    settings = {"rot": (1, 1), "row": (1, 0)}
+    allk = {"rot": (1, 1), "row": (1, 0), "lanerot": (0, 1), "lane": (0, 0)}
+    settings = {k: allk[k] for k in os.environ.get("KERNELS", "rot,row").split(",")}
     for nch in [int(c) for c in args.channels.split(",")]:
         xe = torch.empty(nch * ns, dtype=torch.float64, device=dev)
         for c in range(nch):
@@ -80,7 +82,9 @@ def main():
             t = float(np.median(times[name]))
             line[name] = {"kernel": res[name][0], "s": round(t, 6), "samples_per_s_per_channel": round(ns / t, 1),
                           "max_abs_dstate_ch0_vs_c": res[name][1]}
-        line["max_abs_rot_vs_row_all_channels"] = float(np.max(np.abs(res["rot"][2] - res["row"][2])))
+        names = list(settings)
+        line[f"max_abs_{names[0]}_vs_{names[-1]}_all_channels"] = float(np.max(np.abs(res[names[0]][2] -
+                                                                                   res[names[-1]][2])))
         print(json.dumps(line), flush=True)
         del xe, stt
 

@@ -165,7 +165,8 @@ def test_config3_two_channels_vs_c_restatement():
         print(f"config 3 channel {c}: max |d amp, m, phi, psi| vs C =", worst, "; checked against the oracle:", nfar)
 
 
-@pytest.mark.parametrize("row,rot,kname", [(1, 1, "ekf_rot_kernel"), (1, 0, "ekf_row_kernel"), (0, 1, "ekf_kernel")])
+@pytest.mark.parametrize("row,rot,kname", [(1, 1, "ekf_rot_kernel"), (1, 0, "ekf_row_kernel"),
+                                           (0, 1, "ekf_lane_rot_kernel"), (0, 0, "ekf_kernel")])
 def test_ekf_config5_13_channels_full_length_vs_c_oracle(row, rot, kname):
     """Config 5 at full length on 13 independent channels in ONE dfmi_ekf_fit launch (EKFFitter
     per channel, fitters.py:214-320): 4 channels per wave in the row kernels (sincos by rotation

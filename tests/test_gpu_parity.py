@@ -152,9 +152,10 @@ def test_ekf_matches_reference(manifest):
 
 # EKF kernels: (ekf_row, ekf_rot) tuning and the kernel dfmi_last_demod_kernel reports.
 # rot: 16-lane row per channel, sincos by rotation between anchors (default for few
-# channels, R % 4 == 0); row: the same row with the full sincos per sample; lane: one lane
-# per channel (many channels).
-EKF_KERNELS = {"rot": (1, 1, "ekf_rot_kernel"), "row": (1, 0, "ekf_row_kernel"), "lane": (0, 1, "ekf_kernel")}
+# channels, R % 4 == 0); row: the same row with the full sincos per sample; lanerot / lane:
+# one lane per channel (many channels) with / without the rotation.
+EKF_KERNELS = {"rot": (1, 1, "ekf_rot_kernel"), "row": (1, 0, "ekf_row_kernel"), "lanerot": (0, 1, "ekf_lane_rot_kernel"),
+               "lane": (0, 0, "ekf_kernel")}
 
 
 class _ekf_kernel:
@@ -194,7 +195,7 @@ def _c_ekf(x, init4, R, nbuf, f_samp=200000.0, f_mod=1000.0, qd=(1e-8, 1e-8, 1e-
     return ref
 
 
-@pytest.mark.parametrize("kern", ["rot", "row", "lane"])
+@pytest.mark.parametrize("kern", ["rot", "row", "lanerot", "lane"])
 def test_ekf_long_record_matches_oracle(kern):
     """Config 5 shape on a longer record than the golden one (0.1 s = 20,000 samples,
     5 snapshots): every EKF kernel — one 16-lane row per channel with sincos by rotation
@@ -228,7 +229,7 @@ def _ekf_long_record(dfm, O, lib, kname):
         np.testing.assert_array_equal(many[k], got)
 
 
-@pytest.mark.parametrize("kern", ["rot", "row", "lane"])
+@pytest.mark.parametrize("kern", ["rot", "row", "lanerot", "lane"])
 def test_ekf_config5_full_length_matches_c_oracle(kern):
     """Config 5 at the length BASELINE names (notebooks/2.0 defaults):
     a 2 s = 400,000-sample snr-mode record (m=6, 40 dB) through dfmi_ekf_fit (EKFFitter.fit,
@@ -268,10 +269,11 @@ def _ekf_raw(dfm, m, f_samp, f_mod, seconds, trial):
     return dff.raws["r"]
 
 
+@pytest.mark.parametrize("kern", ["rot", "lanerot"])
 @pytest.mark.parametrize("m,f_samp,f_mod", [(25.0, 32000.0, 400.0), (10.0, 32000.0, 400.0),
                                             (10.0, 32160.0, 400.0), (6.0, 30000.0, 400.0)])
-def test_ekf_rotation_fallback_groups_match_c_oracle(m, f_samp, f_mod):
-    """ekf_rot_kernel where the phase argument moves by more than the rotation's 0.78 rad per
+def test_ekf_rotation_fallback_groups_match_c_oracle(m, f_samp, f_mod, kern):
+    """ekf_rot_kernel / ekf_lane_rot_kernel where the phase argument moves by more than the rotation's 0.78 rad per
     sample (m = 25 / 10 at 400 Hz, 32 kS/s: up to 1.96 / 0.79 rad): those groups are rolled
     back and re-run with the full sincos, the rest rotate; R = 1600 (groups of 16), 1608 (of 8)
     and 1500 (of 4). States within 1e-12 of the scalar C restatement on every snapshot, init_m
@@ -286,15 +288,16 @@ def test_ekf_rotation_fallback_groups_match_c_oracle(m, f_samp, f_mod):
     ref = _c_ekf(x, [1.6, m, 0.0, 0.0], R, nbuf, f_samp, f_mod)
     if ref is None:
         pytest.skip("oracle/libekf_scalar.so not built (make -C oracle)")
-    with _ekf_kernel(lib, "rot"):
+    with _ekf_kernel(lib, kern) as k:
         got = dfm.fitters.ekf_records([raw], 20, init_m=m)[0]
-        assert lib.dfmi_last_demod_kernel().decode() == "ekf_rot_kernel"
+        assert lib.dfmi_last_demod_kernel().decode() == k.kname
     err = np.abs(got - ref)
     assert err.max() <= 1e-12, (err.max(), np.unravel_index(err.argmax(), err.shape))
 
 
-def test_ekf_rotation_channels_independent_and_ragged_tail():
-    """A channel's ekf_rot_kernel result never depends on the other channels of its wave:
+@pytest.mark.parametrize("kern", ["rot", "lanerot"])
+def test_ekf_rotation_channels_independent_and_ragged_tail(kern):
+    """A channel's ekf_rot_kernel / ekf_lane_rot_kernel result never depends on the other channels of its wave:
     channels that take the fallback (m = 25) and channels that rotate (m = 2) in one launch
     equal their single-channel runs bit for bit; a record whose length is not a multiple of
     the group (20,003 samples) fits its tail samples with the full sincos and matches the
@@ -305,11 +308,11 @@ def test_ekf_rotation_channels_independent_and_ragged_tail():
     lib = _lib.load()
     ra = _ekf_raw(dfm, 25.0, 32000.0, 400.0, 0.5, 1)
     rb = _ekf_raw(dfm, 2.0, 32000.0, 400.0, 0.5, 2)
-    with _ekf_kernel(lib, "rot"):
+    with _ekf_kernel(lib, kern) as kk:
         a = dfm.fitters.ekf_records([ra], 20, init_m=6.0)[0]
         b = dfm.fitters.ekf_records([rb], 20, init_m=6.0)[0]
         mix = dfm.fitters.ekf_records([ra, rb, rb, ra, rb], 20, init_m=6.0)
-        assert lib.dfmi_last_demod_kernel().decode() == "ekf_rot_kernel"
+        assert lib.dfmi_last_demod_kernel().decode() == kk.kname
         for k, want in enumerate((a, b, b, a, b)):
             np.testing.assert_array_equal(mix[k], want)
         # ragged tail: 20,003 samples, R = 4000
@@ -322,12 +325,12 @@ def test_ekf_rotation_channels_independent_and_ragged_tail():
         x = np.asarray(raw.samples(), dtype=np.float64)
         x = np.concatenate([x, x[:3]])
         got = _ekf_host(lib, x, 200000.0, 1000.0, 4000, 5)
-        assert lib.dfmi_last_demod_kernel().decode() == "ekf_rot_kernel"
+        assert lib.dfmi_last_demod_kernel().decode() == kk.kname
         ref = O.ekf_record(x, 200000.0, 1000.0, 20)
         assert np.max(np.abs(got - ref)) <= 1e-12
-        # an odd R (1501 samples per snapshot): no group can end on the snapshots -> ekf_row_kernel
+        # an odd R (1501 samples per snapshot): no group can end on the snapshots -> no rotation
         _ekf_host(lib, x[:6 * 1501], 30020.0, 400.0, 1501, 6)
-        assert lib.dfmi_last_demod_kernel().decode() == "ekf_row_kernel"
+        assert lib.dfmi_last_demod_kernel().decode() == ("ekf_row_kernel" if kern == "rot" else "ekf_kernel")
 
 
 def _ekf_host(lib, x, f_samp, f_mod, R, nbuf):

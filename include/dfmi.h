@@ -348,7 +348,7 @@ const char* dfmi_last_error(void);
 const char* dfmi_version(void);
 
 /* Kernel variant of the last demodulation (or EKF fit) this THREAD launched, e.g.
- * "demod_bins_kernel<2,8,rows,pf4>", "ekf_rot_kernel", "ekf_row_kernel" ("" before the first one).
+ * "demod_bins_kernel<2,10,rows,pf4>", "ekf_rot_kernel", "ekf_row_kernel" ("" before the first one).
  * Diagnostics/profiling. */
 const char* dfmi_last_demod_kernel(void);
 

@@ -126,17 +126,6 @@ __device__ __forceinline__ void store_block(const double (&v)[2 * HB], int lane,
   }
 }
 
-#ifndef DFMI_ROW_SC1
-#define DFMI_ROW_SC1 0  // A/B builds: 1 = row stores written through this XCD's L2 (sc1 nt)
-#endif
-__device__ __forceinline__ void row_store(double* p, double v) {
-#if DFMI_ROW_SC1
-  asm volatile("global_store_dwordx2 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
-#else
-  __builtin_nontemporal_store(v, p);
-#endif
-}
-
 // dc part of fold_finish: the lane's partial sum of its bins (returned), and dc itself
 // (wave sum / R) unless the row layout carries it in a spare Q slot.
 template <int VEC, int MAXSLOT, int HB, bool ROWS>
@@ -153,7 +142,7 @@ __device__ __forceinline__ double finish_dc(const double (&y)[MAXSLOT][VEC], int
   if (!ROWS || spare == 0) {
     const double all = wave_sum(tot);
     if (lane == 0) {
-      if constexpr (ROWS) row_store(qi + col * qi_ld + dfmi_row_dc(ndata), all / (double)R);
+      if constexpr (ROWS) __builtin_nontemporal_store(all / (double)R, qi + col * qi_ld + dfmi_row_dc(ndata));
       else dc[col] = all / (double)R;
     }
   }
@@ -201,7 +190,7 @@ __device__ __forceinline__ void finish_block(const double (&y)[MAXSLOT][VEC], co
   if constexpr (ROWS) {
     // one 128-B line, non-temporal: plain row stores cost the bin kernel 3.5 % (0.520 vs
     // 0.502 ms per 100k segments, profiles/r02l_ab_store.log)
-    if ((lane & 3) == 0) row_store(qi + col * qi_ld + hb * 16 + (lane >> 2), acc[0] / (double)R);
+    if ((lane & 3) == 0) __builtin_nontemporal_store(acc[0] / (double)R, qi + col * qi_ld + hb * 16 + (lane >> 2));
   } else {
     store_block<HB>(acc, lane, hb, ndata, qi, qi_ld, col, R);
   }

@@ -198,6 +198,75 @@ def parity_vs_oracle(df, ref):
             "vs": "oracle restatement of fit.py/fitters.py, pinned to the reference by tests/golden"}
 
 
+def free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def self_launch(n, argv, script=None, env_extra=None, timeout=None):
+    """`python bench.py --gpus N` without torchrun: start N rank processes, one per GPU
+    (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), BEFORE this process
+    touches any GPU, wait for all of them and return the worst exit code. The reference's
+    parallel width is likewise an explicit argument (n_cores -> Pool(n_cores),
+    fitters.py:397-399,416-423). Rank 0 prints the JSON line; a rank that fails takes the
+    others down with it."""
+    import subprocess
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port, DFMI_SELF_LAUNCHED="1", **(env_extra or {}))
+        procs.append(subprocess.Popen([sys.executable, "-u", script or os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    t_end = None if timeout is None else time.monotonic() + timeout
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0:
+                    rc = rc or code
+                    for q in pending:  # one rank failed: the barrier would hang the others
+                        q.terminate()
+            if t_end is not None and time.monotonic() > t_end:
+                rc = rc or 124
+                for q in pending:
+                    q.kill()
+            if pending:
+                time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait()
+    return rc
+
+
+def rank_topology(dist, dev, world):
+    """Every rank's (rank, local rank, host, device) all-gathered onto rank 0, and the
+    process-group backend: evidence that N ranks ran on N distinct GPUs."""
+    import socket
+    me = {"rank": int(os.environ.get("RANK", "0")), "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+          "host": socket.gethostname(), "device": str(dev)}
+    if dev is not None and getattr(dev, "type", "") == "cuda":
+        import torch
+        props = torch.cuda.get_device_properties(dev)
+        me["device_index"] = dev.index
+        me["pci_bus_id"] = getattr(props, "pci_bus_id", None)
+        me["uuid"] = str(getattr(props, "uuid", ""))
+    if world == 1:
+        return [me], None
+    allr = [None] * world
+    dist.all_gather_object(allr, me)
+    return allr, dist.get_backend()
+
+
 def _timed_steps(torch, fn, steps, warmup):
     for _ in range(warmup):
         fn()
@@ -334,6 +403,14 @@ def extra_configs(torch, dev, lib, _lib, stream, cfg, cpu_leg):
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:  # no torchrun: one rank process per GPU, launched here before any GPU call
+            return self_launch(args.gpus, sys.argv[1:])
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}: the launcher and the "
+                         "flag disagree")
     import torch
     import torch.distributed as dist
 
@@ -344,8 +421,12 @@ def main():
     pre = cpu_baseline(args) if want_base else None
     # one process per GPU: bind the device first, so RCCL's barrier / all_reduce run
     # on this rank's GPU
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # (local rank modulo the visible GPUs: only a gloo rehearsal puts two ranks on one card;
+    # under RCCL that is refused below)
+    ndev = torch.cuda.device_count()  # counting devices does not initialise HIP
+    dev_index = local % ndev if ndev > 0 else local
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
         # RCCL; DFMI_DIST_BACKEND=gloo rehearses N ranks that share one card (RCCL
         # refuses two ranks on one device)
@@ -354,6 +435,11 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+
+    ranks, backend = rank_topology(dist, dev, world)
+    if world > 1 and len({(r["host"], r.get("pci_bus_id"), r["device"]) for r in ranks}) < world \
+            and os.environ.get("DFMI_DIST_BACKEND", "nccl") == "nccl":
+        raise SystemExit(f"{world} ranks on fewer distinct GPUs: {ranks}")
 
     from deepfmkit_amd import _lib
     from deepfmkit_amd import fit as F
@@ -549,6 +635,9 @@ def main():
                                    f"{nrec} channel{'s' if nrec > 1 else ''}, _fit_parallel chunk size 1",
                        "segments_per_gpu": nseg, "channels": nrec, "R": R, "ndata": NDATA,
                        "parallelism": f"shard{world}"},
+            "world": {"size": world, "backend": backend, "ranks": ranks,
+                      "launcher": "bench.py self-launch" if os.environ.get("DFMI_SELF_LAUNCHED") else
+                      ("torchrun" if world > 1 else "single process")},
             "roofline": roof,
             "kernels_ms": {"step_demod_seed": round(demod_ms, 4), "step_lm": round(lm_step_ms, 4),
                            "demod_rows_alone": round(rows_ms, 4), "lm_alone_all_segments": round(lm_ms, 4)},
@@ -573,4 +662,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -126,9 +126,32 @@ __device__ __forceinline__ void store_block(const double (&v)[2 * HB], int lane,
   }
 }
 
+// One value of a demodulation row. The row lives in global memory (the record pipeline's
+// rows, written once and read once by the LM: non-temporal) or in LDS (the seed step's row,
+// seed.h, fitted in place): ROW_LDS says which, statically, and each case stores through a
+// pointer of its own address space — a global-only store instruction aimed at an LDS
+// address faults (HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION, seen in round 3 with an A/B
+// variant that sent both rows through one global `sc1 nt` store). Built with
+// -DDFMI_DEBUG_ROWS, every store also checks the pointer's aperture against ROW_LDS
+// (__graft_entry__.build() builds it as ab/libdfmi_dbg.so; tests/test_gpu_debug_build.py runs
+// the record pipeline through it once).
+template <bool ROW_LDS>
+__device__ __forceinline__ void row_put(double* p, double v) {
+#if defined(DFMI_DEBUG_ROWS) && defined(__HIP_DEVICE_COMPILE__)
+  if (__builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void*)p) != ROW_LDS) __builtin_trap();
+#endif
+  if constexpr (ROW_LDS) {
+    typedef __attribute__((address_space(3))) double lds_double;
+    *(lds_double*)p = v;  // ds_write_b64
+  } else {
+    typedef __attribute__((address_space(1))) double global_double;
+    __builtin_nontemporal_store(v, (global_double*)p);  // global_store_dwordx2 ... nt
+  }
+}
+
 // dc part of fold_finish: the lane's partial sum of its bins (returned), and dc itself
 // (wave sum / R) unless the row layout carries it in a spare Q slot.
-template <int VEC, int MAXSLOT, int HB, bool ROWS>
+template <int VEC, int MAXSLOT, int HB, bool ROWS, bool ROW_LDS = false>
 __device__ __forceinline__ double finish_dc(const double (&y)[MAXSLOT][VEC], int R, int ndata, int lane,
                                             double* __restrict__ qi, int64_t qi_ld, int64_t col,
                                             double* __restrict__ dc) {
@@ -142,7 +165,7 @@ __device__ __forceinline__ double finish_dc(const double (&y)[MAXSLOT][VEC], int
   if (!ROWS || spare == 0) {
     const double all = wave_sum(tot);
     if (lane == 0) {
-      if constexpr (ROWS) __builtin_nontemporal_store(all / (double)R, qi + col * qi_ld + dfmi_row_dc(ndata));
+      if constexpr (ROWS) row_put<ROW_LDS>(qi + col * qi_ld + dfmi_row_dc(ndata), all / (double)R);
       else dc[col] = all / (double)R;
     }
   }
@@ -151,7 +174,7 @@ __device__ __forceinline__ double finish_dc(const double (&y)[MAXSLOT][VEC], int
 
 // Harmonic block hb of fold_finish: HB harmonics contracted with the basis, reduced by
 // the butterfly and stored (tot: finish_dc's partial sum, for the rows' dc slot).
-template <int VEC, int MAXSLOT, int HB, bool ROWS>
+template <int VEC, int MAXSLOT, int HB, bool ROWS, bool ROW_LDS = false>
 __device__ __forceinline__ void finish_block(const double (&y)[MAXSLOT][VEC], const bool (&pval)[MAXSLOT],
                                              const int (&pbase)[MAXSLOT], double tot, int hb, int R, int L,
                                              int ndata, const double* __restrict__ T, int lane,
@@ -190,7 +213,7 @@ __device__ __forceinline__ void finish_block(const double (&y)[MAXSLOT][VEC], co
   if constexpr (ROWS) {
     // one 128-B line, non-temporal: plain row stores cost the bin kernel 3.5 % (0.520 vs
     // 0.502 ms per 100k segments, profiles/r02l_ab_store.log)
-    if ((lane & 3) == 0) __builtin_nontemporal_store(acc[0] / (double)R, qi + col * qi_ld + hb * 16 + (lane >> 2));
+    if ((lane & 3) == 0) row_put<ROW_LDS>(qi + col * qi_ld + hb * 16 + (lane >> 2), acc[0] / (double)R);
   } else {
     store_block<HB>(acc, lane, hb, ndata, qi, qi_ld, col, R);
   }
@@ -206,15 +229,15 @@ __device__ __forceinline__ void finish_block(const double (&y)[MAXSLOT][VEC], co
 // tree is wave_sum's, so dc is bit-identical to the ROWS = false value. (Scattered
 // 8-B stores into 21 component rows cost 13 % of the demodulation time:
 // profiles/r01_tune_demod_probe.json.)
-template <int VEC, int MAXSLOT, int HB = kHarmBlock, bool ROWS = false>
+template <int VEC, int MAXSLOT, int HB = kHarmBlock, bool ROWS = false, bool ROW_LDS = false>
 __device__ __forceinline__ void fold_finish(const double (&y)[MAXSLOT][VEC], const bool (&pval)[MAXSLOT],
                                             const int (&pbase)[MAXSLOT], int R, int L, int ndata,
                                             const double* __restrict__ T, int lane, double* __restrict__ qi,
                                             int64_t qi_ld, int64_t col, double* __restrict__ dc) {
   const int nblk = (ndata + HB - 1) / HB;
-  const double tot = finish_dc<VEC, MAXSLOT, HB, ROWS>(y, R, ndata, lane, qi, qi_ld, col, dc);
+  const double tot = finish_dc<VEC, MAXSLOT, HB, ROWS, ROW_LDS>(y, R, ndata, lane, qi, qi_ld, col, dc);
   for (int hb = 0; hb < nblk; ++hb)
-    finish_block<VEC, MAXSLOT, HB, ROWS>(y, pval, pbase, tot, hb, R, L, ndata, T, lane, qi, qi_ld, col);
+    finish_block<VEC, MAXSLOT, HB, ROWS, ROW_LDS>(y, pval, pbase, tot, hb, R, L, ndata, T, lane, qi, qi_ld, col);
 }
 
 // One segment, one wavefront: fold + dc + contraction (see the header comment).
@@ -361,7 +384,7 @@ __global__ __launch_bounds__(kBlockThreads) void demod_fold_kernel(
 // the next segment's first PFN chunks (at `next`, if not null) are issued into pf
 // before this segment's contraction, so the wave has loads in flight while it
 // contracts.
-template <int MAXSLOT, int LOADS, bool NT, int HB, bool ROWS, int PFN = 0>
+template <int MAXSLOT, int LOADS, bool NT, int HB, bool ROWS, int PFN = 0, bool ROW_LDS = false>
 __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int R, int L, int ndata,
                                              const double* __restrict__ T, double* __restrict__ ybin, int lane,
                                              const bool (&pval)[MAXSLOT], const int (&pbase)[MAXSLOT],
@@ -462,7 +485,7 @@ __device__ __forceinline__ void bins_segment(const double* __restrict__ xs0, int
       y[j][0] = y[j][1] = 0.0;
     }
   }
-  fold_finish<2, MAXSLOT, HB, ROWS>(y, pval, pbase, R, L, ndata, T, lane, qi, qi_ld, col, dc);
+  fold_finish<2, MAXSLOT, HB, ROWS, ROW_LDS>(y, pval, pbase, R, L, ndata, T, lane, qi, qi_ld, col, dc);
 }
 
 // One wavefront per segment (grid-stride over 4-wave workgroups that share one LDS

@@ -57,6 +57,8 @@ struct Tuning {
   int lm_ladder = 32;    // LM launches of at most lm_ladder x CUs chains / segments (latency-bound: warm-start
                          // chains, small batches) run the parallel lambda ladder (lm.h lm_ladder_kernel);
                          // 0 = always one lane per chain / segment
+  int ws_streams = 4;    // caller streams whose workspaces are kept; a call from one more stream first
+                         // drains the DEVICE (hipDeviceSynchronize) and frees the least recently used set
 };
 Tuning g_tune;
 
@@ -107,7 +109,6 @@ struct StreamWs {
   std::map<std::string, DevBuf> bufs;
   uint64_t last_use = 0;
 };
-constexpr size_t kMaxStreamWs = 4;  // caller streams whose workspaces are kept (LRU beyond)
 
 struct DeviceState {
   bool init = false;
@@ -184,27 +185,47 @@ int ensure_init_locked(int* dev_out) {
 }
 
 // Step-timing marks (dfmi_step_timing): mark(i) records event i of the current step's
-// triple on st when timing is on.
+// triple on st when timing is on. The triple joins ds.ev_steps only by commit(), after
+// its last mark: a call that fails (or turns out not to be fused) half-way hands its
+// events back to the pool in the destructor, so dfmi_step_timing_read never meets an
+// event that was not recorded. At most kMaxMarkedSteps triples wait to be read; further
+// calls are not marked (dfmi_step_timing_read reports how many were).
+constexpr size_t kMaxMarkedSteps = 1 << 16;
 struct StepMarks {
   std::array<hipEvent_t, 3> ev{};
-  bool on = false;
-  int begin(DeviceState& ds) {
-    on = ds.timing;
+  DeviceState* ds = nullptr;
+  bool on = false, committed = false;
+  int begin(DeviceState& d) {
+    ds = &d;
+    on = d.timing && d.ev_steps.size() < kMaxMarkedSteps;
     if (!on) return DFMI_OK;
+    int got = 0;
     for (auto& e : ev) {
-      if (ds.ev_pool.empty()) {
-        HIPCHK(hipEventCreate(&e));
+      if (d.ev_pool.empty()) {
+        if (hipEventCreate(&e) != hipSuccess) {
+          for (int i = 0; i < got; ++i) d.ev_pool.push_back(ev[i]);
+          on = false;
+          return fail(DFMI_ERR_HIP, "hipEventCreate (step timing)");
+        }
       } else {
-        e = ds.ev_pool.back();
-        ds.ev_pool.pop_back();
+        e = d.ev_pool.back();
+        d.ev_pool.pop_back();
       }
+      ++got;
     }
-    ds.ev_steps.push_back(ev);
     return DFMI_OK;
   }
   int mark(int i, hipStream_t st) {
     if (on) HIPCHK(hipEventRecord(ev[i], st));
     return DFMI_OK;
+  }
+  void commit() {
+    if (!on) return;
+    ds->ev_steps.push_back(ev);
+    committed = true;
+  }
+  ~StepMarks() {
+    if (on && !committed) ds->ev_pool.insert(ds->ev_pool.end(), ev.begin(), ev.end());
   }
 };
 
@@ -216,15 +237,17 @@ int free_stream_ws(StreamWs& s) {
 }
 
 // Grow-only scratch buffer `name` of the current caller stream. Workspaces of at most
-// kMaxStreamWs caller streams are kept: a call from a further stream first waits for the
-// device to drain and frees the least recently used stream's set.
+// ws_streams (tuning key, default 4) caller streams are kept: a call from a further stream
+// first waits for the device to drain and frees the least recently used stream's set
+// (include/dfmi.h: a caller cycling over more streams than that serialises on the device,
+// and such a call cannot be captured into a graph).
 int workspace(int dev, const char* name, size_t bytes, void** out) {
   (void)dev;
   const uintptr_t key = t_call ? (uintptr_t)t_call->stream : 0;
   DeviceState& ds = *t_ds;
   auto it = ds.ws.find(key);
   if (it == ds.ws.end()) {
-    if (ds.ws.size() >= kMaxStreamWs) {
+    if (ds.ws.size() >= (size_t)(t_tune.ws_streams > 0 ? t_tune.ws_streams : 1)) {
       auto lru = ds.ws.begin();
       for (auto jt = ds.ws.begin(); jt != ds.ws.end(); ++jt)
         if (jt->second.last_use < lru->second.last_use) lru = jt;
@@ -771,12 +794,11 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
       rc = lm_device(dev, (double*)rw, qs, ndata, nrec, nbuf, 1, nbuf - 1, nchunk, out, nbuf, out_ld, nullptr, c,
                      jtab, out, out_ld, fitok, st, true);
       if (rc) return rc;
-      return sm.mark(2, st);
+      if ((rc = sm.mark(2, st))) return rc;
+      sm.commit();
+      return DFMI_OK;
     }
-    if (sm.on) {  // not fused after all: no marks for this call
-      ds.ev_pool.insert(ds.ev_pool.end(), sm.ev.begin(), sm.ev.end());
-      ds.ev_steps.pop_back();
-    }
+    // not fused after all: no marks for this call (sm hands its events back)
   }
   if (parallel) {  // the seed beside the bulk demodulation (side stream, event)
     HIPCHK(hipEventRecord(ds.ev_in, st));
@@ -838,7 +860,8 @@ const std::map<std::string, Knob>& knobs() {
       {"ekf_row", {&Tuning::ekf_row, {}}},
       {"ekf_rot", {&Tuning::ekf_rot, {0, 1}}},
       {"wdfmi_accel", {&Tuning::wdfmi_accel, {0, 1, 2, 3}}},
-      {"lm_ladder", {&Tuning::lm_ladder, {}}}};
+      {"lm_ladder", {&Tuning::lm_ladder, {}}},
+      {"ws_streams", {&Tuning::ws_streams, {}}}};
   return k;
 }
 // np.mean / np.var of nrec device records on st (moments.hip), numpy-exact.
@@ -1078,11 +1101,12 @@ int dfmi_step_timing_read(double* demod_ms, double* lm_ms, int64_t* nsteps) {
   if (int rc = ensure_init(&dev)) return rc;
   DeviceState& ds = *t_ds;
   double d = 0.0, l = 0.0;
-  for (auto& tr : ds.ev_steps) {
-    HIPCHK(hipEventSynchronize(tr[2]));
+  hipError_t err = hipSuccess;
+  for (auto& tr : ds.ev_steps) {  // every triple goes back to the pool, read or not
     float a = 0.f, b = 0.f;
-    HIPCHK(hipEventElapsedTime(&a, tr[0], tr[1]));
-    HIPCHK(hipEventElapsedTime(&b, tr[1], tr[2]));
+    if (err == hipSuccess) err = hipEventSynchronize(tr[2]);
+    if (err == hipSuccess) err = hipEventElapsedTime(&a, tr[0], tr[1]);
+    if (err == hipSuccess) err = hipEventElapsedTime(&b, tr[1], tr[2]);
     d += a;
     l += b;
     ds.ev_pool.insert(ds.ev_pool.end(), tr.begin(), tr.end());
@@ -1091,6 +1115,7 @@ int dfmi_step_timing_read(double* demod_ms, double* lm_ms, int64_t* nsteps) {
   *demod_ms = d;
   *lm_ms = l;
   ds.ev_steps.clear();
+  if (err != hipSuccess) return fail(DFMI_ERR_HIP, std::string("step timing read: ") + hipGetErrorString(err));
   return DFMI_OK;
 }
 

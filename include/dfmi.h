@@ -271,7 +271,12 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
  * "wdfmi_accel" (bit 0: W-DFMI time axis without division, bit 1: template slopes in
  * LDS; both exact), "lm_ladder" (LM launches of at most lm_ladder x CUs
  * chains or segments run the parallel lambda ladder, 8 lanes per item: warm-start chains,
- * small batches; 0 = never; default 32; same bits), "probe" (1 = diagnostics timestamp
+ * small batches; 0 = never; default 32; same bits), "ws_streams" (caller streams whose
+ * scratch workspaces are kept per device, default 4: a DFMI_MEM_DEVICE call from a stream
+ * beyond that many first DRAINS THE DEVICE (hipDeviceSynchronize) and frees the least
+ * recently used stream's workspaces — a caller cycling over more streams serialises every
+ * call, and such a call must not be made while a stream is being captured into a graph;
+ * raise the key to the number of streams in use), "probe" (1 = diagnostics timestamp
  * buffer on the current device, dfmi_probe_read). */
 int dfmi_set_tuning(const char* key, int64_t value);
 
@@ -281,13 +286,15 @@ int dfmi_get_tuning(const char* key, int64_t* value);
 /* Measurement hook: with enable != 0, dfmi_nls_record records timing events on its
  * stream around the fused seed + demodulation launch and the LM launch of the record
  * pipeline (current device). dfmi_step_timing_read waits for them and returns the
- * summed kernel-span times (ms) of the steps recorded since the last read. */
+ * summed kernel-span times (ms) of the steps recorded since the last read (at most 65,536
+ * steps wait to be read; later calls are not marked, *nsteps says how many were). A call
+ * that fails part-way records no step. */
 int dfmi_step_timing(int32_t enable);
 int dfmi_step_timing_read(double* demod_ms, double* lm_ms, int64_t* nsteps);
 
 /* Frees every scratch workspace of the current device after waiting for it to drain
- * (workspaces are kept per caller stream, at most 4 streams, least recently used freed
- * first). */
+ * (workspaces are kept per caller stream, at most "ws_streams" streams [default 4], least
+ * recently used freed first). */
 int dfmi_release_workspaces(void);
 
 /* Diagnostics: with dfmi_set_tuning("probe", 1) some kernels record

@@ -71,6 +71,24 @@ void hc_bessel_regs(double x, int nb, double* out) {
   }
 }
 
+// ssqf (fit.py:152-167) of the register path's trial evaluation (reg = 1) or of the literal
+// general path (reg = 0) at n points p (n x 4) for ONE segment's QI (2 ndata values)
+void hc_ssq_points(const double* qi, int ndata, const double* p, long n, int reg, double* out) {
+  const dfmi::QGlobal qg{qi, 1, ndata};
+  const DfmiTrigK k = dfmi_trig_k();
+  for (long i = 0; i < n; ++i) {
+    double pp[4] = {p[4 * i], p[4 * i + 1], p[4 * i + 2], p[4 * i + 3]};
+    if (reg && ndata == 10) {
+      dfmi::TrialReg<dfmi::kExactNd | 10> t;
+      out[i] = dfmi::eval_reg_trial<dfmi::kExactNd | 10>(qg, ndata, pp, t, k);
+    } else {
+      dfmi::Eval e;
+      dfmi::eval_gen(qg, ndata, pp, e);
+      out[i] = e.ssq;
+    }
+  }
+}
+
 // qi component-major (qi[c*n + s]); guess n x 4; constants in the reference order.
 int hc_fit_segments(const double* qi, long n, int ndata, const double* guess, const double* consts,
                     const double* lambdas, int n_lambda, double* p_out, double* ssq_out, int* status_out,

@@ -56,3 +56,26 @@ def test_bench_two_ranks_weak_scaling_line(tmp_path):
     assert line["batch_status0_frac"] == 1.0
     assert abs(line["batch_m_mean"] - 6.0) < 1e-3
     assert line["value"] > 0 and "cpu_baseline" not in line and "extra_configs" not in line
+
+
+def test_bench_self_launch_two_ranks(tmp_path):
+    """`python bench.py --gpus 2` with no torchrun: bench.self_launch starts the two rank
+    processes itself (gloo, both on this box's one card); rank 0's line says n_gpus 2 and
+    lists both ranks' devices."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["DFMI_DIST_BACKEND"] = "gloo"
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "5", "--warmup", "1",
+           "--segments", "20000", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [v for v in p.stdout.strip().splitlines() if v.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["world"]["size"] == 2 and line["world"]["backend"] == "gloo"
+    assert line["world"]["launcher"] == "bench.py self-launch"
+    ranks = line["world"]["ranks"]
+    assert [r["rank"] for r in ranks] == [0, 1] and all(r["device"].startswith("cuda:") for r in ranks)
+    assert line["batch_status0_frac"] == 1.0 and line["value"] > 0

@@ -1,26 +1,20 @@
 """Parity at BASELINE.json's full sizes, segment by segment: the GPU record pipeline
 (dfmi_nls_record, _fit_parallel with chunk size 1: every buffer seeded from buffer 0,
-fitters.py:395-428) against the scalar C restatement of the same readout
-(oracle/csrc/nls_scalar.c, pinned to the numpy oracle at 1e-9 in tests/test_oracle_c.py,
-run here on the host with OpenMP) on the same bytes:
+fitters.py:395-428) against the numpy oracle (oracle/nls_oracle.py, bit-exact with the
+reference's fit.fit / _process_fit_chunk on the golden vectors) on the same bytes, run on
+the host's CPU share in a spawn Pool (oracle.fit_file_chunk1):
 
 - config 2: all 100,000 segments of R = 4000 (m = 6, 40 dB, device-generated record);
 - config 4's per-GPU shard: the last 200,000 segments of a 1.25 M-segment shard
-  (fitted as one record with the shard's buffer 0 as its seed).
+  (fitted as one record with the shard's buffer 0 as its seed);
+- config 3: two channels of 50,000 segments as two records of one call.
 
-Gates: status equal on >= 99.9 % of segments; status-0 segments
-|d amp|, |d m|, wrapped |d phi|, |d psi| <= 1e-9 against the C port, and where the two
-restatements disagree by more than that (a handful of segments in 10^5), the GPU's
-parameters against the numpy oracle (bit-exact with the reference's fit.fit) on those
-segments: within 1e-9, or within 2e-9 for at most one segment in 10^5 — the documented
-deviation of DESIGN.md §7: at the noise floor the LM's accept / reject of a sub-1e-9
-step turns on the last bits of ssq, and the register path's Bessel pass rounds
-differently from scipy's jv, so the last accepted step (< 1e-9 by the stopping rule,
-fit.py:254-256) can be taken on one side and not on the other. Measured: 1 segment of
-300,000 at 1.005e-9 (global segment 1,249,633, m); on that segment the host build of
-the same register path lands 1.04e-10 or 1.005e-9 from the reference under 1e-14
-relative changes of the QI, the literal general path at the reference's point.
-dc relative <= 1e-12 (the C port sums in plain order over the phase bins)."""
+Gates, with no exceptions: status equal on every segment; status-0
+segments |d amp|, |d m|, wrapped |d phi|, |d psi| <= 1e-9; dc relative <= 1e-13; ssq
+relative <= 1e-6. (Round 3 allowed one segment in 10^5 at 2e-9: the register path's
+Chebyshev recurrence for cos/sin(j psi) made its ssq differences 2x noisier than the
+reference's, enough to flip the accept test of a last ~1e-9 step; the rotation that
+replaced it (lm.h psi_rotate) is 3x quieter than the reference: DESIGN.md §7.)"""
 import ctypes
 import os
 
@@ -42,20 +36,17 @@ def _gpu():
         pytest.skip("no GPU")
 
 
-def _c_fit(x, nseg, threads=16):
-    so = os.path.join(ROOT, "oracle", "libnls_scalar.so")
-    if not os.path.exists(so):
-        pytest.skip("oracle/libnls_scalar.so not built")
-    lib = ctypes.CDLL(so)
-    P = ctypes.c_void_p
-    lib.nls_scalar_record.argtypes = [P, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_double, P,
-                                      ctypes.c_int, P]
-    out = np.zeros((nseg, 7))
-    g = np.array([1.6, 6.0, 0.0, 0.0])
-    threads = min(threads, os.cpu_count() or 1)
-    assert lib.nls_scalar_record(x.ctypes.data, nseg, R, 10, 2 * np.pi * 1000.0 / 200000.0, g.ctypes.data, threads,
-                                 out.ctypes.data) == 0
-    return out
+def _oracle_fit(x, nseg, tmp_path, name):
+    """The numpy oracle over the same bytes (a raw float64 file, read by spawn workers)."""
+    import bench
+    from oracle import nls_oracle as O
+    path = str(tmp_path / f"{name}.f64")
+    np.ascontiguousarray(x, dtype=np.float64).tofile(path)
+    try:
+        procs = max(1, bench.cpu_share()[0])
+        return O.fit_file_chunk1(path, nseg, R, 10, 1000.0, 200000.0, procs)
+    finally:
+        os.unlink(path)
 
 
 def _gpu_fit(xd, nseg):
@@ -74,35 +65,23 @@ def _gpu_fit(xd, nseg):
     return out.cpu().numpy().T, st.cpu().numpy()
 
 
-def _compare(gp, gs, c, x):
-    from oracle import nls_oracle as O
-    st_c = c[:, 6].astype(int)
-    match = gs == st_c
-    assert match.mean() >= 0.999, match.mean()
-    ok = match & (st_c == 0)
+def _compare(gp, gs, ref):
+    st_r = ref[:, 6].astype(int)
+    np.testing.assert_array_equal(gs, st_r)
+    ok = st_r == 0
     assert ok.mean() >= 0.99
-    d = np.stack([np.abs(gp[:, 0] - c[:, 0]), np.abs(gp[:, 1] - c[:, 1]), wrapped(gp[:, 2] - c[:, 2]),
-                  np.abs(gp[:, 3] - c[:, 3])], axis=1)
+    d = np.stack([np.abs(gp[:, 0] - ref[:, 0]), np.abs(gp[:, 1] - ref[:, 1]), wrapped(gp[:, 2] - ref[:, 2]),
+                  np.abs(gp[:, 3] - ref[:, 3])], axis=1)
     d[~ok] = 0.0
-    far = np.nonzero(d.max(axis=1) > 1e-9)[0]
-    assert far.size <= 20, far.size
-    n_wide = 0
-    if far.size:  # the reference's own answer decides: the oracle on those buffers, same seed
-        w0 = 2 * np.pi * 1000.0 / 200000.0
-        _, seed, _ = O.fit_segment(10, O.demod_buffer(x[:R], 10, w0), np.array([1.6, 6.0, 0.0, 0.0]))
-        for b in far:
-            st, po, _ = O.fit_segment(10, O.demod_buffer(x[b * R:(b + 1) * R], 10, w0), seed.copy())
-            assert st == gs[b]
-            dr = np.array([abs(gp[b, 0] - po[0]), abs(gp[b, 1] - po[1]), wrapped(gp[b, 2] - po[2]),
-                           abs(gp[b, 3] - po[3])])
-            assert dr.max() <= 2e-9, (b, dr, d[b])
-            n_wide += int(dr.max() > 1e-9)
-    assert n_wide <= max(1, gs.size // 100_000), n_wide
-    assert np.all(np.abs(gp[:, 4] - c[:, 4]) <= 1e-12 * np.abs(c[:, 4])), np.abs(gp[:, 4] - c[:, 4]).max()
-    return [float(v) for v in d.max(axis=0)], int(far.size)
+    worst = int(np.argmax(d.max(axis=1)))
+    assert d.max() <= 1e-9, (worst, d[worst], int(np.sum(d.max(axis=1) > 1e-9)))
+    assert np.all(np.abs(gp[:, 4] - ref[:, 4]) <= 1e-13 * np.abs(ref[:, 4])), np.abs(gp[:, 4] - ref[:, 4]).max()
+    rs = np.abs(gp[ok, 5] - ref[ok, 5]) / ref[ok, 5]
+    assert rs.max() <= 1e-6, rs.max()
+    return [float(v) for v in d.max(axis=0)], int(np.sum(d.max(axis=1) > 5e-10))
 
 
-def test_config2_every_segment_vs_c_restatement():
+def test_config2_every_segment_vs_oracle(tmp_path):
     import torch
     import bench
     nseg = 100_000
@@ -110,11 +89,11 @@ def test_config2_every_segment_vs_c_restatement():
     gp, gs = _gpu_fit(xd, nseg)
     x = xd.cpu().numpy()
     del xd
-    worst, nfar = _compare(gp, gs, _c_fit(x, nseg), x)
-    print("config 2, 100k segments: max |d amp, m, phi, psi| vs C =", worst, "; checked against the oracle:", nfar)
+    worst, n5 = _compare(gp, gs, _oracle_fit(x, nseg, tmp_path, "c2"))
+    print("config 2, 100k segments: max |d amp, m, phi, psi| vs the oracle =", worst, "; beyond 5e-10:", n5)
 
 
-def test_config4_shard_far_end_vs_c_restatement():
+def test_config4_shard_far_end_vs_oracle(tmp_path):
     """The far end of a 1.25 M-segment shard (global segments [1.05 M, 1.25 M) of the
     record), with that shard's buffer 0 prepended as the seed buffer."""
     import torch
@@ -127,15 +106,15 @@ def test_config4_shard_far_end_vs_c_restatement():
     gp, gs = _gpu_fit(xd, n_tail + 1)
     x = xd.cpu().numpy()
     del xd
-    worst, nfar = _compare(gp, gs, _c_fit(x, n_tail + 1), x)
-    print("config 4 shard, far end (200k segments): max |d amp, m, phi, psi| vs C =", worst,
-          "; checked against the oracle:", nfar)
+    worst, n5 = _compare(gp, gs, _oracle_fit(x, n_tail + 1, tmp_path, "c4"))
+    print("config 4 shard, far end (200k segments): max |d amp, m, phi, psi| vs the oracle =", worst,
+          "; beyond 5e-10:", n5)
 
 
-def test_config3_two_channels_vs_c_restatement():
+def test_config3_two_channels_vs_oracle(tmp_path):
     """Config 3's shape: two channels (main m = 6, witness m = 4.3) of 50,000 segments as
     two records of ONE dfmi_nls_record call, each seeded by its own buffer 0 (as bench.py
-    times it), against the C restatement of each record."""
+    times it), against the oracle on each record."""
     import torch
     import bench
     from deepfmkit_amd import _lib
@@ -161,8 +140,8 @@ def test_config3_two_channels_vs_c_restatement():
     for c in range(2):
         xc = x[c * nbuf * R:(c + 1) * nbuf * R]
         sl = slice(c * nbuf, (c + 1) * nbuf)
-        worst, nfar = _compare(gp[sl], gs[sl], _c_fit(xc, nbuf), xc)
-        print(f"config 3 channel {c}: max |d amp, m, phi, psi| vs C =", worst, "; checked against the oracle:", nfar)
+        worst, n5 = _compare(gp[sl], gs[sl], _oracle_fit(xc, nbuf, tmp_path, f"c3_{c}"))
+        print(f"config 3 channel {c}: max |d amp, m, phi, psi| vs the oracle =", worst, "; beyond 5e-10:", n5)
 
 
 @pytest.mark.parametrize("row,rot,kname", [(1, 1, "ekf_rot_kernel"), (1, 0, "ekf_row_kernel"),

@@ -569,3 +569,27 @@ def test_raw_file_to_fit_file_end_to_end(tmp_path):
     fb = back.fits["x_ch0"]
     for k in ("amp", "m", "phi", "psi", "dc", "ssq"):
         assert np.asarray(getattr(fb, k)).tobytes() == np.asarray(getattr(fits[None], k), dtype=np.float64).tobytes()
+
+
+@pytest.mark.parametrize("kern", ["rot", "row", "lanerot", "lane"])
+@pytest.mark.parametrize("run", ["c5_default", "c5_tuned"])
+def test_ekf_config5_full_length_vs_reference(manifest, kern, run):
+    """Config 5 at full length against the REFERENCE's own EKFFitter states (2 s = 400,000
+    samples, tests/golden/make_ekf_full_golden.py: the defaults of fitters.py:241-257, and a
+    second record with tuned Q / R), through DeepFitFramework.fit(method='ekf') with every
+    EKF kernel: 1e-9 on all 100 snapshots of amp, m, phi, psi, dc."""
+    import os
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "ekf_full.npz"))
+    e = {r["name"]: r for r in manifest["ekf_full"]}[run]
+    dff = make_record(e)
+    assert sha(dff.raws[run].samples()) == e["sha256"]
+    from deepfmkit_amd import _lib
+    lib = _lib.load()
+    with _ekf_kernel(lib, kern) as k:
+        dff.fit(run, method="ekf", fit_label="f", n=20, **e["fit_kwargs"])
+        assert lib.dfmi_last_demod_kernel().decode() == k.kname
+    df = dff.fits_df["f"]
+    assert len(df) == 100
+    for c in ("amp", "m", "phi", "psi", "dc"):
+        err = np.abs(df[c].to_numpy() - d[f"{run}_{c}"]).max()
+        assert err <= 1e-9, (c, err)

@@ -92,3 +92,33 @@ def test_lm_scalar_c_on_reference_lm_vectors(lm_npz, group):
     out = np.zeros((n, 6))
     assert lib.lm_scalar_fit(qi.ctypes.data, n, nd, g.ctypes.data, 4, out.ctypes.data) == 0
     check_lm_group(lm_npz, group, out[:, 5].astype(int), out[:, :4], out[:, 4])
+
+
+@pytest.mark.parametrize("run", ["c5_default", "c5_tuned"])
+def test_ekf_scalar_c_full_length_vs_reference(run):
+    """The scalar C restatement (config 5's CPU baseline) against the reference's own
+    EKFFitter states at full length (2 s = 400,000 samples, tests/golden/ekf_full.npz,
+    default and tuned Q / R): 1e-12 on every snapshot."""
+    if not os.path.exists(SO):
+        pytest.skip("oracle C restatement not built (run __graft_entry__.build())")
+    import json
+    from conftest import make_record, sha
+    with open(os.path.join(ROOT, "tests", "golden", "manifest.json")) as f:
+        e = {r["name"]: r for r in json.load(f)["ekf_full"]}[run]
+    d = np.load(os.path.join(ROOT, "tests", "golden", "ekf_full.npz"))
+    x = np.ascontiguousarray(make_record(e).raws[run].samples(), dtype=np.float64)
+    assert sha(x) == e["sha256"]
+    kw = e["fit_kwargs"]
+    lib = ctypes.CDLL(SO)
+    P = ctypes.c_void_p
+    lib.ekf_scalar.argtypes = [P, ctypes.c_int64, P, P, P, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                               ctypes.c_int64, ctypes.c_int64, P]
+    x0 = np.array([1.6, 6.0, 0.0, 0.0, np.mean(x)])
+    p0 = np.ones(5)
+    qd = np.array(kw.get("Q_diag", [1e-8, 1e-8, 1e-6, 1e-6, 1e-8]), dtype=np.float64)
+    rv = float(kw["R_val"]) if "R_val" in kw else float(np.var(x))
+    out = np.zeros((100, 5))
+    lib.ekf_scalar(x.ctypes.data, x.size, x0.ctypes.data, p0.ctypes.data, qd.ctypes.data, rv, 2 * np.pi * e["f_mod"],
+                   e["f_samp"], 4000, 100, out.ctypes.data)
+    ref = np.stack([d[f"{run}_{k}"] for k in ("amp", "m", "phi", "psi", "dc")], axis=1)
+    assert np.abs(out - ref).max() <= 1e-12, np.abs(out - ref).max()

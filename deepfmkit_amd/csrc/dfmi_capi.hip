@@ -493,8 +493,9 @@ int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, i
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(dfmi::kBlockThreads), lds, st, x, nseg, stride, R, L, ndata,
                      tab, qi, qi_ld, dc, t_ds->probe);
   HIPCHK(hipGetLastError());
-  g_last_demod = std::string("demod_bins_kernel<") + std::to_string(MS) + "," + std::to_string(DFMI_BINS_LOADS) + (ROWS ? ",rows" : "") +
-                 (PFN && (R >> 7) >= PFN ? ",pf4" : "") + ">";
+  g_last_demod = std::string("demod_bins_kernel<") + std::to_string(MS) + "," + std::to_string(DFMI_BINS_LOADS) +
+                 (ROWS ? ",rows" : "") + "," + std::to_string(PFN) + ">" +
+                 (PFN && (R >> 7) >= PFN ? " (prefetch " + std::to_string(PFN) + ")" : "");
   return DFMI_OK;
 }
 
@@ -701,8 +702,13 @@ int fused_seed_demod(int dev, const double* x, int64_t nrec, int64_t nbuf, int R
                      nbuf * (int64_t)R, nrec, R, L, ndata, tab, rows, qs, gdev, ginl, gdev ? 0 : 1, jtab, c, out,
                      out_ld, nbuf, fitok, t_ds->probe);
   HIPCHK(hipGetLastError());
+  // the template arguments of the instance launched (loads in flight / prefetched chunks
+  // from the build's macros, so A/B builds report their own geometry)
+  const bool geo = nslot <= 2 && ndata <= 12;
   g_last_demod = "demod_seed_bins_kernel<" + std::to_string(nslot <= 2 ? 2 : nslot <= 4 ? 4 : 8) + "," +
-                 std::to_string(ndata <= 12 ? 12 : 16) + (pf && (R >> 7) >= 4 ? ",pf4" : "") + ",rows>";
+                 std::to_string(ndata <= 12 ? 12 : 16) + "," + std::to_string(geo ? DFMI_BINS_PFN : 0) + "," +
+                 std::to_string(geo ? DFMI_BINS_LOADS : 8) + ">" +
+                 (pf && (R >> 7) >= DFMI_BINS_PFN ? " (prefetch " + std::to_string(DFMI_BINS_PFN) + ")" : "");
   return DFMI_OK;
 }
 

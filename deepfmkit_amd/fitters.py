@@ -220,7 +220,12 @@ class StandardNLSFitter(BaseFitter):
         if not _is_device_tensor(x):
             x = np.asarray(x, dtype=np.float64)
         devices = kwargs.get("devices")
-        if devices is not None and parallel and kwargs.get("n_cores") is None:
+        if devices is not None and (not parallel or kwargs.get("n_cores") is not None):
+            # a device list spreads the chunk-size-1 parallel fit only; a warm-start chain
+            # (parallel=False, or the n_cores array_split chains) runs on the current GPU
+            raise ValueError("devices= applies to parallel=True without n_cores (chunk size 1); "
+                             f"got parallel={parallel}, n_cores={kwargs.get('n_cores')}")
+        if devices is not None:
             cols, ok = nls_record_devices(x, main_raw.f_samp, main_raw.f_mod, R, nbuf, devices, ndata,
                                           (init_a, init_m, 0.0, init_psi))
             return frame_from(cols, ok)

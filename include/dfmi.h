@@ -121,8 +121,11 @@ int dfmi_nls_record(const double* x, int64_t nrec, int64_t rec_stride, int64_t n
                     double w0, int32_t period, const double* init_guess, int32_t parallel, int64_t nchunk,
                     const dfmi_lm_config* cfg, double* out, int32_t* fitok, int32_t mem, void* stream);
 
-/* Per-sample EKF (fitters.py:214-320) over nrec independent channels, one lane per
- * channel. x[r*rec_stride + k], k < n_samp. x0[r*5+i] initial state (dc included),
+/* Per-sample EKF (fitters.py:214-320) over nrec independent channels, each a serial
+ * chain over its samples: up to 16 x CUs channels one 16-lane DPP row per channel (4 per
+ * wave; ekf_rot_kernel with sin / cos by rotation between anchors when R % 4 == 0, else
+ * ekf_row_kernel), more channels one lane per channel (ekf_lane_rot_kernel / ekf_kernel);
+ * dfmi_set_tuning "ekf_row" / "ekf_rot" select. x[r*rec_stride + k], k < n_samp. x0[r*5+i] initial state (dc included),
  * p0_diag[5], q_diag[5], r_val[r] measurement variance, w_m = 2*pi*f_mod,
  * f_samp; snapshots every R samples into states[(r*nbuf + b)*5 + i]. */
 int dfmi_ekf(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, const double* x0,
@@ -354,9 +357,12 @@ const char* dfmi_last_error(void);
 /* Library/ABI version, e.g. "dfmi 0.3 gfx950". */
 const char* dfmi_version(void);
 
-/* Kernel variant of the last demodulation (or EKF fit) this THREAD launched, e.g.
- * "demod_bins_kernel<2,10,rows,pf4>", "ekf_rot_kernel", "ekf_row_kernel" ("" before the first one).
- * Diagnostics/profiling. */
+/* Kernel variant of the last demodulation (or EKF fit) this THREAD launched, with the
+ * template arguments of the instance (loads in flight and prefetched chunks come from the
+ * build), e.g. "demod_seed_bins_kernel<2,12,4,10> (prefetch 4)" (the record pipeline's
+ * fused seed + demodulation), "demod_bins_kernel<2,10,rows,4> (prefetch 4)" (dfmi_demod_rows),
+ * "ekf_rot_kernel", "ekf_row_kernel", "ekf_lane_rot_kernel", "ekf_kernel" ("" before the
+ * first one). Diagnostics/profiling. */
 const char* dfmi_last_demod_kernel(void);
 
 #ifdef __cplusplus

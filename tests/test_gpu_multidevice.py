@@ -54,3 +54,35 @@ def test_facade_devices_kwarg():
     b = dff.fit("r", n=20, fit_label="b", devices=[0, 0])
     for k in ("amp", "m", "phi", "psi", "dc", "ssq"):
         np.testing.assert_array_equal(getattr(a, k), getattr(b, k))
+
+
+def test_devices_rejected_where_they_would_be_ignored():
+    """devices= spreads the chunk-size-1 parallel fit only; with parallel=False or n_cores
+    (warm-start chains on one GPU) it is an error, not a silently ignored argument."""
+    import deepfmkit_amd as dfm
+    raw = _raw(8, False)
+    f = dfm.fitters.StandardNLSFitter({"n": 20})
+    with pytest.raises(ValueError, match="devices="):
+        f.fit(raw, parallel=False, devices=[0])
+    with pytest.raises(ValueError, match="devices="):
+        f.fit(raw, parallel=True, n_cores=2, devices=[0])
+
+
+def test_sharded_fit_on_distinct_devices():
+    """Two distinct GPUs (skipped on a one-GPU box): the record lives on cuda:1, shards on
+    [0, 1]; the union equals the one-GPU fit bit for bit."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    import deepfmkit_amd as dfm
+    from deepfmkit_amd.physics import SnrSpec, synth_snr
+    nbuf = 2001
+    x1 = synth_snr(SnrSpec(seed=78, m=6.0, snr_db=40.0), 0, nbuf * 4000,
+                   out=torch.empty(nbuf * 4000, dtype=torch.float64, device="cuda:1"))
+    raw = dfm.DeepRawObject(x1)
+    raw.f_samp, raw.f_mod = 200000.0, 1000.0
+    with torch.cuda.device(1):  # the single-call fit where the record lives
+        one = dfm.fitters.StandardNLSFitter({"n": 20}).fit(raw, parallel=True)
+    many = dfm.fitters.StandardNLSFitter({"n": 20}).fit(raw, parallel=True, devices=[0, 1])
+    for k in COLS:
+        np.testing.assert_array_equal(many[k].to_numpy(), one[k].to_numpy(), err_msg=k)

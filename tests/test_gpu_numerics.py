@@ -151,3 +151,33 @@ def test_init_m_with_parallel_is_accepted():
     ref = O.fit_record_parallel(x, 200000.0, 1000.0, 20, init_m=11.0, n_cores=9)
     assert (df["fitok"].to_numpy() == ref[:, 6]).all()
     assert np.abs(df["m"].to_numpy() - ref[:, 1]).max() <= 1e-9
+
+
+@pytest.mark.parametrize("method,nb", [(1, 14), (2, 18)])
+def test_device_bessel_regs_vs_host_build(method, nb):
+    """The register path's Miller pass on the device takes 2/x and 1/S by v_rcp_f64 + two
+    Newton steps (lm.h rcp_nr), the host build of the same header (tests/hostcheck) by IEEE
+    division: an ulp-level deviation by design. Counted here on 200,000 arguments over the
+    fitted range (|x| in [1e-3, 40], both signs): how many J_k differ and by how many ulps,
+    so any drift shows up as a number (the fit's parity is gated elsewhere)."""
+    import ctypes
+    hc_path = os.path.join(os.path.dirname(__file__), "hostcheck", "libhostcheck.so")
+    if not os.path.exists(hc_path):
+        pytest.skip("hostcheck not built")
+    hc = ctypes.CDLL(hc_path)
+    hc.hc_bessel_regs.argtypes = [ctypes.c_double, ctypes.c_int, ctypes.c_void_p]
+    rng = np.random.default_rng(11)
+    x = rng.uniform(1e-3, 40.0, 200_000) * rng.choice([-1.0, 1.0], 200_000)
+    dev = _bessel(x, nb - 1, method).T
+    host = np.zeros_like(dev)
+    row = np.zeros(nb)
+    for i, v in enumerate(x):
+        hc.hc_bessel_regs(float(v), nb, row.ctypes.data)
+        host[i] = row
+    diff = dev != host
+    ulps = np.abs(dev - host) / np.spacing(np.abs(host))
+    frac = diff.mean()
+    print(f"bessel_regs<{nb}> device vs host: {diff.sum()} of {diff.size} values differ ({frac:.3%}), "
+          f"max {ulps.max():.1f} ulp")
+    assert ulps.max() <= 4.0
+    assert frac <= 0.05

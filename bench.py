@@ -137,11 +137,17 @@ def cpu_baseline(args):
     sim = dfm.DFMIObject("cpu", laser, ifo, f_samp=F_SAMP)
     raw = dfm.SignalGenerator().generate(sim, nseg * R / F_SAMP, mode="snr", snr_db=SNR_DB, trial_num=0)["main"]
     x = raw.samples()
-    with get_context("fork").Pool(procs) as pool:
+    # close + join (not the context manager's terminate): the workers exit on their own,
+    # so a profiled run (rocprofv3) records no SIGTERM abort stacks for them
+    pool = get_context("fork").Pool(procs)
+    try:
         O.fit_record_parallel(x[: 4 * R * procs], F_SAMP, F_MOD, N_CYC, n_cores=procs, pool=pool)  # warm
         t0 = time.perf_counter()
         ref = O.fit_record_parallel(x, F_SAMP, F_MOD, N_CYC, n_cores=procs, pool=pool)
         dt = time.perf_counter() - t0
+    finally:
+        pool.close()
+        pool.join()
     base = {"value": round(nseg / dt, 1), "unit": "segments/s", "cores": procs, "kind": "port",
             "sample": f"{nseg} segments of config 2 (R=4000, ndata=10, m=6, 40 dB; the reference's own snr "
                       f"generator, RandomState(0)), numpy restatement of StandardNLSFitter._fit_parallel with "
@@ -267,6 +273,35 @@ def rank_topology(dist, dev, world):
     return allr, dist.get_backend()
 
 
+def window_breakdown(torch, lib, _lib, fn, stream, k):
+    """Where a K-step window's wall time goes (diagnostic, run AFTER the timed window, same
+    K): the same synchronize -> K steps -> synchronize wall clock, split into the GPU span
+    (an event recorded before the first launch to one after the last: the launch lag of the
+    first step after an idle GPU included) and the kernels themselves (dfmi_step_timing events
+    around each step's two launches). wall - span = the host-side sync costs; span - kernels
+    = the first launch's lag plus the gaps between launches."""
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    _lib.check(lib.dfmi_step_timing(1), "dfmi_step_timing")
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(k):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    _lib.check(lib.dfmi_step_timing(0), "dfmi_step_timing")
+    td, tl, tn = np.zeros(1), np.zeros(1), np.zeros(1, dtype=np.int64)
+    _lib.check(lib.dfmi_step_timing_read(_lib.ptr(td), _lib.ptr(tl), _lib.ptr(tn)), "dfmi_step_timing_read")
+    span = e0.elapsed_time(e1)
+    kern = float(td[0] + tl[0])
+    return {"steps": k, "wall_ms_per_step": round(wall * 1e3 / k, 4), "gpu_span_ms_per_step": round(span / k, 4),
+            "kernels_ms_per_step": round(kern / k, 4), "marked_steps": int(tn[0]),
+            "host_sync_ms": round(wall * 1e3 - span, 4), "launch_lag_and_gaps_ms": round(span - kern, 4),
+            "note": "a second K-step window after the timed one, with events: wall = host sync + GPU span; "
+                    "span = kernels + the first launch's lag + inter-launch gaps"}
+
+
 def _timed_steps(torch, fn, steps, warmup):
     for _ in range(warmup):
         fn()
@@ -276,6 +311,40 @@ def _timed_steps(torch, fn, steps, warmup):
         fn()
     torch.cuda.synchronize()
     return (time.perf_counter() - t0) / steps
+
+
+def facade_end_to_end(torch, x, nseg, R, calls=5):
+    """DeepFitFramework.fit(label, n=20) on a record already on the GPU and on the same
+    record in host memory: wall time per call (each call returns the DeepFitObject, i.e.
+    after the results' D2H), median of `calls` calls after one warm call; both give the same
+    bits."""
+    import deepfmkit_amd as dfm
+    res = {}
+    cols = {}
+    xh = x.cpu().numpy()
+    for name, data in (("device_resident", x), ("host_resident", xh)):
+        raw = dfm.DeepRawObject(data)
+        raw.f_samp, raw.f_mod, raw.label = F_SAMP, F_MOD, name
+        dff = dfm.DeepFitFramework()
+        dff.raws[name] = raw
+        dff.fit(name, n=N_CYC, fit_label="e2e")
+        ts = []
+        for _ in range(calls):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fo = dff.fit(name, n=N_CYC, fit_label="e2e")
+            ts.append(time.perf_counter() - t0)
+        t = float(np.median(ts))
+        cols[name] = np.stack([fo.amp, fo.m, fo.phi, fo.psi, fo.dc, fo.ssq])
+        res[name] = {"ms_per_call": round(t * 1e3, 3), "segments_per_s": round(nseg / t, 1),
+                     "calls": calls, "nbuf": int(fo.nbuf)}
+    res["device_resident"]["includes"] = ("StandardNLSFitter dispatch, dfmi_nls_record (seed + demodulation + LM), "
+                                          "D2H of the 7 result columns, DataFrame, tau, DeepFitObject")
+    res["host_resident"]["includes"] = "the same plus H2D of the 3.2 GB record (pinned staging)"
+    res["bit_identical"] = bool(np.array_equal(cols["device_resident"], cols["host_resident"]))
+    res["workload"] = f"config 2: {nseg} segments x R={R}, DeepFitFramework.fit(label, n={N_CYC}) (parallel=True)"
+    del xh
+    return res
 
 
 def extra_configs(torch, dev, lib, _lib, stream, cfg, cpu_leg):
@@ -383,9 +452,15 @@ def extra_configs(torch, dev, lib, _lib, stream, cfg, cpu_leg):
                                  "status0_frac": float(np.mean(k1.cpu().numpy() == 0)),
                                  "reference_same_path": "724 segments/s on one core of the survey container "
                                                         "(SURVEY.md §6)"}
-    # ---- config 2's record through the sequential path: ONE warm-start chain of 100,000 fits
+    # ---- config 2 end to end through the drop-in facade (SURVEY.md §8(d) "Timing":
+    # end-to-end incl. D2H of the results, reported separately): DeepFitFramework.fit on
+    # the 100,000-segment record (core.py:424-517 -> StandardNLSFitter -> dfmi_nls_record ->
+    # D2H of the 7 columns -> DataFrame -> tau -> DeepFitObject), device-resident and
+    # host-resident (+ H2D of the 3.2 GB record through pinned staging)
     nb2 = 2 * nbuf
     gen_shard(torch, dev, 0, nb2, R, seed=SEED, out=x)
+    out["config2_end_to_end"] = facade_end_to_end(torch, x, nb2, R)
+    # ---- config 2's record through the sequential path: ONE warm-start chain of 100,000 fits
     o4 = torch.empty((6, nb2), dtype=torch.float64, device=dev)
     k4 = torch.empty(nb2, dtype=torch.int32, device=dev)
 
@@ -398,7 +473,41 @@ def extra_configs(torch, dev, lib, _lib, stream, cfg, cpu_leg):
     out["config2_sequential"] = {"workload": "100,000 segments (config 2's record), parallel=False: one warm-start "
                                              "chain", "value": round(nb2 / t2, 1), "unit": "segments/s",
                                  "s_per_record": round(t2, 4), "status0_frac": float(np.mean(k4.cpu().numpy() == 0))}
+    del x, o4, k4
+    torch.cuda.empty_cache()
+    # ---- config 4's per-GPU shard on this one GPU: the same-workload N = 1 point of the
+    # driver's 1 -> 8 curve (each of 8 ranks fits 1.25 M segments = 40 GB of config 4)
+    out["config4_shard_1gpu"] = config4_shard_point(torch, dev, lib, _lib, stream, cfg)
     return out
+
+
+def config4_shard_point(torch, dev, lib, _lib, stream, cfg, steps=20, warmup=5):
+    """bench.py's step over CONFIG4_SEGMENTS / 8 segments on one GPU: rank 0's shard of the
+    10M-segment record at N = 8 (global segments [0, 1.25 M), buffer 0 first)."""
+    from deepfmkit_amd.fitters import w0_of
+    R = int(F_SAMP / F_MOD * N_CYC)
+    nseg = CONFIG4_SEGMENTS // 8
+    x = torch.empty(nseg * R, dtype=torch.float64, device=dev)
+    gen_shard(torch, dev, 0, nseg, R, seed=SEED, out=x)
+    g = np.array([1.6, 6.0, 0.0, 0.0])
+    o = torch.empty((6, nseg), dtype=torch.float64, device=dev)
+    k = torch.empty(nseg, dtype=torch.int32, device=dev)
+    w0 = w0_of(F_MOD, F_SAMP)
+
+    def step():
+        _lib.check(lib.dfmi_nls_record(x.data_ptr(), 1, nseg * R, nseg, R, NDATA, w0, 0, _lib.ptr(g), 1, nseg - 1, cfg,
+                                       o.data_ptr(), k.data_ptr(), _lib.DFMI_MEM_DEVICE, stream.cuda_stream),
+                   "dfmi_nls_record")
+
+    t = _timed_steps(torch, step, steps, warmup)
+    st = k.cpu().numpy()
+    res = {"workload": f"config 4 per-GPU shard: {nseg} segments (40 GB resident) x R={R}, one record, chunk size 1",
+           "value": round(nseg / t, 1), "unit": "segments/s", "ms_per_step": round(t * 1e3, 4), "steps": steps,
+           "warmup": warmup, "status0_frac": float(np.mean(st == 0)),
+           "hbm_frac_end_to_end": round(nseg * (8 * R + 56) / t / 1e9 / HBM_PEAK_GBS, 4)}
+    del x, o, k
+    torch.cuda.empty_cache()
+    return res
 
 
 def main():
@@ -498,36 +607,10 @@ def main():
                                  stream.cuda_stream)
         _lib.check(rc, "dfmi_demod_rows")
 
-    # ---- roofline of the step's dominant kernel, HIP events on the launch stream ----
-    # (measured BEFORE the timed window: these untimed launches also bring the GPU to its
-    # steady clocks, so a short driver window carries no ramp-up)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    # untimed: clocks ramp up over the first ~35 demodulation-sized launches (0.58 -> 0.50 ms,
-    # profiles/r02m kernel trace)
-    for _ in range(40):
-        step()
-    # 200 steps (~0.11 s): the kernel's mean over these dominates any rocprofv3 average of the
-    # same run, ramp launches included (profiles/r03*_frac_check.json)
     nrep = max(200, args.steps)
-    # the step itself with timing events around its kernels (dfmi_step_timing): the fused
-    # seed + demodulation launch (the dominant kernel) and the LM launch, on the step's stream
-    _lib.check(lib.dfmi_step_timing(1), "dfmi_step_timing")
-    for _ in range(nrep):
-        step()
-    _lib.check(lib.dfmi_step_timing(0), "dfmi_step_timing")
-    td, tl, tn = np.zeros(1), np.zeros(1), np.zeros(1, dtype=np.int64)
-    _lib.check(lib.dfmi_step_timing_read(_lib.ptr(td), _lib.ptr(tl), _lib.ptr(tn)), "dfmi_step_timing_read")
-    step_kname = lib.dfmi_last_demod_kernel().decode()
-    if int(tn[0]) != nrep:
-        raise SystemExit(f"step timing: {int(tn[0])} marked steps of {nrep} (pipeline not fused: {step_kname})")
-    demod_ms, lm_step_ms = float(td[0]) / nrep, float(tl[0]) / nrep
-    demod_ms_max = demod_ms
-    if world > 1:  # the slowest rank's dominant kernel (every rank runs the same shape)
-        tt = torch.tensor([demod_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        demod_ms_max = float(tt.item())
-    kname = step_kname
-    # the standalone row demodulation (dfmi_demod_rows, no seed): the same bulk code
+    # ---- side measurements first (untimed): the standalone row demodulation (dfmi_demod_rows,
+    # no seed: the same bulk code) and the LM kernel alone over component-major QI
     for _ in range(5):
         demod()
     ev0.record(stream)
@@ -544,7 +627,6 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    # the LM kernel alone over the same QI (every segment its own chunk), for the record
     lm_out = torch.empty((4, nall), dtype=torch.float64, device=dev)
     lm_ssq = torch.empty(nall, dtype=torch.float64, device=dev)
     lm_st = torch.empty(nall, dtype=torch.int32, device=dev)
@@ -564,7 +646,41 @@ def main():
     ev1.record(stream)
     ev1.synchronize()
     lm_ms = ev0.elapsed_time(ev1) / nrep
-    fn = demod if args.demod_only else step
+    # ---- roofline of the step's dominant kernel, HIP events on the launch stream, over
+    # whole steps: these untimed steps are also the ramp immediately before the window (the
+    # clocks come up over the first ~35 demodulation-sized launches, 0.58 -> 0.50 ms,
+    # profiles/r02m kernel trace), so a short driver window carries no ramp-up
+    for _ in range(40):
+        step()
+    # nrep >= 200 steps (~0.11 s): the kernel's mean over these dominates any rocprofv3 average
+    # of the same run, ramp launches included (profiles/r03*_frac_check.json); dfmi_step_timing
+    # records events around the fused seed + demodulation launch (the dominant kernel) and
+    # the LM launch of every step, on the step's stream
+    _lib.check(lib.dfmi_step_timing(1), "dfmi_step_timing")
+    for _ in range(nrep):
+        step()
+    _lib.check(lib.dfmi_step_timing(0), "dfmi_step_timing")
+    td, tl, tn = np.zeros(1), np.zeros(1), np.zeros(1, dtype=np.int64)
+    _lib.check(lib.dfmi_step_timing_read(_lib.ptr(td), _lib.ptr(tl), _lib.ptr(tn)), "dfmi_step_timing_read")
+    step_kname = lib.dfmi_last_demod_kernel().decode()
+    if int(tn[0]) != nrep:
+        raise SystemExit(f"step timing: {int(tn[0])} marked steps of {nrep} (pipeline not fused: {step_kname})")
+    demod_ms, lm_step_ms = float(td[0]) / nrep, float(tl[0]) / nrep
+    demod_ms_max = demod_ms
+    per_rank = [{"rank": rank, "step_demod_seed_ms": round(demod_ms, 4), "step_lm_ms": round(lm_step_ms, 4)}]
+    if world > 1:  # the slowest rank's dominant kernel (every rank runs the same shape)
+        tt = torch.tensor([demod_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        demod_ms_max = float(tt.item())
+        # every rank's fused launch carries its own fit of the record's buffer 0 (the seed):
+        # reported per rank, so a rank whose seed fit runs long shows here
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, {"rank": rank, "step_demod_seed_ms": round(demod_ms, 4),
+                                          "step_lm_ms": round(lm_step_ms, 4)})
+    kname = step_kname
+    fn = step
+    # ---- the timed window: W untimed warmup steps, barrier + synchronize, exactly K steps,
+    # synchronize + barrier, MAX over ranks
     for _ in range(args.warmup):
         fn()
     torch.cuda.synchronize()
@@ -582,6 +698,7 @@ def main():
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
+    window_diag = window_breakdown(torch, lib, _lib, fn, stream, args.steps)
     ms = el / args.steps * 1e3
     total_segments = nseg * world  # units of work; the seed replicas on ranks > 0 are not counted
     value = total_segments * args.steps / el
@@ -605,7 +722,11 @@ def main():
         if family and family in rec.get("kernel", "") and rec.get("algorithmic_bytes_per_launch") == \
                 nall * bytes_per_seg:
             traffic, traffic_src = rec.get("hbm_bytes_per_launch"), "profiles/pmc_demod.json"
-    e2e = nall * bytes_per_seg / (ms * 1e-3) / 1e9  # the whole step (seed + demodulation + LM) at the same bytes
+    # the whole step (seed + demodulation + LM) at SURVEY.md §8(d)'s algorithmic bytes per
+    # segment: 8 R read + 56 B of results (6 fp64 + the status padded to 8 B); the 168-B
+    # demodulation rows are an intermediate of the step, not its output
+    e2e_bytes_per_seg = 8 * R + 56
+    e2e = nall * e2e_bytes_per_seg / (ms * 1e-3) / 1e9
     roof = {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "traffic_source": traffic_src, "avg_launch_ms": round(demod_ms, 4),
@@ -613,8 +734,8 @@ def main():
                       f"(dfmi_step_timing), mean over {nrep} steps",
             "algorithmic_bytes_per_launch": nall * bytes_per_seg,
             "end_to_end_frac": round(e2e / HBM_PEAK_GBS, 4),
-            "end_to_end_note": "algorithmic bytes of the step / ms_per_step / peak: the LM after the "
-                               "demodulation included"}
+            "end_to_end_note": "SURVEY.md §8(d) algorithmic bytes of the step (8 R + 56 B per segment) / "
+                               "ms_per_step / peak: the seed and the LM after the demodulation included"}
     if world > 1:
         roof["avg_launch_ms_max_over_ranks"] = round(demod_ms_max, 4)
         roof["frac_min_over_ranks"] = round(nall * bytes_per_seg / (demod_ms_max * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
@@ -641,10 +762,10 @@ def main():
             "roofline": roof,
             "kernels_ms": {"step_demod_seed": round(demod_ms, 4), "step_lm": round(lm_step_ms, 4),
                            "demod_rows_alone": round(rows_ms, 4), "lm_alone_all_segments": round(lm_ms, 4)},
+            "window_breakdown": window_diag,
+            "per_rank_kernels_ms": per_rank,
             "batch_status0_frac": float(np.mean(st == 0)),
             "batch_m_mean": float(res[1].mean())}
-    if args.demod_only:
-        line["metric"] = "demod only (profile helper)"
     if args.tune:
         line["tuning"] = args.tune
     if world == 1 and not args.no_extra and nrec == 1 and args.segments is None:

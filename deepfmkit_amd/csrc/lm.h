@@ -501,6 +501,26 @@ DFMI_HDI void eval_gen(const QF& q, int nd, const double (&p)[4], Eval& e) {
   });
 }
 
+// ssqf (fit.py:152-167) on the general path: the ssq part of eval_gen alone, the same
+// operations in the same order (harmonic_term's rq, ri and its two fma accumulations over
+// the descending harmonic walk), so it equals eval_gen(...).ssq bit for bit.
+template <typename QF>
+DFMI_HDI double ssq_gen(const QF& q, int nd, const double (&p)[4]) {
+  const double a = p[0], m = p[1], phi = p[2], psi = p[3];
+  double sph, cph;
+  sincos(phi, &sph, &cph);
+  double ssq = 0.0;
+  harmonic_walk(nd, m, psi, [&](int j, double, double J0, double, double cj, double sj) {
+    const double pt = quarter_turn(j, cph, sph);
+    const double common = a * pt * J0;
+    const double rq = fma(-common, cj, q.qc(j - 1));
+    const double ri = fma(common, sj, q.qs(j - 1));
+    ssq = fma(rq, rq, ssq);
+    ssq = fma(ri, ri, ssq);
+  });
+  return ssq;
+}
+
 // ---------------------------------------------------------------------------
 // Shared LM pieces
 // ---------------------------------------------------------------------------
@@ -624,22 +644,28 @@ DFMI_HDI double lm_descend_flat(Ev&& ev, double (&p)[4], const LMConst& c) {
   return e.ssq;
 }
 
-// Evaluators for the descents: a full literal evaluation per trial + the pivoting
-// 4x4 solve (general path), or the structured register path (trial = ssqf only, the
-// Jacobian added on acceptance, block-diagonal solve).
-template <typename EvalFn>
-struct FullEval {
-  EvalFn f;
+// Evaluators for the descents: trial(p, t) = ssqf at p, accept(p, t, e) = coeffs at an
+// accepted p, solve = msolve. General path (GenSplitEval): the literal evaluation + the
+// pivoting 4x4 solve; register path (SplitEval): the structured evaluation, block-diagonal
+// solve.
+// General path, split like the register path: a trial evaluates ssqf only (ssq_gen), the
+// literal coeffs (eval_gen: J^T J, J^T r) runs at accepted points only; same bits as
+// a full literal evaluation per trial (ssq_gen == eval_gen().ssq), about half the work per rejected rung — the rungs a
+// descent walks at the noise floor or far from the minimum (the record pipeline's seed).
+template <typename QF>
+struct GenSplitEval {
+  const QF& q;
+  int nd;
   struct Trial {
-    Eval e;
+    double ssq;
   };
   DFMI_HDI double trial(const double (&p)[4], Trial& t) {
-    f(p, t.e);
-    return t.e.ssq;
+    t.ssq = ssq_gen(q, nd, p);
+    return t.ssq;
   }
-  DFMI_HDI void accept(const double (&)[4], const Trial& t, Eval& e) { e = t.e; }
+  DFMI_HDI void accept(const double (&p)[4], const Trial&, Eval& e) { eval_gen(q, nd, p, e); }
   DFMI_HDI void solve(const Eval& e, double lam, double (&dp)[4]) { damped_solve(e, lam, dp); }
-  DFMI_HDI static double ssq_of(const Trial& t) { return t.e.ssq; }
+  DFMI_HDI static double ssq_of(const Trial& t) { return t.ssq; }
 };
 
 template <int NDMAX, typename QF>
@@ -867,7 +893,7 @@ DFMI_HDI void m_grid_seed(QF&& Q, int ndata, const double* __restrict__ jtab, co
 }
 
 // fit.py:322-361 (fit): LM, status + grid retry, normalisation, phi wrap.
-// Ev: the evaluator (FullEval / SplitEval); FLAT = false runs the nested descent
+// Ev: the evaluator (GenSplitEval / SplitEval); FLAT = 0 runs the nested descent
 // (host build / equivalence tests). Q: QI accessor for the m-grid re-seed (runtime
 // harmonic index: memory, never a register array).
 template <int FLAT = 1, typename Ev, typename QF>
@@ -926,8 +952,7 @@ __host__ __device__ __forceinline__ int fit_segment_q2(const QE& qe, const QM& q
     SplitEval<NDMAX, QE> ev{qe, ndata, c.trig};
     return fit_segment_t<FLAT>(ev, qm, ndata, jtab, c, p, ssq_out);
   } else {
-    auto evalf = [&](const double (&pp)[4], Eval& e) { eval_gen(qe, ndata, pp, e); };
-    FullEval<decltype(evalf)> ev{evalf};
+    GenSplitEval<QE> ev{qe, ndata};
     return fit_segment_t<FLAT>(ev, qm, ndata, jtab, c, p, ssq_out);
   }
 }

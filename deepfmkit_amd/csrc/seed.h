@@ -22,6 +22,15 @@ namespace dfmi {
 // so the seed (and with it every chunk's start) does not depend on the scheduling.
 constexpr int kSeedPath = 0;
 
+// The seed's fit is run by a WHOLE wave: the lambda ladder of every LM iteration is tried
+// 8 rungs at a time by 8-lane groups (lm_descend_ladder, FLAT = 2: bit-identical to the
+// one-lane descent, tests/test_gpu_numerics.py::test_lm_ladder_bit_identical); every group
+// of the wave runs the same fit and lane 0 writes it. A seed whose descent walks the whole
+// ladder at many iterations (records whose phase the default guess does not reach, e.g.
+// phi = 1.3, psi = 0.4: ~27 ms one lane at a time) then costs ~1/8 of the
+// passes, so it stays hidden under (or close to) the bulk demodulation.
+constexpr int kSeedFlat = 2;
+
 template <int NDMAX>
 __global__ __launch_bounds__(64) void seed_kernel(const double* __restrict__ x, int64_t rec_stride, int R, int L,
                                                   int ndata, double w0, const double* __restrict__ tab,
@@ -35,8 +44,7 @@ __global__ __launch_bounds__(64) void seed_kernel(const double* __restrict__ x, 
   const double* __restrict__ xs = x + r * rec_stride;
   if (L > 0) fold_segment<1, 16>(xs, R, L, ndata, tab, lane, qis, nrec, r, dcs);
   else direct_segment(xs, R, ndata, w0, lane, qis, nrec, r, dcs);
-  __syncthreads();  // QI of this record (global, same workgroup) visible to lane 0
-  if (lane != 0) return;
+  __syncthreads();  // QI of this record (global, same workgroup) visible to the wave
   double p[4] = {0.0, 0.0, 0.0, 0.0};
   if (use_inline) {
 #pragma unroll
@@ -51,7 +59,8 @@ __global__ __launch_bounds__(64) void seed_kernel(const double* __restrict__ x, 
     for (int i = 0; i < 4; ++i) p[i] = guess[r * 4 + i];
   }
   double ssq;
-  const int st = fit_segment<kSeedPath>(qis + r, nrec, ndata, jtab, c, p, ssq);
+  const int st = fit_segment<kSeedPath, kSeedFlat>(qis + r, nrec, ndata, jtab, c, p, ssq);
+  if (lane != 0) return;
   const int64_t sidx = r * nbuf;
   out[0 * out_ld + sidx] = p[0];
   out[1 * out_ld + sidx] = p[1];
@@ -121,7 +130,6 @@ __global__ __launch_bounds__(64) void seed_bins_kernel(const double* __restrict_
                                                         row, 0, 0, nullptr);
   __syncthreads();
   const uint64_t t_fold = __builtin_amdgcn_s_memrealtime();
-  if (lane != 0) return;
   double p[4] = {0.0, 0.0, 0.0, 0.0};
   if (use_inline) {
 #pragma unroll
@@ -137,7 +145,8 @@ __global__ __launch_bounds__(64) void seed_bins_kernel(const double* __restrict_
   }
   double ssq;
   const QRow<1> q{row};
-  const int st = fit_segment_q<kSeedPath>(q, ndata, jtab, c, p, ssq);
+  const int st = fit_segment_q<kSeedPath, QRow<1>, kSeedFlat>(q, ndata, jtab, c, p, ssq);
+  if (lane != 0) return;
   const int64_t sidx = r * nbuf;
   out[0 * out_ld + sidx] = p[0];
   out[1 * out_ld + sidx] = p[1];
@@ -220,7 +229,7 @@ __global__ __launch_bounds__(kBlockThreads) void demod_seed_bins_kernel(
   }
   __syncthreads();
   const uint64_t t_fold = __builtin_amdgcn_s_memrealtime();
-  if (threadIdx.x != 0) return;
+  if (wave != 0) return;
   double p[4] = {0.0, 0.0, 0.0, 0.0};
   if (use_inline) {
 #pragma unroll
@@ -236,7 +245,8 @@ __global__ __launch_bounds__(kBlockThreads) void demod_seed_bins_kernel(
   }
   double ssq;
   const QRow<1> q{row};
-  const int st = fit_segment_q<kSeedPath>(q, ndata, jtab, c, p, ssq);
+  const int st = fit_segment_q<kSeedPath, QRow<1>, kSeedFlat>(q, ndata, jtab, c, p, ssq);
+  if (lane != 0) return;
   const int64_t sidx = r * nbuf;
   out[0 * out_ld + sidx] = p[0];
   out[1 * out_ld + sidx] = p[1];

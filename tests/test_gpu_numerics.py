@@ -181,3 +181,78 @@ def test_device_bessel_regs_vs_host_build(method, nb):
           f"max {ulps.max():.1f} ulp")
     assert ulps.max() <= 4.0
     assert frac <= 0.05
+
+
+@pytest.mark.parametrize("phi,psi,noise_only", [(1.3, 0.4, False), (0.0, 0.0, False), (1.0, 1.0, False),
+                                                (0.0, 0.0, True)])
+def test_seed_wave_ladder_equals_one_lane_general_fit(phi, psi, noise_only):
+    """The record pipeline's seed (buffer 0 of the record, fitted inside the fused seed +
+    demodulation launch by a whole wave on the 8-lane lambda ladder, seed.h kSeedFlat) gives
+    the bits of the one-lane general-path fit of the same QI (dfmi_demod + dfmi_lm with
+    lm_general = 1, lm_ladder = 0): records whose phase the default guess cannot reach
+    (psi = 0.4 / 1.0: the descent walks the whole ladder, status 2, m-grid retry) and a
+    noise-only seed buffer. The phi = 1.3, psi = 0.4 record's step took 29.6 ms with the
+    one-lane seed; it is timed here."""
+    import time
+    import torch
+    import bench
+    from deepfmkit_amd import _lib
+    from deepfmkit_amd import fit as F
+    from deepfmkit_amd.fitters import w0_of
+    from deepfmkit_amd.physics import SnrSpec, synth_snr
+    lib = _lib.load()
+    R, nseg = 4000, 20000
+    dev = torch.device("cuda", 0)
+    x = torch.empty(nseg * R, dtype=torch.float64, device=dev)
+    synth_snr(SnrSpec(seed=bench.SEED, f_samp=200000.0, f_mod=1000.0, m=6.0, phi=phi, psi=psi, snr_db=40.0), 0,
+              nseg * R, out=x)
+    if noise_only:
+        x[:R] = 0.5 + 0.3 * torch.randn(R, dtype=torch.float64, device=dev, generator=torch.Generator(
+            device="cuda").manual_seed(3))
+    w0 = w0_of(1000.0, 200000.0)
+    g = np.array([1.6, 6.0, 0.0, 0.0])
+    st = torch.cuda.current_stream().cuda_stream
+    out = torch.empty((6, nseg), dtype=torch.float64, device=dev)
+    ok = torch.empty(nseg, dtype=torch.int32, device=dev)
+
+    def step():
+        _lib.check(lib.dfmi_nls_record(x.data_ptr(), 1, nseg * R, nseg, R, 10, w0, 0, _lib.ptr(g), 1, nseg - 1,
+                                       F.lm_config(), out.data_ptr(), ok.data_ptr(), _lib.DFMI_MEM_DEVICE, st),
+                   "dfmi_nls_record")
+
+    step()
+    torch.cuda.synchronize()
+    assert lib.dfmi_last_demod_kernel().decode().startswith("demod_seed_bins_kernel")
+    t0 = time.perf_counter()
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / 3 * 1e3
+    seed = out[:, 0].cpu().numpy()
+    seed_st = int(ok[0].item())
+    qi = torch.empty((20, 1), dtype=torch.float64, device=dev)
+    dc = torch.empty(1, dtype=torch.float64, device=dev)
+    _lib.check(lib.dfmi_demod(x.data_ptr(), 1, R, R, 10, w0, 0, qi.data_ptr(), dc.data_ptr(), _lib.DFMI_MEM_DEVICE,
+                              st), "dfmi_demod")
+    gd = torch.tensor([1.6, 6.0, 0.0, 0.0], dtype=torch.float64, device=dev)
+    p = torch.empty((4, 1), dtype=torch.float64, device=dev)
+    ssq = torch.empty(1, dtype=torch.float64, device=dev)
+    s1 = torch.empty(1, dtype=torch.int32, device=dev)
+    old = {k: np.zeros(1, dtype=np.int64) for k in (b"lm_general", b"lm_ladder")}
+    for k in old:
+        _lib.check(lib.dfmi_get_tuning(k, _lib.ptr(old[k])), "get")
+    try:
+        _lib.check(lib.dfmi_set_tuning(b"lm_general", 1), "set")
+        _lib.check(lib.dfmi_set_tuning(b"lm_ladder", 0), "set")
+        _lib.check(lib.dfmi_lm(qi.data_ptr(), 1, 10, gd.data_ptr(), 0, 1, F.lm_config(), p.data_ptr(), ssq.data_ptr(),
+                               s1.data_ptr(), _lib.DFMI_MEM_DEVICE, st), "dfmi_lm")
+        torch.cuda.synchronize()
+    finally:
+        for k, v in old.items():
+            _lib.check(lib.dfmi_set_tuning(k, int(v[0])), "set")
+    np.testing.assert_array_equal(seed[:4], p[:, 0].cpu().numpy())
+    assert seed[5] == ssq[0].item() and seed_st == int(s1[0].item())
+    assert seed[4] == dc[0].item()
+    print(f"phi={phi} psi={psi} noise_only={noise_only}: seed status {seed_st}, step {ms:.3f} ms "
+          f"({nseg} segments)")
+    assert ms < 10.0

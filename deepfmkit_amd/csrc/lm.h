@@ -645,9 +645,31 @@ DFMI_HDI double lm_descend_flat(Ev&& ev, double (&p)[4], const LMConst& c) {
 }
 
 // Evaluators for the descents: trial(p, t) = ssqf at p, accept(p, t, e) = coeffs at an
-// accepted p, solve = msolve. General path (GenSplitEval): the literal evaluation + the
-// pivoting 4x4 solve; register path (SplitEval): the structured evaluation, block-diagonal
-// solve.
+// accepted p, solve = msolve. General path (GenSplitEval one lane per fit, FullGenEval on
+// the lambda ladder): the literal evaluation + the pivoting 4x4 solve; register path
+// (SplitEval): the structured evaluation, block-diagonal solve.
+// General path, one full literal evaluation per trial: the trial state is the whole Eval,
+// so an accepted trial needs no second evaluation. The lambda-ladder descent takes this
+// one (its 8 lanes evaluate 8 rungs at once and accept by shuffling the taken rung's state):
+// with GenSplitEval there the seed of a phi = 1.3, psi = 0.4 record took 17.5 ms against
+// 9.2 ms (tests/test_gpu_numerics.py::test_seed_wave_ladder_equals_one_lane_general_fit,
+// r04c), every accepted iteration paying a second evaluation.
+template <typename QF>
+struct FullGenEval {
+  const QF& q;
+  int nd;
+  struct Trial {
+    Eval e;
+  };
+  DFMI_HDI double trial(const double (&p)[4], Trial& t) {
+    eval_gen(q, nd, p, t.e);
+    return t.e.ssq;
+  }
+  DFMI_HDI void accept(const double (&)[4], const Trial& t, Eval& e) { e = t.e; }
+  DFMI_HDI void solve(const Eval& e, double lam, double (&dp)[4]) { damped_solve(e, lam, dp); }
+  DFMI_HDI static double ssq_of(const Trial& t) { return t.e.ssq; }
+};
+
 // General path, split like the register path: a trial evaluates ssqf only (ssq_gen), the
 // literal coeffs (eval_gen: J^T J, J^T r) runs at accepted points only; same bits as
 // a full literal evaluation per trial (ssq_gen == eval_gen().ssq), about half the work per rejected rung — the rungs a
@@ -951,7 +973,10 @@ __host__ __device__ __forceinline__ int fit_segment_q2(const QE& qe, const QM& q
   if constexpr (NDMAX > 0) {
     SplitEval<NDMAX, QE> ev{qe, ndata, c.trig};
     return fit_segment_t<FLAT>(ev, qm, ndata, jtab, c, p, ssq_out);
-  } else {
+  } else if constexpr (FLAT == 2) {  // lambda ladder: full trials (FullGenEval)
+    FullGenEval<QE> ev{qe, ndata};
+    return fit_segment_t<FLAT>(ev, qm, ndata, jtab, c, p, ssq_out);
+  } else {  // one lane per fit: ssqf-only trials, coeffs at accepted points (GenSplitEval)
     GenSplitEval<QE> ev{qe, ndata};
     return fit_segment_t<FLAT>(ev, qm, ndata, jtab, c, p, ssq_out);
   }

@@ -102,6 +102,11 @@ def main():
         chk(lib.dfmi_nls_record(x.data_ptr(), 1, nseg * R, nseg, R, nd, w0, 0, g.ctypes.data, 0, 1, cfg,
                                 sa[k].data_ptr(), ka[k].data_ptr(), 1, P(st.cuda_stream)), lib)
 
+    for kv in filter(None, os.environ.get("TUNE", "").split(",")):  # e.g. TUNE=lm_general=1 on every library
+        k, v = kv.split("=")
+        for lib in libs.values():
+            lib.dfmi_set_tuning.argtypes = [ctypes.c_char_p, ctypes.c_int64]
+            chk(lib.dfmi_set_tuning(k.encode(), int(v)), lib)
     first = next(iter(libs.values()))
     chk(first.dfmi_demod(x.data_ptr(), nseg, R, R, nd, w0, 0, qi.data_ptr(), dc.data_ptr(), 1, P(st.cuda_stream)),
         first)
@@ -146,7 +151,7 @@ def main():
             "seq_max_abs_dm": float((s1[a][1] - s1[b][1]).abs().max())}
         if seqall:
             eq[f"{a}_vs_{b}"]["seqall"] = bool(torch.equal(sa[a], sa[b]) and torch.equal(ka[a], ka[b]))
-    print(json.dumps({"ms": summary, "bit_identical": eq, "libs": spec, "rounds": rounds,
+    print(json.dumps({"ms": summary, "bit_identical": eq, "libs": spec, "rounds": rounds, "tune": os.environ.get("TUNE", ""),
                       "phi": PHI, "psi": PSI}), flush=True)
 
 

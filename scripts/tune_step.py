@@ -33,7 +33,10 @@ def main():
     dev = torch.device("cuda", 0)
     lib = _lib.load()
     nseg, R, nd = int(os.environ.get("NSEG", 100000)), 4000, 10
-    x = bench.gen_shard(torch, dev, 0, nseg, R, seed=1)
+    from deepfmkit_amd.physics import SnrSpec, synth_snr
+    x = torch.empty(nseg * R, dtype=torch.float64, device=dev)
+    synth_snr(SnrSpec(seed=1, f_samp=200000.0, f_mod=1000.0, m=6.0, phi=float(os.environ.get("PHI", 0.0)),
+                      psi=float(os.environ.get("PSI", 0.0)), snr_db=40.0), 0, nseg * R, out=x)
     st = torch.cuda.current_stream()
     w0 = w0_of(1000.0, 200000.0)
     cfg = F.lm_config()
@@ -68,9 +71,13 @@ def main():
         else:
             d = (cur - ref).abs().max().item()
             print(f"{s}: max|diff| vs first setting = {d:.3e}", file=sys.stderr)
-            assert d <= 1e-8, (s, d)  # settings that change the seed's summation order move results ~1e-11
+            if os.environ.get("BITS") == "1":
+                assert d == 0.0, (s, d)
+            else:
+                assert d <= 1e-8, (s, d)  # settings that change the seed's summation order move results ~1e-11
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     res = {i: [] for i in range(len(settings))}
+    lm = {i: [] for i in range(len(settings))}
     for _ in range(6):
         for i, s in enumerate(settings):
             apply(s)
@@ -81,11 +88,20 @@ def main():
             ev1.record(st)
             ev1.synchronize()
             res[i].append(ev0.elapsed_time(ev1) / 5)
+            # the LM launch of 5 more steps (dfmi_step_timing events around each step's launches)
+            _lib.check(lib.dfmi_step_timing(1), "t")
+            for _ in range(5):
+                step()
+            _lib.check(lib.dfmi_step_timing(0), "t")
+            td, tl, tn = np.zeros(1), np.zeros(1), np.zeros(1, dtype=np.int64)
+            _lib.check(lib.dfmi_step_timing_read(_lib.ptr(td), _lib.ptr(tl), _lib.ptr(tn)), "read")
+            lm[i].append(float(tl[0]) / max(1, int(tn[0])))
     outj = {}
     for i, s in enumerate(settings):
         med = float(np.median(res[i]))
         outj[",".join(f"{k}={v}" for k, v in s.items()) or "default"] = {
-            "ms_per_step": round(med, 4), "Mseg_per_s": round(nseg / med / 1e3, 2)}
+            "ms_per_step": round(med, 4), "Mseg_per_s": round(nseg / med / 1e3, 2),
+            "lm_ms": round(float(np.median(lm[i])), 4)}
     print(json.dumps(outj, indent=1))
 
 

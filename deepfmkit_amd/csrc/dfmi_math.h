@@ -143,6 +143,47 @@ DFMI_HD double dfmi_bessel_series(int k, double x) {
   return t * (1.0 - h * h / (double)(k + 1));
 }
 
+// Large arguments: the backward recurrence starts ~1.1|x| orders up, so at |x| ~ 900 (a
+// descent running away from a guess that cannot reach the data, the seed of DESIGN.md §4)
+// one evaluation walks ~1,000 orders twice. For |x| >= DFMI_BES_LARGE with the wanted orders
+// below |x| / 2: J_0, J_1 by their Hankel asymptotic expansions (Abramowitz & Stegun
+// 9.2.5-9.2.10: J_n = sqrt(2 / (pi x)) (P cos chi - Q sin chi), chi = x - (n/2 + 1/4) pi,
+// P, Q series in 1/x with a_k = prod_{i<=k} (4n^2 - (2i-1)^2) / (k! 8^k), 7 terms each: the
+// next term is < 1e-17 relative at |x| = 64), then J_{k+1} = (2k / x) J_k - J_{k-1} upward
+// (no dominant solution for k < |x|: errors grow ~ k eps). Measured against mpmath for
+// |x| in [64, 5000], orders 0..13: max abs error 4.2e-17 (scripts/study notes,
+// tests/test_host_numerics.py::test_bessel_large_argument_vs_scipy). The phase uses
+// sincos(x) (Cody-Waite in three parts: exact reduction for |x| < 2^19) rotated by pi/4, not
+// sincos(x - pi/4), whose argument would carry x's rounding.
+#define DFMI_BES_LARGE 64.0
+DFMI_HD void dfmi_sincos_fast(double x, double* sn, double* cs);
+DFMI_HD bool dfmi_bessel_use_large(double ax, int N) { return ax >= DFMI_BES_LARGE && 2.0 * (double)(N + 1) <= ax; }
+
+DFMI_HD void dfmi_bessel_j01_large(double ax, double* j0, double* j1) {
+  const double z = 1.0 / ax, z2 = z * z;
+  // (-1)^k a_{2k}(n) and (-1)^k a_{2k+1}(n), n = 0, 1 (exact rationals rounded once)
+  const double p0 = fma(z2, fma(z2, fma(z2, fma(z2, fma(z2, fma(z2, 3038.090510922384, -110.01714026924674),
+                                                       6.074042001273483), -0.5725014209747314),
+                                      0.112152099609375), -0.0703125), 1.0);
+  const double q0 = z * fma(z2, fma(z2, fma(z2, fma(z2, fma(z2, fma(z2, -18257.755474293175, 551.3358961220206),
+                                                            -24.380529699556064), 1.7277275025844574),
+                                           -0.22710800170898438), 0.0732421875), -0.125);
+  const double p1 = fma(z2, fma(z2, fma(z2, fma(z2, fma(z2, fma(z2, -3302.2722944808525, 121.59789187653587),
+                                                       -6.883914268109947), 0.6765925884246826),
+                                      -0.144195556640625), 0.1171875), 1.0);
+  const double q1 = z * fma(z2, fma(z2, fma(z2, fma(z2, fma(z2, fma(z2, 19718.37591223663, -603.8440767050702),
+                                                            27.248827311268542), -1.993531733751297),
+                                           0.2775764465332031), -0.1025390625), 0.375);
+  double sn, cs;
+  dfmi_sincos_fast(ax, &sn, &cs);  // ax < 1e5 (callers): the exact three-part reduction
+  const double r = 0.70710678118654752440;
+  const double c0 = (cs + sn) * r, s0 = (sn - cs) * r;  // cos, sin (x - pi/4)
+  const double c1 = (sn - cs) * r, s1 = -(sn + cs) * r; // cos, sin (x - 3 pi/4)
+  const double amp = sqrt(0.63661977236758134308 * z);  // sqrt(2 / (pi x))
+  *j0 = amp * fma(p0, c0, -(q0 * s0));
+  *j1 = amp * fma(p1, c1, -(q1 * s1));
+}
+
 // Convenience (host tests / tables): J_0..J_N(x) into out[0..N].
 DFMI_HD void dfmi_bessel_table(double x, int N, double* out) {
   if (x == 0.0) {
@@ -157,6 +198,20 @@ DFMI_HD void dfmi_bessel_table(double x, int N, double* out) {
   }
   if (ax < DFMI_BES_TINY) {
     for (int k = 0; k <= N; ++k) out[k] = dfmi_bessel_series(k, x);
+    return;
+  }
+  if (dfmi_bessel_use_large(ax, N)) {
+    double jm1, j0;
+    dfmi_bessel_j01_large(ax, &jm1, &j0);
+    const double tox = 2.0 / ax;
+    out[0] = jm1;
+    if (N >= 1) out[1] = x < 0.0 ? -j0 : j0;
+    for (int k = 1; k < N; ++k) {
+      const double jp1 = fma((double)k * tox, j0, -jm1);
+      out[k + 1] = (x < 0.0 && ((k + 1) & 1)) ? -jp1 : jp1;
+      jm1 = j0;
+      j0 = jp1;
+    }
     return;
   }
   const int M = dfmi_bessel_start(N, ax);

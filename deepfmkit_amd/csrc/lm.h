@@ -161,6 +161,18 @@ DFMI_HDI void bessel_regs(double x, int N, double (&J)[NB]) {
     return;
   }
   static_assert((NB & 1) == 0, "the pair loop below needs an even NB");
+  if (dfmi_bessel_use_large(ax, NB - 1)) {  // runaway descents: O(NB), not ~1.1|x| orders (dfmi_math.h)
+    double j0, j1;
+    dfmi_bessel_j01_large(ax, &j0, &j1);
+    const double tox = 2.0 * rcp_nr(ax);
+    J[0] = j0;
+    J[1] = j1;
+#pragma unroll
+    for (int k = 1; k < NB - 1; ++k) J[k + 1] = fma((double)k * tox, J[k], -J[k - 1]);
+#pragma unroll
+    for (int k = 1; k < NB; k += 2) J[k] = x < 0.0 ? -J[k] : J[k];  // J_k(-x) = (-1)^k J_k(x)
+    return;
+  }
   int M = dfmi_bessel_start(N, ax);
   if (M < NB) M = (NB + 1) & ~1;
   const double tox = 2.0 * rcp_nr(ax);
@@ -431,6 +443,29 @@ DFMI_HDI void harmonic_walk(int ndata, double m, double psi, Body&& body) {
       const double sn = fma(sj, c1, -(cj * s1));
       cj = cn;
       sj = sn;
+    }
+    return;
+  }
+  if (dfmi_bessel_use_large(am, ndata + 1)) {
+    // runaway descents (|m| >= 64, e.g. ~900): J_0, J_1 asymptotically, then upward
+    // (dfmi_math.h), the harmonics visited in ascending order with (cos, sin)(j psi) by
+    // rotation upward from (cos, sin)(psi)
+    double jm1, j0;
+    dfmi_bessel_j01_large(am, &jm1, &j0);
+    const double tox = 2.0 / am;
+    const double sg = m < 0.0 ? -1.0 : 1.0;  // J_k(-x) = (-1)^k J_k(x)
+    double cu = c1, su = s1;                 // (cos, sin)(j psi), j = 1
+    for (int j = 1; j <= ndata; ++j) {
+      const double jp1 = fma((double)j * tox, j0, -jm1);
+      // signs of J_{j-1}, J_j, J_{j+1} at m < 0: (-1)^(j-1), (-1)^j, (-1)^(j+1)
+      const double sj0 = (j & 1) ? sg : 1.0, sjm = (j & 1) ? 1.0 : sg;
+      body(j, sjm * jm1, sj0 * j0, sjm * jp1, cu, su);
+      const double cn = fma(cu, c1, -(su * s1));
+      const double sn = fma(su, c1, cu * s1);
+      cu = cn;
+      su = sn;
+      jm1 = j0;
+      j0 = jp1;
     }
     return;
   }

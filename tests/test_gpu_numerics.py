@@ -291,3 +291,13 @@ def test_lm_park_bit_identical(park):
     np.testing.assert_array_equal(res[park][1], res[0][1])
     st = res[0][1]
     assert (st == 0).sum() > 1000 and (st == 2).sum() > 1000  # both regimes ran
+
+
+@pytest.mark.parametrize("method,nmax", [(0, 17), (1, 13), (2, 17)])
+def test_device_bessel_large_argument(method, nmax):
+    """|x| >= 64 on the device (the Hankel expansion + upward recurrence of dfmi_math.h, in
+    the general path's table and both register-path passes) against scipy.special.jv
+    (tests/golden/bessel_large.npz; scipy's own error there is ~3.3e-15)."""
+    d = np.load(os.path.join(GOLDEN, "bessel_large.npz"))
+    x, jv = d["x"], d["jv"][: nmax + 1]
+    assert np.abs(_bessel(x, nmax, method) - jv).max() <= 1e-14

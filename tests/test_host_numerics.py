@@ -364,3 +364,32 @@ def test_worker_trial_sensitivity_to_qi_ulps():
         spread.append(d)
         assert d <= resolution_tol(nd, qi, po)[1], (t, d)
     assert spread[6] > 1e-9, spread
+
+
+def test_bessel_large_argument_vs_scipy(hc):
+    """|x| >= 64 (runaway descents): the Hankel expansion of J_0, J_1 + the upward recurrence
+    (dfmi_math.h dfmi_bessel_j01_large) in the general path's table and both register-path
+    passes, against scipy.special.jv (tests/golden/bessel_large.npz: orders 0..17, |x| up to
+    1e4, both signs) — scipy's own error there is ~3.3e-15 (mpmath) — and against a 30-digit
+    mpmath evaluation on 40 of the arguments (ours: 4e-17)."""
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "bessel_large.npz"))
+    x, jv = d["x"], d["jv"]
+    out = np.zeros(18)
+    tab = np.zeros((18, x.size))
+    for i, xv in enumerate(x):
+        hc.hc_bessel_table(float(xv), 17, out.ctypes.data)
+        tab[:, i] = out
+    assert np.abs(tab - jv).max() <= 1e-14, np.abs(tab - jv).max()
+    mp = pytest.importorskip("mpmath")
+    mp.mp.dps = 30
+    sub = np.arange(0, x.size, x.size // 40)
+    ex = np.array([[float(mp.besselj(k, mp.mpf(float(x[i])))) for i in sub] for k in range(18)])
+    assert np.abs(tab[:, sub] - ex).max() <= 2e-16, np.abs(tab[:, sub] - ex).max()
+    for nb in (14, 18):
+        regs = np.zeros((nb, x.size))
+        row = np.zeros(nb)
+        for i, xv in enumerate(x):
+            hc.hc_bessel_regs(float(xv), nb, row.ctypes.data)
+            regs[:, i] = row
+        assert np.abs(regs - jv[:nb]).max() <= 1e-14, (nb, np.abs(regs - jv[:nb]).max())
+        assert np.abs(regs[:, sub] - ex[:nb]).max() <= 2e-16, (nb, np.abs(regs[:, sub] - ex[:nb]).max())

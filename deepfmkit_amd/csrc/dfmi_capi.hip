@@ -57,9 +57,6 @@ struct Tuning {
   int lm_ladder = 32;    // LM launches of at most lm_ladder x CUs chains / segments (latency-bound: warm-start
                          // chains, small batches) run the parallel lambda ladder (lm.h lm_ladder_kernel);
                          // 0 = always one lane per chain / segment
-  int lm_park = 0;       // record pipeline LM (rows, ndata 10): 0 one lane per segment (lm_chunks_kernel);
-                         // 2 / 4 / 8: lanes park at their first rejected rung and the wave resumes them on
-                         // the lambda ladder, that many lanes per parked lane (lm.h lm_park_kernel)
   int ws_streams = 4;    // caller streams whose workspaces are kept; a call from one more stream first
                          // drains the DEVICE (hipDeviceSynchronize) and frees the least recently used set
 };
@@ -655,16 +652,6 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
     return DFMI_OK;
   }
   size_t lds = 0;
-  if (rows && !chain && nd_sel == 10 && t_tune.lm_park) {  // ladder walks off the critical lane
-    constexpr int kNd10 = dfmi::kExactNd | 10;
-    auto pk = t_tune.lm_park == 2 ? dfmi::lm_park_kernel<kNd10, 2>
-              : t_tune.lm_park == 4 ? dfmi::lm_park_kernel<kNd10, 4> : dfmi::lm_park_kernel<kNd10, 8>;
-    lds = (size_t)(qi_ld + 12) * 65 * sizeof(double);  // rows + the parked lanes' coeffs
-    hipLaunchKernelGGL(pk, dim3((unsigned)grid), dim3(block), lds, st, qi, qi_ld, ndata, nrec, nbuf, first, nitems,
-                       nchunk, guess_dev, g_rec, g_comp, ginl, use_inline, jtab, c, out, out_ld, status);
-    HIPCHK(hipGetLastError());
-    return DFMI_OK;
-  }
   auto kern = chain ? lm_kernel<true, false>(nd_sel) : rows ? lm_kernel<false, true>(nd_sel)
                                                             : lm_kernel<false, false>(nd_sel);
   if (rows && nd_sel <= 16) lds = (size_t)qi_ld * 65 * sizeof(double);  // the wave's rows, transposed
@@ -880,7 +867,6 @@ const std::map<std::string, Knob>& knobs() {
       {"ekf_rot", {&Tuning::ekf_rot, {0, 1}}},
       {"wdfmi_accel", {&Tuning::wdfmi_accel, {0, 1, 2, 3}}},
       {"lm_ladder", {&Tuning::lm_ladder, {}}},
-      {"lm_park", {&Tuning::lm_park, {0, 2, 4, 8}}},
       {"ws_streams", {&Tuning::ws_streams, {}}}};
   return k;
 }

@@ -412,9 +412,6 @@ __device__ __forceinline__ void ekf_sincos_row_small(double d, const RotCoef& rc
 #ifndef DFMI_EKF_ROT_NEWTON
 #define DFMI_EKF_ROT_NEWTON 1  // 1/S: v_rcp_f64 + one Newton step (without: +6 % but 2.7e-12 from the C oracle, r03s)
 #endif
-#ifndef DFMI_EKF_PF
-#define DFMI_EKF_PF 1  // groups of samples loaded ahead by ekf_rot_kernel (A/B builds)
-#endif
 #ifndef DFMI_EKF_ROT_G
 #define DFMI_EKF_ROT_G 16  // samples per anchor where R % G == 0 (8 measured 4 % slower, r03s; A/B builds)
 #endif
@@ -522,27 +519,17 @@ __global__ __launch_bounds__(64) void ekf_rot_kernel(const double* __restrict__ 
   int64_t k = 0;
   const int64_t ng = n_samp / G;
   int64_t to_snap = R;
-  // samples and phases DFMI_EKF_PF groups ahead (1: the next group's loads in flight while
-  // the chain runs this one; 2: the one after that, one more group of latency hidden)
   double xc[G], wc[G];
-#if DFMI_EKF_PF >= 2
-  double xm[G], wm[G];
-#endif
   if (ng > 0) {
 #pragma unroll
     for (int u = 0; u < G; ++u) {
       xc[u] = xr[u];
       wc[u] = wt[u];
-#if DFMI_EKF_PF >= 2
-      const int64_t k1 = ng > 1 ? G : 0;
-      xm[u] = xr[k1 + u];
-      wm[u] = wt[k1 + u];
-#endif
     }
   }
   for (int64_t g = 0; g < ng; ++g, k += G) {
     double xn[G], wn[G];
-    const int64_t kn = g + DFMI_EKF_PF < ng ? k + DFMI_EKF_PF * G : k;
+    const int64_t kn = g + 1 < ng ? k + G : k;
 #pragma unroll
     for (int u = 0; u < G; ++u) {
       xn[u] = xr[kn + u];
@@ -578,15 +565,8 @@ __global__ __launch_bounds__(64) void ekf_rot_kernel(const double* __restrict__ 
     }
 #pragma unroll
     for (int u = 0; u < G; ++u) {
-#if DFMI_EKF_PF >= 2
-      xc[u] = xm[u];
-      wc[u] = wm[u];
-      xm[u] = xn[u];
-      wm[u] = wn[u];
-#else
       xc[u] = xn[u];
       wc[u] = wn[u];
-#endif
     }
   }
   // the last n_samp % G samples (no snapshot can fall here: R is a multiple of G)

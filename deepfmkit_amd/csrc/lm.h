@@ -679,56 +679,6 @@ DFMI_HDI double lm_descend_flat(Ev&& ev, double (&p)[4], const LMConst& c) {
   return e.ssq;
 }
 
-// lm_descend_flat until the lane's first rung that is not accepted (a rejection, or a step
-// below min_step_norm): the lane then PARKS, returning true with its descent state — p, the
-// coeffs e at p, the accepted iterations `it` and the next rung `li` — for lm_park_kernel's
-// ladder phase to resume exactly where it stopped (lm_ladder_resume). A descent that ends
-// without such a rung (converged, max_steps) returns false with e.ssq its result; so does a
-// ladder of one rung (nothing left to resume).
-template <typename Ev>
-DFMI_HDI bool lm_descend_flat_park(Ev&& ev, double (&p)[4], const LMConst& c, Eval& e, int& it, int& li) {
-  {
-    typename std::decay_t<Ev>::Trial t0;
-    ev.trial(p, t0);
-    ev.accept(p, t0, e);
-  }
-  it = 0;
-  li = 0;
-  bool active = c.max_steps > 0 && c.n_lambda > 0;
-  while (active) {
-    double dp[4];
-    ev.solve(e, c.lambdas[0], dp);  // li == 0 on every pass of this loop
-    bool accepted = false;
-    if (!norm_below(sumsq4(dp[0], dp[1], dp[2], dp[3]), c.min_step_norm)) {
-      double pt[4] = {p[0] + dp[0], p[1] + dp[1], p[2] + dp[2], p[3] + dp[3]};
-      typename std::decay_t<Ev>::Trial tt;
-      const double ssq_try = ev.trial(pt, tt);
-      if (ssq_try < e.ssq) {
-        accepted = true;
-        const double change2 = sumsq4(pt[0] - p[0], pt[1] - p[1], pt[2] - p[2], pt[3] - p[3]);
-        p[0] = pt[0];
-        p[1] = pt[1];
-        p[2] = pt[2];
-        p[3] = pt[3];
-        ++it;
-        if (((ev.ssq_of(tt) - ssq_try) < c.conv_improve && norm_below(change2, c.conv_param_change)) ||
-            it >= c.max_steps) {
-          e.ssq = ev.ssq_of(tt);
-          active = false;
-        } else {
-          ev.accept(p, tt, e);
-        }
-      }
-    }
-    if (!accepted) {
-      li = 1;
-      if (li >= c.n_lambda) return false;  // no lambda improved (a one-rung ladder)
-      return true;                          // park: rungs 1.. of this iteration are the ladder phase's
-    }
-  }
-  return false;
-}
-
 // Evaluators for the descents: trial(p, t) = ssqf at p, accept(p, t, e) = coeffs at an
 // accepted p, solve = msolve. General path (GenSplitEval one lane per fit, FullGenEval on
 // the lambda ladder): the literal evaluation + the pivoting 4x4 solve; register path
@@ -862,8 +812,9 @@ constexpr int kLadderLanes = 8;  // lanes per segment of the parallel-ladder des
 // Every lane of the wave must call this (wave-uniform loop; lanes without work pass
 // active = false through p's group state, see lm_ladder_kernel).
 // The ladder descent from a given state (p, coeffs e at p, accepted iterations `it`, the next
-// rung `base` of the current iteration): lm_descend_ladder's loop, also the resumption of a
-// one-lane descent that parked (lm_park_kernel).
+// rung `base` of the current iteration): lm_descend_ladder's loop. (Round 4 also resumed
+// one-lane descents here that parked at their first rejected rung, lm_park_kernel: same
+// bits, LM 41-45 us against 36 us, removed)
 template <int LPS, typename Ev>
 __device__ __forceinline__ double lm_ladder_resume(Ev&& ev, double (&p)[4], const LMConst& c, Eval& e, int it,
                                                    int base, bool live) {
@@ -1248,192 +1199,6 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
       for (int64_t t = 0; t < len; ++t) one(s0 + t);  // warm-start chain (sequential / n_cores)
     }
   }
-}
-
-#ifndef DFMI_PARK_QREG_A
-#define DFMI_PARK_QREG_A 0  // lm_park_kernel phase A: QI in registers (1) or read from the LDS rows (0)
-#endif
-// The record pipeline's LM with the lambda-ladder walks taken off the critical lane
-// (dfmi_set_tuning "lm_park"; rows, chunk size 1, the exact-ndata register path).
-// In lm_chunks_kernel a wave lasts as long as its slowest lane, and at the noise floor
-// nearly every wave holds a lane that rejects all 8 rungs of its last iteration one pass
-// at a time (~10 passes per wave against a mean of ~5 per lane). Here:
-//  A: every lane runs the one-lane descent until its first rung that is not accepted, and
-//     parks there (lm_descend_flat_park) — or finishes;
-//  B: the wave resumes its parked lanes LPS lanes per lane: round after round, group g of
-//     the wave takes the g-th parked lane's state (p, coeffs, iterations, next rung: by
-//     shuffles; its QI from the wave's LDS rows) and continues the descent with the rungs
-//     tried LPS at a time (lm_ladder_resume: the first improving rung in ladder order, as
-//     the one-lane descent takes it), then hands p and ssq back;
-//  C: every lane finishes its fit (status, the m-grid retry on the one-lane path, sign
-//     normalisation, phi wrap) and stores it.
-// The same accepted points as lm_chunks_kernel: the same bits (tests/test_gpu_numerics.py).
-template <int V, int LPS>
-__global__ __launch_bounds__(64, 2) void lm_park_kernel(
-    const double* __restrict__ qi, int64_t qi_ld, int ndata, int64_t nrec, int64_t nbuf, int64_t first,
-    int64_t nitems, int64_t nchunk, const double* __restrict__ guess, int64_t g_rec, int64_t g_comp,
-    GuessInline ginl, int use_inline, const double* __restrict__ jtab, LMConst c, double* __restrict__ out,
-    int64_t out_ld, int32_t* __restrict__ status) {
-  static_assert(nd_exact(V), "lm_park_kernel: the exact-ndata register path");
-  constexpr int NC = nd_cap(V);
-  extern __shared__ double lds_q[];  // [qi_ld][65]: the wave's rows, transposed; then [12][65] coeffs
-  const int lane = threadIdx.x;
-  const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool valid = id < nrec * nchunk;
-  const int64_t idc = valid ? id : 0;
-  const int64_t r = idc / nchunk;
-  const int64_t k = idc - r * nchunk;
-  const int64_t qn = nitems / nchunk, rm = nitems % nchunk;
-  const int64_t start = k * qn + (k < rm ? k : rm);
-  const int64_t len = qn + (k < rm ? 1 : 0);
-  const int64_t s0 = r * nbuf + first + start;
-  {  // stage the wave's rows into LDS, transposed (lm_chunks_kernel's STAGE)
-    const int QS = (int)qi_ld;
-    const int64_t sl0 = __shfl(s0, 0);
-    const int nv = (int)((nrec * nchunk - (int64_t)blockIdx.x * 64) < 64 ? (nrec * nchunk - (int64_t)blockIdx.x * 64)
-                                                                         : 64);
-    const bool contiguous = __all(!valid || s0 == sl0 + lane);
-    if (contiguous) {
-      const double* __restrict__ base = qi + sl0 * qi_ld;
-      const int tot = nv * QS;
-      constexpr int kStageLoads = 16;
-      typedef double d2v __attribute__((ext_vector_type(2)));
-      for (int e0 = 2 * lane; e0 < tot; e0 += 128 * kStageLoads) {
-        d2v v[kStageLoads];
-#pragma unroll
-        for (int u = 0; u < kStageLoads; ++u) {
-          const int e = e0 + 128 * u;
-          v[u] = e < tot ? *reinterpret_cast<const d2v*>(base + e) : d2v{0.0, 0.0};
-        }
-#pragma unroll
-        for (int u = 0; u < kStageLoads; ++u) {
-          const int e = e0 + 128 * u;
-          if (e < tot) {
-            const int row = e / QS, pos = e - row * QS;
-            lds_q[pos * 65 + row] = v[u].x;
-            lds_q[(pos + 1) * 65 + row] = v[u].y;
-          }
-        }
-      }
-    } else if (valid) {
-      for (int pos = 0; pos < QS; ++pos) lds_q[pos * 65 + lane] = qi[s0 * qi_ld + pos];
-    }
-    __syncthreads();
-  }
-  const bool work = valid && len == 1;
-  double p[4] = {0.0, 0.0, 0.0, 0.0};
-  if (use_inline) {
-#pragma unroll
-    for (int rr = 0; rr < 8; ++rr) {
-      if (r == rr) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) p[i] = ginl.v[rr][i];
-      }
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) p[i] = guess[r * g_rec + i * g_comp];
-  }
-  const QRow<65> q{lds_q + lane};
-  // ---- A: one lane per segment until the first rung that is not accepted
-  Eval e;
-  int it = 0, li = 0;
-  bool parked = false;
-  if (work) {
-#if DFMI_PARK_QREG_A
-    QRegs<NC> qr;
-    qr.load(q);
-    SplitEval<V, QRegs<NC>> ev{qr, ndata, c.trig};
-#else
-    SplitEval<V, QRow<65>> ev{q, ndata, c.trig};
-#endif
-    parked = lm_descend_flat_park(ev, p, c, e, it, li);
-  }
-  // ---- B: the parked lanes' ladders, LPS lanes each, 64 / LPS lanes per round. A parked
-  // lane's coeffs wait in LDS (12 values after the rows, [value][65]): in registers they
-  // would push the kernel past the 256 VGPRs of two waves per SIMD
-  double* lds_e = lds_q + qi_ld * 65;
-  if (parked) {
-    lds_e[0 * 65 + lane] = e.ssq;
-    lds_e[1 * 65 + lane] = e.a00;
-    lds_e[2 * 65 + lane] = e.a01;
-    lds_e[3 * 65 + lane] = e.a02;
-    lds_e[4 * 65 + lane] = e.a11;
-    lds_e[5 * 65 + lane] = e.a12;
-    lds_e[6 * 65 + lane] = e.a22;
-    lds_e[7 * 65 + lane] = e.a33;
-    lds_e[8 * 65 + lane] = e.g0;
-    lds_e[9 * 65 + lane] = e.g1;
-    lds_e[10 * 65 + lane] = e.g2;
-    lds_e[11 * 65 + lane] = e.g3;
-  }
-  // one wave: its LDS operations run in order; the fences keep the compiler from moving
-  // the group's reads above the parked lanes' writes
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  constexpr int G = 64 / LPS;
-  const int grp = lane / LPS;
-  uint64_t pm = __ballot(parked);
-  while (pm != 0) {
-    uint64_t m = pm;  // this group's lane: the grp-th set bit of pm
-    for (int i = 0; i < grp && m != 0; ++i) m &= m - 1;
-    const bool live = m != 0;
-    const int src = live ? (int)__builtin_ctzll(m) : lane;
-    double pg[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) pg[i] = shfl_any(p[i], src);
-    Eval eg;
-    eg.ssq = lds_e[0 * 65 + src];
-    eg.a00 = lds_e[1 * 65 + src];
-    eg.a01 = lds_e[2 * 65 + src];
-    eg.a02 = lds_e[3 * 65 + src];
-    eg.a11 = lds_e[4 * 65 + src];
-    eg.a12 = lds_e[5 * 65 + src];
-    eg.a22 = lds_e[6 * 65 + src];
-    eg.a33 = lds_e[7 * 65 + src];
-    eg.g0 = lds_e[8 * 65 + src];
-    eg.g1 = lds_e[9 * 65 + src];
-    eg.g2 = lds_e[10 * 65 + src];
-    eg.g3 = lds_e[11 * 65 + src];
-    eg.a03 = eg.a13 = eg.a23 = 0.0;  // the register path's block-diagonal J^T J
-    const int itg = __shfl(it, src), lig = __shfl(li, src);
-    const QRow<65> qg{lds_q + src};  // the parked segment's QI, read from the wave's LDS rows
-    SplitEval<V, QRow<65>> evg{qg, ndata, c.trig};
-    const double ssq_g = lm_ladder_resume<LPS>(evg, pg, c, eg, itg, lig, live);
-    // back to the parked lanes of this round: the parked lane of rank j (among pm's bits)
-    // reads group j's first lane
-    const int rank = (int)__builtin_popcountll(pm & ((1ull << lane) - 1));
-    const bool mine = parked && rank < G;
-    const int from = mine ? rank * LPS : lane;
-    double rp[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) rp[i] = shfl_any(pg[i], from);
-    const double rs = shfl_any(ssq_g, from);
-    if (mine) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) p[i] = rp[i];
-      e.ssq = rs;
-      parked = false;
-    }
-    for (int i = 0; i < G && pm != 0; ++i) pm &= pm - 1;  // this round's lanes (uniform)
-  }
-  // ---- C: status, the m-grid retry, normalisation (fit.py:334-360); store
-  if (!work) return;
-  QRegs<NC> qr;
-  qr.load(q);
-  SplitEval<V, QRegs<NC>> ev{qr, ndata, c.trig};
-  double ssq;
-  const int st = fit_finish_t<1>(ev, q, ndata, jtab, c, p, e.ssq, ssq);
-  out[0 * out_ld + s0] = p[0];
-  out[1 * out_ld + s0] = p[1];
-  out[2 * out_ld + s0] = p[2];
-  out[3 * out_ld + s0] = p[3];
-  out[5 * out_ld + s0] = ssq;
-  status[s0] = st;
-  out[4 * out_ld + s0] = q.at(dfmi_row_dc(ndata));
-  if (k == 0)  // segments before `first` (the seed buffer) are fitted elsewhere: carry their dc
-    for (int64_t t = r * nbuf; t < r * nbuf + first; ++t) out[4 * out_ld + t] = qi[t * qi_ld + dfmi_row_dc(ndata)];
 }
 
 // Latency-bound fits (few chains or few segments): kLadderLanes lanes per item, the

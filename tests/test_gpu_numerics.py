@@ -258,41 +258,6 @@ def test_seed_wave_ladder_equals_one_lane_general_fit(phi, psi, noise_only):
     assert ms < 10.0
 
 
-@pytest.mark.parametrize("park", [2, 4, 8])
-def test_lm_park_bit_identical(park):
-    """lm_park (lm.h lm_park_kernel: lanes park at their first rejected rung, the wave resumes
-    them on the lambda ladder, `park` lanes each) accepts the points of the one-lane descent:
-    the record pipeline's results equal lm_park = 0's bit for bit — a config-2 record, records
-    whose phase the default guess does not reach (long descents, status 2, m-grid retries)
-    and noise-only buffers; 3 records of 4001 buffers in one call (waves straddling records)."""
-    import torch
-    from deepfmkit_amd import _lib
-    from deepfmkit_amd.fitters import nls_records
-    from deepfmkit_amd.physics import SnrSpec, synth_snr
-    lib = _lib.load()
-    R, nbuf = 4000, 4001
-    x = torch.empty((3, nbuf * R), dtype=torch.float64, device="cuda")
-    for r, (phi, psi) in enumerate(((0.0, 0.0), (1.3, 0.4), (0.7, 0.05))):
-        synth_snr(SnrSpec(seed=41 + r, f_samp=200000.0, f_mod=1000.0, m=6.0 + r, phi=phi, psi=psi, snr_db=40.0), 0,
-                  nbuf * R, out=x[r])
-    g = torch.Generator(device="cuda").manual_seed(9)
-    x[2, 100 * R:140 * R] = 0.5 + 0.3 * torch.randn(40 * R, dtype=torch.float64, device="cuda", generator=g)
-    old = np.zeros(1, dtype=np.int64)
-    _lib.check(lib.dfmi_get_tuning(b"lm_park", _lib.ptr(old)), "get")
-    res = {}
-    try:
-        for v in (0, park):
-            _lib.check(lib.dfmi_set_tuning(b"lm_park", v), "set")
-            cols, ok = nls_records(x, 200000.0, 1000.0, R, nbuf)
-            res[v] = (cols.cpu().numpy(), ok.cpu().numpy())
-    finally:
-        _lib.check(lib.dfmi_set_tuning(b"lm_park", int(old[0])), "set")
-    np.testing.assert_array_equal(res[park][0], res[0][0])
-    np.testing.assert_array_equal(res[park][1], res[0][1])
-    st = res[0][1]
-    assert (st == 0).sum() > 1000 and (st == 2).sum() > 1000  # both regimes ran
-
-
 @pytest.mark.parametrize("method,nmax", [(0, 17), (1, 13), (2, 17)])
 def test_device_bessel_large_argument(method, nmax):
     """|x| >= 64 on the device (the Hankel expansion + upward recurrence of dfmi_math.h, in

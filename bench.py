@@ -25,6 +25,7 @@ oracle on the same sample).
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -409,11 +410,22 @@ def extra_configs(torch, dev, lib, _lib, stream, cfg, cpu_leg):
                      "samples_per_s_aggregate": round(nch * ns / t, 1),
                      "kernel": lib.dfmi_last_demod_kernel().decode()}
         if nch == 1:
+            passes = (ctypes.c_int32 * 1)()
+            _lib.check(lib.dfmi_ekf_pit_passes(ctypes.cast(passes, ctypes.c_void_p), 1), "dfmi_ekf_pit_passes")
+            res5[1]["pit_passes"] = int(passes[0])
             x1 = xe.cpu().numpy()
             s1 = stt[0].cpu().numpy()
+            # the same channel through the sequential row kernel (ekf_pit off)
+            _lib.check(lib.dfmi_set_tuning(b"ekf_pit", 0), "tune")
+            ts = _timed_steps(torch, ekf, 3, 1)
+            res5["seq"] = {"s_per_fit": round(ts, 5), "samples_per_s_per_channel": round(ns / ts, 1),
+                           "kernel": lib.dfmi_last_demod_kernel().decode(),
+                           "max_abs_dstate_vs_parallel_in_time": float(np.max(np.abs(stt[0].cpu().numpy() - s1)))}
+            _lib.check(lib.dfmi_set_tuning(b"ekf_pit", 8), "tune")
         del xe, stt
     c5 = {"workload": "EKFFitter.fit, 2 s = 400,000 samples @200 kS/s (m=6, 40 dB), snapshots every R=4000",
-          "one_channel": res5[1], "channels_1024": res5[1024], "unit": "samples/s"}
+          "one_channel": res5[1], "one_channel_sequential": res5["seq"], "channels_1024": res5[1024],
+          "unit": "samples/s"}
     if cpu_leg:  # the host baseline: the oracle's scalar C restatement of the same loop, one core
         import ctypes
         lib_c = os.path.join(ROOT, "oracle", "libekf_scalar.so")

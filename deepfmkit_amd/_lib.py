@@ -25,7 +25,7 @@ SYMBOLS = ("dfmi_lm_config_default", "dfmi_demod", "dfmi_lm", "dfmi_nls_record",
            "dfmi_probe_read", "dfmi_get_tuning", "dfmi_txt_parse_header", "dfmi_txt_shape", "dfmi_txt_read",
            "dfmi_fit_txt_write", "dfmi_py_repr", "dfmi_txt_last_error", "dfmi_wdfmi_fit", "dfmi_ekf_fit",
            "dfmi_record_moments", "dfmi_synth_asd", "dfmi_synth_snr", "dfmi_bessel_eval",
-           "dfmi_release_workspaces", "dfmi_step_timing", "dfmi_step_timing_read")
+           "dfmi_release_workspaces", "dfmi_step_timing", "dfmi_step_timing_read", "dfmi_ekf_pit_passes")
 
 
 class DFMIError(RuntimeError):
@@ -115,6 +115,8 @@ def load():
         lib.dfmi_ekf.restype = ctypes.c_int
         lib.dfmi_ekf_fit.argtypes = [P, i64, i64, i64, P, P, P, P, dbl, dbl, i32, i64, P, i32, P]
         lib.dfmi_ekf_fit.restype = ctypes.c_int
+        lib.dfmi_ekf_pit_passes.argtypes = [P, i64]
+        lib.dfmi_ekf_pit_passes.restype = ctypes.c_int
         lib.dfmi_record_moments.argtypes = [P, i64, i64, i64, P, P, i32, P]
         lib.dfmi_record_moments.restype = ctypes.c_int
         lib.dfmi_synth_asd.argtypes = [P, i64, i64, dbl, P, i32, P]

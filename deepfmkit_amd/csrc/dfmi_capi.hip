@@ -20,6 +20,7 @@
 #include "demod.h"
 #include "dfmi_math.h"
 #include "ekf.h"
+#include "ekf_pit.h"
 #include "lm.h"
 #include "seed.h"
 #include "np_sum.h"
@@ -59,6 +60,12 @@ struct Tuning {
                          // 0 = always one lane per chain / segment
   int ws_streams = 4;    // caller streams whose workspaces are kept; a call from one more stream first
                          // drains the DEVICE (hipDeviceSynchronize) and frees the least recently used set
+  int ekf_pit = 8;       // EKF parallel in time (ekf_pit.h) for up to this many channels of at least
+                         // ekf_pit_min samples; 0 = the sequential kernels always
+  int ekf_pit_min = 32768;    // samples per channel below which the sequential kernels run
+  int ekf_pit_block = 0;      // samples per block (0: ~n / 8192, at least 16)
+  int ekf_pit_passes = 12;    // relinearization passes before a channel falls back to the lane kernel
+  int ekf_pit_head = 512;     // samples the sequential EKF runs first to seed the trajectory (ekf_pit_head_kernel)
 };
 Tuning g_tune;
 
@@ -867,7 +874,12 @@ const std::map<std::string, Knob>& knobs() {
       {"ekf_rot", {&Tuning::ekf_rot, {0, 1}}},
       {"wdfmi_accel", {&Tuning::wdfmi_accel, {0, 1, 2, 3}}},
       {"lm_ladder", {&Tuning::lm_ladder, {}}},
-      {"ws_streams", {&Tuning::ws_streams, {}}}};
+      {"ws_streams", {&Tuning::ws_streams, {}}},
+      {"ekf_pit", {&Tuning::ekf_pit, {}}},
+      {"ekf_pit_min", {&Tuning::ekf_pit_min, {}}},
+      {"ekf_pit_block", {&Tuning::ekf_pit_block, {}}},
+      {"ekf_pit_passes", {&Tuning::ekf_pit_passes, {}}},
+      {"ekf_pit_head", {&Tuning::ekf_pit_head, {}}}};
   return k;
 }
 // np.mean / np.var of nrec device records on st (moments.hip), numpy-exact.
@@ -880,6 +892,70 @@ int moments_dev(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
   void* nodes;
   if ((rc = workspace(dev, "m_nodes", (size_t)nrec * 2 * nl * 8, &nodes))) return rc;
   HIPCHK(dfmi::moments_launch(dx, nrec, rs, n, plan, nl, (double*)nodes, mean, mean_stride, var, var_stride, st));
+  return DFMI_OK;
+}
+
+// The EKF parallel in time (ekf_pit.h) for nrec few long channels: gather, then up to
+// ekf_pit_passes x (aggregate, scan, [top scan], blocks, check), the passes of a converged
+// channel returning at once, then the lane-kernel fallback for any channel still moving.
+// wt: ekf_phase_kernel's table (the fallback's). Pass counts stay readable through
+// dfmi_ekf_pit_passes until the next EKF call on this thread.
+thread_local int64_t g_pit_nrec = 0;
+thread_local int* g_pit_flag = nullptr;
+constexpr double kPitTol = 1e-11;  // relative move of xbar at which a channel is converged
+
+int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, const double* dx0, const double* dp0,
+                const double* dq, const double* dr, const double* wt, double w_m, double f_samp, int32_t R,
+                int64_t nbuf, double* dstates, hipStream_t st) {
+  int64_t B = t_tune.ekf_pit_block > 0 ? t_tune.ekf_pit_block : (n + 8191) / 8192;
+  if (B < 16) B = 16;
+  int64_t nb = (n + B - 1) / B;
+  const int64_t ngmax = dfmi::kPitWg;  // the top-level scan is one workgroup
+  if (nb > dfmi::kPitWg * ngmax) {
+    B = (n + dfmi::kPitWg * ngmax - 1) / (dfmi::kPitWg * ngmax);
+    nb = (n + B - 1) / B;
+  }
+  const int64_t ng = (nb + dfmi::kPitWg - 1) / dfmi::kPitWg, slots = B * nb;
+  void *xt, *wtt, *xbar, *agg, *tot, *conv, *flag, *hst;
+  int rc;
+  const int64_t T0 = std::min<int64_t>(std::max(t_tune.ekf_pit_head, 0), n);
+  if ((rc = workspace(dev, "p_xt", (size_t)(nrec * slots) * 8, &xt))) return rc;
+  if ((rc = workspace(dev, "p_wt", (size_t)slots * 8, &wtt))) return rc;
+  if ((rc = workspace(dev, "p_xbar", (size_t)(nrec * 5 * slots) * 8, &xbar))) return rc;
+  if ((rc = workspace(dev, "p_agg", (size_t)(nrec * dfmi::kPitEl * nb) * 8, &agg))) return rc;
+  if ((rc = workspace(dev, "p_tot", (size_t)(nrec * dfmi::kPitEl * ng) * 8, &tot))) return rc;
+  if ((rc = workspace(dev, "p_conv", (size_t)(nrec * nb) * 8, &conv))) return rc;
+  if ((rc = workspace(dev, "p_flag", (size_t)(nrec * 2) * sizeof(int), &flag))) return rc;
+  if ((rc = workspace(dev, "p_hst", (size_t)(nrec * 5) * 8, &hst))) return rc;
+  const DfmiTrigK tk = dfmi_trig_k();
+  const unsigned nr = (unsigned)nrec;
+  hipLaunchKernelGGL(dfmi::ekf_pit_head_kernel, dim3((unsigned)((nrec + 63) / 64)), dim3(64), 0, st, dx, nrec, rs, T0,
+                     dx0, dp0, dq, dr, w_m, f_samp, B, nb, (double*)xbar, (double*)hst, tk);
+  hipLaunchKernelGGL(dfmi::ekf_pit_gather_kernel, dim3((unsigned)((slots + 255) / 256), nr), dim3(256), 0, st, dx, rs,
+                     n, (const double*)hst, T0, B, nb, w_m, f_samp, (double*)xt, (double*)wtt, (double*)xbar,
+                     (int*)flag);
+  const dim3 lanes((unsigned)((nb + 63) / 64), nr);
+  for (int pass = 0; pass < t_tune.ekf_pit_passes; ++pass) {
+    hipLaunchKernelGGL(dfmi::ekf_pit_aggregate_kernel, lanes, dim3(64), 0, st, (const double*)xt,
+                       (const double*)wtt, (const double*)xbar, n, B, nb, dx0, dp0, dq, dr, (const int*)flag,
+                       (double*)agg, tk);
+    hipLaunchKernelGGL(dfmi::ekf_pit_scan_kernel, dim3((unsigned)ng, nr), dim3(dfmi::kPitWg), 0, st, (double*)agg,
+                       nb, nb, ng > 1 ? (double*)tot : nullptr, (const int*)flag);
+    if (ng > 1)
+      hipLaunchKernelGGL(dfmi::ekf_pit_scan_kernel, dim3(1, nr), dim3(dfmi::kPitWg), 0, st, (double*)tot, ng, ng,
+                         (double*)nullptr, (const int*)flag);
+    hipLaunchKernelGGL(dfmi::ekf_pit_blocks_kernel, lanes, dim3(64), 0, st, (const double*)xt, (const double*)wtt,
+                       (double*)xbar, n, B, nb, dx0, dp0, dq, dr, (const double*)agg, (const double*)tot,
+                       (const int*)flag, (double*)conv, (int)R, nbuf, dstates, tk);
+    hipLaunchKernelGGL(dfmi::ekf_pit_check_kernel, dim3(nr), dim3(256), 0, st, (const double*)conv, nb, kPitTol,
+                       (int*)flag);
+  }
+  hipLaunchKernelGGL(dfmi::ekf_pit_fallback_kernel, dim3((unsigned)((nrec + 63) / 64)), dim3(64), 0, st, dx, nrec,
+                     rs, n, dx0, dp0, dq, dr, wt, (int)R, nbuf, dstates, (int*)flag, tk);
+  HIPCHK(hipGetLastError());
+  g_last_demod = "ekf_pit (B=" + std::to_string(B) + ", nb=" + std::to_string(nb) + ")";
+  g_pit_nrec = nrec;
+  g_pit_flag = (int*)flag;
   return DFMI_OK;
 }
 
@@ -968,24 +1044,31 @@ int ekf_impl(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
   if (n_samp > 0)
     hipLaunchKernelGGL(dfmi::ekf_phase_kernel, dim3((unsigned)((n_samp + 255) / 256)), dim3(256), 0, st,
                        (double*)wtw, n_samp, w_m, f_samp);
-  const int64_t grid = row ? (nrec + 3) / 4 : (nrec + block - 1) / block;
-  // rotation between anchors: groups of 16 (8, 4) samples whose ends carry the snapshots
-  const bool rot = t_tune.ekf_rot && R % 4 == 0;
-  using EK = void (*)(const double*, int64_t, int64_t, int64_t, const double*, const double*, const double*,
-                      const double*, const double*, int, int64_t, double*, DfmiTrigK);
-  EK ek;
-  if (row)
-    ek = !rot ? dfmi::ekf_row_kernel<DFMI_EKF_SPLIT != 0>
-         : R % DFMI_EKF_ROT_G == 0 ? dfmi::ekf_rot_kernel<DFMI_EKF_ROT_G>
-         : R % 8 == 0              ? dfmi::ekf_rot_kernel<8>
-                                   : dfmi::ekf_rot_kernel<4>;
-  else
-    ek = !rot ? dfmi::ekf_kernel : R % 8 == 0 ? dfmi::ekf_lane_rot_kernel<8> : dfmi::ekf_lane_rot_kernel<4>;
-  hipLaunchKernelGGL(ek, dim3((unsigned)grid), dim3(block), 0, st, dx, nrec, rs, n_samp, dx0, dp0, dq, dr,
-                     (const double*)wtw, (int)R, nbuf, dstates, dfmi_trig_k());
-  // also reports the EKF variant
-  g_last_demod = row ? (rot ? "ekf_rot_kernel" : "ekf_row_kernel") : (rot ? "ekf_lane_rot_kernel" : "ekf_kernel");
-  HIPCHK(hipGetLastError());
+  if (t_tune.ekf_pit > 0 && nrec <= t_tune.ekf_pit && n_samp >= t_tune.ekf_pit_min && n_samp >= 2) {
+    rc = ekf_pit_run(dev, dx, nrec, rs, n_samp, dx0, dp0, dq, dr, (const double*)wtw, w_m, f_samp, R, nbuf, dstates,
+                     st);
+    if (rc) return rc;
+  } else {
+    g_pit_nrec = 0;
+    const int64_t grid = row ? (nrec + 3) / 4 : (nrec + block - 1) / block;
+    // rotation between anchors: groups of 16 (8, 4) samples whose ends carry the snapshots
+    const bool rot = t_tune.ekf_rot && R % 4 == 0;
+    using EK = void (*)(const double*, int64_t, int64_t, int64_t, const double*, const double*, const double*,
+                        const double*, const double*, int, int64_t, double*, DfmiTrigK);
+    EK ek;
+    if (row)
+      ek = !rot ? dfmi::ekf_row_kernel<DFMI_EKF_SPLIT != 0>
+           : R % DFMI_EKF_ROT_G == 0 ? dfmi::ekf_rot_kernel<DFMI_EKF_ROT_G>
+           : R % 8 == 0              ? dfmi::ekf_rot_kernel<8>
+                                     : dfmi::ekf_rot_kernel<4>;
+    else
+      ek = !rot ? dfmi::ekf_kernel : R % 8 == 0 ? dfmi::ekf_lane_rot_kernel<8> : dfmi::ekf_lane_rot_kernel<4>;
+    hipLaunchKernelGGL(ek, dim3((unsigned)grid), dim3(block), 0, st, dx, nrec, rs, n_samp, dx0, dp0, dq, dr,
+                       (const double*)wtw, (int)R, nbuf, dstates, dfmi_trig_k());
+    // also reports the EKF variant
+    g_last_demod = row ? (rot ? "ekf_rot_kernel" : "ekf_row_kernel") : (rot ? "ekf_lane_rot_kernel" : "ekf_kernel");
+    HIPCHK(hipGetLastError());
+  }
   if (host) {
     if (sb) HIPCHK(hipMemcpyAsync(states, dstates, sb, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -1395,6 +1478,24 @@ int dfmi_ekf_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_sa
   if (!init4) return fail(DFMI_ERR_ARG, "null init4");
   return ekf_impl(x, nrec, rec_stride, n_samp, nullptr, init4, p0_diag, q_diag, r_val, w_m, f_samp, R, nbuf, states,
                   mem, stream);
+}
+
+int dfmi_ekf_pit_passes(int32_t* passes, int64_t nrec) {
+  CallScope cs;
+  if (!passes || nrec < 0) return fail(DFMI_ERR_ARG, "bad pass buffer");
+  if (g_pit_nrec == 0 || !g_pit_flag) {
+    for (int64_t r = 0; r < nrec; ++r) passes[r] = 0;
+    return DFMI_OK;
+  }
+  if (nrec != g_pit_nrec) return fail(DFMI_ERR_ARG, "nrec differs from the last EKF call's");
+  int dev;
+  int rc = ensure_init(&dev);
+  if (rc) return rc;
+  std::vector<int> f((size_t)nrec * 2);
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(f.data(), g_pit_flag, f.size() * sizeof(int), hipMemcpyDeviceToHost));
+  for (int64_t r = 0; r < nrec; ++r) passes[r] = f[2 * r + 1];
+  return DFMI_OK;
 }
 
 int dfmi_synth_asd(const dfmi_synth_trial* trials, int64_t ntrial, int64_t n_samp, double f_samp, double* out,

@@ -1,0 +1,603 @@
+// ekf_pit.h — the EKF of fitters.py:214-320 parallel in time, for few long channels.
+//
+// The sequential kernels (ekf.h) run one channel's samples in order: ~410 clocks per
+// sample on one SIMD, a floor of the dependent fp64 chain (DESIGN.md §5, r04c PMC), so a
+// single 400k-sample channel takes ~69 ms however large the GPU is. Here the channel is cut
+// into nb blocks of B samples and the filter is solved as a fixed point:
+//
+//   1. linearize the measurement h(x) = a cos(phi + m cos(w_m t_k + psi)) + dc at a
+//      trajectory xbar_k (predicted states; xbar = x0 on the first pass), so the model is
+//      linear-Gaussian: x_k = x_{k-1} + q, y_k = H_k x_k + d_k + r (F = I as in the reference);
+//   2. the linear Kalman filter of that model is an associative prefix scan over filtering
+//      elements (A, b, C, eta, J) (Sarkka & Garcia-Fernandez, "Temporal parallelization of
+//      Bayesian smoothers", IEEE TAC 2021): every block folds its B elements in order
+//      (ekf_pit_aggregate_kernel, a rank-1 form of the combine per sample), the block
+//      aggregates are scanned (ekf_pit_scan_kernel: Hillis-Steele in LDS, 256 per workgroup,
+//      then over the workgroup totals), and the inclusive prefix at block b-1 is the filtered
+//      (mean, covariance) entering block b;
+//   3. each block then runs the TRUE EKF (ekf_step, the lane kernel's arithmetic) from that
+//      entry state (ekf_pit_blocks_kernel), which gives the next xbar and the snapshots.
+//
+// When xbar stops moving (max |dx| / max(1, |x|) <= tol over the channel, tested on the
+// device by ekf_pit_check_kernel) the block entry states are the EKF's own states at those
+// samples to the scan's rounding (~1e-13; the iteration converges quadratically once close:
+// scripts/study/ekf_pit_proto.py), so the output is the sequential EKF's to rounding. A
+// converged channel's later kernels return at once (flag per channel, no host round trip);
+// a channel still moving after the last pass is re-run by the sequential lane kernel
+// (ekf_pit_fallback_kernel), so the result never depends on the iteration having converged.
+//
+// Layouts (all channel-major, blocks fastest so lane b of a wave reads address b):
+//   xt[r][i][b], wtt[i][b] (sample k = b B + i), xbar[r][c][i][b], agg[r][65][nb], tot[r][65][ng].
+// Element components: A 0..24 (row-major), b 25..29, C 30..44 (upper triangle, row-major),
+// eta 45..49, J 50..64 (upper triangle).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dfmi_math.h"
+#include "ekf.h"
+
+namespace dfmi {
+
+constexpr int kPitEl = 65;
+constexpr int kPitA = 0, kPitB = 25, kPitC = 30, kPitE = 45, kPitJ = 50;
+constexpr int kPitWg = 256;  // elements per scan workgroup
+__host__ __device__ constexpr int pit_sy(int i, int j) {
+  return i <= j ? i * 5 - i * (i - 1) / 2 + (j - i) : j * 5 - j * (j - 1) / 2 + (i - j);
+}
+__host__ __device__ constexpr double pit_identity(int c) {
+  return (c < kPitB && c / 5 == c % 5) ? 1.0 : 0.0;  // A = I, everything else 0
+}
+
+// a filtering element read through a strided pointer (global SoA or LDS)
+struct PitEl {
+  const double* p;
+  int64_t ld;
+  __device__ __forceinline__ double operator()(int c) const { return p[c * ld]; }
+  __device__ __forceinline__ double A(int r, int c) const { return p[(kPitA + r * 5 + c) * ld]; }
+  __device__ __forceinline__ double C(int i, int j) const { return p[(kPitC + pit_sy(i, j)) * ld]; }
+  __device__ __forceinline__ double J(int i, int j) const { return p[(kPitJ + pit_sy(i, j)) * ld]; }
+};
+
+// o = ei (x) ej, ei the earlier element (Sarkka & Garcia-Fernandez, Lemma 8):
+//   M = (I + C_i J_j)^-1, A = A_j M A_i, b = A_j M (b_i + C_i eta_j) + b_j,
+//   C = A_j M C_i A_j^T + C_j, eta = A_i^T M^T (eta_j - J_j b_i) + eta_i,
+//   J = A_i^T M^T J_j A_i + J_i.
+// M by Gauss-Jordan with partial pivoting (I + C J with C, J PSD has eigenvalues >= 1 but
+// its leading minors can vanish); the row swaps are selects, so every index stays static.
+__device__ __forceinline__ void pit_combine(const PitEl& ei, const PitEl& ej, double (&o)[kPitEl]) {
+  double T[5][10];
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      double s = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) s = fma(ei.C(r, k), ej.J(k, c), s);
+      T[r][c] = s;
+      T[r][5 + c] = (r == c) ? 1.0 : 0.0;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    int p = k;
+    double best = fabs(T[k][k]);
+#pragma unroll
+    for (int r = k + 1; r < 5; ++r) {
+      const double v = fabs(T[r][k]);
+      if (v > best) {
+        best = v;
+        p = r;
+      }
+    }
+#pragma unroll
+    for (int r = k + 1; r < 5; ++r) {
+      const bool sw = p == r;
+#pragma unroll
+      for (int c = k; c < 10; ++c) {
+        const double t = T[k][c];
+        T[k][c] = sw ? T[r][c] : t;
+        T[r][c] = sw ? t : T[r][c];
+      }
+    }
+    const double ip = 1.0 / T[k][k];
+#pragma unroll
+    for (int c = k + 1; c < 10; ++c) T[k][c] *= ip;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      if (r == k) continue;
+      const double f = T[r][k];
+#pragma unroll
+      for (int c = k + 1; c < 10; ++c) T[r][c] = fma(-f, T[k][c], T[r][c]);
+    }
+  }
+  // M = T[.][5..9]
+  auto M = [&](int r, int c) -> double { return T[r][5 + c]; };
+  double X[5][5];  // M A_i
+#pragma unroll
+  for (int r = 0; r < 5; ++r)
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) s = fma(M(r, k), ei.A(k, c), s);
+      X[r][c] = s;
+    }
+#pragma unroll
+  for (int r = 0; r < 5; ++r)
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) s = fma(ej.A(r, k), X[k][c], s);
+      o[kPitA + r * 5 + c] = s;
+    }
+  {
+    double w[5], mw[5];
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      double s = ei(kPitB + r);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) s = fma(ei.C(r, k), ej(kPitE + k), s);
+      w[r] = s;
+    }
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) s = fma(M(r, k), w[k], s);
+      mw[r] = s;
+    }
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      double s = ej(kPitB + r);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) s = fma(ej.A(r, k), mw[k], s);
+      o[kPitB + r] = s;
+    }
+  }
+  // C = A_j (M C_i) A_j^T + C_j: X = M C_i, Y = X A_j^T, C = A_j Y (upper triangle)
+#pragma unroll
+  for (int r = 0; r < 5; ++r)
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) s = fma(M(r, k), ei.C(k, c), s);
+      X[r][c] = s;
+    }
+  {
+    double Y[5][5];
+#pragma unroll
+    for (int r = 0; r < 5; ++r)
+#pragma unroll
+      for (int c = 0; c < 5; ++c) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) s = fma(X[r][k], ej.A(c, k), s);
+        Y[r][c] = s;
+      }
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+      for (int j = i; j < 5; ++j) {
+        double s = ej.C(i, j);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) s = fma(ej.A(i, k), Y[k][j], s);
+        o[kPitC + pit_sy(i, j)] = s;
+      }
+  }
+  // eta = A_i^T M^T (eta_j - J_j b_i) + eta_i
+  {
+    double y[5], z[5];
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      double s = ej(kPitE + r);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) s = fma(-ej.J(r, k), ei(kPitB + k), s);
+      y[r] = s;
+    }
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) s = fma(M(k, r), y[k], s);
+      z[r] = s;
+    }
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      double s = ei(kPitE + r);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) s = fma(ei.A(k, r), z[k], s);
+      o[kPitE + r] = s;
+    }
+  }
+  // J = A_i^T (M^T J_j) A_i + J_i: X = M^T J_j, Y = X A_i, J = A_i^T Y (upper triangle)
+#pragma unroll
+  for (int r = 0; r < 5; ++r)
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) s = fma(M(k, r), ej.J(k, c), s);
+      X[r][c] = s;
+    }
+  {
+    double Y[5][5];
+#pragma unroll
+    for (int r = 0; r < 5; ++r)
+#pragma unroll
+      for (int c = 0; c < 5; ++c) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) s = fma(X[r][k], ei.A(k, c), s);
+        Y[r][c] = s;
+      }
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+      for (int j = i; j < 5; ++j) {
+        double s = ei.J(i, j);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) s = fma(ei.A(k, i), Y[k][j], s);
+        o[kPitJ + pit_sy(i, j)] = s;
+      }
+  }
+}
+
+// The first pass's trajectory. A pass linearizes every sample at xbar, and where xbar is far
+// from the filter's path (the start-up transient from x0, P0 = I) the fixed point is only
+// reached one block per pass (scripts/study/ekf_pit_proto.py: 9 passes of crawling before
+// quadratic convergence for init_m = 6 on an m = 4.3 record). So the sequential EKF (lane
+// arithmetic) runs the first T0 samples, their predicted states seed xbar there, and every
+// later sample starts at the state entering sample T0. One lane per channel.
+__global__ __launch_bounds__(64) void ekf_pit_head_kernel(const double* __restrict__ x, int64_t nrec, int64_t rs,
+                                                          int64_t T0, const double* __restrict__ x0,
+                                                          const double* __restrict__ p0,
+                                                          const double* __restrict__ qd,
+                                                          const double* __restrict__ rv, double w_m, double f_samp,
+                                                          int64_t B, int64_t nb, double* __restrict__ xbar,
+                                                          double* __restrict__ hst, DfmiTrigK tk) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrec) return;
+  const int64_t slots = B * nb;
+  double st[5], P[5][5], Q[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    st[i] = x0[r * 5 + i];
+    Q[i] = qd[i];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) P[i][j] = (i == j) ? p0[i] : 0.0;
+  }
+  const double Rv = rv[r];
+  for (int64_t k = 0; k < T0; ++k) {
+    const int64_t b = k / B, s = (k - b * B) * nb + b;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) xbar[(r * 5 + c) * slots + s] = st[c];
+    ekf_step(st, P, Q, Rv, x[r * rs + k], w_m * ((double)k / f_samp), tk);
+  }
+#pragma unroll
+  for (int c = 0; c < 5; ++c) hst[r * 5 + c] = st[c];
+}
+
+// Transposes the channel data into blocks, tabulates w_m t_k (ekf_phase_kernel's
+// expression: same bits), sets xbar from sample T0 on to the head's state (hst) and clears
+// the per-channel flags. One thread per (sample slot, channel); grid.y = channel.
+__global__ __launch_bounds__(256) void ekf_pit_gather_kernel(const double* __restrict__ x, int64_t rs, int64_t n,
+                                                             const double* __restrict__ hst, int64_t T0, int64_t B,
+                                                             int64_t nb, double w_m, double f_samp,
+                                                             double* __restrict__ xt, double* __restrict__ wtt,
+                                                             double* __restrict__ xbar, int* __restrict__ flag) {
+  const int64_t r = blockIdx.y;
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // s = i nb + b
+  const int64_t slots = B * nb;
+  if (s == 0) {
+    flag[2 * r] = 0;      // converged
+    flag[2 * r + 1] = 0;  // passes run
+  }
+  if (s >= slots) return;
+  const int64_t i = s / nb, b = s - i * nb;
+  const int64_t k = b * B + i;
+  xt[r * slots + s] = k < n ? x[r * rs + k] : 0.0;
+  if (r == 0) wtt[s] = w_m * ((double)k / f_samp);
+  if (k >= T0) {
+#pragma unroll
+    for (int c = 0; c < 5; ++c) xbar[(r * 5 + c) * slots + s] = hst[r * 5 + c];
+  }
+}
+
+// Step 1 + the in-block fold of step 2: lane = block. The element of sample k (F = I,
+// Q diagonal) is A_k = I - K h^T, b_k = K e, C_k = Q - (Qh)(Qh)^T / S, eta_k = h e / S,
+// J_k = h h^T / S (S = h^T Q h + R, K = Q h / S, e = y_k - d_k); folding it into the
+// running aggregate (A, b, C, eta, J) is the general combine with a rank-1 J_j, which
+// reduces to (g = (C + Q) h, gamma = h.g + R, v = g / gamma, r = A^T h, eps = e - h.b):
+//   A -= v r^T, b += v eps, C += Q - g v^T, eta += r eps / gamma, J += r r^T / gamma
+// (tests/test_ekf_pit_host.py checks it against the general combine). Block 0 starts from
+// the prior element (A = 0, b = x0, C = P0), the others from the identity.
+__global__ __launch_bounds__(64) void ekf_pit_aggregate_kernel(const double* __restrict__ xt,
+                                                               const double* __restrict__ wtt,
+                                                               const double* __restrict__ xbar, int64_t n, int64_t B,
+                                                               int64_t nb, const double* __restrict__ x0,
+                                                               const double* __restrict__ p0,
+                                                               const double* __restrict__ qd,
+                                                               const double* __restrict__ rv,
+                                                               const int* __restrict__ flag,
+                                                               double* __restrict__ agg, DfmiTrigK tk) {
+  const int64_t r = blockIdx.y;
+  if (flag[2 * r]) return;
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  const int64_t slots = B * nb;
+  double A[25], bv[5], C[15], et[5], J[15], q[5];
+  const bool first = b == 0;
+#pragma unroll
+  for (int c = 0; c < 25; ++c) A[c] = (!first && c / 5 == c % 5) ? 1.0 : 0.0;
+#pragma unroll
+  for (int c = 0; c < 15; ++c) C[c] = J[c] = 0.0;
+#pragma unroll
+  for (int c = 0; c < 5; ++c) {
+    bv[c] = first ? x0[r * 5 + c] : 0.0;
+    et[c] = 0.0;
+    q[c] = qd[c];
+    if (first) C[pit_sy(c, c)] = p0[c];
+  }
+  const double Rv = rv[r];
+  const int64_t kend = (b + 1) * B < n ? B : n - b * B;
+  for (int64_t i = 0; i < kend; ++i) {
+    const int64_t s = i * nb + b;
+    double xb[5];
+#pragma unroll
+    for (int c = 0; c < 5; ++c) xb[c] = xbar[(r * 5 + c) * slots + s];
+    const double a = xb[0], m = xb[1];
+    const double th = wtt[s] + xb[3];
+    double sth, cth, sa, ca;
+    dfmi_sincos_k(th, tk, &sth, &cth);
+    const double arg = fma(m, cth, xb[2]);
+    dfmi_sincos_k(arg, tk, &sa, &ca);
+    const double hv = fma(a, ca, xb[4]);
+    const double h[5] = {ca, (-a * cth) * sa, -a * sa, ((a * m) * sth) * sa, 1.0};
+    // eps = e - h.b with e = y - hv + h.xbar
+    double eps = xt[r * slots + s] - hv;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) eps = fma(h[c], xb[c] - bv[c], eps);
+    double g[5], rr[5];
+#pragma unroll
+    for (int i2 = 0; i2 < 5; ++i2) {
+      double s2 = q[i2] * h[i2];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) s2 = fma(C[pit_sy(i2, j)], h[j], s2);
+      g[i2] = s2;
+    }
+    double gam = Rv;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) gam = fma(h[c], g[c], gam);
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      double s2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) s2 = fma(A[k * 5 + c], h[k], s2);
+      rr[c] = s2;
+    }
+    const double ig = 1.0 / gam;
+    const double ei = eps * ig;
+    double v[5], ri[5];
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      v[c] = g[c] * ig;
+      ri[c] = rr[c] * ig;
+    }
+#pragma unroll
+    for (int r2 = 0; r2 < 5; ++r2)
+#pragma unroll
+      for (int c = 0; c < 5; ++c) A[r2 * 5 + c] = fma(-v[r2], rr[c], A[r2 * 5 + c]);
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      bv[c] = fma(v[c], eps, bv[c]);
+      et[c] = fma(rr[c], ei, et[c]);
+    }
+#pragma unroll
+    for (int i2 = 0; i2 < 5; ++i2)
+#pragma unroll
+      for (int j = i2; j < 5; ++j) {
+        const int y = pit_sy(i2, j);
+        C[y] = fma(-g[i2], v[j], i2 == j ? C[y] + q[i2] : C[y]);
+        J[y] = fma(ri[i2], rr[j], J[y]);
+      }
+  }
+  double* o = agg + r * kPitEl * nb + b;
+#pragma unroll
+  for (int c = 0; c < 25; ++c) o[(kPitA + c) * nb] = A[c];
+#pragma unroll
+  for (int c = 0; c < 5; ++c) {
+    o[(kPitB + c) * nb] = bv[c];
+    o[(kPitE + c) * nb] = et[c];
+  }
+#pragma unroll
+  for (int c = 0; c < 15; ++c) {
+    o[(kPitC + c) * nb] = C[c];
+    o[(kPitJ + c) * nb] = J[c];
+  }
+}
+
+// Inclusive Hillis-Steele scan of n_el elements el[r][65][ld] in workgroups of 256 (LDS
+// [65][256], 133 KB: one workgroup per CU), in place; the workgroup totals go to
+// tot[r][65][gridDim.x] when tot is given (the top-level pass scans those with one
+// workgroup and tot = nullptr). Padding elements are the identity.
+__global__ __launch_bounds__(kPitWg) void ekf_pit_scan_kernel(double* __restrict__ el, int64_t n_el, int64_t ld,
+                                                              double* __restrict__ tot, const int* __restrict__ flag) {
+  const int64_t r = blockIdx.y;
+  if (flag[2 * r]) return;
+  __shared__ double s[kPitEl * kPitWg];
+  const int t = threadIdx.x;
+  const int64_t e = (int64_t)blockIdx.x * kPitWg + t;
+  const bool live = e < n_el;
+  double* base = el + r * kPitEl * ld + e;
+#pragma unroll
+  for (int c = 0; c < kPitEl; ++c) s[c * kPitWg + t] = live ? base[c * ld] : pit_identity(c);
+  __syncthreads();
+  for (int off = 1; off < kPitWg; off <<= 1) {
+    double o[kPitEl];
+    const bool act = t >= off;
+    if (act) pit_combine(PitEl{s + t - off, kPitWg}, PitEl{s + t, kPitWg}, o);
+    __syncthreads();
+    if (act) {
+#pragma unroll
+      for (int c = 0; c < kPitEl; ++c) s[c * kPitWg + t] = o[c];
+    }
+    __syncthreads();
+  }
+  if (live) {
+#pragma unroll
+    for (int c = 0; c < kPitEl; ++c) base[c * ld] = s[c * kPitWg + t];
+  }
+  if (tot && t == kPitWg - 1) {
+    const int64_t ng = gridDim.x;
+#pragma unroll
+    for (int c = 0; c < kPitEl; ++c) tot[(r * kPitEl + c) * ng + blockIdx.x] = s[c * kPitWg + t];
+  }
+}
+
+// Step 3: lane = block. Entry state: (x0, P0) for block 0; else the filtered (mean, cov)
+// after block b-1, i.e. the inclusive prefix: agg[b-1] (scanned within its workgroup)
+// preceded by tot[g-1] (scanned workgroup totals) when b-1 lies past the first workgroup.
+// Then ekf_step over the block (the lane kernel's arithmetic), writing the next xbar (the
+// state entering each following sample), its largest relative move into conv[r][b], and
+// the snapshots (fitters.py:305-307).
+__global__ __launch_bounds__(64) void ekf_pit_blocks_kernel(const double* __restrict__ xt,
+                                                            const double* __restrict__ wtt,
+                                                            double* __restrict__ xbar, int64_t n, int64_t B, int64_t nb,
+                                                            const double* __restrict__ x0,
+                                                            const double* __restrict__ p0,
+                                                            const double* __restrict__ qd,
+                                                            const double* __restrict__ rv,
+                                                            const double* __restrict__ agg,
+                                                            const double* __restrict__ tot, const int* __restrict__ flag,
+                                                            double* __restrict__ conv, int R, int64_t nbuf,
+                                                            double* __restrict__ states, DfmiTrigK tk) {
+  const int64_t r = blockIdx.y;
+  if (flag[2 * r]) return;
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  const int64_t slots = B * nb;
+  double st[5], P[5][5], Q[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) Q[i] = qd[i];
+  if (b == 0) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      st[i] = x0[r * 5 + i];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) P[i][j] = (i == j) ? p0[i] : 0.0;
+    }
+  } else {
+    const int64_t p = b - 1, g = p / kPitWg;
+    const PitEl loc{agg + r * kPitEl * nb + p, nb};
+    if (g == 0) {
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        st[i] = loc(kPitB + i);
+#pragma unroll
+        for (int j = i; j < 5; ++j) P[i][j] = loc.C(i, j);
+      }
+    } else {
+      const int64_t ng = (nb + kPitWg - 1) / kPitWg;
+      double o[kPitEl];
+      pit_combine(PitEl{tot + r * kPitEl * ng + (g - 1), ng}, loc, o);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        st[i] = o[kPitB + i];
+#pragma unroll
+        for (int j = i; j < 5; ++j) P[i][j] = o[kPitC + pit_sy(i, j)];
+      }
+    }
+  }
+  const double Rv = rv[r];
+  double dmax = 0.0;
+  const int64_t kend = (b + 1) * B < n ? B : n - b * B;
+  for (int64_t i = 0; i < kend; ++i) {
+    const int64_t s = i * nb + b;
+    ekf_step(st, P, Q, Rv, xt[r * slots + s], wtt[s], tk);
+    const int64_t k = b * B + i;
+    if (k + 1 < n) {
+      const int64_t s1 = i + 1 < B ? s + nb : b + 1;  // slot of sample k + 1
+#pragma unroll
+      for (int c = 0; c < 5; ++c) {
+        double* px = xbar + (r * 5 + c) * slots + s1;
+        const double d = fabs(st[c] - *px) / fmax(1.0, fabs(st[c]));
+        dmax = d <= dmax ? dmax : d;  // NaN propagates (never "converged")
+        *px = st[c];
+      }
+    }
+    if ((k + 1) % R == 0) {
+      const int64_t bi = (k + 1) / R - 1;
+      if (bi < nbuf) {
+#pragma unroll
+        for (int c = 0; c < 5; ++c) states[(r * nbuf + bi) * 5 + c] = st[c];
+      }
+    }
+  }
+  conv[r * nb + b] = dmax;
+}
+
+// One workgroup per channel: converged when every block moved xbar by at most tol
+// (relative, see ekf_pit_blocks_kernel); counts the passes that ran.
+__global__ __launch_bounds__(256) void ekf_pit_check_kernel(const double* __restrict__ conv, int64_t nb, double tol,
+                                                            int* __restrict__ flag) {
+  const int64_t r = blockIdx.x;
+  if (flag[2 * r]) return;
+  __shared__ double red[256];
+  double m = 0.0;
+  for (int64_t b = threadIdx.x; b < nb; b += 256) {
+    const double v = conv[r * nb + b];
+    m = v <= m ? m : v;
+  }
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      const double v = red[threadIdx.x + w];
+      red[threadIdx.x] = v <= red[threadIdx.x] ? red[threadIdx.x] : v;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    flag[2 * r + 1] += 1;
+    if (red[0] <= tol) flag[2 * r] = 1;
+  }
+}
+
+// A channel the passes left unconverged: the sequential EKF (ekf_kernel's loop) from x0.
+__global__ __launch_bounds__(64) void ekf_pit_fallback_kernel(const double* __restrict__ x, int64_t nrec, int64_t rs,
+                                                              int64_t n, const double* __restrict__ x0,
+                                                              const double* __restrict__ p0,
+                                                              const double* __restrict__ qd,
+                                                              const double* __restrict__ rv,
+                                                              const double* __restrict__ wt, int R, int64_t nbuf,
+                                                              double* __restrict__ states, int* __restrict__ flag,
+                                                              DfmiTrigK tk) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrec || flag[2 * r]) return;
+  flag[2 * r + 1] = -flag[2 * r + 1];  // reported as a negative pass count
+  const double* __restrict__ xr = x + r * rs;
+  double st[5], P[5][5], Q[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    st[i] = x0[r * 5 + i];
+    Q[i] = qd[i];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) P[i][j] = (i == j) ? p0[i] : 0.0;
+  }
+  const double Rv = rv[r];
+  for (int64_t k = 0; k < n; ++k) {
+    ekf_step(st, P, Q, Rv, xr[k], wt[k], tk);
+    if ((k + 1) % R == 0) {
+      const int64_t bi = (k + 1) / R - 1;
+      if (bi < nbuf) {
+#pragma unroll
+        for (int c = 0; c < 5; ++c) states[(r * nbuf + bi) * 5 + c] = st[c];
+      }
+    }
+  }
+}
+
+}  // namespace dfmi

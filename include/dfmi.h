@@ -125,7 +125,11 @@ int dfmi_nls_record(const double* x, int64_t nrec, int64_t rec_stride, int64_t n
  * chain over its samples: up to 16 x CUs channels one 16-lane DPP row per channel (4 per
  * wave; ekf_rot_kernel with sin / cos by rotation between anchors when R % 4 == 0, else
  * ekf_row_kernel), more channels one lane per channel (ekf_lane_rot_kernel / ekf_kernel);
- * dfmi_set_tuning "ekf_row" / "ekf_rot" select. x[r*rec_stride + k], k < n_samp. x0[r*5+i] initial state (dc included),
+ * dfmi_set_tuning "ekf_row" / "ekf_rot" select. Up to "ekf_pit" (8) channels of at least
+ * "ekf_pit_min" (32768) samples run parallel in time instead (ekf_pit.h): relinearization
+ * passes of an associative linear Kalman scan over blocks, each ending in the true EKF per
+ * block, until the trajectory stops moving (relative 1e-11), else the lane kernel; the same
+ * states to rounding (~1e-13). x[r*rec_stride + k], k < n_samp. x0[r*5+i] initial state (dc included),
  * p0_diag[5], q_diag[5], r_val[r] measurement variance, w_m = 2*pi*f_mod,
  * f_samp; snapshots every R samples into states[(r*nbuf + b)*5 + i]. */
 int dfmi_ekf(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, const double* x0,
@@ -140,6 +144,12 @@ int dfmi_ekf(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
 int dfmi_ekf_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, const double* init4,
                  const double* p0_diag, const double* q_diag, const double* r_val, double w_m, double f_samp,
                  int32_t R, int64_t nbuf, double* states, int32_t mem, void* stream);
+
+/* Passes the last dfmi_ekf / dfmi_ekf_fit call on this thread ran per channel (nrec as
+ * that call's): 0 = sequential kernels, k > 0 = converged after k passes, -k = not
+ * converged after k passes and re-run by the lane kernel. Synchronises the device; read it
+ * before the next EKF call. */
+int dfmi_ekf_pit_passes(int32_t* passes, int64_t nrec);
 
 /* np.mean / np.var of nrec float64 records x[r*rec_stride .. + n] (1 <= n < 2^31),
  * bit-exact with numpy's pairwise summation (numpy 2.x _methods._mean / _var); var

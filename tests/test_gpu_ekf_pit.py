@@ -1,0 +1,176 @@
+"""The EKF parallel in time (deepfmkit_amd/csrc/ekf_pit.h) against the sequential lane
+kernel and the oracle's scalar C restatement of EKFFitter.fit's loop (fitters.py:274-307,
+oracle/csrc/ekf_scalar.c, pinned to the numpy oracle by tests/test_oracle_c.py and to the
+reference's own states by tests/test_oracle_golden.py::test_oracle_ekf_full_length).
+
+The parallel form is the sequential filter to rounding (every block runs the true EKF from
+an entry state the converged scan supplies), so it is held to the same 1e-12 of the C
+oracle as the sequential kernels; a channel that has not converged after the last pass is
+re-run by the lane kernel, bit for bit."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+QD = np.array([1e-8, 1e-8, 1e-6, 1e-6, 1e-8])
+
+
+def _raw(dfm, m, seconds, trial, psi=0.0, phi=0.0):
+    laser, ifo = dfm.LaserConfig(), dfm.InterferometerConfig()
+    laser.psi = psi
+    ifo.phi = phi
+    dfm.set_laser_df_for_effect(laser, ifo, m)
+    dff = dfm.DeepFitFramework()
+    dff.load_sim(dfm.DFMIObject("p", laser, ifo, f_samp=200000.0))
+    dff.simulate("p", n_seconds=seconds, mode="snr", snr_db=40.0, trial_num=trial)
+    return np.ascontiguousarray(dff.raws["p"].samples(), dtype=np.float64)
+
+
+def _c_ekf(x, init4, R, nbuf, qd=QD, r_val=None):
+    so = os.path.join(ROOT, "oracle", "libekf_scalar.so")
+    if not os.path.exists(so):
+        pytest.skip("oracle/libekf_scalar.so not built (make -C oracle)")
+    cl = ctypes.CDLL(so)
+    P = ctypes.c_void_p
+    cl.ekf_scalar.argtypes = [P, ctypes.c_int64, P, P, P, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                              ctypes.c_int64, ctypes.c_int64, P]
+    x0 = np.array(list(init4) + [np.mean(x)])
+    p0, q = np.ones(5), np.ascontiguousarray(qd, dtype=np.float64)
+    st = np.zeros((nbuf, 5))
+    cl.ekf_scalar(x.ctypes.data, x.size, x0.ctypes.data, p0.ctypes.data, q.ctypes.data,
+                  float(np.var(x) if r_val is None else r_val), 2 * np.pi * 1000.0, 200000.0, R, nbuf, st.ctypes.data)
+    return st
+
+
+class _tune:
+    """dfmi_set_tuning for the duration of a block, restoring the defaults."""
+    DEFAULTS = {"ekf_row": 1, "ekf_rot": 1, "ekf_pit": 8, "ekf_pit_min": 32768, "ekf_pit_block": 0,
+                "ekf_pit_passes": 12, "ekf_pit_head": 512}
+
+    def __init__(self, lib, **kw):
+        self.lib, self.kw = lib, kw
+
+    def __enter__(self):
+        from deepfmkit_amd import _lib
+        for k, v in self.kw.items():
+            _lib.check(self.lib.dfmi_set_tuning(k.encode(), v), "tune")
+        return self
+
+    def __exit__(self, *exc):
+        from deepfmkit_amd import _lib
+        for k in self.kw:
+            _lib.check(self.lib.dfmi_set_tuning(k.encode(), self.DEFAULTS[k]), "tune")
+
+
+def _ekf(lib, xs, R, nbuf, init4=(1.6, 6.0, 0.0, 0.0), qd=QD, r_val=None):
+    """dfmi_ekf_fit over the records xs (equal lengths, host memory): states (nrec, nbuf, 5),
+    the reported kernel and the pass counts."""
+    from deepfmkit_amd import _lib
+    x = np.ascontiguousarray(np.concatenate(xs), dtype=np.float64)
+    n = xs[0].size
+    st = np.zeros((len(xs), nbuf, 5))
+    i4 = np.array(init4, dtype=np.float64)
+    p0, q = np.ones(5), np.ascontiguousarray(qd, dtype=np.float64)
+    rv = None if r_val is None else _lib.ptr(np.array([r_val]))
+    _lib.check(lib.dfmi_ekf_fit(_lib.ptr(x), len(xs), n, n, _lib.ptr(i4), _lib.ptr(p0), _lib.ptr(q), rv,
+                                2 * np.pi * 1000.0, 200000.0, R, nbuf, _lib.ptr(st), _lib.DFMI_MEM_HOST, None),
+               "dfmi_ekf_fit")
+    kname = lib.dfmi_last_demod_kernel().decode()
+    passes = (ctypes.c_int32 * len(xs))()
+    _lib.check(lib.dfmi_ekf_pit_passes(ctypes.cast(passes, ctypes.c_void_p), len(xs)), "passes")
+    return st, kname, list(passes)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from deepfmkit_amd import _lib
+    return _lib.load()
+
+
+@pytest.fixture(scope="module")
+def c5():
+    import deepfmkit_amd as dfm
+    return _raw(dfm, 6.0, 2.0, 7)
+
+
+def test_pit_config5_default_path_matches_c_oracle(lib, c5):
+    """One 400,000-sample channel takes the parallel form by default and converges in a few
+    passes; every snapshot within 1e-12 of the C restatement, the sequential row kernel within
+    1e-12 of it too."""
+    ref = _c_ekf(c5, (1.6, 6.0, 0.0, 0.0), 4000, 100)
+    got, kname, passes = _ekf(lib, [c5], 4000, 100)
+    assert kname.startswith("ekf_pit"), kname
+    assert 1 <= passes[0] <= 12, passes
+    err = np.abs(got[0] - ref)
+    print("pit passes", passes, "max |d state| vs C oracle", err.max())
+    assert err.max() <= 1e-12, (err.max(), np.unravel_index(err.argmax(), err.shape))
+    with _tune(lib, ekf_pit=0):
+        seq, kseq, ps = _ekf(lib, [c5], 4000, 100)
+    assert kseq == "ekf_rot_kernel" and ps == [0]
+    assert np.abs(seq[0] - got[0]).max() <= 1e-12
+
+
+@pytest.mark.parametrize("block", [16, 49, 700, 5000])
+def test_pit_block_sizes_ragged(lib, block):
+    """Block sizes from 16 (2,501 blocks: ten scan workgroups and the top-level scan) to 5000
+    (one workgroup), a 40,003-sample record (no block size divides it), R = 3000 (snapshots
+    mid-block) and R = 7: all within 1e-12 of the C oracle."""
+    import deepfmkit_amd as dfm
+    x = _raw(dfm, 6.0, 0.2, 3)
+    x = np.concatenate([x, x[:3]])
+    assert x.size == 40_003
+    with _tune(lib, ekf_pit_block=block):
+        for R, nbuf in ((3000, 13), (7, 5714)):
+            ref = _c_ekf(x, (1.6, 6.0, 0.0, 0.0), R, nbuf)
+            got, kname, passes = _ekf(lib, [x], R, nbuf)
+            assert kname.startswith(f"ekf_pit (B={block},"), kname
+            assert passes[0] >= 1
+            err = np.abs(got[0] - ref).max()
+            print("B", block, "R", R, "passes", passes, "err", err)
+            assert err <= 1e-12, err
+
+
+def test_pit_channels_independent(lib):
+    """Several channels in one call (different m, phi, psi; one tuned): each channel equals its
+    own single-channel run bit for bit, and the C oracle within 1e-12."""
+    import deepfmkit_amd as dfm
+    xs = [_raw(dfm, 6.0, 0.25, 11), _raw(dfm, 4.3, 0.25, 12, psi=0.3, phi=0.7), _raw(dfm, 9.0, 0.25, 13, phi=1.3)]
+    many, kname, passes = _ekf(lib, xs, 4000, 12)
+    assert kname.startswith("ekf_pit") and all(p >= 1 for p in passes), (kname, passes)
+    for c, x in enumerate(xs):
+        one, _, _ = _ekf(lib, [x], 4000, 12)
+        np.testing.assert_array_equal(many[c], one[0])
+        ref = _c_ekf(x, (1.6, 6.0, 0.0, 0.0), 4000, 12)
+        assert np.abs(one[0] - ref).max() <= 1e-12
+
+
+def test_pit_unconverged_falls_back_bit_exact(lib, c5):
+    """With one pass allowed the channel has not converged: it is re-run by the lane kernel
+    (ekf_pit_fallback_kernel = ekf_kernel's loop), reported as -1 pass, and its states equal
+    ekf_kernel's bit for bit."""
+    x = c5[:100_000]
+    with _tune(lib, ekf_pit_passes=1):
+        got, kname, passes = _ekf(lib, [x], 4000, 25)
+    assert kname.startswith("ekf_pit") and passes == [-1], (kname, passes)
+    with _tune(lib, ekf_pit=0, ekf_row=0, ekf_rot=0):
+        lane, kl, _ = _ekf(lib, [x], 4000, 25)
+    assert kl == "ekf_kernel"
+    np.testing.assert_array_equal(got, lane)
+
+
+def test_pit_tuned_noise_matches_c_oracle(lib):
+    """The tuned configuration of the golden set (Q_diag 1e-9/1e-7, R_val 1e-3, m=4.3 record,
+    init at the reference defaults): a stiffer filter, still within 1e-12 of the C oracle."""
+    import deepfmkit_amd as dfm
+    x = _raw(dfm, 4.3, 1.0, 11, psi=0.3, phi=0.7)
+    qd = np.array([1e-9, 1e-9, 1e-7, 1e-7, 1e-9])
+    ref = _c_ekf(x, (1.6, 6.0, 0.0, 0.0), 4000, 50, qd=qd, r_val=0.001)
+    got, kname, passes = _ekf(lib, [x], 4000, 50, qd=qd, r_val=0.001)
+    assert kname.startswith("ekf_pit") and passes[0] >= 1, (kname, passes)
+    err = np.abs(got[0] - ref).max()
+    print("tuned passes", passes, "err", err)
+    assert err <= 1e-12, err

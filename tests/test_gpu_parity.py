@@ -154,24 +154,34 @@ def test_ekf_matches_reference(manifest):
 # rot: 16-lane row per channel, sincos by rotation between anchors (default for few
 # channels, R % 4 == 0); row: the same row with the full sincos per sample; lanerot / lane:
 # one lane per channel (many channels) with / without the rotation.
+# pit: parallel in time (ekf_pit.h), the default for up to 8 channels of >= 32768 samples;
+# here forced on from 1024 samples so the shorter records take it too.
 EKF_KERNELS = {"rot": (1, 1, "ekf_rot_kernel"), "row": (1, 0, "ekf_row_kernel"), "lanerot": (0, 1, "ekf_lane_rot_kernel"),
-               "lane": (0, 0, "ekf_kernel")}
+               "lane": (0, 0, "ekf_kernel"), "pit": (1, 1, "ekf_pit")}
 
 
 class _ekf_kernel:
+    """Selects one EKF kernel by tuning; kname: the prefix dfmi_last_demod_kernel reports."""
+
     def __init__(self, lib, name):
         self.lib, self.row, self.rot, self.kname = lib, *EKF_KERNELS[name]
+        self.pit = name == "pit"
 
     def __enter__(self):
         from deepfmkit_amd import _lib
         _lib.check(self.lib.dfmi_set_tuning(b"ekf_row", self.row), "tune")
         _lib.check(self.lib.dfmi_set_tuning(b"ekf_rot", self.rot), "tune")
+        _lib.check(self.lib.dfmi_set_tuning(b"ekf_pit", 8 if self.pit else 0), "tune")
+        _lib.check(self.lib.dfmi_set_tuning(b"ekf_pit_min", 1024 if self.pit else 32768), "tune")
         return self
 
     def __exit__(self, *exc):
         from deepfmkit_amd import _lib
-        _lib.check(self.lib.dfmi_set_tuning(b"ekf_row", 1), "tune")
-        _lib.check(self.lib.dfmi_set_tuning(b"ekf_rot", 1), "tune")
+        for key, v in ((b"ekf_row", 1), (b"ekf_rot", 1), (b"ekf_pit", 8), (b"ekf_pit_min", 32768)):
+            _lib.check(self.lib.dfmi_set_tuning(key, v), "tune")
+
+    def used(self):
+        return self.lib.dfmi_last_demod_kernel().decode().startswith(self.kname)
 
 
 def _c_ekf(x, init4, R, nbuf, f_samp=200000.0, f_mod=1000.0, qd=(1e-8, 1e-8, 1e-6, 1e-6, 1e-8)):
@@ -195,7 +205,7 @@ def _c_ekf(x, init4, R, nbuf, f_samp=200000.0, f_mod=1000.0, qd=(1e-8, 1e-8, 1e-
     return ref
 
 
-@pytest.mark.parametrize("kern", ["rot", "row", "lanerot", "lane"])
+@pytest.mark.parametrize("kern", ["rot", "row", "lanerot", "lane", "pit"])
 def test_ekf_long_record_matches_oracle(kern):
     """Config 5 shape on a longer record than the golden one (0.1 s = 20,000 samples,
     5 snapshots): every EKF kernel — one 16-lane row per channel with sincos by rotation
@@ -208,10 +218,10 @@ def test_ekf_long_record_matches_oracle(kern):
     from oracle import nls_oracle as O
     lib = _lib.load()
     with _ekf_kernel(lib, kern) as k:
-        _ekf_long_record(dfm, O, lib, k.kname)
+        _ekf_long_record(dfm, O, lib, k)
 
 
-def _ekf_long_record(dfm, O, lib, kname):
+def _ekf_long_record(dfm, O, lib, kk):
     laser = dfm.LaserConfig()
     ifo = dfm.InterferometerConfig()
     dfm.set_laser_df_for_effect(laser, ifo, 6.0)
@@ -222,14 +232,14 @@ def _ekf_long_record(dfm, O, lib, kname):
     x = np.asarray(raw.samples(), dtype=np.float64)
     ref = O.ekf_record(x, 200000.0, 1000.0, 20)
     got = dfm.fitters.ekf_records([raw], 20)[0]
-    assert lib.dfmi_last_demod_kernel().decode() == kname
+    assert kk.used(), lib.dfmi_last_demod_kernel()
     assert np.max(np.abs(got - ref)) <= 1e-12, np.max(np.abs(got - ref))
     many = dfm.fitters.ekf_records([raw] * 6, 20)  # row kernel: a second wave, rows past the end
     for k in range(6):
         np.testing.assert_array_equal(many[k], got)
 
 
-@pytest.mark.parametrize("kern", ["rot", "row", "lanerot", "lane"])
+@pytest.mark.parametrize("kern", ["rot", "row", "lanerot", "lane", "pit"])
 def test_ekf_config5_full_length_matches_c_oracle(kern):
     """Config 5 at the length BASELINE names (notebooks/2.0 defaults):
     a 2 s = 400,000-sample snr-mode record (m=6, 40 dB) through dfmi_ekf_fit (EKFFitter.fit,
@@ -252,7 +262,7 @@ def test_ekf_config5_full_length_matches_c_oracle(kern):
         pytest.skip("oracle/libekf_scalar.so not built (make -C oracle)")
     with _ekf_kernel(lib, kern) as k:
         got = dfm.fitters.ekf_records([raw], 20)[0]
-        assert lib.dfmi_last_demod_kernel().decode() == k.kname
+        assert k.used(), lib.dfmi_last_demod_kernel()
     assert got.shape == (100, 5)
     err = np.abs(got - ref)
     assert err.max() <= 1e-12, (err.max(), np.unravel_index(err.argmax(), err.shape))
@@ -290,7 +300,7 @@ def test_ekf_rotation_fallback_groups_match_c_oracle(m, f_samp, f_mod, kern):
         pytest.skip("oracle/libekf_scalar.so not built (make -C oracle)")
     with _ekf_kernel(lib, kern) as k:
         got = dfm.fitters.ekf_records([raw], 20, init_m=m)[0]
-        assert lib.dfmi_last_demod_kernel().decode() == k.kname
+        assert k.used(), lib.dfmi_last_demod_kernel()
     err = np.abs(got - ref)
     assert err.max() <= 1e-12, (err.max(), np.unravel_index(err.argmax(), err.shape))
 
@@ -312,7 +322,7 @@ def test_ekf_rotation_channels_independent_and_ragged_tail(kern):
         a = dfm.fitters.ekf_records([ra], 20, init_m=6.0)[0]
         b = dfm.fitters.ekf_records([rb], 20, init_m=6.0)[0]
         mix = dfm.fitters.ekf_records([ra, rb, rb, ra, rb], 20, init_m=6.0)
-        assert lib.dfmi_last_demod_kernel().decode() == kk.kname
+        assert kk.used(), lib.dfmi_last_demod_kernel()
         for k, want in enumerate((a, b, b, a, b)):
             np.testing.assert_array_equal(mix[k], want)
         # ragged tail: 20,003 samples, R = 4000
@@ -325,7 +335,7 @@ def test_ekf_rotation_channels_independent_and_ragged_tail(kern):
         x = np.asarray(raw.samples(), dtype=np.float64)
         x = np.concatenate([x, x[:3]])
         got = _ekf_host(lib, x, 200000.0, 1000.0, 4000, 5)
-        assert lib.dfmi_last_demod_kernel().decode() == kk.kname
+        assert kk.used(), lib.dfmi_last_demod_kernel()
         ref = O.ekf_record(x, 200000.0, 1000.0, 20)
         assert np.max(np.abs(got - ref)) <= 1e-12
         # an odd R (1501 samples per snapshot): no group can end on the snapshots -> no rotation
@@ -571,7 +581,7 @@ def test_raw_file_to_fit_file_end_to_end(tmp_path):
         assert np.asarray(getattr(fb, k)).tobytes() == np.asarray(getattr(fits[None], k), dtype=np.float64).tobytes()
 
 
-@pytest.mark.parametrize("kern", ["rot", "row", "lanerot", "lane"])
+@pytest.mark.parametrize("kern", ["rot", "row", "lanerot", "lane", "pit"])
 @pytest.mark.parametrize("run", ["c5_default", "c5_tuned"])
 def test_ekf_config5_full_length_vs_reference(manifest, kern, run):
     """Config 5 at full length against the REFERENCE's own EKFFitter states (2 s = 400,000
@@ -587,7 +597,7 @@ def test_ekf_config5_full_length_vs_reference(manifest, kern, run):
     lib = _lib.load()
     with _ekf_kernel(lib, kern) as k:
         dff.fit(run, method="ekf", fit_label="f", n=20, **e["fit_kwargs"])
-        assert lib.dfmi_last_demod_kernel().decode() == k.kname
+        assert k.used(), lib.dfmi_last_demod_kernel()
     df = dff.fits_df["f"]
     assert len(df) == 100
     for c in ("amp", "m", "phi", "psi", "dc"):

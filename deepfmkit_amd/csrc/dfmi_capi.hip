@@ -63,9 +63,9 @@ struct Tuning {
   int ekf_pit = 8;       // EKF parallel in time (ekf_pit.h) for up to this many channels of at least
                          // ekf_pit_min samples; 0 = the sequential kernels always
   int ekf_pit_min = 32768;    // samples per channel below which the sequential kernels run
-  int ekf_pit_block = 0;      // samples per block (0: ~n / 8192, at least 16)
+  int ekf_pit_block = 0;      // samples per block (0: ~n / 16384, at least 16)
   int ekf_pit_passes = 12;    // relinearization passes before a channel falls back to the lane kernel
-  int ekf_pit_head = 512;     // samples the sequential EKF runs first to seed the trajectory (ekf_pit_head_kernel)
+  int ekf_pit_head = 256;     // samples the sequential EKF runs first to seed the trajectory (ekf_pit_head_kernel)
 };
 Tuning g_tune;
 
@@ -907,7 +907,7 @@ constexpr double kPitTol = 1e-11;  // relative move of xbar at which a channel i
 int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, const double* dx0, const double* dp0,
                 const double* dq, const double* dr, const double* wt, double w_m, double f_samp, int32_t R,
                 int64_t nbuf, double* dstates, hipStream_t st) {
-  int64_t B = t_tune.ekf_pit_block > 0 ? t_tune.ekf_pit_block : (n + 8191) / 8192;
+  int64_t B = t_tune.ekf_pit_block > 0 ? t_tune.ekf_pit_block : (n + 16383) / 16384;
   if (B < 16) B = 16;
   int64_t nb = (n + B - 1) / B;
   const int64_t ngmax = dfmi::kPitWg;  // the top-level scan is one workgroup
@@ -924,7 +924,7 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
   if ((rc = workspace(dev, "p_xbar", (size_t)(nrec * 5 * slots) * 8, &xbar))) return rc;
   if ((rc = workspace(dev, "p_agg", (size_t)(nrec * dfmi::kPitEl * nb) * 8, &agg))) return rc;
   if ((rc = workspace(dev, "p_tot", (size_t)(nrec * dfmi::kPitEl * ng) * 8, &tot))) return rc;
-  if ((rc = workspace(dev, "p_conv", (size_t)(nrec * nb) * 8, &conv))) return rc;
+  if ((rc = workspace(dev, "p_conv", (size_t)nrec * 8, &conv))) return rc;
   if ((rc = workspace(dev, "p_flag", (size_t)(nrec * 2) * sizeof(int), &flag))) return rc;
   if ((rc = workspace(dev, "p_hst", (size_t)(nrec * 5) * 8, &hst))) return rc;
   const DfmiTrigK tk = dfmi_trig_k();
@@ -933,7 +933,7 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
                      dx0, dp0, dq, dr, w_m, f_samp, B, nb, (double*)xbar, (double*)hst, tk);
   hipLaunchKernelGGL(dfmi::ekf_pit_gather_kernel, dim3((unsigned)((slots + 255) / 256), nr), dim3(256), 0, st, dx, rs,
                      n, (const double*)hst, T0, B, nb, w_m, f_samp, (double*)xt, (double*)wtt, (double*)xbar,
-                     (int*)flag);
+                     (int*)flag, (double*)conv);
   const dim3 lanes((unsigned)((nb + 63) / 64), nr);
   for (int pass = 0; pass < t_tune.ekf_pit_passes; ++pass) {
     hipLaunchKernelGGL(dfmi::ekf_pit_aggregate_kernel, lanes, dim3(64), 0, st, (const double*)xt,
@@ -947,8 +947,8 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
     hipLaunchKernelGGL(dfmi::ekf_pit_blocks_kernel, lanes, dim3(64), 0, st, (const double*)xt, (const double*)wtt,
                        (double*)xbar, n, B, nb, dx0, dp0, dq, dr, (const double*)agg, (const double*)tot,
                        (const int*)flag, (double*)conv, (int)R, nbuf, dstates, tk);
-    hipLaunchKernelGGL(dfmi::ekf_pit_check_kernel, dim3(nr), dim3(256), 0, st, (const double*)conv, nb, kPitTol,
-                       (int*)flag);
+    hipLaunchKernelGGL(dfmi::ekf_pit_check_kernel, dim3((unsigned)((nrec + 63) / 64)), dim3(64), 0, st,
+                       (double*)conv, nrec, kPitTol, (int*)flag);
   }
   hipLaunchKernelGGL(dfmi::ekf_pit_fallback_kernel, dim3((unsigned)((nrec + 63) / 64)), dim3(64), 0, st, dx, nrec,
                      rs, n, dx0, dp0, dq, dr, wt, (int)R, nbuf, dstates, (int*)flag, tk);
@@ -999,30 +999,21 @@ int ekf_impl(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
     void *b, *e;
     if ((rc = workspace(dev, "e_x0", (size_t)nrec * 5 * 8, &b))) return rc;
     if ((rc = workspace(dev, "e_r", (size_t)nrec * 8, &e))) return rc;
-    // host-side staging: init4 in every row, then the device fills x0[r*5+4] and r
-    // (an empty record keeps numpy's NaN mean / variance)
-    std::vector<double> hx0((size_t)nrec * 5), hr((size_t)nrec, NAN);
-    double i4[4];
-    if (host) memcpy(i4, init4, sizeof(i4));
-    else HIPCHK(hipMemcpy(i4, init4, sizeof(i4), hipMemcpyDeviceToHost));
-    for (int64_t r = 0; r < nrec; ++r) {
-      for (int i = 0; i < 4; ++i) hx0[r * 5 + i] = i4[i];
-      hx0[r * 5 + 4] = NAN;
+    // init4 in every row (from the device copy when it lives there: no host round trip),
+    // then the moments kernels fill x0[r*5+4] and r (an empty record keeps numpy's NaN
+    // mean / variance)
+    dfmi::EkfInit hv{};
+    if (host) {
+      memcpy(hv.i4, init4, sizeof(hv.i4));
+      if (r_val) hv.rv = *r_val;
     }
-    if (r_val) {
-      double rv;
-      if (host) rv = *r_val;
-      else HIPCHK(hipMemcpy(&rv, r_val, 8, hipMemcpyDeviceToHost));
-      for (auto& v : hr) v = rv;
-    }
-    HIPCHK(hipMemcpyAsync(b, hx0.data(), hx0.size() * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(e, hr.data(), hr.size() * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(dfmi::ekf_x0_kernel, dim3((unsigned)((nrec + 63) / 64)), dim3(64), 0, st, (double*)b, (double*)e,
+                       nrec, host ? (const double*)nullptr : init4, host ? (const double*)nullptr : r_val,
+                       r_val != nullptr, hv);
     if (n_samp >= 1) {
       if ((rc = moments_dev(dev, dx, nrec, rs, n_samp, (double*)b + 4, 5, r_val ? nullptr : (double*)e, 1, st)))
         return rc;
     }
-    // the staging vectors must outlive the async copies
-    HIPCHK(hipStreamSynchronize(st));
     dx0 = (const double*)b;
     dr = (const double*)e;
   } else if (host) {

@@ -28,6 +28,24 @@ __global__ __launch_bounds__(256) void ekf_phase_kernel(double* __restrict__ wt,
   if (k < n) wt[k] = w_m * ((double)k / f_samp);
 }
 
+// x0 = [init4, NaN] and r_val per record for dfmi_ekf_fit (the mean and, without a given
+// r_val, the variance are written by the moments kernels after this): init4 / r_val from
+// device pointers when given (no host round trip), else from the by-value copies.
+struct EkfInit {
+  double i4[4];
+  double rv;
+};
+__global__ __launch_bounds__(64) void ekf_x0_kernel(double* __restrict__ x0, double* __restrict__ rv, int64_t nrec,
+                                                    const double* __restrict__ i4p, const double* __restrict__ rvp,
+                                                    bool have_rv, EkfInit hv) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrec) return;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) x0[r * 5 + i] = i4p ? i4p[i] : hv.i4[i];
+  x0[r * 5 + 4] = __builtin_nan("");
+  rv[r] = !have_rv ? __builtin_nan("") : rvp ? rvp[0] : hv.rv;
+}
+
 // One EKF step (fitters.py:274-302) on the lane's state; P symmetric: only its upper
 // triangle P[i][j], i <= j, is read and written (constant-bound loops, fully unrolled:
 // every index is a compile-time register).

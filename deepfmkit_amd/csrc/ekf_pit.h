@@ -63,43 +63,31 @@ struct PitEl {
 //   M = (I + C_i J_j)^-1, A = A_j M A_i, b = A_j M (b_i + C_i eta_j) + b_j,
 //   C = A_j M C_i A_j^T + C_j, eta = A_i^T M^T (eta_j - J_j b_i) + eta_i,
 //   J = A_i^T M^T J_j A_i + J_i.
-// M by Gauss-Jordan with partial pivoting (I + C J with C, J PSD has eigenvalues >= 1 but
-// its leading minors can vanish); the row swaps are selects, so every index stays static.
+// M by Gauss-Jordan (I + C J with C, J PSD has eigenvalues >= 1 but its leading minors can
+// vanish: a pivot below 1/4 redoes it with partial pivoting, whose row swaps are selects so
+// every index stays static).
 __device__ __forceinline__ void pit_combine(const PitEl& ei, const PitEl& ej, double (&o)[kPitEl]) {
   double T[5][10];
+  auto init_T = [&]() {
 #pragma unroll
-  for (int r = 0; r < 5; ++r) {
+    for (int r = 0; r < 5; ++r) {
 #pragma unroll
-    for (int c = 0; c < 5; ++c) {
-      double s = (r == c) ? 1.0 : 0.0;
+      for (int c = 0; c < 5; ++c) {
+        double s = (r == c) ? 1.0 : 0.0;
 #pragma unroll
-      for (int k = 0; k < 5; ++k) s = fma(ei.C(r, k), ej.J(k, c), s);
-      T[r][c] = s;
-      T[r][5 + c] = (r == c) ? 1.0 : 0.0;
+        for (int k = 0; k < 5; ++k) s = fma(ei.C(r, k), ej.J(k, c), s);
+        T[r][c] = s;
+        T[r][5 + c] = (r == c) ? 1.0 : 0.0;
+      }
     }
-  }
+  };
+  init_T();
+  // without pivoting first (T = I + C J is I plus a small term for every element the passes
+  // meet: pivots near 1); any pivot below 1/4 in magnitude redoes it with partial pivoting
+  double pmin = 1.0;
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
-    int p = k;
-    double best = fabs(T[k][k]);
-#pragma unroll
-    for (int r = k + 1; r < 5; ++r) {
-      const double v = fabs(T[r][k]);
-      if (v > best) {
-        best = v;
-        p = r;
-      }
-    }
-#pragma unroll
-    for (int r = k + 1; r < 5; ++r) {
-      const bool sw = p == r;
-#pragma unroll
-      for (int c = k; c < 10; ++c) {
-        const double t = T[k][c];
-        T[k][c] = sw ? T[r][c] : t;
-        T[r][c] = sw ? t : T[r][c];
-      }
-    }
+    pmin = fmin(pmin, fabs(T[k][k]));
     const double ip = 1.0 / T[k][k];
 #pragma unroll
     for (int c = k + 1; c < 10; ++c) T[k][c] *= ip;
@@ -109,6 +97,42 @@ __device__ __forceinline__ void pit_combine(const PitEl& ei, const PitEl& ej, do
       const double f = T[r][k];
 #pragma unroll
       for (int c = k + 1; c < 10; ++c) T[r][c] = fma(-f, T[k][c], T[r][c]);
+    }
+  }
+  if (__builtin_expect(!(pmin >= 0.25), 0)) {
+    init_T();
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      int p = k;
+      double best = fabs(T[k][k]);
+#pragma unroll
+      for (int r = k + 1; r < 5; ++r) {
+        const double v = fabs(T[r][k]);
+        if (v > best) {
+          best = v;
+          p = r;
+        }
+      }
+#pragma unroll
+      for (int r = k + 1; r < 5; ++r) {
+        const bool sw = p == r;
+#pragma unroll
+        for (int c = k; c < 10; ++c) {
+          const double t = T[k][c];
+          T[k][c] = sw ? T[r][c] : t;
+          T[r][c] = sw ? t : T[r][c];
+        }
+      }
+      const double ip = 1.0 / T[k][k];
+#pragma unroll
+      for (int c = k + 1; c < 10; ++c) T[k][c] *= ip;
+#pragma unroll
+      for (int r = 0; r < 5; ++r) {
+        if (r == k) continue;
+        const double f = T[r][k];
+#pragma unroll
+        for (int c = k + 1; c < 10; ++c) T[r][c] = fma(-f, T[k][c], T[r][c]);
+      }
     }
   }
   // M = T[.][5..9]
@@ -156,15 +180,17 @@ __device__ __forceinline__ void pit_combine(const PitEl& ei, const PitEl& ej, do
       o[kPitB + r] = s;
     }
   }
-  // C = A_j (M C_i) A_j^T + C_j: X = M C_i, Y = X A_j^T, C = A_j Y (upper triangle)
+  // C = A_j (M C_i) A_j^T + C_j: X = M C_i (= (C_i^-1 + J_j)^-1, symmetric: upper triangle
+  // formed, mirrored), Y = X A_j^T, C = A_j Y (upper triangle)
 #pragma unroll
   for (int r = 0; r < 5; ++r)
 #pragma unroll
-    for (int c = 0; c < 5; ++c) {
+    for (int c = r; c < 5; ++c) {
       double s = 0.0;
 #pragma unroll
       for (int k = 0; k < 5; ++k) s = fma(M(r, k), ei.C(k, c), s);
       X[r][c] = s;
+      X[c][r] = s;
     }
   {
     double Y[5][5];
@@ -212,15 +238,17 @@ __device__ __forceinline__ void pit_combine(const PitEl& ei, const PitEl& ej, do
       o[kPitE + r] = s;
     }
   }
-  // J = A_i^T (M^T J_j) A_i + J_i: X = M^T J_j, Y = X A_i, J = A_i^T Y (upper triangle)
+  // J = A_i^T (M^T J_j) A_i + J_i: X = M^T J_j (= (J_j^-1 + C_i)^-1, symmetric), Y = X A_i,
+  // J = A_i^T Y (upper triangle)
 #pragma unroll
   for (int r = 0; r < 5; ++r)
 #pragma unroll
-    for (int c = 0; c < 5; ++c) {
+    for (int c = r; c < 5; ++c) {
       double s = 0.0;
 #pragma unroll
       for (int k = 0; k < 5; ++k) s = fma(M(k, r), ej.J(k, c), s);
       X[r][c] = s;
+      X[c][r] = s;
     }
   {
     double Y[5][5];
@@ -270,12 +298,39 @@ __global__ __launch_bounds__(64) void ekf_pit_head_kernel(const double* __restri
     for (int j = 0; j < 5; ++j) P[i][j] = (i == j) ? p0[i] : 0.0;
   }
   const double Rv = rv[r];
-  for (int64_t k = 0; k < T0; ++k) {
-    const int64_t b = k / B, s = (k - b * B) * nb + b;
+  const double* __restrict__ xr = x + r * rs;
+  // the samples 8 at a time, the next group's loads in flight (a load per sample in the
+  // chain would expose its latency every step)
+  double xc[8];
+  const int64_t T8 = T0 & ~(int64_t)7;
+  if (T8 > 0) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xc[u] = xr[u];
+  }
+  int64_t s = 0, bi = 0, ii = 0;  // slot of sample k: block bi, index ii (no division per sample)
+  auto step = [&](int64_t k, double xk) {
 #pragma unroll
     for (int c = 0; c < 5; ++c) xbar[(r * 5 + c) * slots + s] = st[c];
-    ekf_step(st, P, Q, Rv, x[r * rs + k], w_m * ((double)k / f_samp), tk);
+    ekf_step(st, P, Q, Rv, xk, w_m * ((double)k / f_samp), tk);
+    if (++ii == B) {
+      ii = 0;
+      s = ++bi;
+    } else {
+      s += nb;
+    }
+  };
+  int64_t k = 0;
+  for (; k < T8; k += 8) {
+    double xn[8];
+    const int64_t kn = k + 8 < T8 ? k + 8 : k;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xn[u] = xr[kn + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) step(k + u, xc[u]);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xc[u] = xn[u];
   }
+  for (; k < T0; ++k) step(k, xr[k]);
 #pragma unroll
   for (int c = 0; c < 5; ++c) hst[r * 5 + c] = st[c];
 }
@@ -287,13 +342,15 @@ __global__ __launch_bounds__(256) void ekf_pit_gather_kernel(const double* __res
                                                              const double* __restrict__ hst, int64_t T0, int64_t B,
                                                              int64_t nb, double w_m, double f_samp,
                                                              double* __restrict__ xt, double* __restrict__ wtt,
-                                                             double* __restrict__ xbar, int* __restrict__ flag) {
+                                                             double* __restrict__ xbar, int* __restrict__ flag,
+                                                             double* __restrict__ conv) {
   const int64_t r = blockIdx.y;
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // s = i nb + b
   const int64_t slots = B * nb;
   if (s == 0) {
     flag[2 * r] = 0;      // converged
     flag[2 * r + 1] = 0;  // passes run
+    conv[r] = 0.0;        // largest move of the pass (ekf_pit_blocks_kernel)
   }
   if (s >= slots) return;
   const int64_t i = s / nb, b = s - i * nb;
@@ -304,6 +361,73 @@ __global__ __launch_bounds__(256) void ekf_pit_gather_kernel(const double* __res
 #pragma unroll
     for (int c = 0; c < 5; ++c) xbar[(r * 5 + c) * slots + s] = hst[r * 5 + c];
   }
+}
+
+// Fold one sample's element (h, eps = e - h.b) into the running aggregate (see
+// ekf_pit_aggregate_kernel).
+__device__ __forceinline__ void pit_fold(double (&A)[25], double (&bv)[5], double (&C)[15], double (&et)[5],
+                                         double (&J)[15], const double (&q)[5], double Rv, const double (&h)[5],
+                                         double eps) {
+  double g[5], rr[5];
+#pragma unroll
+  for (int i2 = 0; i2 < 5; ++i2) {
+    double s2 = q[i2] * h[i2];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) s2 = fma(C[pit_sy(i2, j)], h[j], s2);
+    g[i2] = s2;
+  }
+  double gam = Rv;
+#pragma unroll
+  for (int c = 0; c < 5; ++c) gam = fma(h[c], g[c], gam);
+#pragma unroll
+  for (int c = 0; c < 5; ++c) {
+    double s2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) s2 = fma(A[k * 5 + c], h[k], s2);
+    rr[c] = s2;
+  }
+  const double ig = 1.0 / gam;
+  const double ei = eps * ig;
+  double v[5], ri[5];
+#pragma unroll
+  for (int c = 0; c < 5; ++c) {
+    v[c] = g[c] * ig;
+    ri[c] = rr[c] * ig;
+  }
+#pragma unroll
+  for (int r2 = 0; r2 < 5; ++r2)
+#pragma unroll
+    for (int c = 0; c < 5; ++c) A[r2 * 5 + c] = fma(-v[r2], rr[c], A[r2 * 5 + c]);
+#pragma unroll
+  for (int c = 0; c < 5; ++c) {
+    bv[c] = fma(v[c], eps, bv[c]);
+    et[c] = fma(rr[c], ei, et[c]);
+  }
+#pragma unroll
+  for (int i2 = 0; i2 < 5; ++i2)
+#pragma unroll
+    for (int j = i2; j < 5; ++j) {
+      const int y = pit_sy(i2, j);
+      C[y] = fma(-g[i2], v[j], i2 == j ? C[y] + q[i2] : C[y]);
+      J[y] = fma(ri[i2], rr[j], J[y]);
+    }
+}
+
+// one sample's inputs: xbar (5), w_m t_k, y_k
+struct PitSamp {
+  double xb[5];
+  double w, y;
+};
+constexpr int kPitG = 4;  // samples per prefetch group
+// sample i of block b (clamped into the block: the padded slots are allocated)
+__device__ __forceinline__ void pit_load_agg(PitSamp& d, const double* __restrict__ xt, const double* __restrict__ wtt,
+                                             const double* __restrict__ xbar, int64_t r, int64_t slots, int64_t nb,
+                                             int64_t B, int64_t b, int64_t i) {
+  const int64_t s = (i < B ? i : B - 1) * nb + b;
+#pragma unroll
+  for (int c = 0; c < 5; ++c) d.xb[c] = xbar[(r * 5 + c) * slots + s];
+  d.w = wtt[s];
+  d.y = xt[r * slots + s];
 }
 
 // Step 1 + the in-block fold of step 2: lane = block. The element of sample k (F = I,
@@ -343,66 +467,34 @@ __global__ __launch_bounds__(64) void ekf_pit_aggregate_kernel(const double* __r
   }
   const double Rv = rv[r];
   const int64_t kend = (b + 1) * B < n ? B : n - b * B;
-  for (int64_t i = 0; i < kend; ++i) {
-    const int64_t s = i * nb + b;
-    double xb[5];
+  // the samples kPitG at a time, the next group's loads in flight while this one folds
+  // (one wave per SIMD: nothing else hides a load's latency)
+  PitSamp cur[kPitG], nxt[kPitG];
 #pragma unroll
-    for (int c = 0; c < 5; ++c) xb[c] = xbar[(r * 5 + c) * slots + s];
-    const double a = xb[0], m = xb[1];
-    const double th = wtt[s] + xb[3];
-    double sth, cth, sa, ca;
-    dfmi_sincos_k(th, tk, &sth, &cth);
-    const double arg = fma(m, cth, xb[2]);
-    dfmi_sincos_k(arg, tk, &sa, &ca);
-    const double hv = fma(a, ca, xb[4]);
-    const double h[5] = {ca, (-a * cth) * sa, -a * sa, ((a * m) * sth) * sa, 1.0};
-    // eps = e - h.b with e = y - hv + h.xbar
-    double eps = xt[r * slots + s] - hv;
+  for (int u = 0; u < kPitG; ++u) pit_load_agg(cur[u], xt, wtt, xbar, r, slots, nb, B, b, u);
+  for (int64_t i0 = 0; i0 < kend; i0 += kPitG) {
 #pragma unroll
-    for (int c = 0; c < 5; ++c) eps = fma(h[c], xb[c] - bv[c], eps);
-    double g[5], rr[5];
+    for (int u = 0; u < kPitG; ++u) pit_load_agg(nxt[u], xt, wtt, xbar, r, slots, nb, B, b, i0 + kPitG + u);
 #pragma unroll
-    for (int i2 = 0; i2 < 5; ++i2) {
-      double s2 = q[i2] * h[i2];
+    for (int u = 0; u < kPitG; ++u) {
+      if (i0 + u >= kend) break;
+      const double* xb = cur[u].xb;
+      const double a = xb[0], m = xb[1];
+      const double th = cur[u].w + xb[3];
+      double sth, cth, sa, ca;
+      dfmi_sincos_k(th, tk, &sth, &cth);
+      const double arg = fma(m, cth, xb[2]);
+      dfmi_sincos_k(arg, tk, &sa, &ca);
+      const double hv = fma(a, ca, xb[4]);
+      const double h[5] = {ca, (-a * cth) * sa, -a * sa, ((a * m) * sth) * sa, 1.0};
+      // eps = e - h.b with e = y - hv + h.xbar
+      double eps = cur[u].y - hv;
 #pragma unroll
-      for (int j = 0; j < 5; ++j) s2 = fma(C[pit_sy(i2, j)], h[j], s2);
-      g[i2] = s2;
-    }
-    double gam = Rv;
-#pragma unroll
-    for (int c = 0; c < 5; ++c) gam = fma(h[c], g[c], gam);
-#pragma unroll
-    for (int c = 0; c < 5; ++c) {
-      double s2 = 0.0;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) s2 = fma(A[k * 5 + c], h[k], s2);
-      rr[c] = s2;
-    }
-    const double ig = 1.0 / gam;
-    const double ei = eps * ig;
-    double v[5], ri[5];
-#pragma unroll
-    for (int c = 0; c < 5; ++c) {
-      v[c] = g[c] * ig;
-      ri[c] = rr[c] * ig;
+      for (int c = 0; c < 5; ++c) eps = fma(h[c], xb[c] - bv[c], eps);
+      pit_fold(A, bv, C, et, J, q, Rv, h, eps);
     }
 #pragma unroll
-    for (int r2 = 0; r2 < 5; ++r2)
-#pragma unroll
-      for (int c = 0; c < 5; ++c) A[r2 * 5 + c] = fma(-v[r2], rr[c], A[r2 * 5 + c]);
-#pragma unroll
-    for (int c = 0; c < 5; ++c) {
-      bv[c] = fma(v[c], eps, bv[c]);
-      et[c] = fma(rr[c], ei, et[c]);
-    }
-#pragma unroll
-    for (int i2 = 0; i2 < 5; ++i2)
-#pragma unroll
-      for (int j = i2; j < 5; ++j) {
-        const int y = pit_sy(i2, j);
-        C[y] = fma(-g[i2], v[j], i2 == j ? C[y] + q[i2] : C[y]);
-        J[y] = fma(ri[i2], rr[j], J[y]);
-      }
+    for (int u = 0; u < kPitG; ++u) cur[u] = nxt[u];
   }
   double* o = agg + r * kPitEl * nb + b;
 #pragma unroll
@@ -435,7 +527,9 @@ __global__ __launch_bounds__(kPitWg) void ekf_pit_scan_kernel(double* __restrict
 #pragma unroll
   for (int c = 0; c < kPitEl; ++c) s[c * kPitWg + t] = live ? base[c * ld] : pit_identity(c);
   __syncthreads();
-  for (int off = 1; off < kPitWg; off <<= 1) {
+  const int64_t nlive = n_el - (int64_t)blockIdx.x * kPitWg;  // live elements here (the rest: identities)
+  const int span = nlive < kPitWg ? (int)nlive : kPitWg;
+  for (int off = 1; off < span; off <<= 1) {
     double o[kPitEl];
     const bool act = t >= off;
     if (act) pit_combine(PitEl{s + t - off, kPitWg}, PitEl{s + t, kPitWg}, o);
@@ -461,8 +555,8 @@ __global__ __launch_bounds__(kPitWg) void ekf_pit_scan_kernel(double* __restrict
 // after block b-1, i.e. the inclusive prefix: agg[b-1] (scanned within its workgroup)
 // preceded by tot[g-1] (scanned workgroup totals) when b-1 lies past the first workgroup.
 // Then ekf_step over the block (the lane kernel's arithmetic), writing the next xbar (the
-// state entering each following sample), its largest relative move into conv[r][b], and
-// the snapshots (fitters.py:305-307).
+// state entering each following sample), its largest relative move into conv[r] (max over
+// the channel's blocks) and the snapshots (fitters.py:305-307).
 __global__ __launch_bounds__(64) void ekf_pit_blocks_kernel(const double* __restrict__ xt,
                                                             const double* __restrict__ wtt,
                                                             double* __restrict__ xbar, int64_t n, int64_t B, int64_t nb,
@@ -476,8 +570,9 @@ __global__ __launch_bounds__(64) void ekf_pit_blocks_kernel(const double* __rest
                                                             double* __restrict__ states, DfmiTrigK tk) {
   const int64_t r = blockIdx.y;
   if (flag[2 * r]) return;
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nb) return;
+  const int64_t b0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = b0 < nb;  // lanes past the last block stay for the wave's max (no work)
+  const int64_t b = live ? b0 : nb - 1;
   const int64_t slots = B * nb;
   double st[5], P[5][5], Q[5];
 #pragma unroll
@@ -513,57 +608,69 @@ __global__ __launch_bounds__(64) void ekf_pit_blocks_kernel(const double* __rest
   }
   const double Rv = rv[r];
   double dmax = 0.0;
-  const int64_t kend = (b + 1) * B < n ? B : n - b * B;
-  for (int64_t i = 0; i < kend; ++i) {
-    const int64_t s = i * nb + b;
-    ekf_step(st, P, Q, Rv, xt[r * slots + s], wtt[s], tk);
-    const int64_t k = b * B + i;
-    if (k + 1 < n) {
-      const int64_t s1 = i + 1 < B ? s + nb : b + 1;  // slot of sample k + 1
+  const int64_t kend = !live ? 0 : (b + 1) * B < n ? B : n - b * B;
+  // inputs kPitG samples ahead (see ekf_pit_aggregate_kernel): y_k, w_m t_k and the xbar of
+  // sample k + 1 this block overwrites
+  PitSamp cur[kPitG], nxt[kPitG];
+  auto load = [&](PitSamp& d, int64_t i) {
+    const int64_t ic = i < B ? i : B - 1;
+    const int64_t s = ic * nb + b, s1 = ic + 1 < B ? s + nb : b + 1;  // slot of sample k + 1
+    d.w = wtt[s];
+    d.y = xt[r * slots + s];
 #pragma unroll
-      for (int c = 0; c < 5; ++c) {
-        double* px = xbar + (r * 5 + c) * slots + s1;
-        const double d = fabs(st[c] - *px) / fmax(1.0, fabs(st[c]));
-        dmax = d <= dmax ? dmax : d;  // NaN propagates (never "converged")
-        *px = st[c];
+    for (int c = 0; c < 5; ++c) d.xb[c] = xbar[(r * 5 + c) * slots + s1];
+  };
+#pragma unroll
+  for (int u = 0; u < kPitG; ++u) load(cur[u], u);
+  for (int64_t i0 = 0; i0 < kend; i0 += kPitG) {
+#pragma unroll
+    for (int u = 0; u < kPitG; ++u) load(nxt[u], i0 + kPitG + u);
+#pragma unroll
+    for (int u = 0; u < kPitG; ++u) {
+      const int64_t i = i0 + u;
+      if (i >= kend) break;
+      ekf_step(st, P, Q, Rv, cur[u].y, cur[u].w, tk);
+      const int64_t k = b * B + i;
+      if (k + 1 < n) {
+        const int64_t s1 = i + 1 < B ? i * nb + b + nb : b + 1;
+#pragma unroll
+        for (int c = 0; c < 5; ++c) {
+          const double d = fabs(st[c] - cur[u].xb[c]) / fmax(1.0, fabs(st[c]));
+          dmax = d <= dmax ? dmax : d;  // NaN propagates (never "converged")
+          xbar[(r * 5 + c) * slots + s1] = st[c];
+        }
+      }
+      if ((k + 1) % R == 0) {
+        const int64_t bi = (k + 1) / R - 1;
+        if (bi < nbuf) {
+#pragma unroll
+          for (int c = 0; c < 5; ++c) states[(r * nbuf + bi) * 5 + c] = st[c];
+        }
       }
     }
-    if ((k + 1) % R == 0) {
-      const int64_t bi = (k + 1) / R - 1;
-      if (bi < nbuf) {
 #pragma unroll
-        for (int c = 0; c < 5; ++c) states[(r * nbuf + bi) * 5 + c] = st[c];
-      }
-    }
+    for (int u = 0; u < kPitG; ++u) cur[u] = nxt[u];
   }
-  conv[r * nb + b] = dmax;
+  // the channel's largest move: a non-negative double (or NaN, above every finite value
+  // and inf) orders as its bits, so the wave's max goes to conv[r] by one integer atomic
+  unsigned long long bits = __builtin_bit_cast(unsigned long long, dmax);
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const unsigned long long o = __shfl_xor(bits, w, 64);
+    bits = o > bits ? o : bits;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax((unsigned long long*)conv + r, bits);
 }
 
-// One workgroup per channel: converged when every block moved xbar by at most tol
-// (relative, see ekf_pit_blocks_kernel); counts the passes that ran.
-__global__ __launch_bounds__(256) void ekf_pit_check_kernel(const double* __restrict__ conv, int64_t nb, double tol,
-                                                            int* __restrict__ flag) {
-  const int64_t r = blockIdx.x;
-  if (flag[2 * r]) return;
-  __shared__ double red[256];
-  double m = 0.0;
-  for (int64_t b = threadIdx.x; b < nb; b += 256) {
-    const double v = conv[r * nb + b];
-    m = v <= m ? m : v;
-  }
-  red[threadIdx.x] = m;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) {
-      const double v = red[threadIdx.x + w];
-      red[threadIdx.x] = v <= red[threadIdx.x] ? red[threadIdx.x] : v;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    flag[2 * r + 1] += 1;
-    if (red[0] <= tol) flag[2 * r] = 1;
-  }
+// One thread per channel: converged when no block moved xbar by more than tol (relative,
+// see ekf_pit_blocks_kernel); counts the passes that ran and clears conv for the next.
+__global__ __launch_bounds__(64) void ekf_pit_check_kernel(double* __restrict__ conv, int64_t nrec, double tol,
+                                                           int* __restrict__ flag) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrec || flag[2 * r]) return;
+  flag[2 * r + 1] += 1;
+  if (conv[r] <= tol) flag[2 * r] = 1;
+  conv[r] = 0.0;
 }
 
 // A channel the passes left unconverged: the sequential EKF (ekf_kernel's loop) from x0.

@@ -5,10 +5,11 @@
 // numpy 2.x _methods._mean / _var: mean = umr_sum(arr) / n; var = umr_sum(x * x) / n
 // with x = arr - mean, each elementwise step rounded on its own; umr_sum is the
 // pairwise tree of np_sum.h (8-accumulator leaves of <= 128 elements, 8192-element
-// buffer chunks chained left to right), planned on the host. One workgroup per
-// record: leaves in parallel straight from HBM, the tree's internal nodes level by
-// level in a global workspace. This translation unit is compiled without FMA
-// contraction, so (x - mean)^2 and the leaf additions round like numpy's.
+// buffer chunks chained left to right), planned on the host. The leaves in parallel
+// straight from HBM (8 lanes per leaf, every record's leaves across the whole GPU), then
+// one workgroup per record adds the tree's internal nodes level by level in LDS. This
+// translation unit is compiled without FMA contraction, so (x - mean)^2 and the leaf
+// additions round like numpy's.
 #include "moments.h"
 
 #include "np_sum.h"
@@ -17,75 +18,81 @@ namespace dfmi {
 namespace {
 
 constexpr int kT = 256;
+constexpr int kTreeLds = 16384;  // nodes (2 per leaf) the tree kernel keeps in LDS: records up to ~1M samples
 
-// dfmi_np_leaf_sum over s_i = (a_i - mean) * (a_i - mean)
-__device__ __forceinline__ double sq(const double* a, int i, double mean) {
-  const double d = a[i] - mean;
-  return d * d;
-}
-
-__device__ double leaf_sum_sq(const double* a, int n, double mean) {
-  if (n < 8) {
-    double r = 0.0;
-    for (int i = 0; i < n; ++i) r += sq(a, i, mean);
-    return r;
-  }
-  double r0 = sq(a, 0, mean), r1 = sq(a, 1, mean), r2 = sq(a, 2, mean), r3 = sq(a, 3, mean);
-  double r4 = sq(a, 4, mean), r5 = sq(a, 5, mean), r6 = sq(a, 6, mean), r7 = sq(a, 7, mean);
-  int i = 8;
-  const int e = n - (n % 8);
-  for (; i < e; i += 8) {
-    r0 += sq(a, i + 0, mean);
-    r1 += sq(a, i + 1, mean);
-    r2 += sq(a, i + 2, mean);
-    r3 += sq(a, i + 3, mean);
-    r4 += sq(a, i + 4, mean);
-    r5 += sq(a, i + 5, mean);
-    r6 += sq(a, i + 6, mean);
-    r7 += sq(a, i + 7, mean);
-  }
-  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-  for (; i < n; ++i) res += sq(a, i, mean);
-  return res;
-}
-
-// The plan's tree over x (SQ: over (x - mean)^2); every thread returns the root.
+// leaf element: a_i, or (a_i - mean)^2 rounded as numpy's x = arr - mean; x * x
 template <bool SQ>
-__device__ double plan_sum(const double* __restrict__ x, const int* __restrict__ plan, double* nodes, double mean) {
-  const int nl = plan[0], H = plan[1];
-  const int* off = plan + 2;
-  const int* lvl = off + nl + 1;
-  const int* tri = lvl + H + 1;
-  for (int t = threadIdx.x; t < nl; t += kT) {
-    const int o = off[t], len = off[t + 1] - o;
-    nodes[t] = SQ ? leaf_sum_sq(x + o, len, mean) : dfmi_np_leaf_sum(x + o, len);
+__device__ __forceinline__ double leaf_el(const double* a, int i, double mean) {
+  if constexpr (SQ) {
+    const double d = a[i] - mean;
+    return d * d;
+  } else {
+    return a[i];
   }
-  __syncthreads();
+}
+
+// The plan's leaves (dfmi_np_leaf_sum over each), 8 lanes per leaf: lane j carries the
+// leaf's accumulator r_j (elements j, j + 8, ... in order, as numpy's unrolled loop), the
+// three shuffle levels add them as ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) (each
+// add commutes, so every lane of a pair holds the same sum), lane 0 adds the tail. The
+// 8 lanes of a leaf read 64 contiguous bytes per step: a record's leaves stream from HBM
+// in parallel instead of one 1-KiB leaf per thread in sequence. grid (leaves / 32, nrec).
+template <bool SQ>
+__global__ __launch_bounds__(kT) void moments_leaf_kernel(const double* __restrict__ x, int64_t rec_stride,
+                                                           const int* __restrict__ plan, int64_t nl,
+                                                           double* __restrict__ nodes,
+                                                           const double* __restrict__ mean, int64_t mean_stride) {
+  const int64_t r = blockIdx.y;
+  const int64_t t = (int64_t)blockIdx.x * kT + threadIdx.x;
+  const int64_t leaf = t >> 3;
+  const int j = (int)(t & 7);
+  if (leaf >= nl) return;  // uniform over the leaf's 8 lanes
+  const int* off = plan + 2;
+  const int o = off[leaf], len = off[leaf + 1] - o;
+  const double* a = x + r * rec_stride + o;
+  const double m = SQ ? mean[r * mean_stride] : 0.0;
+  double res;
+  if (len < 8) {
+    res = 0.0;
+    for (int i = 0; i < len; ++i) res += leaf_el<SQ>(a, i, m);
+  } else {
+    const int e = len - (len % 8);
+    double acc = leaf_el<SQ>(a, j, m);
+    for (int i = 8 + j; i < e; i += 8) acc += leaf_el<SQ>(a, i, m);
+    acc += __shfl_xor(acc, 1, 8);
+    acc += __shfl_xor(acc, 2, 8);
+    acc += __shfl_xor(acc, 4, 8);
+    res = acc;
+    for (int i = e; i < len; ++i) res += leaf_el<SQ>(a, i, m);
+  }
+  if (j == 0) nodes[r * 2 * nl + leaf] = res;
+}
+
+// The plan's internal nodes level by level (one workgroup per record; in LDS when the
+// record's 2 nl nodes fit, else in the global node array), then root / n -> out.
+template <bool LDS>
+__global__ __launch_bounds__(kT) void moments_tree_kernel(const int* __restrict__ plan, int64_t nl,
+                                                           double* __restrict__ nodes, int64_t n, double* out,
+                                                           int64_t out_stride) {
+  __shared__ double s[LDS ? kTreeLds : 1];
+  const int64_t r = blockIdx.x;
+  double* g = nodes + r * 2 * nl;
+  double* v = LDS ? s : g;
+  const int H = plan[1];
+  const int* lvl = plan + 2 + nl + 1;
+  const int* tri = lvl + H + 1;
+  if (LDS) {
+    for (int64_t t = threadIdx.x; t < nl; t += kT) v[t] = g[t];
+    __syncthreads();
+  }
   for (int h = 0; h < H; ++h) {
     for (int j = lvl[h] + threadIdx.x; j < lvl[h + 1]; j += kT) {
       const int* q = tri + 3 * j;
-      nodes[q[0]] = nodes[q[1]] + nodes[q[2]];
+      v[q[0]] = v[q[1]] + v[q[2]];
     }
     __syncthreads();
   }
-  const double s = nodes[nl > 1 ? 2 * nl - 2 : 0];
-  __syncthreads();
-  return s;
-}
-
-__global__ __launch_bounds__(kT) void moments_kernel(const double* __restrict__ x, int64_t rec_stride, int64_t n,
-                                                      const int* __restrict__ plan, int64_t n_leaves, double* nodes,
-                                                      double* mean, int64_t mean_stride, double* var,
-                                                      int64_t var_stride) {
-  const int64_t r = blockIdx.x;
-  const double* xr = x + r * rec_stride;
-  double* nr = nodes + r * 2 * n_leaves;
-  const double m = plan_sum<false>(xr, plan, nr, 0.0) / (double)n;
-  if (threadIdx.x == 0) mean[r * mean_stride] = m;
-  if (var) {
-    const double v = plan_sum<true>(xr, plan, nr, m) / (double)n;
-    if (threadIdx.x == 0) var[r * var_stride] = v;
-  }
+  if (threadIdx.x == 0) out[r * out_stride] = v[nl > 1 ? 2 * nl - 2 : 0] / (double)n;
 }
 
 }  // namespace
@@ -94,8 +101,24 @@ hipError_t moments_launch(const double* x, int64_t nrec, int64_t rec_stride, int
                           int64_t n_leaves, double* nodes, double* mean, int64_t mean_stride, double* var,
                           int64_t var_stride, hipStream_t st) {
   if (nrec == 0) return hipSuccess;
-  hipLaunchKernelGGL(moments_kernel, dim3((unsigned)nrec), dim3(kT), 0, st, x, rec_stride, n, plan, n_leaves, nodes,
-                     mean, mean_stride, var, var_stride);
+  const dim3 lg((unsigned)((n_leaves * 8 + kT - 1) / kT), (unsigned)nrec);
+  const bool lds = 2 * n_leaves <= kTreeLds;
+  auto tree = [&](double* out, int64_t os) {
+    if (lds)
+      hipLaunchKernelGGL(moments_tree_kernel<true>, dim3((unsigned)nrec), dim3(kT), 0, st, plan, n_leaves, nodes, n,
+                         out, os);
+    else
+      hipLaunchKernelGGL(moments_tree_kernel<false>, dim3((unsigned)nrec), dim3(kT), 0, st, plan, n_leaves, nodes, n,
+                         out, os);
+  };
+  hipLaunchKernelGGL(moments_leaf_kernel<false>, lg, dim3(kT), 0, st, x, rec_stride, plan, n_leaves, nodes,
+                     (const double*)nullptr, (int64_t)0);
+  tree(mean, mean_stride);
+  if (var) {
+    hipLaunchKernelGGL(moments_leaf_kernel<true>, lg, dim3(kT), 0, st, x, rec_stride, plan, n_leaves, nodes,
+                       (const double*)mean, mean_stride);
+    tree(var, var_stride);
+  }
   return hipGetLastError();
 }
 

@@ -79,7 +79,7 @@ def main():
                                     "max_abs_dstate_vs_seq": float(np.max(np.abs(got - seq)))})
             print(json.dumps(out["variants"][-1]), flush=True)
         _lib.check(lib.dfmi_set_tuning(b"ekf_pit_block", 0), "tune")
-        _lib.check(lib.dfmi_set_tuning(b"ekf_pit_head", 512), "tune")
+        _lib.check(lib.dfmi_set_tuning(b"ekf_pit_head", 256), "tune")
         _lib.check(lib.dfmi_set_tuning(b"ekf_pit", 8), "tune")
         del xe, stt
     print(json.dumps(out))

@@ -164,7 +164,6 @@ def cpu_baseline_c(x, nseg, R, threads, ref):
     evaluation, the quadratures through the basis period's phase bins) with OpenMP over
     the same host CPU share, on the same sample fitted 50 times over (one fit of the sample
     takes milliseconds); status-0 parameters against the numpy port's."""
-    import ctypes
     path = os.path.join(ROOT, "oracle", "libnls_scalar.so")
     if not os.path.exists(path):
         return {"error": "oracle/libnls_scalar.so not built"}
@@ -427,7 +426,6 @@ def extra_configs(torch, dev, lib, _lib, stream, cfg, cpu_leg):
           "one_channel": res5[1], "one_channel_sequential": res5["seq"], "channels_1024": res5[1024],
           "unit": "samples/s"}
     if cpu_leg:  # the host baseline: the oracle's scalar C restatement of the same loop, one core
-        import ctypes
         lib_c = os.path.join(ROOT, "oracle", "libekf_scalar.so")
         if os.path.exists(lib_c):
             cl = ctypes.CDLL(lib_c)

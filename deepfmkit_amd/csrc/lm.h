@@ -139,6 +139,19 @@ DFMI_HDI double rcp_nr(double d) {
 // that the unrolled low-order part of the pass (orders < NB <= 18) grows by at
 // most ~1e70, so only the runtime part of the pass (orders >= NB) carries the
 // exact power-of-two rescaling of dfmi_math.h.
+// dfmi_bessel_j01_large out of line on the device: inlined, its ~30 polynomial constants and
+// the sincos are hoisted into registers across the LM kernels and push lm_chunks_kernel from
+// 248 VGPRs (2 waves per SIMD) to 256 + 34 AGPRs (1 wave); as a call on this rare branch
+// (|m| >= 64: runaway descents) the hot path keeps its allocation.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(DFMI_BES_LARGE_INLINE)
+__device__ __attribute__((noinline)) void bessel_j01_large_ool(double ax, double* j0, double* j1) {
+  dfmi_bessel_j01_large(ax, j0, j1);
+}
+DFMI_HDI void bessel_j01_large_call(double ax, double& j0, double& j1) { bessel_j01_large_ool(ax, &j0, &j1); }
+#else
+DFMI_HDI void bessel_j01_large_call(double ax, double& j0, double& j1) { dfmi_bessel_j01_large(ax, &j0, &j1); }
+#endif
+
 template <int NB>
 DFMI_HDI void bessel_regs(double x, int N, double (&J)[NB]) {
   const double ax = fabs(x);
@@ -163,7 +176,7 @@ DFMI_HDI void bessel_regs(double x, int N, double (&J)[NB]) {
   static_assert((NB & 1) == 0, "the pair loop below needs an even NB");
   if (dfmi_bessel_use_large(ax, NB - 1)) {  // runaway descents: O(NB), not ~1.1|x| orders (dfmi_math.h)
     double j0, j1;
-    dfmi_bessel_j01_large(ax, &j0, &j1);
+    bessel_j01_large_call(ax, j0, j1);
     const double tox = 2.0 * rcp_nr(ax);
     J[0] = j0;
     J[1] = j1;

@@ -275,7 +275,7 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
                    int32_t* fitok, int32_t mem, void* stream);
 
 /* Performance tuning hook, process-wide; each call works on a snapshot taken at its
- * start. Results are unaffected (ekf_rot: rounding only). Keys: "demod_kernel" (1 phase bins in LDS where they
+ * start. Results are unaffected (ekf_rot, ekf_pit*: rounding only). Keys: "demod_kernel" (1 phase bins in LDS where they
  * apply [default], 0 cycle-aligned fold), "lm_general" (1 = two-pass general LM path
  * for every ndata), "demod_spw" (segments per wave the bin grid is sized for; 0 =
  * persistent), "ekf_row" (EKF row kernel up to ekf_row x 16 x CUs channels, 0 = lane
@@ -289,8 +289,13 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
  * beyond that many first DRAINS THE DEVICE (hipDeviceSynchronize) and frees the least
  * recently used stream's workspaces — a caller cycling over more streams serialises every
  * call, and such a call must not be made while a stream is being captured into a graph;
- * raise the key to the number of streams in use), "probe" (1 = diagnostics timestamp
- * buffer on the current device, dfmi_probe_read). */
+ * raise the key to the number of streams in use), "ekf_pit" (EKF parallel in time for up
+ * to this many channels, default 8; 0 = the sequential kernels always), "ekf_pit_min"
+ * (samples per channel below which the sequential kernels run, default 32768),
+ * "ekf_pit_block" (samples per block, 0 = ~n / 16384, at least 16), "ekf_pit_passes"
+ * (relinearization passes before the lane-kernel fallback, default 12), "ekf_pit_head"
+ * (samples the sequential EKF seeds the trajectory with, default 256), "probe" (1 =
+ * diagnostics timestamp buffer on the current device, dfmi_probe_read). */
 int dfmi_set_tuning(const char* key, int64_t value);
 
 /* Current value of a tuning key (see dfmi_set_tuning). */

@@ -66,6 +66,7 @@ struct Tuning {
   int ekf_pit_block = 0;      // samples per block (0: ~n / 16384, at least 16)
   int ekf_pit_passes = 12;    // relinearization passes before a channel falls back to the lane kernel
   int ekf_pit_head = 256;     // samples the sequential EKF runs first to seed the trajectory (ekf_pit_head_kernel)
+  int ekf_pit_fused = 1;      // 1: EKF + fold in one kernel per pass (ekf_pit_pass_kernel); 0: separate kernels
 };
 Tuning g_tune;
 
@@ -879,7 +880,8 @@ const std::map<std::string, Knob>& knobs() {
       {"ekf_pit_min", {&Tuning::ekf_pit_min, {}}},
       {"ekf_pit_block", {&Tuning::ekf_pit_block, {}}},
       {"ekf_pit_passes", {&Tuning::ekf_pit_passes, {}}},
-      {"ekf_pit_head", {&Tuning::ekf_pit_head, {}}}};
+      {"ekf_pit_head", {&Tuning::ekf_pit_head, {}}},
+      {"ekf_pit_fused", {&Tuning::ekf_pit_fused, {0, 1}}}};
   return k;
 }
 // np.mean / np.var of nrec device records on st (moments.hip), numpy-exact.
@@ -909,21 +911,26 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
                 int64_t nbuf, double* dstates, hipStream_t st) {
   int64_t B = t_tune.ekf_pit_block > 0 ? t_tune.ekf_pit_block : (n + 16383) / 16384;
   if (B < 16) B = 16;
-  int64_t nb = (n + B - 1) / B;
-  const int64_t ngmax = dfmi::kPitWg;  // the top-level scan is one workgroup
-  if (nb > dfmi::kPitWg * ngmax) {
-    B = (n + dfmi::kPitWg * ngmax - 1) / (dfmi::kPitWg * ngmax);
-    nb = (n + B - 1) / B;
-  }
-  const int64_t ng = (nb + dfmi::kPitWg - 1) / dfmi::kPitWg, slots = B * nb;
-  void *xt, *wtt, *xbar, *agg, *tot, *conv, *flag, *hst;
+  const int64_t nb = (n + B - 1) / B, slots = B * nb;
+  // the scan hierarchy: level 0 = the block aggregates, level l+1 = the workgroup totals of
+  // level l, up to the first level that fits one workgroup
+  std::vector<int64_t> lsz = {nb};
+  while (lsz.back() > dfmi::kPitWg) lsz.push_back((lsz.back() + dfmi::kPitWg - 1) / dfmi::kPitWg);
+  const int L = (int)lsz.size() - 1;
+  void *xt, *wtt, *xbar, *conv, *flag, *hst;
+  std::vector<double*> lv[2];  // per aggregate buffer: level arrays [r][65][lsz[l]]
   int rc;
   const int64_t T0 = std::min<int64_t>(std::max(t_tune.ekf_pit_head, 0), n);
   if ((rc = workspace(dev, "p_xt", (size_t)(nrec * slots) * 8, &xt))) return rc;
   if ((rc = workspace(dev, "p_wt", (size_t)slots * 8, &wtt))) return rc;
   if ((rc = workspace(dev, "p_xbar", (size_t)(nrec * 5 * slots) * 8, &xbar))) return rc;
-  if ((rc = workspace(dev, "p_agg", (size_t)(nrec * dfmi::kPitEl * nb) * 8, &agg))) return rc;
-  if ((rc = workspace(dev, "p_tot", (size_t)(nrec * dfmi::kPitEl * ng) * 8, &tot))) return rc;
+  for (int bf = 0; bf < 2; ++bf)
+    for (int l = 0; l <= L; ++l) {
+      void* a;
+      const std::string name = "p_lv" + std::to_string(bf) + "_" + std::to_string(l);
+      if ((rc = workspace(dev, name.c_str(), (size_t)(nrec * dfmi::kPitEl * lsz[l]) * 8, &a))) return rc;
+      lv[bf].push_back((double*)a);
+    }
   if ((rc = workspace(dev, "p_conv", (size_t)nrec * 8, &conv))) return rc;
   if ((rc = workspace(dev, "p_flag", (size_t)(nrec * 2) * sizeof(int), &flag))) return rc;
   if ((rc = workspace(dev, "p_hst", (size_t)(nrec * 5) * 8, &hst))) return rc;
@@ -935,20 +942,53 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
                      n, (const double*)hst, T0, B, nb, w_m, f_samp, (double*)xt, (double*)wtt, (double*)xbar,
                      (int*)flag, (double*)conv);
   const dim3 lanes((unsigned)((nb + 63) / 64), nr);
-  for (int pass = 0; pass < t_tune.ekf_pit_passes; ++pass) {
-    hipLaunchKernelGGL(dfmi::ekf_pit_aggregate_kernel, lanes, dim3(64), 0, st, (const double*)xt,
-                       (const double*)wtt, (const double*)xbar, n, B, nb, dx0, dp0, dq, dr, (const int*)flag,
-                       (double*)agg, tk);
-    hipLaunchKernelGGL(dfmi::ekf_pit_scan_kernel, dim3((unsigned)ng, nr), dim3(dfmi::kPitWg), 0, st, (double*)agg,
-                       nb, nb, ng > 1 ? (double*)tot : nullptr, (const int*)flag);
-    if (ng > 1)
-      hipLaunchKernelGGL(dfmi::ekf_pit_scan_kernel, dim3(1, nr), dim3(dfmi::kPitWg), 0, st, (double*)tot, ng, ng,
-                         (double*)nullptr, (const int*)flag);
-    hipLaunchKernelGGL(dfmi::ekf_pit_blocks_kernel, lanes, dim3(64), 0, st, (const double*)xt, (const double*)wtt,
-                       (double*)xbar, n, B, nb, dx0, dp0, dq, dr, (const double*)agg, (const double*)tot,
-                       (const int*)flag, (double*)conv, (int)R, nbuf, dstates, tk);
+  // scan of one buffer's hierarchy: every level bottom-up, then the fix-ups top-down; the
+  // pass kernels read level 0 (prefixes within workgroups) and level 1 (true prefixes)
+  auto scan = [&](std::vector<double*>& a) {
+    for (int l = 0; l <= L; ++l)
+      hipLaunchKernelGGL(dfmi::ekf_pit_scan_kernel<dfmi::kPitWg>,
+                         dim3((unsigned)((lsz[l] + dfmi::kPitWg - 1) / dfmi::kPitWg), nr), dim3(4 * dfmi::kPitWg), 0,
+                         st, a[l], lsz[l], lsz[l], l < L ? a[l + 1] : nullptr, (const int*)flag);
+    for (int l = L - 1; l >= 1; --l)
+      if (lsz[l] > dfmi::kPitWg)
+        hipLaunchKernelGGL(dfmi::ekf_pit_fixup_kernel, dim3((unsigned)((lsz[l] - dfmi::kPitWg + 63) / 64), nr), dim3(64),
+                           0, st, a[l], lsz[l], (const double*)a[l + 1], lsz[l + 1], (const int*)flag);
+  };
+  const double* top0 = L >= 1 ? lv[0][1] : nullptr;
+  const double* top1 = L >= 1 ? lv[1][1] : nullptr;
+  auto check = [&]() {
     hipLaunchKernelGGL(dfmi::ekf_pit_check_kernel, dim3((unsigned)((nrec + 63) / 64)), dim3(64), 0, st,
                        (double*)conv, nrec, kPitTol, (int*)flag);
+  };
+  if (t_tune.ekf_pit_fused) {
+    // first aggregates at the seeded trajectory, then per pass: EKF + fold (ekf_pit_pass_kernel,
+    // aggregates into the other buffer), check, scan of the new aggregates
+    void* ent;
+    if ((rc = workspace(dev, "p_ent", (size_t)(nrec * 5 * nb) * 8, &ent))) return rc;
+    HIPCHK(hipMemsetAsync(ent, 0xFF, (size_t)(nrec * 5 * nb) * 8, st));  // NaN: no previous entry
+    const double* tops[2] = {top0, top1};
+    hipLaunchKernelGGL(dfmi::ekf_pit_aggregate_kernel, lanes, dim3(64), 0, st, (const double*)xt, (const double*)wtt,
+                       (const double*)xbar, n, B, nb, dx0, dp0, dq, dr, (const int*)flag, lv[0][0], tk);
+    scan(lv[0]);
+    int cur = 0;
+    for (int pass = 0; pass < t_tune.ekf_pit_passes; ++pass, cur ^= 1) {
+      hipLaunchKernelGGL(dfmi::ekf_pit_pass_kernel, lanes, dim3(64), 0, st, (const double*)xt, (const double*)wtt, n,
+                         B, nb, dx0, dp0, dq, dr, (const double*)lv[cur][0], tops[cur], lv[cur ^ 1][0],
+                         (double*)ent, (const int*)flag, (double*)conv, (int)R, nbuf, dstates, tk);
+      check();
+      if (pass + 1 < t_tune.ekf_pit_passes) scan(lv[cur ^ 1]);
+    }
+  } else {
+    for (int pass = 0; pass < t_tune.ekf_pit_passes; ++pass) {
+      hipLaunchKernelGGL(dfmi::ekf_pit_aggregate_kernel, lanes, dim3(64), 0, st, (const double*)xt,
+                         (const double*)wtt, (const double*)xbar, n, B, nb, dx0, dp0, dq, dr, (const int*)flag,
+                         lv[0][0], tk);
+      scan(lv[0]);
+      hipLaunchKernelGGL(dfmi::ekf_pit_blocks_kernel, lanes, dim3(64), 0, st, (const double*)xt, (const double*)wtt,
+                         (double*)xbar, n, B, nb, dx0, dp0, dq, dr, (const double*)lv[0][0], top0, (const int*)flag,
+                         (double*)conv, (int)R, nbuf, dstates, tk);
+      check();
+    }
   }
   hipLaunchKernelGGL(dfmi::ekf_pit_fallback_kernel, dim3((unsigned)((nrec + 63) / 64)), dim3(64), 0, st, dx, nrec,
                      rs, n, dx0, dp0, dq, dr, wt, (int)R, nbuf, dstates, (int*)flag, tk);

@@ -59,8 +59,17 @@ __global__ __launch_bounds__(64) void ekf_x0_kernel(double* __restrict__ x0, dou
 // v_rcp_f64 (~1 ulp), phi + m cos(theta) is one fma. Every change is a rounding-order
 // change against numpy's expressions (the reference itself moves by ~1e-15 under 1-ulp
 // changes; tests/test_gpu_parity.py holds the kernel to 1e-12 of the oracle).
+// ekf_step that also hands out the measurement row H and h = h(x) at the predicted state
+// (the EKF parallel in time folds the sample's linearized element from them, ekf_pit.h)
+__device__ __forceinline__ void ekf_step_h(double (&st)[5], double (&P)[5][5], const double (&Q)[5], double Rv,
+                                           double xk, double wt, const DfmiTrigK& tk, double (&H)[5], double& h);
 __device__ __forceinline__ void ekf_step(double (&st)[5], double (&P)[5][5], const double (&Q)[5], double Rv,
                                          double xk, double wt, const DfmiTrigK& tk) {
+  double H[5], h;
+  ekf_step_h(st, P, Q, Rv, xk, wt, tk, H, h);
+}
+__device__ __forceinline__ void ekf_step_h(double (&st)[5], double (&P)[5][5], const double (&Q)[5], double Rv,
+                                           double xk, double wt, const DfmiTrigK& tk, double (&H)[5], double& h) {
 #pragma unroll
   for (int i = 0; i < 5; ++i) P[i][i] = P[i][i] + Q[i];  // predict: F = I
   const double a = st[0], m = st[1], phi = st[2], psi = st[3], dc = st[4];
@@ -71,8 +80,12 @@ __device__ __forceinline__ void ekf_step(double (&st)[5], double (&P)[5][5], con
   const double acth = -a * cth, amsth = (a * m) * sth;
   double sa, ca;
   dfmi_sincos_k(arg, tk, &sa, &ca);
-  const double h = fma(a, ca, dc);
-  const double H[5] = {ca, acth * sa, -a * sa, amsth * sa, 1.0};
+  h = fma(a, ca, dc);
+  H[0] = ca;
+  H[1] = acth * sa;
+  H[2] = -a * sa;
+  H[3] = amsth * sa;
+  H[4] = 1.0;
   const double y = xk - h;
   auto Pu = [&](int i, int j) -> double { return i <= j ? P[i][j] : P[j][i]; };
   double HP[5];

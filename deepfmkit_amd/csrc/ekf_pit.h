@@ -41,7 +41,7 @@ namespace dfmi {
 
 constexpr int kPitEl = 65;
 constexpr int kPitA = 0, kPitB = 25, kPitC = 30, kPitE = 45, kPitJ = 50;
-constexpr int kPitWg = 256;  // elements per scan workgroup
+constexpr int kPitWg = 64;  // elements per scan workgroup (every level of the scan hierarchy)
 __host__ __device__ constexpr int pit_sy(int i, int j) {
   return i <= j ? i * 5 - i * (i - 1) / 2 + (j - i) : j * 5 - j * (j - 1) / 2 + (i - j);
 }
@@ -66,7 +66,7 @@ struct PitEl {
 // M by Gauss-Jordan (I + C J with C, J PSD has eigenvalues >= 1 but its leading minors can
 // vanish: a pivot below 1/4 redoes it with partial pivoting, whose row swaps are selects so
 // every index stays static).
-__device__ __forceinline__ void pit_combine(const PitEl& ei, const PitEl& ej, double (&o)[kPitEl]) {
+__device__ __forceinline__ void pit_minv(const PitEl& ei, const PitEl& ej, double (&M)[5][5]) {
   double T[5][10];
   auto init_T = [&]() {
 #pragma unroll
@@ -135,65 +135,93 @@ __device__ __forceinline__ void pit_combine(const PitEl& ei, const PitEl& ej, do
       }
     }
   }
-  // M = T[.][5..9]
-  auto M = [&](int r, int c) -> double { return T[r][5 + c]; };
-  double X[5][5];  // M A_i
 #pragma unroll
   for (int r = 0; r < 5; ++r)
 #pragma unroll
-    for (int c = 0; c < 5; ++c) {
-      double s = 0.0;
+    for (int c = 0; c < 5; ++c) M[r][c] = T[r][5 + c];
+}
+
+// The combine split in four roles with no shared intermediate beyond M, so four waves can
+// form one element's result side by side (ekf_pit_scan_kernel): role 0 A (25 outputs), role 1
+// b and eta (10), role 2 C (15), role 3 J (15). pit_role_comp maps a role's output slot to
+// the element component it holds.
+template <int ROLE>
+__host__ __device__ constexpr int pit_role_n() {
+  return ROLE == 0 ? 25 : ROLE == 1 ? 10 : 15;
+}
+template <int ROLE>
+__host__ __device__ constexpr int pit_role_comp(int i) {
+  return ROLE == 0 ? kPitA + i : ROLE == 1 ? (i < 5 ? kPitB + i : kPitE + i - 5) : ROLE == 2 ? kPitC + i : kPitJ + i;
+}
+template <int ROLE>
+__device__ __forceinline__ void pit_role(const PitEl& ei, const PitEl& ej, const double (&M)[5][5], double (&o)[25]) {
+  if constexpr (ROLE == 0) {  // A = A_j (M A_i)
+    double X[5][5];
 #pragma unroll
-      for (int k = 0; k < 5; ++k) s = fma(M(r, k), ei.A(k, c), s);
-      X[r][c] = s;
-    }
+    for (int r = 0; r < 5; ++r)
 #pragma unroll
-  for (int r = 0; r < 5; ++r)
+      for (int c = 0; c < 5; ++c) {
+        double s = 0.0;
 #pragma unroll
-    for (int c = 0; c < 5; ++c) {
-      double s = 0.0;
+        for (int k = 0; k < 5; ++k) s = fma(M[r][k], ei.A(k, c), s);
+        X[r][c] = s;
+      }
 #pragma unroll
-      for (int k = 0; k < 5; ++k) s = fma(ej.A(r, k), X[k][c], s);
-      o[kPitA + r * 5 + c] = s;
-    }
-  {
-    double w[5], mw[5];
+    for (int r = 0; r < 5; ++r)
+#pragma unroll
+      for (int c = 0; c < 5; ++c) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) s = fma(ej.A(r, k), X[k][c], s);
+        o[r * 5 + c] = s;
+      }
+  } else if constexpr (ROLE == 1) {  // b = A_j M (b_i + C_i eta_j) + b_j; eta = A_i^T M^T (eta_j - J_j b_i) + eta_i
+    double w[5], mw[5], y[5], z[5];
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
       double s = ei(kPitB + r);
 #pragma unroll
       for (int k = 0; k < 5; ++k) s = fma(ei.C(r, k), ej(kPitE + k), s);
       w[r] = s;
+      double t = ej(kPitE + r);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) t = fma(-ej.J(r, k), ei(kPitB + k), t);
+      y[r] = t;
     }
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
-      double s = 0.0;
+      double s = 0.0, t = 0.0;
 #pragma unroll
-      for (int k = 0; k < 5; ++k) s = fma(M(r, k), w[k], s);
+      for (int k = 0; k < 5; ++k) {
+        s = fma(M[r][k], w[k], s);
+        t = fma(M[k][r], y[k], t);
+      }
       mw[r] = s;
+      z[r] = t;
     }
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
-      double s = ej(kPitB + r);
+      double s = ej(kPitB + r), t = ei(kPitE + r);
 #pragma unroll
-      for (int k = 0; k < 5; ++k) s = fma(ej.A(r, k), mw[k], s);
-      o[kPitB + r] = s;
+      for (int k = 0; k < 5; ++k) {
+        s = fma(ej.A(r, k), mw[k], s);
+        t = fma(ei.A(k, r), z[k], t);
+      }
+      o[r] = s;
+      o[5 + r] = t;
     }
-  }
-  // C = A_j (M C_i) A_j^T + C_j: X = M C_i (= (C_i^-1 + J_j)^-1, symmetric: upper triangle
-  // formed, mirrored), Y = X A_j^T, C = A_j Y (upper triangle)
+  } else if constexpr (ROLE == 2) {  // C = A_j (M C_i) A_j^T + C_j, M C_i symmetric
+    double X[5][5], Y[5][5];
 #pragma unroll
-  for (int r = 0; r < 5; ++r)
+    for (int r = 0; r < 5; ++r)
 #pragma unroll
-    for (int c = r; c < 5; ++c) {
-      double s = 0.0;
+      for (int c = r; c < 5; ++c) {
+        double s = 0.0;
 #pragma unroll
-      for (int k = 0; k < 5; ++k) s = fma(M(r, k), ei.C(k, c), s);
-      X[r][c] = s;
-      X[c][r] = s;
-    }
-  {
-    double Y[5][5];
+        for (int k = 0; k < 5; ++k) s = fma(M[r][k], ei.C(k, c), s);
+        X[r][c] = s;
+        X[c][r] = s;
+      }
 #pragma unroll
     for (int r = 0; r < 5; ++r)
 #pragma unroll
@@ -210,48 +238,20 @@ __device__ __forceinline__ void pit_combine(const PitEl& ei, const PitEl& ej, do
         double s = ej.C(i, j);
 #pragma unroll
         for (int k = 0; k < 5; ++k) s = fma(ej.A(i, k), Y[k][j], s);
-        o[kPitC + pit_sy(i, j)] = s;
+        o[pit_sy(i, j)] = s;
       }
-  }
-  // eta = A_i^T M^T (eta_j - J_j b_i) + eta_i
-  {
-    double y[5], z[5];
+  } else {  // J = A_i^T (M^T J_j) A_i + J_i, M^T J_j symmetric
+    double X[5][5], Y[5][5];
 #pragma unroll
-    for (int r = 0; r < 5; ++r) {
-      double s = ej(kPitE + r);
+    for (int r = 0; r < 5; ++r)
 #pragma unroll
-      for (int k = 0; k < 5; ++k) s = fma(-ej.J(r, k), ei(kPitB + k), s);
-      y[r] = s;
-    }
+      for (int c = r; c < 5; ++c) {
+        double s = 0.0;
 #pragma unroll
-    for (int r = 0; r < 5; ++r) {
-      double s = 0.0;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) s = fma(M(k, r), y[k], s);
-      z[r] = s;
-    }
-#pragma unroll
-    for (int r = 0; r < 5; ++r) {
-      double s = ei(kPitE + r);
-#pragma unroll
-      for (int k = 0; k < 5; ++k) s = fma(ei.A(k, r), z[k], s);
-      o[kPitE + r] = s;
-    }
-  }
-  // J = A_i^T (M^T J_j) A_i + J_i: X = M^T J_j (= (J_j^-1 + C_i)^-1, symmetric), Y = X A_i,
-  // J = A_i^T Y (upper triangle)
-#pragma unroll
-  for (int r = 0; r < 5; ++r)
-#pragma unroll
-    for (int c = r; c < 5; ++c) {
-      double s = 0.0;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) s = fma(M(k, r), ej.J(k, c), s);
-      X[r][c] = s;
-      X[c][r] = s;
-    }
-  {
-    double Y[5][5];
+        for (int k = 0; k < 5; ++k) s = fma(M[k][r], ej.J(k, c), s);
+        X[r][c] = s;
+        X[c][r] = s;
+      }
 #pragma unroll
     for (int r = 0; r < 5; ++r)
 #pragma unroll
@@ -268,8 +268,42 @@ __device__ __forceinline__ void pit_combine(const PitEl& ei, const PitEl& ej, do
         double s = ei.J(i, j);
 #pragma unroll
         for (int k = 0; k < 5; ++k) s = fma(ei.A(k, i), Y[k][j], s);
-        o[kPitJ + pit_sy(i, j)] = s;
+        o[pit_sy(i, j)] = s;
       }
+  }
+}
+
+template <int ROLE>
+__device__ __forceinline__ void pit_role_into(const PitEl& ei, const PitEl& ej, const double (&M)[5][5],
+                                              double (&o)[kPitEl]) {
+  double t[25];
+  pit_role<ROLE>(ei, ej, M, t);
+#pragma unroll
+  for (int i = 0; i < pit_role_n<ROLE>(); ++i) o[pit_role_comp<ROLE>(i)] = t[i];
+}
+
+// the whole combine in one lane
+__device__ __forceinline__ void pit_combine(const PitEl& ei, const PitEl& ej, double (&o)[kPitEl]) {
+  double M[5][5];
+  pit_minv(ei, ej, M);
+  pit_role_into<0>(ei, ej, M, o);
+  pit_role_into<1>(ei, ej, M, o);
+  pit_role_into<2>(ei, ej, M, o);
+  pit_role_into<3>(ei, ej, M, o);
+}
+
+// only the mean and covariance of ei (x) ej (an entry state: ei = a prefix from block 0)
+__device__ __forceinline__ void pit_combine_state(const PitEl& ei, const PitEl& ej, double (&st)[5],
+                                                  double (&P)[5][5]) {
+  double M[5][5], t[25], c[25];
+  pit_minv(ei, ej, M);
+  pit_role<1>(ei, ej, M, t);
+  pit_role<2>(ei, ej, M, c);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    st[i] = t[i];
+#pragma unroll
+    for (int j = i; j < 5; ++j) P[i][j] = c[pit_sy(i, j)];
   }
 }
 
@@ -511,43 +545,131 @@ __global__ __launch_bounds__(64) void ekf_pit_aggregate_kernel(const double* __r
   }
 }
 
-// Inclusive Hillis-Steele scan of n_el elements el[r][65][ld] in workgroups of 256 (LDS
-// [65][256], 133 KB: one workgroup per CU), in place; the workgroup totals go to
-// tot[r][65][gridDim.x] when tot is given (the top-level pass scans those with one
-// workgroup and tot = nullptr). Padding elements are the identity.
-__global__ __launch_bounds__(kPitWg) void ekf_pit_scan_kernel(double* __restrict__ el, int64_t n_el, int64_t ld,
-                                                              double* __restrict__ tot, const int* __restrict__ flag) {
+// Inclusive Hillis-Steele scan of n_el elements el[r][65][ld] in workgroups of WGE elements
+// (LDS [65][WGE]), in place; the workgroup totals (the last live element's prefix) go to
+// tot[r][65][gridDim.x] when tot is given: the next level of the hierarchy, scanned the same
+// way until one workgroup holds a level (tot = nullptr), then made true prefixes top-down by
+// ekf_pit_fixup_kernel. Padding elements are the identity. Each combine is formed by FOUR waves
+// side by side, one role each (pit_role: A / b, eta / C / J; every role forms M itself):
+// wave w holds elements 64 (w / 4) .. + 63 in role w % 4, so a wave never diverges and a level
+// costs one role's chain (~650 fp64 instructions) instead of the whole combine's (~1,500).
+template <int WGE>
+__global__ __launch_bounds__(4 * WGE) void ekf_pit_scan_kernel(double* __restrict__ el, int64_t n_el, int64_t ld,
+                                                               double* __restrict__ tot,
+                                                               const int* __restrict__ flag) {
+  static_assert(WGE % 64 == 0, "whole waves per role");
   const int64_t r = blockIdx.y;
   if (flag[2 * r]) return;
-  __shared__ double s[kPitEl * kPitWg];
+  __shared__ double s[kPitEl * WGE];
   const int t = threadIdx.x;
-  const int64_t e = (int64_t)blockIdx.x * kPitWg + t;
-  const bool live = e < n_el;
-  double* base = el + r * kPitEl * ld + e;
-#pragma unroll
-  for (int c = 0; c < kPitEl; ++c) s[c * kPitWg + t] = live ? base[c * ld] : pit_identity(c);
+  const int w = t >> 6, role = w & 3, e = ((w >> 2) << 6) + (t & 63);
+  const int64_t e0 = (int64_t)blockIdx.x * WGE;
+  const int64_t nlive = n_el - e0;  // live elements here (the rest: identities)
+  const int span = nlive < WGE ? (int)nlive : WGE;
+  double* base = el + r * kPitEl * ld + e0;
+  for (int i = t; i < kPitEl * WGE; i += 4 * WGE) {
+    const int c = i / WGE, k = i - c * WGE;
+    s[i] = k < span ? base[c * ld + k] : pit_identity(c);
+  }
   __syncthreads();
-  const int64_t nlive = n_el - (int64_t)blockIdx.x * kPitWg;  // live elements here (the rest: identities)
-  const int span = nlive < kPitWg ? (int)nlive : kPitWg;
   for (int off = 1; off < span; off <<= 1) {
-    double o[kPitEl];
-    const bool act = t >= off;
-    if (act) pit_combine(PitEl{s + t - off, kPitWg}, PitEl{s + t, kPitWg}, o);
+    double o[25];
+    const bool act = e >= off && e < span;
+    if (act) {
+      const PitEl ei{s + e - off, WGE}, ej{s + e, WGE};
+      double M[5][5];
+      pit_minv(ei, ej, M);
+      if (role == 0) pit_role<0>(ei, ej, M, o);
+      else if (role == 1) pit_role<1>(ei, ej, M, o);
+      else if (role == 2) pit_role<2>(ei, ej, M, o);
+      else pit_role<3>(ei, ej, M, o);
+    }
     __syncthreads();
     if (act) {
+      if (role == 0) {
 #pragma unroll
-      for (int c = 0; c < kPitEl; ++c) s[c * kPitWg + t] = o[c];
+        for (int i = 0; i < pit_role_n<0>(); ++i) s[pit_role_comp<0>(i) * WGE + e] = o[i];
+      } else if (role == 1) {
+#pragma unroll
+        for (int i = 0; i < pit_role_n<1>(); ++i) s[pit_role_comp<1>(i) * WGE + e] = o[i];
+      } else if (role == 2) {
+#pragma unroll
+        for (int i = 0; i < pit_role_n<2>(); ++i) s[pit_role_comp<2>(i) * WGE + e] = o[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < pit_role_n<3>(); ++i) s[pit_role_comp<3>(i) * WGE + e] = o[i];
+      }
     }
     __syncthreads();
   }
-  if (live) {
-#pragma unroll
-    for (int c = 0; c < kPitEl; ++c) base[c * ld] = s[c * kPitWg + t];
+  for (int i = t; i < kPitEl * WGE; i += 4 * WGE) {
+    const int c = i / WGE, k = i - c * WGE;
+    if (k < span) base[c * ld + k] = s[i];
   }
-  if (tot && t == kPitWg - 1) {
+  if (tot && t < kPitEl) {
     const int64_t ng = gridDim.x;
+    tot[(r * kPitEl + t) * ng + blockIdx.x] = s[t * WGE + span - 1];
+  }
+}
+
+// Level l of the scan hierarchy after its own scan holds prefixes within its workgroups of
+// kPitWg; element g of a later workgroup becomes the true prefix from element 0 by the
+// (already true) prefix of the previous workgroups one level up: el[g] = up[g / kPitWg - 1]
+// (x) el[g]. A prefix from block 0 is (0, b, C, 0, 0) (block 0's A is 0), so only b and C
+// are formed (pit_combine_state). One lane per element; the hierarchy is fixed top-down.
+__global__ __launch_bounds__(64) void ekf_pit_fixup_kernel(double* __restrict__ el, int64_t n_el,
+                                                           const double* __restrict__ up, int64_t n_up,
+                                                           const int* __restrict__ flag) {
+  const int64_t r = blockIdx.y;
+  if (flag[2 * r]) return;
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + kPitWg;  // the first workgroup is exact
+  if (g >= n_el) return;
+  double st[5], P[5][5];
+  double* e = el + r * kPitEl * n_el + g;
+  pit_combine_state(PitEl{up + r * kPitEl * n_up + (g / kPitWg - 1), n_up}, PitEl{e, n_el}, st, P);
 #pragma unroll
-    for (int c = 0; c < kPitEl; ++c) tot[(r * kPitEl + c) * ng + blockIdx.x] = s[c * kPitWg + t];
+  for (int c = 0; c < 25; ++c) e[(kPitA + c) * n_el] = 0.0;
+#pragma unroll
+  for (int c = 0; c < 5; ++c) {
+    e[(kPitB + c) * n_el] = st[c];
+    e[(kPitE + c) * n_el] = 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+#pragma unroll
+    for (int j = i; j < 5; ++j) {
+      e[(kPitC + pit_sy(i, j)) * n_el] = P[i][j];
+      e[(kPitJ + pit_sy(i, j)) * n_el] = 0.0;
+    }
+}
+
+// The state (x, P) entering block b: (x0, P0) for block 0, else the filtered (mean, cov)
+// after block b-1 = the inclusive prefix: agg[b-1] (scanned within its workgroup) preceded by
+// tot[g-1] (the scanned workgroup totals) when b-1 lies past the first workgroup.
+__device__ __forceinline__ void pit_entry(int64_t r, int64_t b, int64_t nb, const double* __restrict__ x0,
+                                          const double* __restrict__ p0, const double* __restrict__ agg,
+                                          const double* __restrict__ tot, double (&st)[5], double (&P)[5][5]) {
+  if (b == 0) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      st[i] = x0[r * 5 + i];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) P[i][j] = (i == j) ? p0[i] : 0.0;
+    }
+  } else {
+    const int64_t p = b - 1, g = p / kPitWg;
+    const PitEl loc{agg + r * kPitEl * nb + p, nb};
+    if (g == 0) {
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        st[i] = loc(kPitB + i);
+#pragma unroll
+        for (int j = i; j < 5; ++j) P[i][j] = loc.C(i, j);
+      }
+    } else {
+      const int64_t ng = (nb + kPitWg - 1) / kPitWg;
+      pit_combine_state(PitEl{tot + r * kPitEl * ng + (g - 1), ng}, loc, st, P);
+    }
   }
 }
 
@@ -577,35 +699,7 @@ __global__ __launch_bounds__(64) void ekf_pit_blocks_kernel(const double* __rest
   double st[5], P[5][5], Q[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) Q[i] = qd[i];
-  if (b == 0) {
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      st[i] = x0[r * 5 + i];
-#pragma unroll
-      for (int j = 0; j < 5; ++j) P[i][j] = (i == j) ? p0[i] : 0.0;
-    }
-  } else {
-    const int64_t p = b - 1, g = p / kPitWg;
-    const PitEl loc{agg + r * kPitEl * nb + p, nb};
-    if (g == 0) {
-#pragma unroll
-      for (int i = 0; i < 5; ++i) {
-        st[i] = loc(kPitB + i);
-#pragma unroll
-        for (int j = i; j < 5; ++j) P[i][j] = loc.C(i, j);
-      }
-    } else {
-      const int64_t ng = (nb + kPitWg - 1) / kPitWg;
-      double o[kPitEl];
-      pit_combine(PitEl{tot + r * kPitEl * ng + (g - 1), ng}, loc, o);
-#pragma unroll
-      for (int i = 0; i < 5; ++i) {
-        st[i] = o[kPitB + i];
-#pragma unroll
-        for (int j = i; j < 5; ++j) P[i][j] = o[kPitC + pit_sy(i, j)];
-      }
-    }
-  }
+  pit_entry(r, b, nb, x0, p0, agg, tot, st, P);
   const double Rv = rv[r];
   double dmax = 0.0;
   const int64_t kend = !live ? 0 : (b + 1) * B < n ? B : n - b * B;
@@ -653,6 +747,124 @@ __global__ __launch_bounds__(64) void ekf_pit_blocks_kernel(const double* __rest
   }
   // the channel's largest move: a non-negative double (or NaN, above every finite value
   // and inf) orders as its bits, so the wave's max goes to conv[r] by one integer atomic
+  unsigned long long bits = __builtin_bit_cast(unsigned long long, dmax);
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const unsigned long long o = __shfl_xor(bits, w, 64);
+    bits = o > bits ? o : bits;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax((unsigned long long*)conv + r, bits);
+}
+
+// Steps 3 and 1 of the next pass in one kernel (the default): lane = block runs the true EKF
+// from its entry state (pit_entry over the scan in agg / tot) and folds every sample's element
+// into the block's next aggregate (agg_out, scanned next) as it goes. The element of sample k
+// is linearized at the state entering k — the EKF step's own predicted state, whose H and
+// h(x) ekf_step_h has just formed — so the fold costs only the rank-1 update, and no
+// trajectory is written or re-read. Convergence: the entry state's largest relative move
+// since the previous pass (ent, NaN before the first) into conv[r] as in
+// ekf_pit_blocks_kernel. Snapshots as there.
+__global__ __launch_bounds__(64) void ekf_pit_pass_kernel(const double* __restrict__ xt,
+                                                          const double* __restrict__ wtt, int64_t n, int64_t B,
+                                                          int64_t nb, const double* __restrict__ x0,
+                                                          const double* __restrict__ p0,
+                                                          const double* __restrict__ qd,
+                                                          const double* __restrict__ rv,
+                                                          const double* __restrict__ agg,
+                                                          const double* __restrict__ tot,
+                                                          double* __restrict__ agg_out, double* __restrict__ ent,
+                                                          const int* __restrict__ flag, double* __restrict__ conv,
+                                                          int R, int64_t nbuf, double* __restrict__ states,
+                                                          DfmiTrigK tk) {
+  const int64_t r = blockIdx.y;
+  if (flag[2 * r]) return;
+  const int64_t b0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = b0 < nb;  // lanes past the last block stay for the wave's max (no work)
+  const int64_t b = live ? b0 : nb - 1;
+  const int64_t slots = B * nb;
+  double st[5], P[5][5], Q[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) Q[i] = qd[i];
+  pit_entry(r, b, nb, x0, p0, agg, tot, st, P);
+  double dmax = 0.0;
+  if (live) {
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      double* pe = ent + (r * 5 + c) * nb + b;
+      const double d = fabs(st[c] - *pe) / fmax(1.0, fabs(st[c]));
+      dmax = d <= dmax ? dmax : d;  // NaN (the first pass) propagates: never "converged"
+      *pe = st[c];
+    }
+  }
+  // the block's next aggregate: block 0 from the prior element, the others from the identity
+  double A[25], bv[5], C[15], et[5], J[15];
+  const bool first = b == 0;
+#pragma unroll
+  for (int c = 0; c < 25; ++c) A[c] = (!first && c / 5 == c % 5) ? 1.0 : 0.0;
+#pragma unroll
+  for (int c = 0; c < 15; ++c) C[c] = J[c] = 0.0;
+#pragma unroll
+  for (int c = 0; c < 5; ++c) {
+    bv[c] = first ? x0[r * 5 + c] : 0.0;
+    et[c] = 0.0;
+    if (first) C[pit_sy(c, c)] = p0[c];
+  }
+  const double Rv = rv[r];
+  const int64_t kend = !live ? 0 : (b + 1) * B < n ? B : n - b * B;
+  double yc[kPitG], wc[kPitG], yn[kPitG], wn[kPitG];
+  auto load = [&](double& y, double& w, int64_t i) {
+    const int64_t s = (i < B ? i : B - 1) * nb + b;
+    w = wtt[s];
+    y = xt[r * slots + s];
+  };
+#pragma unroll
+  for (int u = 0; u < kPitG; ++u) load(yc[u], wc[u], u);
+  for (int64_t i0 = 0; i0 < kend; i0 += kPitG) {
+#pragma unroll
+    for (int u = 0; u < kPitG; ++u) load(yn[u], wn[u], i0 + kPitG + u);
+#pragma unroll
+    for (int u = 0; u < kPitG; ++u) {
+      const int64_t i = i0 + u;
+      if (i >= kend) break;
+      double xp[5], H[5], hv;
+#pragma unroll
+      for (int c = 0; c < 5; ++c) xp[c] = st[c];
+      ekf_step_h(st, P, Q, Rv, yc[u], wc[u], tk, H, hv);
+      // eps = e - h.b with e = y - hv + h.xbar, xbar = the predicted state
+      double eps = yc[u] - hv;
+#pragma unroll
+      for (int c = 0; c < 5; ++c) eps = fma(H[c], xp[c] - bv[c], eps);
+      pit_fold(A, bv, C, et, J, Q, Rv, H, eps);
+      const int64_t k = b * B + i;
+      if ((k + 1) % R == 0) {
+        const int64_t bi = (k + 1) / R - 1;
+        if (bi < nbuf) {
+#pragma unroll
+          for (int c = 0; c < 5; ++c) states[(r * nbuf + bi) * 5 + c] = st[c];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kPitG; ++u) {
+      yc[u] = yn[u];
+      wc[u] = wn[u];
+    }
+  }
+  if (live) {
+    double* o = agg_out + r * kPitEl * nb + b;
+#pragma unroll
+    for (int c = 0; c < 25; ++c) o[(kPitA + c) * nb] = A[c];
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      o[(kPitB + c) * nb] = bv[c];
+      o[(kPitE + c) * nb] = et[c];
+    }
+#pragma unroll
+    for (int c = 0; c < 15; ++c) {
+      o[(kPitC + c) * nb] = C[c];
+      o[(kPitJ + c) * nb] = J[c];
+    }
+  }
   unsigned long long bits = __builtin_bit_cast(unsigned long long, dmax);
 #pragma unroll
   for (int w = 32; w >= 1; w >>= 1) {

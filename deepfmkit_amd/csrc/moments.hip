@@ -85,14 +85,24 @@ __global__ __launch_bounds__(kT) void moments_tree_kernel(const int* __restrict_
     for (int64_t t = threadIdx.x; t < nl; t += kT) v[t] = g[t];
     __syncthreads();
   }
-  for (int h = 0; h < H; ++h) {
+  // the levels from hs on hold one node each (numpy's left-to-right chain over the 8192-sample
+  // chunks: ~n / 8192 levels): one thread adds them in order without a barrier per level
+  int hs = H;
+  while (hs > 0 && lvl[hs] - lvl[hs - 1] == 1) --hs;
+  for (int h = 0; h < hs; ++h) {
     for (int j = lvl[h] + threadIdx.x; j < lvl[h + 1]; j += kT) {
       const int* q = tri + 3 * j;
       v[q[0]] = v[q[1]] + v[q[2]];
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[r * out_stride] = v[nl > 1 ? 2 * nl - 2 : 0] / (double)n;
+  if (threadIdx.x == 0) {
+    for (int j = lvl[hs]; j < lvl[H]; ++j) {
+      const int* q = tri + 3 * j;
+      v[q[0]] = v[q[1]] + v[q[2]];
+    }
+    out[r * out_stride] = v[nl > 1 ? 2 * nl - 2 : 0] / (double)n;
+  }
 }
 
 }  // namespace

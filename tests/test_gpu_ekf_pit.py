@@ -49,7 +49,7 @@ def _c_ekf(x, init4, R, nbuf, qd=QD, r_val=None):
 class _tune:
     """dfmi_set_tuning for the duration of a block, restoring the defaults."""
     DEFAULTS = {"ekf_row": 1, "ekf_rot": 1, "ekf_pit": 8, "ekf_pit_min": 32768, "ekf_pit_block": 0,
-                "ekf_pit_passes": 12, "ekf_pit_head": 256}
+                "ekf_pit_passes": 12, "ekf_pit_head": 256, "ekf_pit_fused": 1}
 
     def __init__(self, lib, **kw):
         self.lib, self.kw = lib, kw
@@ -97,12 +97,15 @@ def c5():
     return _raw(dfm, 6.0, 2.0, 7)
 
 
-def test_pit_config5_default_path_matches_c_oracle(lib, c5):
+@pytest.mark.parametrize("fused", [1, 0])
+def test_pit_config5_default_path_matches_c_oracle(lib, c5, fused):
     """One 400,000-sample channel takes the parallel form by default and converges in a few
-    passes; every snapshot within 1e-12 of the C restatement, the sequential row kernel within
-    1e-12 of it too."""
+    passes — the EKF and the next pass's fold in one kernel (fused, the default) or as separate
+    aggregate / blocks kernels; every snapshot within 1e-12 of the C restatement, the sequential
+    row kernel within 1e-12 of it too."""
     ref = _c_ekf(c5, (1.6, 6.0, 0.0, 0.0), 4000, 100)
-    got, kname, passes = _ekf(lib, [c5], 4000, 100)
+    with _tune(lib, ekf_pit_fused=fused):
+        got, kname, passes = _ekf(lib, [c5], 4000, 100)
     assert kname.startswith("ekf_pit"), kname
     assert 1 <= passes[0] <= 12, passes
     err = np.abs(got[0] - ref)
@@ -114,16 +117,18 @@ def test_pit_config5_default_path_matches_c_oracle(lib, c5):
     assert np.abs(seq[0] - got[0]).max() <= 1e-12
 
 
+@pytest.mark.parametrize("fused", [1, 0])
 @pytest.mark.parametrize("block", [16, 49, 700, 5000])
-def test_pit_block_sizes_ragged(lib, block):
-    """Block sizes from 16 (2,501 blocks: ten scan workgroups and the top-level scan) to 5000
-    (one workgroup), a 40,003-sample record (no block size divides it), R = 3000 (snapshots
-    mid-block) and R = 7: all within 1e-12 of the C oracle."""
+def test_pit_block_sizes_ragged(lib, block, fused):
+    """Block sizes from 16 (2,501 blocks: 40 scan workgroups and a second level) to 5000 (9
+    blocks, one workgroup), a 40,003-sample record (no block size divides it), R = 3000
+    (snapshots mid-block) and R = 7: all within 1e-12 of the C oracle. (Config 5's 16,000
+    blocks in the test above run three levels and the top-down fix-up.)"""
     import deepfmkit_amd as dfm
     x = _raw(dfm, 6.0, 0.2, 3)
     x = np.concatenate([x, x[:3]])
     assert x.size == 40_003
-    with _tune(lib, ekf_pit_block=block):
+    with _tune(lib, ekf_pit_block=block, ekf_pit_fused=fused):
         for R, nbuf in ((3000, 13), (7, 5714)):
             ref = _c_ekf(x, (1.6, 6.0, 0.0, 0.0), R, nbuf)
             got, kname, passes = _ekf(lib, [x], R, nbuf)

@@ -204,6 +204,34 @@ def parity_vs_oracle(df, ref):
             "vs": "oracle restatement of fit.py/fitters.py, pinned to the reference by tests/golden"}
 
 
+_ROCTX = None
+
+
+def _roctx():
+    """libroctx64 (ROCm's marker API) or False when absent: markers are diagnostics only."""
+    global _ROCTX
+    if _ROCTX is None:
+        try:
+            lib = ctypes.CDLL("libroctx64.so")
+            lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+            _ROCTX = lib
+        except OSError:
+            _ROCTX = False
+    return _ROCTX
+
+
+def roctx_push(name):
+    lib = _roctx()
+    if lib:
+        lib.roctxRangePushA(name.encode())
+
+
+def roctx_pop():
+    lib = _roctx()
+    if lib:
+        lib.roctxRangePop()
+
+
 def free_port():
     import socket
     with socket.socket() as sk:
@@ -690,13 +718,15 @@ def main():
     kname = step_kname
     fn = step
     # ---- the timed window: W untimed warmup steps, barrier + synchronize, exactly K steps,
-    # synchronize + barrier, MAX over ranks
+    # synchronize + barrier, MAX over ranks. A roctx range "timed_window" brackets it (seen by
+    # rocprofv3 --marker-trace; scripts/window_check.py accounts the window from a trace).
     for _ in range(args.warmup):
         fn()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    roctx_push("timed_window")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         fn()
@@ -704,6 +734,7 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    roctx_pop()
     if world > 1:
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)

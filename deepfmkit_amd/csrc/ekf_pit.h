@@ -10,16 +10,22 @@
 //      linear-Gaussian: x_k = x_{k-1} + q, y_k = H_k x_k + d_k + r (F = I as in the reference);
 //   2. the linear Kalman filter of that model is an associative prefix scan over filtering
 //      elements (A, b, C, eta, J) (Sarkka & Garcia-Fernandez, "Temporal parallelization of
-//      Bayesian smoothers", IEEE TAC 2021): every block folds its B elements in order
-//      (ekf_pit_aggregate_kernel, a rank-1 form of the combine per sample), the block
-//      aggregates are scanned (ekf_pit_scan_kernel: Hillis-Steele in LDS, 256 per workgroup,
-//      then over the workgroup totals), and the inclusive prefix at block b-1 is the filtered
-//      (mean, covariance) entering block b;
+//      Bayesian smoothers", IEEE TAC 2021): every block folds its B elements in order (a
+//      rank-1 form of the combine per sample), the block aggregates are scanned
+//      (ekf_pit_scan_kernel: Hillis-Steele in LDS, 64 per workgroup, four waves per combine,
+//      over a hierarchy of workgroup totals made true prefixes top-down by
+//      ekf_pit_fixup_kernel), and the inclusive prefix at block b-1 is the filtered (mean,
+//      covariance) entering block b;
 //   3. each block then runs the TRUE EKF (ekf_step, the lane kernel's arithmetic) from that
-//      entry state (ekf_pit_blocks_kernel), which gives the next xbar and the snapshots.
+//      entry state, which gives the snapshots and the next trajectory. ekf_pit_pass_kernel
+//      does 3 and the next pass's fold of 2 in one sweep: the element of a sample is
+//      linearized at the state entering it, which is the EKF step's own predicted state (its H
+//      and h(x) are already formed). The first pass's aggregates come from
+//      ekf_pit_aggregate_kernel at the seeded trajectory (ekf_pit_head_kernel); the separate
+//      aggregate / ekf_pit_blocks_kernel pair per pass remains behind the ekf_pit_fused knob.
 //
-// When xbar stops moving (max |dx| / max(1, |x|) <= tol over the channel, tested on the
-// device by ekf_pit_check_kernel) the block entry states are the EKF's own states at those
+// When the block entry states stop moving (max |dx| / max(1, |x|) <= tol over the channel,
+// tested on the device by ekf_pit_check_kernel) they are the EKF's own states at those
 // samples to the scan's rounding (~1e-13; the iteration converges quadratically once close:
 // scripts/study/ekf_pit_proto.py), so the output is the sequential EKF's to rounding. A
 // converged channel's later kernels return at once (flag per channel, no host round trip);
@@ -27,7 +33,9 @@
 // (ekf_pit_fallback_kernel), so the result never depends on the iteration having converged.
 //
 // Layouts (all channel-major, blocks fastest so lane b of a wave reads address b):
-//   xt[r][i][b], wtt[i][b] (sample k = b B + i), xbar[r][c][i][b], agg[r][65][nb], tot[r][65][ng].
+//   xt[r][i][b], wtt[i][b] (sample k = b B + i), xbar[r][c][i][b] (the seeded trajectory),
+//   scan level l: [r][65][n_l] with n_0 = nb, n_{l+1} = ceil(n_l / 64), two buffers (a pass
+//   reads one and writes the other), ent[r][c][b] (the previous pass's entry states).
 // Element components: A 0..24 (row-major), b 25..29, C 30..44 (upper triangle, row-major),
 // eta 45..49, J 50..64 (upper triangle).
 #pragma once
@@ -310,9 +318,9 @@ __device__ __forceinline__ void pit_combine_state(const PitEl& ei, const PitEl& 
 // The first pass's trajectory. A pass linearizes every sample at xbar, and where xbar is far
 // from the filter's path (the start-up transient from x0, P0 = I) the fixed point is only
 // reached one block per pass (scripts/study/ekf_pit_proto.py: 9 passes of crawling before
-// quadratic convergence for init_m = 6 on an m = 4.3 record). So the sequential EKF (lane
-// arithmetic) runs the first T0 samples, their predicted states seed xbar there, and every
-// later sample starts at the state entering sample T0. One lane per channel.
+// quadratic convergence for init_m = 6 on an m = 4.3 record). So the sequential EKF runs the
+// first T0 samples, their predicted states seed xbar there, and every later sample starts at
+// the state entering sample T0.
 __global__ __launch_bounds__(64) void ekf_pit_head_kernel(const double* __restrict__ x, int64_t nrec, int64_t rs,
                                                           int64_t T0, const double* __restrict__ x0,
                                                           const double* __restrict__ p0,
@@ -320,21 +328,33 @@ __global__ __launch_bounds__(64) void ekf_pit_head_kernel(const double* __restri
                                                           const double* __restrict__ rv, double w_m, double f_samp,
                                                           int64_t B, int64_t nb, double* __restrict__ xbar,
                                                           double* __restrict__ hst, DfmiTrigK tk) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= nrec) return;
+  // the row form of ekf_row_kernel (16 lanes per channel, 4 channels per wave, lane-split
+  // sincos: ~1.4x the lane form's rate); these states only seed the trajectory, the passes
+  // re-derive every sample
+  const int lane = threadIdx.x & 63;
+  const int64_t r0 = (int64_t)blockIdx.x * 4 + (lane >> 4);
+  const bool live = r0 < nrec;
+  const int64_t r = live ? r0 : nrec - 1;
+  int j = lane & 15;
+  if (j > 4) j = 4;
   const int64_t slots = B * nb;
-  double st[5], P[5][5], Q[5];
+  double st[5], Pc[5], qv[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
     st[i] = x0[r * 5 + i];
-    Q[i] = qd[i];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) P[i][j] = (i == j) ? p0[i] : 0.0;
+    Pc[i] = (i == j) ? p0[i] : 0.0;
+    qv[i] = (i == j) ? qd[i] : 0.0;
   }
   const double Rv = rv[r];
+  const bool writer = live && (lane & 15) == 0;
+  const bool odd = lane & 1;
+  const RowSplitCoef rc = row_split_coef(tk, odd);
+  RowRegs rr;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) rr.HP[i] = 0.0;
+  rr.sth = rr.cth = rr.sa = rr.ca = 0.0;
   const double* __restrict__ xr = x + r * rs;
-  // the samples 8 at a time, the next group's loads in flight (a load per sample in the
-  // chain would expose its latency every step)
+  // the samples 8 at a time, the next group's loads in flight
   double xc[8];
   const int64_t T8 = T0 & ~(int64_t)7;
   if (T8 > 0) {
@@ -343,9 +363,11 @@ __global__ __launch_bounds__(64) void ekf_pit_head_kernel(const double* __restri
   }
   int64_t s = 0, bi = 0, ii = 0;  // slot of sample k: block bi, index ii (no division per sample)
   auto step = [&](int64_t k, double xk) {
+    if (writer) {
 #pragma unroll
-    for (int c = 0; c < 5; ++c) xbar[(r * 5 + c) * slots + s] = st[c];
-    ekf_step(st, P, Q, Rv, xk, w_m * ((double)k / f_samp), tk);
+      for (int c = 0; c < 5; ++c) xbar[(r * 5 + c) * slots + s] = st[c];
+    }
+    ekf_row_step<true>(st, Pc, qv, Rv, xk, w_m * ((double)k / f_samp), tk, rr, rc, odd);
     if (++ii == B) {
       ii = 0;
       s = ++bi;
@@ -365,8 +387,10 @@ __global__ __launch_bounds__(64) void ekf_pit_head_kernel(const double* __restri
     for (int u = 0; u < 8; ++u) xc[u] = xn[u];
   }
   for (; k < T0; ++k) step(k, xr[k]);
+  if (writer) {
 #pragma unroll
-  for (int c = 0; c < 5; ++c) hst[r * 5 + c] = st[c];
+    for (int c = 0; c < 5; ++c) hst[r * 5 + c] = st[c];
+  }
 }
 
 // Transposes the channel data into blocks, tabulates w_m t_k (ekf_phase_kernel's

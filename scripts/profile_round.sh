@@ -1,7 +1,8 @@
 #!/bin/bash
 # rocprofv3 passes for the judged profiles (run on the GPU box via gpurun):
-#  1) --kernel-trace --stats over the driver's exact bench command
-#     (bench.py --gpus 1 --steps 20 --warmup 5)
+#  1) --kernel-trace --marker-trace --stats over the driver's exact bench command
+#     (bench.py --gpus 1 --steps 20 --warmup 5); window_check.json accounts its timed window
+#     (the roctx range bench.py puts around it) from that trace
 #  2) PMC pass: FETCH_SIZE over a short bench run (the step's fused kernel)
 #  3) PMC pass: WRITE_SIZE over the same
 #  4) profiles/pmc_demod.json from 2) + 3) (scripts/pmc_summary.py), for the step's
@@ -10,10 +11,11 @@
 # Each step has its own time limit; the script stops at the first failure.
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
-OUT=$PWD/gpurun_out/prof_${TAG:-r03}
+OUT=$PWD/gpurun_out/prof_${TAG:-r04}
 mkdir -p "$OUT"
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o bench -- \
+timeout -k 10 600 rocprofv3 --kernel-trace --marker-trace --stats --output-format csv -d "$OUT/trace" -o bench -- \
     python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_trace.json" 2> "$OUT/trace.err" || exit $?
+python3 scripts/window_check.py "$OUT/trace" 20 > "$OUT/window_check.json" || true
 PMC_CMD="bench.py --no-cpu-baseline --no-extra --steps 5 --warmup 1"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o step -- \
     python3 $PMC_CMD > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err" || exit $?

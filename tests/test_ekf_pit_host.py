@@ -166,3 +166,64 @@ def test_relinearized_scan_converges_to_sequential_ekf():
     assert moved <= 1e-11, (it, moved)
     assert it <= 8, it
     assert np.max(np.abs(new - seq)) <= 1e-12, np.max(np.abs(new - seq))
+
+
+def _hier_scan(el, W):
+    """ekf_pit_run's scan hierarchy in numpy: Hillis-Steele within groups of W, group totals
+    one level up (recursively until one group holds a level), then the fix-ups top-down with
+    the (0, b, C, 0, 0) form of a prefix from element 0. Returns levels 0 and 1 as the pass
+    kernels read them."""
+    levels = [list(el)]
+    while len(levels[-1]) > W:
+        cur = levels[-1]
+        tot = []
+        for g0 in range(0, len(cur), W):
+            grp = cur[g0:g0 + W]
+            off = 1
+            while off < len(grp):
+                grp = [grp[i] if i < off else combine(grp[i - off], grp[i]) for i in range(len(grp))]
+                off *= 2
+            cur[g0:g0 + W] = grp
+            tot.append(grp[-1])
+        levels.append(tot)
+    top = levels[-1]
+    off = 1
+    while off < len(top):
+        top = [top[i] if i < off else combine(top[i - off], top[i]) for i in range(len(top))]
+        off *= 2
+    levels[-1] = top
+    for lv in range(len(levels) - 2, 0, -1):
+        up, cur = levels[lv + 1], levels[lv]
+        for g in range(W, len(cur)):
+            _, b, C, _, _ = combine(up[g // W - 1], cur[g])
+            cur[g] = (np.zeros((5, 5)), b, C, np.zeros(5), np.zeros((5, 5)))
+    return levels
+
+
+def test_scan_hierarchy_with_fixups_gives_every_entry_state():
+    """37 block aggregates, groups of 4 (levels 37 -> 10 -> 3, two fix-up levels): the entry
+    state of every block read as the pass kernels do (level 0 within its group, preceded by
+    the fixed level-1 prefix of the earlier groups) equals the sequential prefix."""
+    rng = np.random.default_rng(11)
+    q, Rv = np.array([1e-3, 2e-3, 1e-2, 1e-2, 1e-3]), 0.05
+    aggs = []
+    for b in range(37):
+        a = (np.zeros((5, 5)), rng.standard_normal(5), I5.copy(), np.zeros(5), np.zeros((5, 5))) if b == 0 \
+            else identity()
+        for _ in range(3):
+            a = fold(a, rng.standard_normal(5), rng.standard_normal(), q, Rv)
+        aggs.append(a)
+    seq = [aggs[0]]
+    for a in aggs[1:]:
+        seq.append(combine(seq[-1], a))
+    W = 4
+    levels = _hier_scan(aggs, W)
+    for b in range(1, 37):
+        p = b - 1
+        loc = levels[0][p]
+        if p // W == 0:
+            st, C = loc[1], loc[2]
+        else:
+            _, st, C, _, _ = combine(levels[1][p // W - 1], loc)
+        np.testing.assert_allclose(st, seq[p][1], rtol=1e-9, atol=1e-11)
+        np.testing.assert_allclose(C, seq[p][2], rtol=1e-9, atol=1e-11)

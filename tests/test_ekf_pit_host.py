@@ -119,6 +119,74 @@ def _ekf_step(st, P, xk, wt, q, Rv):
     return st + K * (xk - (a * np.cos(arg) + dc)), P - np.outer(K, H @ P)
 
 
+def _step_h(st, P, xk, wt, q, Rv):
+    """_ekf_step that also returns H and h at the predicted state (ekf_step_h)."""
+    P = P + np.diag(q)
+    a, m, phi, psi, dc = st
+    th = wt + psi
+    arg = phi + m * np.cos(th)
+    sa = np.sin(arg)
+    H = np.array([np.cos(arg), -a * sa * np.cos(th), -a * sa, a * m * sa * np.sin(th), 1.0])
+    h = a * np.cos(arg) + dc
+    S = H @ P @ H + Rv
+    K = P @ H / S
+    return st + K * (xk - h), P - np.outer(K, H @ P), H, h
+
+
+def test_fused_pass_converges_to_sequential_ekf():
+    """ekf_pit_pass_kernel's iteration: each block runs the EKF from its scanned entry and
+    folds every sample's element linearized at the EKF's own predicted state (its H, h), the
+    new aggregates are scanned for the next pass; converged when the entry states stop moving
+    (1e-11): the states equal the sequential EKF's to ~1e-13."""
+    fs, fm, n, B = 200000.0, 1000.0, 2400, 48
+    wt = 2 * np.pi * fm * (np.arange(n) / fs)
+    rng = np.random.default_rng(9)
+    x = 1.1 * np.cos(0.4 + 6.0 * np.cos(wt + 0.1)) + 0.5 + 0.01 * rng.standard_normal(n)
+    q, Rv = np.array([1e-8, 1e-8, 1e-6, 1e-6, 1e-8]), float(np.var(x))
+    x0 = np.array([1.6, 6.0, 0.0, 0.0, np.mean(x)])
+    st, P, seq = x0.copy(), I5.copy(), []
+    for k in range(n):
+        st, P = _ekf_step(st, P, x[k], wt[k], q, Rv)
+        seq.append(st)
+    seq = np.array(seq)
+    nb = n // B
+    # first aggregates at the trajectory held at x0 (no head here)
+    aggs = []
+    for b in range(nb):
+        a = (np.zeros((5, 5)), x0.copy(), I5.copy(), np.zeros(5), np.zeros((5, 5))) if b == 0 else identity()
+        for k in range(b * B, (b + 1) * B):
+            xa, m, phi, psi, dc = x0
+            th = wt[k] + psi
+            arg = phi + m * np.cos(th)
+            sa = np.sin(arg)
+            h = np.array([np.cos(arg), -xa * sa * np.cos(th), -xa * sa, xa * m * sa * np.sin(th), 1.0])
+            a = fold(a, h, x[k] - (xa * np.cos(arg) + dc) + h @ x0, q, Rv)
+        aggs.append(a)
+    prev = None
+    for it in range(14):
+        pre = [aggs[0]]
+        for a in aggs[1:]:
+            pre.append(combine(pre[-1], a))
+        ent = [(x0.copy(), I5.copy())] + [(pre[b - 1][1].copy(), pre[b - 1][2].copy()) for b in range(1, nb)]
+        new, aggs = np.empty_like(seq), []
+        for b in range(nb):
+            st, P = ent[b]
+            a = (np.zeros((5, 5)), x0.copy(), I5.copy(), np.zeros(5), np.zeros((5, 5))) if b == 0 else identity()
+            for k in range(b * B, (b + 1) * B):
+                xp = st.copy()
+                st, P, H, h = _step_h(st, P, x[k], wt[k], q, Rv)
+                a = fold(a, H, x[k] - h + H @ xp, q, Rv)
+                new[k] = st
+            aggs.append(a)
+        e = np.array([v[0] for v in ent])
+        moved = np.inf if prev is None else np.max(np.abs(e - prev) / np.maximum(1.0, np.abs(e)))
+        prev = e
+        if moved <= 1e-11:
+            break
+    assert moved <= 1e-11, (it, moved)
+    assert np.max(np.abs(new - seq)) <= 1e-12, np.max(np.abs(new - seq))
+
+
 def test_relinearized_scan_converges_to_sequential_ekf():
     """The kernel sequence on a 2,400-sample record (a = 1.1, m = 6, phi = 0.4, psi = 0.1,
     dc = 0.5, 40 dB white noise; fitters.py defaults: Q, P0 = I, x0 = (1.6, 6, 0, 0, mean),

@@ -208,15 +208,19 @@ _ROCTX = None
 
 
 def _roctx():
-    """libroctx64 (ROCm's marker API) or False when absent: markers are diagnostics only."""
+    """ROCm's marker API (rocprofiler-sdk's roctx, which rocprofv3 --marker-trace records) or
+    False when absent: markers are diagnostics only."""
     global _ROCTX
     if _ROCTX is None:
-        try:
-            lib = ctypes.CDLL("libroctx64.so")
-            lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
-            _ROCTX = lib
-        except OSError:
-            _ROCTX = False
+        _ROCTX = False
+        for name in ("librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so"):
+            try:
+                lib = ctypes.CDLL(name)
+                lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                _ROCTX = lib
+                break
+            except (OSError, AttributeError):
+                continue
     return _ROCTX
 
 

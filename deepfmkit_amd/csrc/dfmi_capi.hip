@@ -934,13 +934,15 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
   if ((rc = workspace(dev, "p_conv", (size_t)nrec * 8, &conv))) return rc;
   if ((rc = workspace(dev, "p_flag", (size_t)(nrec * 2) * sizeof(int), &flag))) return rc;
   if ((rc = workspace(dev, "p_hst", (size_t)(nrec * 5) * 8, &hst))) return rc;
+  void* done;
+  if ((rc = workspace(dev, "p_done", (size_t)nrec * sizeof(unsigned), &done))) return rc;
   const DfmiTrigK tk = dfmi_trig_k();
   const unsigned nr = (unsigned)nrec;
   hipLaunchKernelGGL(dfmi::ekf_pit_head_kernel, dim3((unsigned)((nrec + 3) / 4)), dim3(64), 0, st, dx, nrec, rs, T0,
                      dx0, dp0, dq, dr, w_m, f_samp, B, nb, (double*)xbar, (double*)hst, tk);
   hipLaunchKernelGGL(dfmi::ekf_pit_gather_kernel, dim3((unsigned)((slots + 255) / 256), nr), dim3(256), 0, st, dx, rs,
                      n, (const double*)hst, T0, B, nb, w_m, f_samp, (double*)xt, (double*)wtt, (double*)xbar,
-                     (int*)flag, (double*)conv);
+                     (int*)flag, (double*)conv, (unsigned*)done);
   const dim3 lanes((unsigned)((nb + 63) / 64), nr);
   // scan of one buffer's hierarchy: every level bottom-up, then the fix-ups top-down; the
   // pass kernels read level 0 (prefixes within workgroups) and level 1 (true prefixes)
@@ -974,8 +976,8 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
     for (int pass = 0; pass < t_tune.ekf_pit_passes; ++pass, cur ^= 1) {
       hipLaunchKernelGGL(dfmi::ekf_pit_pass_kernel, lanes, dim3(64), 0, st, (const double*)xt, (const double*)wtt, n,
                          B, nb, dx0, dp0, dq, dr, (const double*)lv[cur][0], tops[cur], lv[cur ^ 1][0],
-                         (double*)ent, (const int*)flag, (double*)conv, (int)R, nbuf, dstates, tk);
-      check();
+                         (double*)ent, (int*)flag, (double*)conv, (unsigned*)done, kPitTol, (int)R, nbuf, dstates,
+                         tk);
       if (pass + 1 < t_tune.ekf_pit_passes) scan(lv[cur ^ 1]);
     }
   } else {

@@ -401,7 +401,7 @@ __global__ __launch_bounds__(256) void ekf_pit_gather_kernel(const double* __res
                                                              int64_t nb, double w_m, double f_samp,
                                                              double* __restrict__ xt, double* __restrict__ wtt,
                                                              double* __restrict__ xbar, int* __restrict__ flag,
-                                                             double* __restrict__ conv) {
+                                                             double* __restrict__ conv, unsigned* __restrict__ done) {
   const int64_t r = blockIdx.y;
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // s = i nb + b
   const int64_t slots = B * nb;
@@ -409,6 +409,7 @@ __global__ __launch_bounds__(256) void ekf_pit_gather_kernel(const double* __res
     flag[2 * r] = 0;      // converged
     flag[2 * r + 1] = 0;  // passes run
     conv[r] = 0.0;        // largest move of the pass (ekf_pit_blocks_kernel)
+    done[r] = 0;          // workgroups of the pass kernel finished (ekf_pit_pass_kernel)
   }
   if (s >= slots) return;
   const int64_t i = s / nb, b = s - i * nb;
@@ -797,8 +798,9 @@ __global__ __launch_bounds__(64) void ekf_pit_pass_kernel(const double* __restri
                                                           const double* __restrict__ agg,
                                                           const double* __restrict__ tot,
                                                           double* __restrict__ agg_out, double* __restrict__ ent,
-                                                          const int* __restrict__ flag, double* __restrict__ conv,
-                                                          int R, int64_t nbuf, double* __restrict__ states,
+                                                          int* __restrict__ flag, double* __restrict__ conv,
+                                                          unsigned* __restrict__ done, double tol, int R,
+                                                          int64_t nbuf, double* __restrict__ states,
                                                           DfmiTrigK tk) {
   const int64_t r = blockIdx.y;
   if (flag[2 * r]) return;
@@ -895,7 +897,21 @@ __global__ __launch_bounds__(64) void ekf_pit_pass_kernel(const double* __restri
     const unsigned long long o = __shfl_xor(bits, w, 64);
     bits = o > bits ? o : bits;
   }
-  if ((threadIdx.x & 63) == 0) atomicMax((unsigned long long*)conv + r, bits);
+  // the channel's check (ekf_pit_check_kernel's, without a launch): the last workgroup of
+  // the channel to finish (one wave each: lane 0 made the atomicMax) reads the max and sets
+  // the flag; every other workgroup of this launch had passed its flag test by then
+  if (threadIdx.x == 0) {
+    atomicMax((unsigned long long*)conv + r, bits);
+    __threadfence();
+    if (atomicAdd(done + r, 1u) == gridDim.x - 1) {
+      __threadfence();
+      const double c = __builtin_bit_cast(double, atomicAdd((unsigned long long*)conv + r, 0ull));
+      flag[2 * r + 1] += 1;
+      if (c <= tol) flag[2 * r] = 1;
+      atomicExch((unsigned long long*)conv + r, 0ull);
+      atomicExch(done + r, 0u);
+    }
+  }
 }
 
 // One thread per channel: converged when no block moved xbar by more than tol (relative,

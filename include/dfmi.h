@@ -294,7 +294,9 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
  * (samples per channel below which the sequential kernels run, default 32768),
  * "ekf_pit_block" (samples per block, 0 = ~n / 16384, at least 16), "ekf_pit_passes"
  * (relinearization passes before the lane-kernel fallback, default 12), "ekf_pit_head"
- * (samples the sequential EKF seeds the trajectory with, default 256), "probe" (1 =
+ * (samples the sequential EKF seeds the trajectory with, default 256), "ekf_pit_fused" (1
+ * [default]: the EKF and the next pass's fold in one kernel per pass; 0: separate kernels),
+ * "probe" (1 =
  * diagnostics timestamp buffer on the current device, dfmi_probe_read). */
 int dfmi_set_tuning(const char* key, int64_t value);
 

@@ -60,8 +60,9 @@ struct Tuning {
                          // 0 = always one lane per chain / segment
   int ws_streams = 4;    // caller streams whose workspaces are kept; a call from one more stream first
                          // drains the DEVICE (hipDeviceSynchronize) and frees the least recently used set
-  int ekf_pit = 8;       // EKF parallel in time (ekf_pit.h) for up to this many channels of at least
-                         // ekf_pit_min samples; 0 = the sequential kernels always
+  int ekf_pit = 256;     // EKF parallel in time (ekf_pit.h) for up to this many channels of at least
+                         // ekf_pit_min samples (measured crossover with the row kernel ~400 channels at
+                         // 400k samples, r04s); 0 = the sequential kernels always
   int ekf_pit_min = 32768;    // samples per channel below which the sequential kernels run
   int ekf_pit_block = 0;      // samples per block (0: ~n / 16384, at least 16)
   int ekf_pit_passes = 12;    // relinearization passes before a channel falls back to the lane kernel

@@ -24,7 +24,7 @@ def main():
     from deepfmkit_amd.physics import SnrSpec, synth_snr
     lib = _lib.load()
     dev = torch.device("cuda:0")
-    F_SAMP, F_MOD, R = 200000.0, 1000.0, 4000
+    F_SAMP, F_MOD, R = 200000.0, 1000.0, int(os.environ.get("R_", "4000"))
     ns = int(float(os.environ.get("SECONDS_", "2.0")) * F_SAMP)
     nb5 = ns // R
     reps = int(os.environ.get("REPS", "5"))
@@ -82,7 +82,7 @@ def main():
             print(json.dumps(out["variants"][-1]), flush=True)
         _lib.check(lib.dfmi_set_tuning(b"ekf_pit_block", 0), "tune")
         _lib.check(lib.dfmi_set_tuning(b"ekf_pit_head", 256), "tune")
-        _lib.check(lib.dfmi_set_tuning(b"ekf_pit", 8), "tune")
+        _lib.check(lib.dfmi_set_tuning(b"ekf_pit", 256), "tune")
         _lib.check(lib.dfmi_set_tuning(b"ekf_pit_min", 32768), "tune")
         del xe, stt
     print(json.dumps(out))

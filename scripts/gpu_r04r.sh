@@ -3,10 +3,12 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-VARIANTS=0:256 CHANNELS=1,32,128,512 REPS=3 timeout -k 10 400 python scripts/ekf_pit_ab.py > gpurun_out/r04r_channels.json 2> gpurun_out/r04r_channels.err || exit 1
-tail -1 gpurun_out/r04r_channels.json
+timeout -k 10 500 python -u -m pytest tests/test_gpu_ekf_pit.py tests/test_gpu_full_scale.py -k "ekf or pit" -v -rP --timeout 300 --timeout-method thread > gpurun_out/r04r_pit.log 2>&1
+rc=$?
+tail -3 gpurun_out/r04r_pit.log
+if [ $rc -ne 0 ]; then grep -E "Error|assert" gpurun_out/r04r_pit.log | head; exit $rc; fi
 for sec in 0.01 0.02 0.05 0.1; do
-  SECONDS_=$sec PITMIN=1024 VARIANTS=0:256 CHANNELS=1,8 REPS=5 timeout -k 10 200 python scripts/ekf_pit_ab.py > gpurun_out/r04r_short_$sec.json 2> gpurun_out/r04r_short_$sec.err || exit 1
+  R_=400 SECONDS_=$sec PITMIN=1024 VARIANTS=0:256 CHANNELS=1,8 REPS=5 timeout -k 10 200 python scripts/ekf_pit_ab.py > gpurun_out/r04r_short_$sec.json 2> gpurun_out/r04r_short_$sec.err || exit 1
   tail -1 gpurun_out/r04r_short_$sec.json
 done
 OUT=gpurun_out/prof_r04r

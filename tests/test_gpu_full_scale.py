@@ -144,13 +144,14 @@ def test_config3_two_channels_vs_oracle(tmp_path):
         print(f"config 3 channel {c}: max |d amp, m, phi, psi| vs the oracle =", worst, "; beyond 5e-10:", n5)
 
 
-@pytest.mark.parametrize("row,rot,kname", [(1, 1, "ekf_rot_kernel"), (1, 0, "ekf_row_kernel"),
-                                           (0, 1, "ekf_lane_rot_kernel"), (0, 0, "ekf_kernel")])
-def test_ekf_config5_13_channels_full_length_vs_c_oracle(row, rot, kname):
+@pytest.mark.parametrize("row,rot,pit,kname", [(1, 1, 0, "ekf_rot_kernel"), (1, 0, 0, "ekf_row_kernel"),
+                                               (0, 1, 0, "ekf_lane_rot_kernel"), (0, 0, 0, "ekf_kernel"),
+                                               (1, 1, 256, "ekf_pit")])
+def test_ekf_config5_13_channels_full_length_vs_c_oracle(row, rot, pit, kname):
     """Config 5 at full length on 13 independent channels in ONE dfmi_ekf_fit launch (EKFFitter
     per channel, fitters.py:214-320): 4 channels per wave in the row kernels (sincos by rotation
-    or in full), the 13th wave row shadowed (13 = 3 x 4 + 1), 13 lanes in the lane kernel;
-    every channel's 100 snapshots
+    or in full), the 13th wave row shadowed (13 = 3 x 4 + 1), 13 lanes in the lane kernel, 13
+    channels parallel in time (the default); every channel's 100 snapshots
     against the scalar C restatement of the loop (oracle/csrc/ekf_scalar.c) at 1e-12."""
     import deepfmkit_amd as dfm
     from deepfmkit_amd import _lib
@@ -182,12 +183,14 @@ def test_ekf_config5_13_channels_full_length_vs_c_oracle(row, rot, kname):
         refs.append(ref)
     _lib.check(lib.dfmi_set_tuning(b"ekf_row", row), "tune")
     _lib.check(lib.dfmi_set_tuning(b"ekf_rot", rot), "tune")
+    _lib.check(lib.dfmi_set_tuning(b"ekf_pit", pit), "tune")
     try:
         got = dfm.fitters.ekf_records(raws, 20)
-        assert lib.dfmi_last_demod_kernel().decode() == kname
+        assert lib.dfmi_last_demod_kernel().decode().startswith(kname)
     finally:
         _lib.check(lib.dfmi_set_tuning(b"ekf_row", 1), "tune")
         _lib.check(lib.dfmi_set_tuning(b"ekf_rot", 1), "tune")
+        _lib.check(lib.dfmi_set_tuning(b"ekf_pit", 256), "tune")
     for ch in range(13):
         err = np.abs(np.asarray(got[ch]) - refs[ch])
         assert err.max() <= 1e-12, (ch, err.max())

@@ -63,7 +63,8 @@ struct Tuning {
   int ekf_pit = 256;     // EKF parallel in time (ekf_pit.h) for up to this many channels of at least
                          // ekf_pit_min samples (measured crossover with the row kernel ~400 channels at
                          // 400k samples, r04s); 0 = the sequential kernels always
-  int ekf_pit_min = 32768;    // samples per channel below which the sequential kernels run
+  int ekf_pit_min = 4096;     // samples per channel below which the sequential kernels run (crossover
+                              // ~3,000 samples: 2,000 0.8x, 4,000 1.45x the row kernel, r04r)
   int ekf_pit_block = 0;      // samples per block (0: ~n / 16384, at least 16)
   int ekf_pit_passes = 12;    // relinearization passes before a channel falls back to the lane kernel
   int ekf_pit_head = 256;     // samples the sequential EKF runs first to seed the trajectory (ekf_pit_head_kernel)

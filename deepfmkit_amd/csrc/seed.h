@@ -173,10 +173,20 @@ namespace dfmi {
 // (demod_bins_kernel's work). Lower block indices dispatch first, so the seeds are
 // resident from the start without a second queue, an event, or idle "spacer"
 // workgroups; the LM follows on the same stream. Records are contiguous (segment s
-// at x + s*R). The seed's 162 VGPRs share the
-// bin kernel's 3-waves-per-SIMD register budget (168), so occupancy is unchanged.
+// at x + s*R). The kernel is held to the bin kernel's 3-waves-per-SIMD register budget
+// (168 VGPRs): the seed's whole-wave ladder fit (round 4) wants 223, which cost the BULK
+// demodulation a third of its occupancy (0.497 -> 0.530 ms, r04q); capped, the seed's
+// overflow goes to scratch in the one wave that fits (DFMI_SEED_WAVES 0: no cap, A/B builds).
+#ifndef DFMI_SEED_WAVES
+#define DFMI_SEED_WAVES 3
+#endif
+#if DFMI_SEED_WAVES > 0
+#define DFMI_SEED_BOUNDS __launch_bounds__(kBlockThreads, DFMI_SEED_WAVES)
+#else
+#define DFMI_SEED_BOUNDS __launch_bounds__(kBlockThreads)
+#endif
 template <int MAXSLOT, int NDMAX, int PFN = 0, int LOADS = 8>
-__global__ __launch_bounds__(kBlockThreads) void demod_seed_bins_kernel(
+__global__ DFMI_SEED_BOUNDS void demod_seed_bins_kernel(
     const double* __restrict__ x, int64_t nseg, int64_t rec_stride, int64_t nrec, int R, int L, int ndata,
     const double* __restrict__ tab, double* __restrict__ rows, int64_t row_ld, const double* __restrict__ guess,
     GuessInline ginl, int use_inline, const double* __restrict__ jtab, LMConst c, double* __restrict__ out,

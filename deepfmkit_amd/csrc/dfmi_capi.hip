@@ -1079,7 +1079,16 @@ int ekf_impl(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
   if (n_samp > 0)
     hipLaunchKernelGGL(dfmi::ekf_phase_kernel, dim3((unsigned)((n_samp + 255) / 256)), dim3(256), 0, st,
                        (double*)wtw, n_samp, w_m, f_samp);
-  if (t_tune.ekf_pit > 0 && nrec <= t_tune.ekf_pit && n_samp >= t_tune.ekf_pit_min && n_samp >= 2) {
+  // the parallel form's scratch (~(6 x 8 B per sample + 2 x 65 doubles per block) per
+  // channel, ~37 MB for 400k samples) must fit in half of the free device memory; past
+  // that the sequential kernels run (same states to rounding)
+  bool pit = t_tune.ekf_pit > 0 && nrec <= t_tune.ekf_pit && n_samp >= t_tune.ekf_pit_min && n_samp >= 2;
+  if (pit) {
+    size_t fr = 0, tot = 0;
+    const double need = (double)nrec * ((double)n_samp * 8.0 * 6.0 + (double)n_samp / 16.0 * 8.0 * 2.2 * dfmi::kPitEl);
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && need > 0.5 * (double)fr) pit = false;
+  }
+  if (pit) {
     rc = ekf_pit_run(dev, dx, nrec, rs, n_samp, dx0, dp0, dq, dr, (const double*)wtw, w_m, f_samp, R, nbuf, dstates,
                      st);
     if (rc) return rc;

@@ -65,7 +65,7 @@ struct Tuning {
                          // 400k samples, r04s); 0 = the sequential kernels always
   int ekf_pit_min = 4096;     // samples per channel below which the sequential kernels run (crossover
                               // ~3,000 samples: 2,000 0.8x, 4,000 1.45x the row kernel, r04r)
-  int ekf_pit_block = 0;      // samples per block (0: ~n / 16384, at least 16)
+  int ekf_pit_block = 0;      // samples per block (0: ~n nrec^(2/3) / 16384, at least 16)
   int ekf_pit_passes = 12;    // relinearization passes before a channel falls back to the lane kernel
   int ekf_pit_head = 256;     // samples the sequential EKF runs first to seed the trajectory (ekf_pit_head_kernel)
   int ekf_pit_fused = 1;      // 1: EKF + fold in one kernel per pass (ekf_pit_pass_kernel); 0: separate kernels
@@ -911,7 +911,12 @@ constexpr double kPitTol = 1e-11;  // relative move of xbar at which a channel i
 int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, const double* dx0, const double* dp0,
                 const double* dq, const double* dr, const double* wt, double w_m, double f_samp, int32_t R,
                 int64_t nbuf, double* dstates, hipStream_t st) {
-  int64_t B = t_tune.ekf_pit_block > 0 ? t_tune.ekf_pit_block : (n + 16383) / 16384;
+  // samples per block: the measured best keeps ~16k x nrec^(1/3) blocks in flight over all
+  // channels (1 channel: B = 25 at 400k samples; 4: 64; 16: 128; 64: 512; 256: 1024,
+  // profiles/r04w..y): one channel is latency-bound (many short blocks), many channels fill
+  // the GPU anyway and fewer, longer blocks cut the scan's work
+  int64_t B = t_tune.ekf_pit_block;
+  if (B <= 0) B = (int64_t)std::ceil((double)n * std::pow((double)nrec, 2.0 / 3.0) / 16384.0);
   if (B < 16) B = 16;
   const int64_t nb = (n + B - 1) / B, slots = B * nb;
   // the scan hierarchy: level 0 = the block aggregates, level l+1 = the workgroup totals of

@@ -140,17 +140,22 @@ def test_pit_block_sizes_ragged(lib, block, fused):
 
 
 def test_pit_channels_independent(lib):
-    """Several channels in one call (different m, phi, psi; one tuned): each channel equals its
-    own single-channel run bit for bit, and the C oracle within 1e-12."""
+    """Several channels in one call (different m, phi, psi): at a fixed block size each channel
+    equals its own single-channel run bit for bit; at the default block size (which grows with
+    the channel count) every channel is within 1e-12 of the C oracle."""
     import deepfmkit_amd as dfm
     xs = [_raw(dfm, 6.0, 0.25, 11), _raw(dfm, 4.3, 0.25, 12, psi=0.3, phi=0.7), _raw(dfm, 9.0, 0.25, 13, phi=1.3)]
-    many, kname, passes = _ekf(lib, xs, 4000, 12)
+    with _tune(lib, ekf_pit_block=25):
+        many, kname, passes = _ekf(lib, xs, 4000, 12)
+        assert kname.startswith("ekf_pit (B=25,") and all(p >= 1 for p in passes), (kname, passes)
+        for c, x in enumerate(xs):
+            one, _, _ = _ekf(lib, [x], 4000, 12)
+            np.testing.assert_array_equal(many[c], one[0])
+    dflt, kname, passes = _ekf(lib, xs, 4000, 12)
     assert kname.startswith("ekf_pit") and all(p >= 1 for p in passes), (kname, passes)
     for c, x in enumerate(xs):
-        one, _, _ = _ekf(lib, [x], 4000, 12)
-        np.testing.assert_array_equal(many[c], one[0])
         ref = _c_ekf(x, (1.6, 6.0, 0.0, 0.0), 4000, 12)
-        assert np.abs(one[0] - ref).max() <= 1e-12
+        assert np.abs(dflt[c] - ref).max() <= 1e-12
 
 
 def test_pit_unconverged_falls_back_bit_exact(lib, c5):

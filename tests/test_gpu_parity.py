@@ -234,7 +234,9 @@ def _ekf_long_record(dfm, O, lib, kk):
     got = dfm.fitters.ekf_records([raw], 20)[0]
     assert kk.used(), lib.dfmi_last_demod_kernel()
     assert np.max(np.abs(got - ref)) <= 1e-12, np.max(np.abs(got - ref))
-    many = dfm.fitters.ekf_records([raw] * 6, 20)  # row kernel: a second wave, rows past the end
+    # row kernel: a second wave, rows past the end; parallel in time: 20,000 samples give the
+    # minimum block (16) for 1 and for 6 channels alike, so the runs are bit-comparable
+    many = dfm.fitters.ekf_records([raw] * 6, 20)
     for k in range(6):
         np.testing.assert_array_equal(many[k], got)
 

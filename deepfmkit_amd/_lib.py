@@ -99,6 +99,14 @@ def load():
             return _lib
         if not os.path.exists(LIB_PATH):
             raise DFMIError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        # PyTorch first when it is installed: the library then binds to the HIP runtime torch
+        # loaded. Loaded the other way round and initialised by a host-memory call, the
+        # library's runtime held the device and torch.cuda.is_available() turned False in that
+        # process (scripts/probe_init_order.py, r04za).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = ctypes.CDLL(LIB_PATH)
         P = ctypes.c_void_p
         i64, i32, dbl = ctypes.c_int64, ctypes.c_int32, ctypes.c_double

@@ -87,6 +87,11 @@ def _ekf(lib, xs, R, nbuf, init4=(1.6, 6.0, 0.0, 0.0), qd=QD, r_val=None):
 
 @pytest.fixture(scope="module")
 def lib():
+    # torch first, as in the other GPU test files (its runtime then owns the device before the
+    # library's first call)
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
     from deepfmkit_amd import _lib
     return _lib.load()
 

@@ -452,7 +452,7 @@ def extra_configs(torch, dev, lib, _lib, stream, cfg, cpu_leg):
             res5["seq"] = {"s_per_fit": round(ts, 5), "samples_per_s_per_channel": round(ns / ts, 1),
                            "kernel": lib.dfmi_last_demod_kernel().decode(),
                            "max_abs_dstate_vs_parallel_in_time": float(np.max(np.abs(stt[0].cpu().numpy() - s1)))}
-            _lib.check(lib.dfmi_set_tuning(b"ekf_pit", 256), "tune")
+            _lib.check(lib.dfmi_set_tuning(b"ekf_pit", 1024), "tune")
         del xe, stt
     c5 = {"workload": "EKFFitter.fit, 2 s = 400,000 samples @200 kS/s (m=6, 40 dB), snapshots every R=4000",
           "one_channel": res5[1], "one_channel_sequential": res5["seq"], "channels_1024": res5[1024],

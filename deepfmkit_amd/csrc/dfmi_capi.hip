@@ -60,9 +60,9 @@ struct Tuning {
                          // 0 = always one lane per chain / segment
   int ws_streams = 4;    // caller streams whose workspaces are kept; a call from one more stream first
                          // drains the DEVICE (hipDeviceSynchronize) and frees the least recently used set
-  int ekf_pit = 256;     // EKF parallel in time (ekf_pit.h) for up to this many channels of at least
-                         // ekf_pit_min samples (measured crossover with the row kernel ~400 channels at
-                         // 400k samples, r04s); 0 = the sequential kernels always
+  int ekf_pit = 1024;    // EKF parallel in time (ekf_pit.h) for up to this many channels of at least
+                         // ekf_pit_min samples (1,024 channels at 400k samples: 48 vs 71 ms for the row
+                         // kernel, r04z); 0 = the sequential kernels always
   int ekf_pit_min = 4096;     // samples per channel below which the sequential kernels run (crossover
                               // ~3,000 samples: 2,000 0.8x, 4,000 1.45x the row kernel, r04r)
   int ekf_pit_block = 0;      // samples per block (0: ~n nrec^(2/3) / 16384, at least 16)

@@ -125,7 +125,7 @@ int dfmi_nls_record(const double* x, int64_t nrec, int64_t rec_stride, int64_t n
  * chain over its samples: up to 16 x CUs channels one 16-lane DPP row per channel (4 per
  * wave; ekf_rot_kernel with sin / cos by rotation between anchors when R % 4 == 0, else
  * ekf_row_kernel), more channels one lane per channel (ekf_lane_rot_kernel / ekf_kernel);
- * dfmi_set_tuning "ekf_row" / "ekf_rot" select. Up to "ekf_pit" (256) channels of at least
+ * dfmi_set_tuning "ekf_row" / "ekf_rot" select. Up to "ekf_pit" (1024) channels of at least
  * "ekf_pit_min" (4096) samples run parallel in time instead (ekf_pit.h): relinearization
  * passes of an associative linear Kalman scan over blocks, each ending in the true EKF per
  * block, until the trajectory stops moving (relative 1e-11), else the lane kernel; the same
@@ -290,7 +290,7 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
  * recently used stream's workspaces — a caller cycling over more streams serialises every
  * call, and such a call must not be made while a stream is being captured into a graph;
  * raise the key to the number of streams in use), "ekf_pit" (EKF parallel in time for up
- * to this many channels, default 256; 0 = the sequential kernels always), "ekf_pit_min"
+ * to this many channels, default 1024; 0 = the sequential kernels always), "ekf_pit_min"
  * (samples per channel below which the sequential kernels run, default 4096),
  * "ekf_pit_block" (samples per block, 0 = ~n nrec^(2/3) / 16384, at least 16), "ekf_pit_passes"
  * (relinearization passes before the lane-kernel fallback, default 12), "ekf_pit_head"

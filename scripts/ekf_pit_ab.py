@@ -82,7 +82,7 @@ def main():
             print(json.dumps(out["variants"][-1]), flush=True)
         _lib.check(lib.dfmi_set_tuning(b"ekf_pit_block", 0), "tune")
         _lib.check(lib.dfmi_set_tuning(b"ekf_pit_head", 256), "tune")
-        _lib.check(lib.dfmi_set_tuning(b"ekf_pit", 256), "tune")
+        _lib.check(lib.dfmi_set_tuning(b"ekf_pit", 1024), "tune")
         _lib.check(lib.dfmi_set_tuning(b"ekf_pit_min", 4096), "tune")
         del xe, stt
     print(json.dumps(out))

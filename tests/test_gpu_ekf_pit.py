@@ -48,7 +48,7 @@ def _c_ekf(x, init4, R, nbuf, qd=QD, r_val=None):
 
 class _tune:
     """dfmi_set_tuning for the duration of a block, restoring the defaults."""
-    DEFAULTS = {"ekf_row": 1, "ekf_rot": 1, "ekf_pit": 256, "ekf_pit_min": 4096, "ekf_pit_block": 0,
+    DEFAULTS = {"ekf_row": 1, "ekf_rot": 1, "ekf_pit": 1024, "ekf_pit_min": 4096, "ekf_pit_block": 0,
                 "ekf_pit_passes": 12, "ekf_pit_head": 256, "ekf_pit_fused": 1}
 
     def __init__(self, lib, **kw):

@@ -146,7 +146,7 @@ def test_config3_two_channels_vs_oracle(tmp_path):
 
 @pytest.mark.parametrize("row,rot,pit,kname", [(1, 1, 0, "ekf_rot_kernel"), (1, 0, 0, "ekf_row_kernel"),
                                                (0, 1, 0, "ekf_lane_rot_kernel"), (0, 0, 0, "ekf_kernel"),
-                                               (1, 1, 256, "ekf_pit")])
+                                               (1, 1, 1024, "ekf_pit")])
 def test_ekf_config5_13_channels_full_length_vs_c_oracle(row, rot, pit, kname):
     """Config 5 at full length on 13 independent channels in ONE dfmi_ekf_fit launch (EKFFitter
     per channel, fitters.py:214-320): 4 channels per wave in the row kernels (sincos by rotation
@@ -190,7 +190,7 @@ def test_ekf_config5_13_channels_full_length_vs_c_oracle(row, rot, pit, kname):
     finally:
         _lib.check(lib.dfmi_set_tuning(b"ekf_row", 1), "tune")
         _lib.check(lib.dfmi_set_tuning(b"ekf_rot", 1), "tune")
-        _lib.check(lib.dfmi_set_tuning(b"ekf_pit", 256), "tune")
+        _lib.check(lib.dfmi_set_tuning(b"ekf_pit", 1024), "tune")
     for ch in range(13):
         err = np.abs(np.asarray(got[ch]) - refs[ch])
         assert err.max() <= 1e-12, (ch, err.max())

@@ -154,7 +154,7 @@ def test_ekf_matches_reference(manifest):
 # rot: 16-lane row per channel, sincos by rotation between anchors (default for few
 # channels, R % 4 == 0); row: the same row with the full sincos per sample; lanerot / lane:
 # one lane per channel (many channels) with / without the rotation.
-# pit: parallel in time (ekf_pit.h), the default for up to 256 channels of >= 4096 samples;
+# pit: parallel in time (ekf_pit.h), the default for up to 1024 channels of >= 4096 samples;
 # here forced on from 1024 samples so the shorter records take it too.
 EKF_KERNELS = {"rot": (1, 1, "ekf_rot_kernel"), "row": (1, 0, "ekf_row_kernel"), "lanerot": (0, 1, "ekf_lane_rot_kernel"),
                "lane": (0, 0, "ekf_kernel"), "pit": (1, 1, "ekf_pit")}
@@ -171,13 +171,13 @@ class _ekf_kernel:
         from deepfmkit_amd import _lib
         _lib.check(self.lib.dfmi_set_tuning(b"ekf_row", self.row), "tune")
         _lib.check(self.lib.dfmi_set_tuning(b"ekf_rot", self.rot), "tune")
-        _lib.check(self.lib.dfmi_set_tuning(b"ekf_pit", 256 if self.pit else 0), "tune")
+        _lib.check(self.lib.dfmi_set_tuning(b"ekf_pit", 1024 if self.pit else 0), "tune")
         _lib.check(self.lib.dfmi_set_tuning(b"ekf_pit_min", 1024 if self.pit else 4096), "tune")
         return self
 
     def __exit__(self, *exc):
         from deepfmkit_amd import _lib
-        for key, v in ((b"ekf_row", 1), (b"ekf_rot", 1), (b"ekf_pit", 256), (b"ekf_pit_min", 4096)):
+        for key, v in ((b"ekf_row", 1), (b"ekf_rot", 1), (b"ekf_pit", 1024), (b"ekf_pit_min", 4096)):
             _lib.check(self.lib.dfmi_set_tuning(key, v), "tune")
 
     def used(self):

@@ -1,12 +1,14 @@
-// ekf_pit.h — the EKF of fitters.py:214-320 parallel in time, for few long channels.
+// ekf_pit.h — the EKF of fitters.py:214-320 parallel in time (the default for up to 1,024
+// channels of >= 4,096 samples; the block size grows with the channel count, ekf_pit_run).
 //
 // The sequential kernels (ekf.h) run one channel's samples in order: ~410 clocks per
-// sample on one SIMD, a floor of the dependent fp64 chain (DESIGN.md §5, r04c PMC), so a
+// sample on one SIMD, a floor of the dependent fp64 chain (DESIGN.md §4, r04c PMC), so a
 // single 400k-sample channel takes ~69 ms however large the GPU is. Here the channel is cut
 // into nb blocks of B samples and the filter is solved as a fixed point:
 //
 //   1. linearize the measurement h(x) = a cos(phi + m cos(w_m t_k + psi)) + dc at a
-//      trajectory xbar_k (predicted states; xbar = x0 on the first pass), so the model is
+//      trajectory xbar_k (predicted states; on the first pass the head's sequential EKF over
+//      the first 256 samples, then the state entering sample 256), so the model is
 //      linear-Gaussian: x_k = x_{k-1} + q, y_k = H_k x_k + d_k + r (F = I as in the reference);
 //   2. the linear Kalman filter of that model is an associative prefix scan over filtering
 //      elements (A, b, C, eta, J) (Sarkka & Garcia-Fernandez, "Temporal parallelization of
@@ -25,9 +27,11 @@
 //      aggregate / ekf_pit_blocks_kernel pair per pass remains behind the ekf_pit_fused knob.
 //
 // When the block entry states stop moving (max |dx| / max(1, |x|) <= tol over the channel,
-// tested on the device by ekf_pit_check_kernel) they are the EKF's own states at those
-// samples to the scan's rounding (~1e-13; the iteration converges quadratically once close:
-// scripts/study/ekf_pit_proto.py), so the output is the sequential EKF's to rounding. A
+// tested on the device by the pass kernel's last workgroup, or ekf_pit_check_kernel on the
+// unfused path) they are the EKF's own states at those
+// samples to the scan's rounding (~1e-13; once past the start-up transient the error falls
+// ~100x per pass: scripts/study/ekf_pit_proto.py), so the output is the sequential EKF's to
+// rounding. A
 // converged channel's later kernels return at once (flag per channel, no host round trip);
 // a channel still moving after the last pass is re-run by the sequential lane kernel
 // (ekf_pit_fallback_kernel), so the result never depends on the iteration having converged.

@@ -357,11 +357,12 @@ def _ekf_host(lib, x, f_samp, f_mod, R, nbuf):
     return states[0]
 
 
-@pytest.mark.parametrize("n", [1, 7, 8, 127, 129, 4000, 8191, 8192, 8193, 30001, 400000])
+@pytest.mark.parametrize("n", [1, 7, 8, 127, 129, 4000, 8191, 8192, 8193, 30001, 400000, 800000])
 def test_record_moments_bit_exact(n):
     """dfmi_record_moments == np.mean / np.var bit for bit (numpy's pairwise tree, its
     8192-element buffer chunks, (x - mean)^2 rounded per operation), for 3 strided
-    records, from host and from device memory."""
+    records, from host and from device memory; 800,000 samples take the tree kernel's
+    global-memory node path (more nodes than its LDS holds)."""
     import torch
     from deepfmkit_amd import _lib
     lib = _lib.load()

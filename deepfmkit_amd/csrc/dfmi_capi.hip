@@ -945,11 +945,13 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
   if ((rc = workspace(dev, "p_done", (size_t)nrec * sizeof(unsigned), &done))) return rc;
   const DfmiTrigK tk = dfmi_trig_k();
   const unsigned nr = (unsigned)nrec;
+  void* hs;
+  if ((rc = workspace(dev, "p_hs", (size_t)(nrec * (T0 > 0 ? T0 : 1) * 5) * 8, &hs))) return rc;
   hipLaunchKernelGGL(dfmi::ekf_pit_head_kernel, dim3((unsigned)((nrec + 3) / 4)), dim3(64), 0, st, dx, nrec, rs, T0,
-                     dx0, dp0, dq, dr, w_m, f_samp, B, nb, (double*)xbar, (double*)hst, tk);
+                     dx0, dp0, dq, dr, wt, (double*)hs, (double*)hst, tk);
   hipLaunchKernelGGL(dfmi::ekf_pit_gather_kernel, dim3((unsigned)((slots + 255) / 256), nr), dim3(256), 0, st, dx, rs,
-                     n, (const double*)hst, T0, B, nb, w_m, f_samp, (double*)xt, (double*)wtt, (double*)xbar,
-                     (int*)flag, (double*)conv, (unsigned*)done);
+                     n, (const double*)hs, (const double*)hst, T0, B, nb, w_m, f_samp, (double*)xt, (double*)wtt,
+                     (double*)xbar, (int*)flag, (double*)conv, (unsigned*)done);
   const dim3 lanes((unsigned)((nb + 63) / 64), nr);
   // scan of one buffer's hierarchy: every level bottom-up, then the fix-ups top-down; the
   // pass kernels read level 0 (prefixes within workgroups) and level 1 (true prefixes)

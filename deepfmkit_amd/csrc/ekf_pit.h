@@ -46,6 +46,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "dfmi_math.h"
 #include "ekf.h"
 
@@ -329,19 +331,20 @@ __global__ __launch_bounds__(64) void ekf_pit_head_kernel(const double* __restri
                                                           int64_t T0, const double* __restrict__ x0,
                                                           const double* __restrict__ p0,
                                                           const double* __restrict__ qd,
-                                                          const double* __restrict__ rv, double w_m, double f_samp,
-                                                          int64_t B, int64_t nb, double* __restrict__ xbar,
-                                                          double* __restrict__ hst, DfmiTrigK tk) {
-  // the row form of ekf_row_kernel (16 lanes per channel, 4 channels per wave, lane-split
-  // sincos: ~1.4x the lane form's rate); these states only seed the trajectory, the passes
-  // re-derive every sample
+                                                          const double* __restrict__ rv,
+                                                          const double* __restrict__ wt,
+                                                          double* __restrict__ hs, double* __restrict__ hst,
+                                                          DfmiTrigK tk) {
+  // the row form of ekf_rot_kernel (16 lanes per channel, 4 channels per wave; sin / cos by
+  // rotation between anchors every 8 samples, ~2x the lane form's rate); these states only
+  // seed the trajectory (the passes re-derive every sample), so a group whose arguments move
+  // too far for the rotation is not rolled back here
   const int lane = threadIdx.x & 63;
   const int64_t r0 = (int64_t)blockIdx.x * 4 + (lane >> 4);
   const bool live = r0 < nrec;
   const int64_t r = live ? r0 : nrec - 1;
   int j = lane & 15;
   if (j > 4) j = 4;
-  const int64_t slots = B * nb;
   double st[5], Pc[5], qv[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
@@ -353,44 +356,52 @@ __global__ __launch_bounds__(64) void ekf_pit_head_kernel(const double* __restri
   const bool writer = live && (lane & 15) == 0;
   const bool odd = lane & 1;
   const RowSplitCoef rc = row_split_coef(tk, odd);
-  RowRegs rr;
+  const RotCoef ro = rot_coef(tk, odd);
+  RotRegs rr;
 #pragma unroll
   for (int i = 0; i < 5; ++i) rr.HP[i] = 0.0;
-  rr.sth = rr.cth = rr.sa = rr.ca = 0.0;
+  rr.sth = rr.cth = rr.sa = rr.ca = rr.thp = rr.argp = rr.sd = rr.cd = 0.0;
+  double dmax = 0.0;
   const double* __restrict__ xr = x + r * rs;
-  // the samples 8 at a time, the next group's loads in flight
-  double xc[8];
+  // the samples 8 at a time (data and ekf_phase_kernel's w_m t_k), the next group's loads in
+  // flight; the predicted state entering each sample goes to hs[r][k][5] (contiguous per
+  // sample; ekf_pit_gather_kernel moves it into the block layout)
+  double xc[8], wc[8];
   const int64_t T8 = T0 & ~(int64_t)7;
   if (T8 > 0) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) xc[u] = xr[u];
+    for (int u = 0; u < 8; ++u) {
+      xc[u] = xr[u];
+      wc[u] = wt[u];
+    }
   }
-  int64_t s = 0, bi = 0, ii = 0;  // slot of sample k: block bi, index ii (no division per sample)
-  auto step = [&](int64_t k, double xk) {
+  double* __restrict__ hr = hs + r * T0 * 5;
+  auto step = [&](auto rot, int64_t k, double xk, double w) {
     if (writer) {
 #pragma unroll
-      for (int c = 0; c < 5; ++c) xbar[(r * 5 + c) * slots + s] = st[c];
+      for (int c = 0; c < 5; ++c) hr[k * 5 + c] = st[c];
     }
-    ekf_row_step<true>(st, Pc, qv, Rv, xk, w_m * ((double)k / f_samp), tk, rr, rc, odd);
-    if (++ii == B) {
-      ii = 0;
-      s = ++bi;
-    } else {
-      s += nb;
-    }
+    ekf_rot_step<decltype(rot)::value>(st, Pc, qv, Rv, xk, w, tk, rr, rc, ro, odd, dmax);
   };
   int64_t k = 0;
   for (; k < T8; k += 8) {
-    double xn[8];
+    double xn[8], wn[8];
     const int64_t kn = k + 8 < T8 ? k + 8 : k;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) xn[u] = xr[kn + u];
+    for (int u = 0; u < 8; ++u) {
+      xn[u] = xr[kn + u];
+      wn[u] = wt[kn + u];
+    }
+    step(std::false_type{}, k, xc[0], wc[0]);  // the anchor
 #pragma unroll
-    for (int u = 0; u < 8; ++u) step(k + u, xc[u]);
+    for (int u = 1; u < 8; ++u) step(std::true_type{}, k + u, xc[u], wc[u]);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) xc[u] = xn[u];
+    for (int u = 0; u < 8; ++u) {
+      xc[u] = xn[u];
+      wc[u] = wn[u];
+    }
   }
-  for (; k < T0; ++k) step(k, xr[k]);
+  for (; k < T0; ++k) step(std::false_type{}, k, xr[k], wt[k]);
   if (writer) {
 #pragma unroll
     for (int c = 0; c < 5; ++c) hst[r * 5 + c] = st[c];
@@ -398,9 +409,10 @@ __global__ __launch_bounds__(64) void ekf_pit_head_kernel(const double* __restri
 }
 
 // Transposes the channel data into blocks, tabulates w_m t_k (ekf_phase_kernel's
-// expression: same bits), sets xbar from sample T0 on to the head's state (hst) and clears
-// the per-channel flags. One thread per (sample slot, channel); grid.y = channel.
+// expression: same bits), sets xbar from the head (its per-sample states below T0, the state
+// entering T0 from there on) and clears the per-channel flags. One thread per (sample slot, channel); grid.y = channel.
 __global__ __launch_bounds__(256) void ekf_pit_gather_kernel(const double* __restrict__ x, int64_t rs, int64_t n,
+                                                             const double* __restrict__ hs,
                                                              const double* __restrict__ hst, int64_t T0, int64_t B,
                                                              int64_t nb, double w_m, double f_samp,
                                                              double* __restrict__ xt, double* __restrict__ wtt,
@@ -420,10 +432,9 @@ __global__ __launch_bounds__(256) void ekf_pit_gather_kernel(const double* __res
   const int64_t k = b * B + i;
   xt[r * slots + s] = k < n ? x[r * rs + k] : 0.0;
   if (r == 0) wtt[s] = w_m * ((double)k / f_samp);
-  if (k >= T0) {
+  const double* src = k < T0 ? hs + (r * T0 + k) * 5 : hst + r * 5;
 #pragma unroll
-    for (int c = 0; c < 5; ++c) xbar[(r * 5 + c) * slots + s] = hst[r * 5 + c];
-  }
+  for (int c = 0; c < 5; ++c) xbar[(r * 5 + c) * slots + s] = src[c];
 }
 
 // Fold one sample's element (h, eps = e - h.b) into the running aggregate (see

@@ -66,7 +66,9 @@ struct Tuning {
   int ekf_pit_min = 4096;     // samples per channel below which the sequential kernels run (crossover
                               // ~3,000 samples: 2,000 0.8x, 4,000 1.45x the row kernel, r04r)
   int ekf_pit_block = 0;      // samples per block (0: ~n nrec^(2/3) / 16384, at least 16)
-  int ekf_pit_passes = 12;    // relinearization passes before a channel falls back to the lane kernel
+  int ekf_pit_passes = 10;    // relinearization passes before a channel falls back to the lane kernel (the
+                              // tests' records converge in 4-6; every pass launched after convergence
+                              // costs ~6-12 us of launches that return at once, r04zg)
   int ekf_pit_head = 256;     // samples the sequential EKF runs first to seed the trajectory (ekf_pit_head_kernel)
   int ekf_pit_fused = 1;      // 1: EKF + fold in one kernel per pass (ekf_pit_pass_kernel); 0: separate kernels
 };
@@ -899,8 +901,8 @@ int moments_dev(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
   return DFMI_OK;
 }
 
-// The EKF parallel in time (ekf_pit.h) for nrec few long channels: gather, then up to
-// ekf_pit_passes x (aggregate, scan, [top scan], blocks, check), the passes of a converged
+// The EKF parallel in time (ekf_pit.h) for nrec long channels: head, gather, the first
+// aggregates and their scan, then up to ekf_pit_passes x (pass kernel, scan hierarchy), the passes of a converged
 // channel returning at once, then the lane-kernel fallback for any channel still moving.
 // wt: ekf_phase_kernel's table (the fallback's). Pass counts stay readable through
 // dfmi_ekf_pit_passes until the next EKF call on this thread.

@@ -66,9 +66,10 @@ struct Tuning {
   int ekf_pit_min = 4096;     // samples per channel below which the sequential kernels run (crossover
                               // ~3,000 samples: 2,000 0.8x, 4,000 1.45x the row kernel, r04r)
   int ekf_pit_block = 0;      // samples per block (0: ~n nrec^(2/3) / 16384, at least 16)
-  int ekf_pit_passes = 10;    // relinearization passes before a channel falls back to the lane kernel (the
-                              // tests' records converge in 4-6; every pass launched after convergence
-                              // costs ~6-12 us of launches that return at once, r04zg)
+  int ekf_pit_passes = 12;    // relinearization passes before a channel falls back to the lane kernel (most
+                              // records converge in 4-6, an init_m = 6 fit of an m = 9, phi = 1.3 record at
+                              // 16-sample blocks took 11; every pass launched after convergence costs
+                              // ~6-12 us of launches that return at once, r04zg)
   int ekf_pit_head = 256;     // samples the sequential EKF runs first to seed the trajectory (ekf_pit_head_kernel)
   int ekf_pit_fused = 1;      // 1: EKF + fold in one kernel per pass (ekf_pit_pass_kernel); 0: separate kernels
 };

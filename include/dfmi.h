@@ -293,7 +293,7 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
  * to this many channels, default 1024; 0 = the sequential kernels always), "ekf_pit_min"
  * (samples per channel below which the sequential kernels run, default 4096),
  * "ekf_pit_block" (samples per block, 0 = ~n nrec^(2/3) / 16384, at least 16), "ekf_pit_passes"
- * (relinearization passes before the lane-kernel fallback, default 10), "ekf_pit_head"
+ * (relinearization passes before the lane-kernel fallback, default 12), "ekf_pit_head"
  * (samples the sequential EKF seeds the trajectory with, default 256), "ekf_pit_fused" (1
  * [default]: the EKF and the next pass's fold in one kernel per pass; 0: separate kernels),
  * "probe" (1 =

@@ -3,7 +3,7 @@ the sequential row kernel (ekf_rot_kernel). Input resident in HBM (dfmi_ekf_fit,
 memory, the bench's call); HIP-event time per call (median of REPS), the passes each
 variant ran and its largest state difference from the sequential kernel. One JSON line.
 
-FUSED: ekf_pit_fused (default 1). PASSES: ekf_pit_passes (default 10). PITMIN: ekf_pit_min for the parallel variants. SECONDS_: record length. VARIANTS: comma list of block:head pairs (ekf_pit_block, 0 = auto; ekf_pit_head samples).
+FUSED: ekf_pit_fused (default 1). PASSES: ekf_pit_passes (default 12). PITMIN: ekf_pit_min for the parallel variants. SECONDS_: record length. VARIANTS: comma list of block:head pairs (ekf_pit_block, 0 = auto; ekf_pit_head samples).
 CHANNELS: channel counts.
 """
 import ctypes
@@ -68,7 +68,7 @@ def main():
         _lib.check(lib.dfmi_set_tuning(b"ekf_pit", 1024), "tune")
         _lib.check(lib.dfmi_set_tuning(b"ekf_pit_min", int(os.environ.get("PITMIN", "32768"))), "tune")
         _lib.check(lib.dfmi_set_tuning(b"ekf_pit_fused", int(os.environ.get("FUSED", "1"))), "tune")
-        _lib.check(lib.dfmi_set_tuning(b"ekf_pit_passes", int(os.environ.get("PASSES", "10"))), "tune")
+        _lib.check(lib.dfmi_set_tuning(b"ekf_pit_passes", int(os.environ.get("PASSES", "12"))), "tune")
         for B, head in variants:
             _lib.check(lib.dfmi_set_tuning(b"ekf_pit_block", B), "tune")
             _lib.check(lib.dfmi_set_tuning(b"ekf_pit_head", head), "tune")
@@ -85,7 +85,7 @@ def main():
         _lib.check(lib.dfmi_set_tuning(b"ekf_pit_head", 256), "tune")
         _lib.check(lib.dfmi_set_tuning(b"ekf_pit", 1024), "tune")
         _lib.check(lib.dfmi_set_tuning(b"ekf_pit_min", 4096), "tune")
-        _lib.check(lib.dfmi_set_tuning(b"ekf_pit_passes", 10), "tune")
+        _lib.check(lib.dfmi_set_tuning(b"ekf_pit_passes", 12), "tune")
         del xe, stt
     print(json.dumps(out))
 

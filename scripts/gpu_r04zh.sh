@@ -1,4 +1,4 @@
-# round 4, call zh: the whole GPU suite, smoke() and the bench line after the pass budget moved to 10
+# round 4, call zh: the whole GPU suite, smoke() and the bench line at the final HEAD
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -v -rP --timeout 300 --timeout-method thread > gpurun_out/r04zh_pytest.log 2>&1

@@ -66,6 +66,11 @@ def parse():
     ap.add_argument("--tune", default="", help="A/B helper: dfmi_set_tuning knobs as key=value[,key=value]")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the extra config keys (config 3, config 5, config 1 sequential) after the timed window")
+    ap.add_argument("--rdzv-timeout", type=float, default=120.0,
+                    help="seconds a rank waits for the others in init_process_group before it fails")
+    ap.add_argument("--launch-timeout", type=float, default=None,
+                    help="seconds the self-launcher (--gpus N without torchrun) waits for its ranks "
+                         "(default: launch_timeout(), from --steps, --warmup and the segments per rank)")
     return ap.parse_args()
 
 
@@ -243,22 +248,69 @@ def free_port():
         return sk.getsockname()[1]
 
 
+def launch_timeout(args, world):
+    """Wall-clock bound of a self-launched N-rank job: process start-up and imports (180 s),
+    the rendezvous (--rdzv-timeout), the CPU baseline leg (rank 0 only at N = 1: not here),
+    input generation and the timed / side windows at a generous 100 ns per segment per step
+    (the measured step is ~5 ns per segment: BENCH_r04) plus the extra configs (300 s)."""
+    nseg = args.segments if args.segments is not None else CONFIG4_SEGMENTS // max(world, 1)
+    steps = args.steps + args.warmup + max(200, args.steps) + 40
+    return 180.0 + args.rdzv_timeout + steps * nseg * 1e-7 + (0.0 if args.no_extra else 300.0)
+
+
+def join_group(dist, backend, dev, timeout_s):
+    """init_process_group with a bounded rendezvous: a rank that does not arrive within
+    timeout_s makes the others raise instead of waiting forever (then self_launch reports
+    which rank never arrived: every rank leaves a marker in DFMI_RDZV_DIR when it reaches the
+    rendezvous and another when it has joined).
+    DFMI_RDZV_DELAY="rank:seconds" delays that rank before it joins (test hook:
+    tests/test_bench_launch.py)."""
+    from datetime import timedelta
+    rank = int(os.environ.get("RANK", "0"))
+    delay = os.environ.get("DFMI_RDZV_DELAY", "")
+    if delay:
+        r, sec = delay.split(":")
+        if int(r) == rank:
+            time.sleep(float(sec))
+    mark = os.environ.get("DFMI_RDZV_DIR")
+
+    def stamp(what):
+        if mark:
+            with open(os.path.join(mark, f"rank{rank}.{what}"), "w") as f:
+                f.write(str(os.getpid()))
+    stamp("arrived")
+    kw = {"timeout": timedelta(seconds=timeout_s)}
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev, **kw)
+    else:
+        dist.init_process_group(backend, **kw)
+    stamp("joined")
+
+
 def self_launch(n, argv, script=None, env_extra=None, timeout=None):
     """`python bench.py --gpus N` without torchrun: start N rank processes, one per GPU
     (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), BEFORE this process
     touches any GPU, wait for all of them and return the worst exit code. The reference's
     parallel width is likewise an explicit argument (n_cores -> Pool(n_cores),
-    fitters.py:397-399,416-423). Rank 0 prints the JSON line; a rank that fails takes the
-    others down with it."""
+    fitters.py:397-399,416-423), and its Pool context manager propagates a worker's failure
+    (fitters.py:421-423): here rank 0 prints the JSON line; a rank that fails takes the
+    others down with it; past `timeout` seconds every rank is killed (exit 124). On any
+    failure the ranks that never reached the rendezvous (no marker, join_group) are named
+    on stderr."""
+    import shutil
     import subprocess
+    import tempfile
     port = str(free_port())
+    mark = tempfile.mkdtemp(prefix="dfmi_rdzv_")
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port, DFMI_SELF_LAUNCHED="1", **(env_extra or {}))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port, DFMI_SELF_LAUNCHED="1", DFMI_RDZV_DIR=mark,
+                   **(env_extra or {}))
         procs.append(subprocess.Popen([sys.executable, "-u", script or os.path.abspath(__file__)] + list(argv), env=env,
                                       stdout=None if r == 0 else subprocess.DEVNULL))
     rc = 0
+    why = ""
     t_end = None if timeout is None else time.monotonic() + timeout
     try:
         pending = list(procs)
@@ -269,10 +321,14 @@ def self_launch(n, argv, script=None, env_extra=None, timeout=None):
                     continue
                 pending.remove(p)
                 if code != 0:
+                    if not rc:
+                        why = f"rank {procs.index(p)} exited with {code}"
                     rc = rc or code
                     for q in pending:  # one rank failed: the barrier would hang the others
                         q.terminate()
-            if t_end is not None and time.monotonic() > t_end:
+            if t_end is not None and time.monotonic() > t_end and pending:
+                if not rc:
+                    why = f"launch timeout {timeout:.0f} s"
                 rc = rc or 124
                 for q in pending:
                     q.kill()
@@ -283,6 +339,12 @@ def self_launch(n, argv, script=None, env_extra=None, timeout=None):
             if p.poll() is None:
                 p.kill()
             p.wait()
+        if rc:
+            def without(what):
+                return [r for r in range(n) if not os.path.exists(os.path.join(mark, f"rank{r}.{what}"))]
+            print(f"bench: {n}-rank job failed ({why}); ranks that never reached the rendezvous: {without('arrived')}; "
+                  f"ranks that did not complete it: {without('joined')}", file=sys.stderr, flush=True)
+        shutil.rmtree(mark, ignore_errors=True)
     return rc
 
 
@@ -558,7 +620,8 @@ def main():
         raise SystemExit("--gpus must be >= 1")
     if "WORLD_SIZE" not in os.environ:
         if args.gpus > 1:  # no torchrun: one rank process per GPU, launched here before any GPU call
-            return self_launch(args.gpus, sys.argv[1:])
+            t = args.launch_timeout if args.launch_timeout is not None else launch_timeout(args, args.gpus)
+            return self_launch(args.gpus, sys.argv[1:], timeout=t)
     elif int(os.environ["WORLD_SIZE"]) != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}: the launcher and the "
                          "flag disagree")
@@ -581,11 +644,7 @@ def main():
     if world > 1:
         # RCCL; DFMI_DIST_BACKEND=gloo rehearses N ranks that share one card (RCCL
         # refuses two ranks on one device)
-        backend = os.environ.get("DFMI_DIST_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+        join_group(dist, os.environ.get("DFMI_DIST_BACKEND", "nccl"), dev, args.rdzv_timeout)
 
     ranks, backend = rank_topology(dist, dev, world)
     if world > 1 and len({(r["host"], r.get("pci_bus_id"), r["device"]) for r in ranks}) < world \

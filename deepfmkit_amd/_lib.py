@@ -7,7 +7,9 @@ is missing, every compute call raises DFMIError.
 from __future__ import annotations
 
 import ctypes
+import importlib.util
 import os
+import sys
 import threading
 
 import numpy as np
@@ -25,7 +27,8 @@ SYMBOLS = ("dfmi_lm_config_default", "dfmi_demod", "dfmi_lm", "dfmi_nls_record",
            "dfmi_probe_read", "dfmi_get_tuning", "dfmi_txt_parse_header", "dfmi_txt_shape", "dfmi_txt_read",
            "dfmi_fit_txt_write", "dfmi_py_repr", "dfmi_txt_last_error", "dfmi_wdfmi_fit", "dfmi_ekf_fit",
            "dfmi_record_moments", "dfmi_synth_asd", "dfmi_synth_snr", "dfmi_bessel_eval",
-           "dfmi_release_workspaces", "dfmi_step_timing", "dfmi_step_timing_read", "dfmi_ekf_pit_passes")
+           "dfmi_release_workspaces", "dfmi_step_timing", "dfmi_step_timing_read", "dfmi_ekf_pit_passes",
+           "dfmi_ekf_pit_trace")
 
 
 class DFMIError(RuntimeError):
@@ -89,6 +92,54 @@ WDFMI_METHODS = {"wdfmi_nls": 0, "wdfmi_ortho": 1, "wdfmi_seq": 2, "hwdfmi": 3}
 
 _lock = threading.Lock()
 _lib = None
+RUNTIME = None  # the HIP runtime file libdfmi.so was bound to (set by load())
+
+
+def _torch_hip_runtime():
+    """Path of the HIP runtime PyTorch ships (torch/lib/libamdhip64.so), found WITHOUT
+    importing torch; None when torch is absent or is not a ROCm build."""
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return None
+    if spec is None or not spec.origin:
+        return None
+    p = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    return p if os.path.exists(p) else None
+
+
+def _bind_runtime():
+    """Pick the HIP runtime libdfmi.so binds to, before loading it.
+
+    libdfmi.so needs libamdhip64.so.7 (RUNPATH /opt/rocm/lib). PyTorch-ROCm ships its own copy
+    (torch/lib/libamdhip64.so, same soname) and its libraries ask for it by the unversioned
+    name, so if libdfmi.so is loaded first and torch imported later, the process maps TWO HIP
+    and two HSA runtimes (/proc/self/maps), both driving /dev/kfd: whichever initialises first
+    holds the device and the other reports no GPU (r04za: torch.cuda.is_available() False
+    after a host-memory EKF call). One runtime per process is the fix:
+      - torch already imported: its runtime is mapped and the soname match binds to it;
+      - torch installed but not imported: torch's runtime FILE is loaded by path (torch itself
+        is not imported: no import cost, no import failure), libdfmi.so binds to it by soname,
+        and a later `import torch` finds the same file already mapped (glibc matches it by
+        device and inode) instead of mapping a second runtime;
+      - no torch, or DFMI_HIP_RUNTIME=system: the system runtime /opt/rocm/lib (what the
+        numpy + ctypes binding of INTEGRATION.md §B gets).
+    Returns the path of the runtime file that will be used, or None for the system one."""
+    global RUNTIME
+    if os.environ.get("DFMI_HIP_RUNTIME", "") == "system":
+        return None
+    if "torch" in sys.modules:
+        RUNTIME = _torch_hip_runtime()
+        return RUNTIME
+    p = _torch_hip_runtime()
+    if p is None:
+        return None
+    try:
+        ctypes.CDLL(p)
+    except OSError:
+        return None
+    RUNTIME = p
+    return p
 
 
 def load():
@@ -99,14 +150,7 @@ def load():
             return _lib
         if not os.path.exists(LIB_PATH):
             raise DFMIError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
-        # PyTorch first when it is installed: the library then binds to the HIP runtime torch
-        # loaded. Loaded the other way round and initialised by a host-memory call, the
-        # library's runtime held the device and torch.cuda.is_available() turned False in that
-        # process (scripts/probe_init_order.py, r04za).
-        try:
-            import torch  # noqa: F401
-        except ImportError:
-            pass
+        _bind_runtime()
         lib = ctypes.CDLL(LIB_PATH)
         P = ctypes.c_void_p
         i64, i32, dbl = ctypes.c_int64, ctypes.c_int32, ctypes.c_double
@@ -125,6 +169,8 @@ def load():
         lib.dfmi_ekf_fit.restype = ctypes.c_int
         lib.dfmi_ekf_pit_passes.argtypes = [P, i64]
         lib.dfmi_ekf_pit_passes.restype = ctypes.c_int
+        lib.dfmi_ekf_pit_trace.argtypes = [P, i64, i32]
+        lib.dfmi_ekf_pit_trace.restype = ctypes.c_int
         lib.dfmi_record_moments.argtypes = [P, i64, i64, i64, P, P, i32, P]
         lib.dfmi_record_moments.restype = ctypes.c_int
         lib.dfmi_synth_asd.argtypes = [P, i64, i64, dbl, P, i32, P]

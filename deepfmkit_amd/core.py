@@ -221,6 +221,7 @@ class DeepFitFramework:
 
     def fit(self, main_label, method="nls", fit_label=None, **kwargs):
         """core.py:424-517: strategy dispatch -> DataFrame -> DeepFitObject."""
+        _fitters.mark("fit")
         fitter_map = _fitters.FITTER_MAP
         if method not in fitter_map:
             log.error(f"Unknown fit method: '{method}'. Available: {list(fitter_map.keys())}")
@@ -252,6 +253,7 @@ class DeepFitFramework:
     def _finish(self, fit_label, main_label, raw, method, df, n, R, fs, nbuf):
         if method in ("nls", "ekf"):
             df["tau"] = df["m"] / (2 * np.pi * raw.sim.laser.df) if raw.sim else 0.0
+        _fitters.mark("tau")
         self.fits_df[fit_label] = df
         fit = DeepFitObject()
         # core.py:511-514 records ndata/init_a/init_m as 0 in the fit object
@@ -259,9 +261,11 @@ class DeepFitFramework:
         fit.t0, fit.f_samp, fit.f_mod = raw.t0, raw.f_samp, raw.f_mod
         for k in ("ssq", "amp", "m", "tau", "phi", "psi", "dc"):
             setattr(fit, k, df[k].to_numpy())
+        _fitters.mark("columns")
         fit.time = np.arange(0, fit.ssq.shape[0] / fit.fs, 1.0 / fit.fs)
         fit.label = fit_label
         self.fits[fit_label] = fit
+        _fitters.mark("fitobj")
         return fit
 
     def fit_many(self, labels, method="nls", **kwargs):

@@ -66,10 +66,17 @@ struct Tuning {
   int ekf_pit_min = 4096;     // samples per channel below which the sequential kernels run (crossover
                               // ~3,000 samples: 2,000 0.8x, 4,000 1.45x the row kernel, r04r)
   int ekf_pit_block = 0;      // samples per block (0: ~n nrec^(2/3) / 16384, at least 16)
-  int ekf_pit_passes = 12;    // relinearization passes before a channel falls back to the lane kernel (most
-                              // records converge in 4-6, an init_m = 6 fit of an m = 9, phi = 1.3 record at
-                              // 16-sample blocks took 11; every pass launched after convergence costs
-                              // ~6-12 us of launches that return at once, r04zg)
+  int ekf_pit_passes = 48;    // pass cap: a channel still passing then goes to the sequential kernel (a
+                              // pass of one 400k-sample channel is ~0.06 ms, the sequential kernel ~68 ms)
+  int ekf_pit_first = 5;      // passes enqueued before the host first reads how many channels still pass
+                              // (then every ekf_pit_every); config 5's record converges in 5
+  int ekf_pit_every = 2;
+  int ekf_pit_tol = 13;       // stop rule: distance from the fixed point bounded by 10^-ekf_pit_tol (pit_decide)
+  int ekf_pit_stall = 3;      // passes in a row not contracting fast enough to meet the bound within the cap
+                              // before the sequential kernel (pit_decide)
+  int ekf_pit_trace = 0;      // 1: record every pass's move per channel (dfmi_ekf_pit_trace)
+  int ekf_pit_seq = 1;        // 0 (diagnostics only): leave an unconverged channel's last pass in place
+  int ekf_pit_measure = 0;    // the stop rule's move: 0 the output snapshots, 1 (diagnostics) the block entries
   int ekf_pit_head = 256;     // samples the sequential EKF runs first to seed the trajectory (ekf_pit_head_kernel)
   int ekf_pit_fused = 1;      // 1: EKF + fold in one kernel per pass (ekf_pit_pass_kernel); 0: separate kernels
 };
@@ -142,6 +149,8 @@ struct DeviceState {
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::array<hipEvent_t, 3>> ev_steps;
+  void* pin = nullptr;  // pinned host scratch for the EKF's pass control read-backs
+  size_t pin_n = 0;
 };
 
 std::map<int, DeviceState> g_dev;
@@ -885,6 +894,13 @@ const std::map<std::string, Knob>& knobs() {
       {"ekf_pit_min", {&Tuning::ekf_pit_min, {}}},
       {"ekf_pit_block", {&Tuning::ekf_pit_block, {}}},
       {"ekf_pit_passes", {&Tuning::ekf_pit_passes, {}}},
+      {"ekf_pit_first", {&Tuning::ekf_pit_first, {}}},
+      {"ekf_pit_every", {&Tuning::ekf_pit_every, {}}},
+      {"ekf_pit_tol", {&Tuning::ekf_pit_tol, {}}},
+      {"ekf_pit_stall", {&Tuning::ekf_pit_stall, {}}},
+      {"ekf_pit_trace", {&Tuning::ekf_pit_trace, {0, 1}}},
+      {"ekf_pit_seq", {&Tuning::ekf_pit_seq, {0, 1}}},
+      {"ekf_pit_measure", {&Tuning::ekf_pit_measure, {0, 1}}},
       {"ekf_pit_head", {&Tuning::ekf_pit_head, {}}},
       {"ekf_pit_fused", {&Tuning::ekf_pit_fused, {0, 1}}}};
   return k;
@@ -902,15 +918,64 @@ int moments_dev(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
   return DFMI_OK;
 }
 
-// The EKF parallel in time (ekf_pit.h) for nrec long channels: head, gather, the first
-// aggregates and their scan, then up to ekf_pit_passes x (pass kernel, scan hierarchy), the passes of a converged
-// channel returning at once, then the lane-kernel fallback for any channel still moving.
-// wt: ekf_phase_kernel's table (the fallback's). Pass counts stay readable through
-// dfmi_ekf_pit_passes until the next EKF call on this thread.
-thread_local int64_t g_pit_nrec = 0;
-thread_local int* g_pit_flag = nullptr;
-constexpr double kPitTol = 1e-11;  // relative move of xbar at which a channel is converged
+// Pass counts (and, with ekf_pit_trace, every pass's move) of the last EKF call on this
+// thread, copied to the host at the end of that call: dfmi_ekf_pit_passes /
+// dfmi_ekf_pit_trace read these, never a device workspace.
+thread_local std::vector<int32_t> g_pit_passes;
+thread_local std::vector<double> g_pit_hist;
+thread_local int g_pit_hist_n = 0;
+constexpr int kPitNoMem = 1;  // ekf_pit_run: a workspace could not be allocated (nothing launched)
 
+// Pinned host scratch of the current device (grow-only).
+int pinned(size_t bytes, void** out) {
+  DeviceState& ds = *t_ds;
+  if (ds.pin_n < bytes) {
+    if (ds.pin) HIPCHK(hipHostFree(ds.pin));
+    ds.pin = nullptr;
+    ds.pin_n = 0;
+    HIPCHK(hipHostMalloc(&ds.pin, bytes, hipHostMallocDefault));
+    ds.pin_n = bytes;
+  }
+  *out = ds.pin;
+  return DFMI_OK;
+}
+
+// The sequential EKF kernels over nrec channels (device pointers): few channels one 16-lane
+// row each (ekf_rot_kernel with sin / cos by rotation between anchors when R % 4 == 0, else
+// ekf_row_kernel, ~1.7x the per-channel rate), many one lane each (ekf_lane_rot_kernel /
+// ekf_kernel, 16x the channels per instruction). Returns the variant's name in *name.
+int ekf_seq_launch(const double* dx, int64_t nrec, int64_t rs, int64_t n, const double* dx0, const double* dp0,
+                   const double* dq, const double* dr, const double* wt, int32_t R, int64_t nbuf, double* dstates,
+                   hipStream_t st, const char** name) {
+  const int block = 64;
+  const bool row = t_tune.ekf_row && nrec <= (int64_t)t_tune.ekf_row * t_ds->n_cu * 16;
+  const int64_t grid = row ? (nrec + 3) / 4 : (nrec + block - 1) / block;
+  // rotation between anchors: groups of 16 (8, 4) samples whose ends carry the snapshots
+  const bool rot = t_tune.ekf_rot && R % 4 == 0;
+  using EK = void (*)(const double*, int64_t, int64_t, int64_t, const double*, const double*, const double*,
+                      const double*, const double*, int, int64_t, double*, DfmiTrigK);
+  EK ek;
+  if (row)
+    ek = !rot ? dfmi::ekf_row_kernel<DFMI_EKF_SPLIT != 0>
+         : R % DFMI_EKF_ROT_G == 0 ? dfmi::ekf_rot_kernel<DFMI_EKF_ROT_G>
+         : R % 8 == 0              ? dfmi::ekf_rot_kernel<8>
+                                   : dfmi::ekf_rot_kernel<4>;
+  else
+    ek = !rot ? dfmi::ekf_kernel : R % 8 == 0 ? dfmi::ekf_lane_rot_kernel<8> : dfmi::ekf_lane_rot_kernel<4>;
+  hipLaunchKernelGGL(ek, dim3((unsigned)grid), dim3(block), 0, st, dx, nrec, rs, n, dx0, dp0, dq, dr, wt, (int)R, nbuf,
+                     dstates, dfmi_trig_k());
+  HIPCHK(hipGetLastError());
+  *name = row ? (rot ? "ekf_rot_kernel" : "ekf_row_kernel") : (rot ? "ekf_lane_rot_kernel" : "ekf_kernel");
+  return DFMI_OK;
+}
+
+// The EKF parallel in time (ekf_pit.h) for nrec long channels: head, gather, the first
+// aggregates and their scan, then passes (pass kernel + scan hierarchy), a converged
+// channel's kernels returning at once. The host reads the number of channels still passing
+// after ekf_pit_first passes and then every ekf_pit_every (one stream sync each) and stops at
+// zero or at the cap ekf_pit_passes; the channels that stopped contracting or hit the cap are
+// re-run by the sequential kernel. wt: ekf_phase_kernel's table (the sequential kernel's).
+// Returns kPitNoMem, with nothing launched, when a workspace cannot be allocated.
 int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, const double* dx0, const double* dp0,
                 const double* dq, const double* dr, const double* wt, double w_m, double f_samp, int32_t R,
                 int64_t nbuf, double* dstates, hipStream_t st) {
@@ -927,34 +992,56 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
   std::vector<int64_t> lsz = {nb};
   while (lsz.back() > dfmi::kPitWg) lsz.push_back((lsz.back() + dfmi::kPitWg - 1) / dfmi::kPitWg);
   const int L = (int)lsz.size() - 1;
-  void *xt, *wtt, *xbar, *conv, *flag, *hst;
-  std::vector<double*> lv[2];  // per aggregate buffer: level arrays [r][65][lsz[l]]
-  int rc;
   const int64_t T0 = std::min<int64_t>(std::max(t_tune.ekf_pit_head, 0), n);
-  if ((rc = workspace(dev, "p_xt", (size_t)(nrec * slots) * 8, &xt))) return rc;
-  if ((rc = workspace(dev, "p_wt", (size_t)slots * 8, &wtt))) return rc;
-  if ((rc = workspace(dev, "p_xbar", (size_t)(nrec * 5 * slots) * 8, &xbar))) return rc;
-  for (int bf = 0; bf < 2; ++bf)
-    for (int l = 0; l <= L; ++l) {
-      void* a;
-      const std::string name = "p_lv" + std::to_string(bf) + "_" + std::to_string(l);
-      if ((rc = workspace(dev, name.c_str(), (size_t)(nrec * dfmi::kPitEl * lsz[l]) * 8, &a))) return rc;
-      lv[bf].push_back((double*)a);
+  const int hist_n = t_tune.ekf_pit_trace ? std::max(t_tune.ekf_pit_passes, 1) : 0;
+  void *xt, *wtt, *xbar, *conv, *chan, *hst, *done, *hs, *ent = nullptr, *hist = nullptr, *pin;
+  std::vector<double*> lv[2];  // per aggregate buffer: level arrays [r][65][lsz[l]]
+  // every allocation before the first launch: a failure leaves the sequential kernels to run
+  {
+    int rc = 0;
+    auto ws = [&](const char* name, size_t bytes, void** p) {
+      if (!rc) rc = workspace(dev, name, bytes, p);
+    };
+    ws("p_xt", (size_t)(nrec * slots) * 8, &xt);
+    ws("p_wt", (size_t)slots * 8, &wtt);
+    ws("p_xbar", (size_t)(nrec * 5 * slots) * 8, &xbar);
+    for (int bf = 0; bf < 2 && !rc; ++bf)
+      for (int l = 0; l <= L && !rc; ++l) {
+        void* a = nullptr;
+        const std::string name = "p_lv" + std::to_string(bf) + "_" + std::to_string(l);
+        ws(name.c_str(), (size_t)(nrec * dfmi::kPitEl * lsz[l]) * 8, &a);
+        lv[bf].push_back((double*)a);
+      }
+    ws("p_conv", (size_t)nrec * 8, &conv);
+    ws("p_chan", (size_t)nrec * sizeof(dfmi::PitChan), &chan);
+    ws("p_hst", (size_t)(nrec * 5) * 8, &hst);
+    ws("p_done", (size_t)nrec * sizeof(unsigned), &done);
+    ws("p_hs", (size_t)(nrec * (T0 > 0 ? T0 : 1) * 5) * 8, &hs);
+    if (t_tune.ekf_pit_fused && t_tune.ekf_pit_measure == 1) ws("p_ent", (size_t)(nrec * 5 * nb) * 8, &ent);
+    if (hist_n) ws("p_hist", (size_t)nrec * hist_n * 8, &hist);
+    if (!rc) rc = pinned((size_t)nrec * sizeof(dfmi::PitChan) + 64, &pin);
+    if (rc) {
+      (void)hipGetLastError();  // clear the failed allocation
+      g_err.clear();
+      return kPitNoMem;
     }
-  if ((rc = workspace(dev, "p_conv", (size_t)nrec * 8, &conv))) return rc;
-  if ((rc = workspace(dev, "p_flag", (size_t)(nrec * 2) * sizeof(int), &flag))) return rc;
-  if ((rc = workspace(dev, "p_hst", (size_t)(nrec * 5) * 8, &hst))) return rc;
-  void* done;
-  if ((rc = workspace(dev, "p_done", (size_t)nrec * sizeof(unsigned), &done))) return rc;
+  }
+  dfmi::PitChan* ch = (dfmi::PitChan*)chan;
   const DfmiTrigK tk = dfmi_trig_k();
   const unsigned nr = (unsigned)nrec;
-  void* hs;
-  if ((rc = workspace(dev, "p_hs", (size_t)(nrec * (T0 > 0 ? T0 : 1) * 5) * 8, &hs))) return rc;
+  dfmi::PitRule rule;
+  rule.tol = std::pow(10.0, -(double)t_tune.ekf_pit_tol);
+  rule.noise = rule.tol;
+  rule.stall_max = std::max(t_tune.ekf_pit_stall, 1);
+  rule.cap = std::max(t_tune.ekf_pit_passes, 1);
+  rule.hist_n = hist_n;
+  rule.measure = t_tune.ekf_pit_measure;
+  if (hist_n) HIPCHK(hipMemsetAsync(hist, 0xFF, (size_t)nrec * hist_n * 8, st));  // NaN: pass not run
   hipLaunchKernelGGL(dfmi::ekf_pit_head_kernel, dim3((unsigned)((nrec + 3) / 4)), dim3(64), 0, st, dx, nrec, rs, T0,
                      dx0, dp0, dq, dr, wt, (double*)hs, (double*)hst, tk);
   hipLaunchKernelGGL(dfmi::ekf_pit_gather_kernel, dim3((unsigned)((slots + 255) / 256), nr), dim3(256), 0, st, dx, rs,
                      n, (const double*)hs, (const double*)hst, T0, B, nb, w_m, f_samp, (double*)xt, (double*)wtt,
-                     (double*)xbar, (int*)flag, (double*)conv, (unsigned*)done);
+                     (double*)xbar, ch, (double*)conv, (unsigned*)done);
   const dim3 lanes((unsigned)((nb + 63) / 64), nr);
   // scan of one buffer's hierarchy: every level bottom-up, then the fix-ups top-down; the
   // pass kernels read level 0 (prefixes within workgroups) and level 1 (true prefixes)
@@ -962,54 +1049,103 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
     for (int l = 0; l <= L; ++l)
       hipLaunchKernelGGL(dfmi::ekf_pit_scan_kernel<dfmi::kPitWg>,
                          dim3((unsigned)((lsz[l] + dfmi::kPitWg - 1) / dfmi::kPitWg), nr), dim3(4 * dfmi::kPitWg), 0,
-                         st, a[l], lsz[l], lsz[l], l < L ? a[l + 1] : nullptr, (const int*)flag);
+                         st, a[l], lsz[l], lsz[l], l < L ? a[l + 1] : nullptr, (const dfmi::PitChan*)ch);
     for (int l = L - 1; l >= 1; --l)
       if (lsz[l] > dfmi::kPitWg)
         hipLaunchKernelGGL(dfmi::ekf_pit_fixup_kernel, dim3((unsigned)((lsz[l] - dfmi::kPitWg + 63) / 64), nr), dim3(64),
-                           0, st, a[l], lsz[l], (const double*)a[l + 1], lsz[l + 1], (const int*)flag);
+                           0, st, a[l], lsz[l], (const double*)a[l + 1], lsz[l + 1], (const dfmi::PitChan*)ch);
   };
-  const double* top0 = L >= 1 ? lv[0][1] : nullptr;
-  const double* top1 = L >= 1 ? lv[1][1] : nullptr;
-  auto check = [&]() {
-    hipLaunchKernelGGL(dfmi::ekf_pit_check_kernel, dim3((unsigned)((nrec + 63) / 64)), dim3(64), 0, st,
-                       (double*)conv, nrec, kPitTol, (int*)flag);
-  };
+  const double* tops[2] = {L >= 1 ? lv[0][1] : nullptr, L >= 1 ? lv[1][1] : nullptr};
+  const int cap = std::max(t_tune.ekf_pit_passes, 1);
+  const int every = std::max(t_tune.ekf_pit_every, 1);
+  int next_check = std::min(std::max(t_tune.ekf_pit_first, 1), cap);
   if (t_tune.ekf_pit_fused) {
     // first aggregates at the seeded trajectory, then per pass: EKF + fold (ekf_pit_pass_kernel,
-    // aggregates into the other buffer), check, scan of the new aggregates
-    void* ent;
-    if ((rc = workspace(dev, "p_ent", (size_t)(nrec * 5 * nb) * 8, &ent))) return rc;
-    HIPCHK(hipMemsetAsync(ent, 0xFF, (size_t)(nrec * 5 * nb) * 8, st));  // NaN: no previous entry
-    const double* tops[2] = {top0, top1};
+    // aggregates into the other buffer, the stop rule by its last workgroup per channel), scan
+    // of the new aggregates
+    if (ent) HIPCHK(hipMemsetAsync(ent, 0xFF, (size_t)(nrec * 5 * nb) * 8, st));  // NaN: no previous entry
     hipLaunchKernelGGL(dfmi::ekf_pit_aggregate_kernel, lanes, dim3(64), 0, st, (const double*)xt, (const double*)wtt,
-                       (const double*)xbar, n, B, nb, dx0, dp0, dq, dr, (const int*)flag, lv[0][0], tk);
+                       (const double*)xbar, n, B, nb, dx0, dp0, dq, dr, (const dfmi::PitChan*)ch, lv[0][0], tk);
     scan(lv[0]);
-    int cur = 0;
-    for (int pass = 0; pass < t_tune.ekf_pit_passes; ++pass, cur ^= 1) {
+  }
+  int cur = 0;
+  bool fresh = false;  // pin holds the channels' final control blocks
+  for (int pass = 1;; ++pass) {
+    if (t_tune.ekf_pit_fused) {
       hipLaunchKernelGGL(dfmi::ekf_pit_pass_kernel, lanes, dim3(64), 0, st, (const double*)xt, (const double*)wtt, n,
-                         B, nb, dx0, dp0, dq, dr, (const double*)lv[cur][0], tops[cur], lv[cur ^ 1][0],
-                         (double*)ent, (int*)flag, (double*)conv, (unsigned*)done, kPitTol, (int)R, nbuf, dstates,
-                         tk);
-      if (pass + 1 < t_tune.ekf_pit_passes) scan(lv[cur ^ 1]);
-    }
-  } else {
-    for (int pass = 0; pass < t_tune.ekf_pit_passes; ++pass) {
+                         B, nb, dx0, dp0, dq, dr, (const double*)lv[cur][0], tops[cur], lv[cur ^ 1][0], (double*)ent,
+                         ch, (double*)conv, (unsigned*)done, rule, (double*)hist, (int)R, nbuf,
+                         dstates, tk);
+    } else {
       hipLaunchKernelGGL(dfmi::ekf_pit_aggregate_kernel, lanes, dim3(64), 0, st, (const double*)xt,
-                         (const double*)wtt, (const double*)xbar, n, B, nb, dx0, dp0, dq, dr, (const int*)flag,
-                         lv[0][0], tk);
+                         (const double*)wtt, (const double*)xbar, n, B, nb, dx0, dp0, dq, dr,
+                         (const dfmi::PitChan*)ch, lv[0][0], tk);
       scan(lv[0]);
       hipLaunchKernelGGL(dfmi::ekf_pit_blocks_kernel, lanes, dim3(64), 0, st, (const double*)xt, (const double*)wtt,
-                         (double*)xbar, n, B, nb, dx0, dp0, dq, dr, (const double*)lv[0][0], top0, (const int*)flag,
-                         (double*)conv, (int)R, nbuf, dstates, tk);
-      check();
+                         (double*)xbar, n, B, nb, dx0, dp0, dq, dr, (const double*)lv[0][0], tops[0],
+                         (const dfmi::PitChan*)ch, (double*)conv, (int)R, nbuf, dstates, rule.measure, tk);
+      hipLaunchKernelGGL(dfmi::ekf_pit_check_kernel, dim3((unsigned)((nrec + 63) / 64)), dim3(64), 0, st,
+                         (double*)conv, nrec, rule, ch, (double*)hist);
+    }
+    HIPCHK(hipGetLastError());
+    if (pass >= cap) break;
+    if (pass == next_check) {
+      // the channels' control blocks to the host (one copy, one stream sync): the check and,
+      // when no channel is left passing, the outcome below
+      HIPCHK(hipMemcpyAsync(pin, ch, (size_t)nrec * sizeof(dfmi::PitChan), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      const dfmi::PitChan* hc = (const dfmi::PitChan*)pin;
+      bool any = false;
+      for (int64_t r = 0; r < nrec && !any; ++r) any = hc[r].status == 0;
+      if (!any) {
+        fresh = true;
+        break;
+      }
+      next_check = std::min(pass + every, cap);
+    }
+    if (t_tune.ekf_pit_fused) {
+      scan(lv[cur ^ 1]);
+      cur ^= 1;
     }
   }
-  hipLaunchKernelGGL(dfmi::ekf_pit_fallback_kernel, dim3((unsigned)((nrec + 63) / 64)), dim3(64), 0, st, dx, nrec,
-                     rs, n, dx0, dp0, dq, dr, wt, (int)R, nbuf, dstates, (int*)flag, tk);
-  HIPCHK(hipGetLastError());
+  // the channels' outcomes on the host; the ones not converged go to the sequential kernel
+  if (!fresh) HIPCHK(hipMemcpyAsync(pin, ch, (size_t)nrec * sizeof(dfmi::PitChan), hipMemcpyDeviceToHost, st));
+  if (hist_n) {
+    g_pit_hist.assign((size_t)nrec * hist_n, 0.0);
+    HIPCHK(hipMemcpyAsync(g_pit_hist.data(), hist, g_pit_hist.size() * 8, hipMemcpyDeviceToHost, st));
+    g_pit_hist_n = hist_n;
+  }
+  if (!fresh || hist_n) HIPCHK(hipStreamSynchronize(st));
+  const dfmi::PitChan* hc = (const dfmi::PitChan*)pin;
+  std::vector<int> seq;
+  g_pit_passes.assign((size_t)nrec, 0);
+  for (int64_t r = 0; r < nrec; ++r) {
+    g_pit_passes[r] = hc[r].status == 1 ? hc[r].passes : -hc[r].passes;
+    if (hc[r].status != 1) seq.push_back((int)r);
+  }
   g_last_demod = "ekf_pit (B=" + std::to_string(B) + ", nb=" + std::to_string(nb) + ")";
-  g_pit_nrec = nrec;
-  g_pit_flag = (int*)flag;
+  if (!seq.empty() && t_tune.ekf_pit_seq) {
+    const int64_t ns = (int64_t)seq.size();
+    void *idx, *xs, *x0s, *rvs, *ss;
+    int rc;
+    if ((rc = workspace(dev, "p_sidx", (size_t)ns * sizeof(int), &idx))) return rc;
+    if ((rc = workspace(dev, "p_sx", (size_t)(ns * n) * 8, &xs))) return rc;
+    if ((rc = workspace(dev, "p_sx0", (size_t)ns * 5 * 8, &x0s))) return rc;
+    if ((rc = workspace(dev, "p_srv", (size_t)ns * 8, &rvs))) return rc;
+    if ((rc = workspace(dev, "p_sst", (size_t)(ns * (nbuf > 0 ? nbuf : 1) * 5) * 8, &ss))) return rc;
+    HIPCHK(hipMemcpy(idx, seq.data(), (size_t)ns * sizeof(int), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(dfmi::ekf_pit_pick_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)ns), dim3(256), 0, st,
+                       dx, rs, n, dx0, dr, (const int*)idx, (double*)xs, (double*)x0s, (double*)rvs);
+    const char* kname;
+    if ((rc = ekf_seq_launch((const double*)xs, ns, n, n, (const double*)x0s, dp0, dq, (const double*)rvs, wt, R, nbuf,
+                             (double*)ss, st, &kname)))
+      return rc;
+    if (nbuf > 0)
+      hipLaunchKernelGGL(dfmi::ekf_pit_put_kernel, dim3((unsigned)((nbuf * 5 + 255) / 256), (unsigned)ns), dim3(256),
+                         0, st, (const double*)ss, nbuf, (const int*)idx, dstates);
+    HIPCHK(hipGetLastError());
+    g_last_demod += std::string(" + ") + kname + " x" + std::to_string(ns);
+  }
   return DFMI_OK;
 }
 
@@ -1023,6 +1159,9 @@ int ekf_impl(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
   if (nrec < 0 || n_samp < 0 || R <= 0 || nbuf < 0) return fail(DFMI_ERR_ARG, "bad ekf geometry");
   if (nrec > 1 && rec_stride < n_samp) return fail(DFMI_ERR_ARG, "rec_stride < n_samp");
   if (init4 && n_samp > INT32_MAX) return fail(DFMI_ERR_ARG, "n_samp >= 2^31");
+  g_pit_passes.clear();  // this call's outcome replaces the last one's, whatever path it takes
+  g_pit_hist.clear();
+  g_pit_hist_n = 0;
   int dev;
   int rc = ensure_init(&dev);
   if (rc) return rc;
@@ -1080,48 +1219,26 @@ int ekf_impl(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, 
     dr = (const double*)e;
   }
   if (sb) HIPCHK(hipMemsetAsync(dstates, 0, sb, st));
-  const int block = 64;
-  // few channels: one 16-lane row per channel (ekf_row_kernel, ~1.7x the per-channel
-  // rate); many: one lane per channel (ekf_kernel, 16x the channels per instruction)
-  const bool row = t_tune.ekf_row && nrec <= (int64_t)t_tune.ekf_row * t_ds->n_cu * 16;
   void* wtw = nullptr;
   if ((rc = workspace(dev, "e_wt", (size_t)(n_samp > 0 ? n_samp : 1) * 8, &wtw))) return rc;
   if (n_samp > 0)
     hipLaunchKernelGGL(dfmi::ekf_phase_kernel, dim3((unsigned)((n_samp + 255) / 256)), dim3(256), 0, st,
                        (double*)wtw, n_samp, w_m, f_samp);
-  // the parallel form's scratch (~(6 x 8 B per sample + 2 x 65 doubles per block) per
-  // channel, ~37 MB for 400k samples) must fit in half of the free device memory; past
-  // that the sequential kernels run (same states to rounding)
+  // the parallel form by channel count and length alone (the same input always takes the same
+  // path); only when its scratch (~6 x 8 B per sample + 2 x 65 doubles per block per channel,
+  // ~37 MB for 400k samples) cannot be allocated do the sequential kernels run instead
   bool pit = t_tune.ekf_pit > 0 && nrec <= t_tune.ekf_pit && n_samp >= t_tune.ekf_pit_min && n_samp >= 2;
-  if (pit) {
-    size_t fr = 0, tot = 0;
-    const double need = (double)nrec * ((double)n_samp * 8.0 * 6.0 + (double)n_samp / 16.0 * 8.0 * 2.2 * dfmi::kPitEl);
-    if (hipMemGetInfo(&fr, &tot) == hipSuccess && need > 0.5 * (double)fr) pit = false;
-  }
   if (pit) {
     rc = ekf_pit_run(dev, dx, nrec, rs, n_samp, dx0, dp0, dq, dr, (const double*)wtw, w_m, f_samp, R, nbuf, dstates,
                      st);
-    if (rc) return rc;
-  } else {
-    g_pit_nrec = 0;
-    const int64_t grid = row ? (nrec + 3) / 4 : (nrec + block - 1) / block;
-    // rotation between anchors: groups of 16 (8, 4) samples whose ends carry the snapshots
-    const bool rot = t_tune.ekf_rot && R % 4 == 0;
-    using EK = void (*)(const double*, int64_t, int64_t, int64_t, const double*, const double*, const double*,
-                        const double*, const double*, int, int64_t, double*, DfmiTrigK);
-    EK ek;
-    if (row)
-      ek = !rot ? dfmi::ekf_row_kernel<DFMI_EKF_SPLIT != 0>
-           : R % DFMI_EKF_ROT_G == 0 ? dfmi::ekf_rot_kernel<DFMI_EKF_ROT_G>
-           : R % 8 == 0              ? dfmi::ekf_rot_kernel<8>
-                                     : dfmi::ekf_rot_kernel<4>;
-    else
-      ek = !rot ? dfmi::ekf_kernel : R % 8 == 0 ? dfmi::ekf_lane_rot_kernel<8> : dfmi::ekf_lane_rot_kernel<4>;
-    hipLaunchKernelGGL(ek, dim3((unsigned)grid), dim3(block), 0, st, dx, nrec, rs, n_samp, dx0, dp0, dq, dr,
-                       (const double*)wtw, (int)R, nbuf, dstates, dfmi_trig_k());
-    // also reports the EKF variant
-    g_last_demod = row ? (rot ? "ekf_rot_kernel" : "ekf_row_kernel") : (rot ? "ekf_lane_rot_kernel" : "ekf_kernel");
-    HIPCHK(hipGetLastError());
+    if (rc == kPitNoMem) pit = false;
+    else if (rc) return rc;
+  }
+  if (!pit) {
+    const char* kname;
+    if ((rc = ekf_seq_launch(dx, nrec, rs, n_samp, dx0, dp0, dq, dr, (const double*)wtw, R, nbuf, dstates, st, &kname)))
+      return rc;
+    g_last_demod = kname;  // also reports the EKF variant
   }
   if (host) {
     if (sb) HIPCHK(hipMemcpyAsync(states, dstates, sb, hipMemcpyDeviceToHost, st));
@@ -1272,6 +1389,9 @@ int dfmi_release_workspaces(void) {
   for (auto& kv : t_ds->ws)
     if (int rc = free_stream_ws(kv.second)) return rc;
   t_ds->ws.clear();
+  if (t_ds->pin) HIPCHK(hipHostFree(t_ds->pin));
+  t_ds->pin = nullptr;
+  t_ds->pin_n = 0;
   return DFMI_OK;
 }
 
@@ -1537,18 +1657,23 @@ int dfmi_ekf_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_sa
 int dfmi_ekf_pit_passes(int32_t* passes, int64_t nrec) {
   CallScope cs;
   if (!passes || nrec < 0) return fail(DFMI_ERR_ARG, "bad pass buffer");
-  if (g_pit_nrec == 0 || !g_pit_flag) {
+  if (g_pit_passes.empty()) {
     for (int64_t r = 0; r < nrec; ++r) passes[r] = 0;
     return DFMI_OK;
   }
-  if (nrec != g_pit_nrec) return fail(DFMI_ERR_ARG, "nrec differs from the last EKF call's");
-  int dev;
-  int rc = ensure_init(&dev);
-  if (rc) return rc;
-  std::vector<int> f((size_t)nrec * 2);
-  HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(f.data(), g_pit_flag, f.size() * sizeof(int), hipMemcpyDeviceToHost));
-  for (int64_t r = 0; r < nrec; ++r) passes[r] = f[2 * r + 1];
+  if (nrec != (int64_t)g_pit_passes.size()) return fail(DFMI_ERR_ARG, "nrec differs from the last EKF call's");
+  memcpy(passes, g_pit_passes.data(), (size_t)nrec * sizeof(int32_t));
+  return DFMI_OK;
+}
+
+int dfmi_ekf_pit_trace(double* moves, int64_t nrec, int32_t max_pass) {
+  CallScope cs;
+  if (!moves || nrec < 0 || max_pass < 0) return fail(DFMI_ERR_ARG, "bad trace buffer");
+  if (g_pit_hist_n == 0) return fail(DFMI_ERR_ARG, "no trace: set ekf_pit_trace to 1 before a parallel-in-time EKF call");
+  if ((size_t)nrec * g_pit_hist_n != g_pit_hist.size()) return fail(DFMI_ERR_ARG, "nrec differs from the last EKF call's");
+  for (int64_t r = 0; r < nrec; ++r)
+    for (int32_t p = 0; p < max_pass; ++p)
+      moves[r * max_pass + p] = p < g_pit_hist_n ? g_pit_hist[(size_t)r * g_pit_hist_n + p] : __builtin_nan("");
   return DFMI_OK;
 }
 

@@ -26,15 +26,17 @@
 //      ekf_pit_aggregate_kernel at the seeded trajectory (ekf_pit_head_kernel); the separate
 //      aggregate / ekf_pit_blocks_kernel pair per pass remains behind the ekf_pit_fused knob.
 //
-// When the block entry states stop moving (max |dx| / max(1, |x|) <= tol over the channel,
-// tested on the device by the pass kernel's last workgroup, or ekf_pit_check_kernel on the
-// unfused path) they are the EKF's own states at those
-// samples to the scan's rounding (~1e-13; once past the start-up transient the error falls
-// ~100x per pass: scripts/study/ekf_pit_proto.py), so the output is the sequential EKF's to
-// rounding. A
-// converged channel's later kernels return at once (flag per channel, no host round trip);
-// a channel still moving after the last pass is re-run by the sequential lane kernel
-// (ekf_pit_fallback_kernel), so the result never depends on the iteration having converged.
+// Convergence (pit_decide, on the device: the pass kernel's last workgroup of a channel, or
+// ekf_pit_check_kernel on the unfused path) bounds the distance of the output snapshots from
+// the iteration's fixed point by rho / (1 - rho) d_k <= 1e-13, with d_k their largest relative
+// move in pass k and rho the contraction measured per channel; the fixed point is the EKF
+// itself to the scan's rounding, so the output is the sequential EKF's to rounding. A
+// converged channel's later kernels return at once (status per channel); the host reads the
+// count of channels still passing after the first ekf_pit_first passes and then every
+// ekf_pit_every, and stops when none is left. A channel that stops contracting (or reaches
+// the pass cap) is re-run by the sequential row / lane kernel (ekf_pit_pick_kernel /
+// ekf_pit_put_kernel around it), so the result never depends on the iteration having
+// converged.
 //
 // Layouts (all channel-major, blocks fastest so lane b of a wave reads address b):
 //   xt[r][i][b], wtt[i][b] (sample k = b B + i), xbar[r][c][i][b] (the seeded trajectory),
@@ -61,6 +63,120 @@ __host__ __device__ constexpr int pit_sy(int i, int j) {
 }
 __host__ __device__ constexpr double pit_identity(int c) {
   return (c < kPitB && c / 5 == c % 5) ? 1.0 : 0.0;  // A = I, everything else 0
+}
+
+// Per-channel control of the passes (device, 64 B). status: 0 passing, 1 converged, 2 not
+// contracting (the host re-runs it with the sequential kernel); every pass kernel of a channel
+// whose status is set returns at once.
+constexpr int kPitTrend = 4;  // passes over which the stall test measures the contraction
+struct PitChan {
+  int status;
+  int passes;  // passes run
+  int stall;   // consecutive passes that did not contract fast enough (pit_decide)
+  int pad;
+  double dprev;              // the previous pass's move d (NaN before the second pass)
+  double rho;                // the last trusted contraction d_k / d_{k-1} (-1: none yet)
+  double dold[kPitTrend];    // moves of the passes k-1 .. k-kPitTrend (NaN: none)
+};
+
+// The stop rule (round 5). d_k = the largest relative move, max |x_k - x_{k-1}| / max(1, |x_k|),
+// of the channel's OUTPUT snapshots (fitters.py:305-307) between passes k-1 and k (measure 0;
+// measure 1, diagnostics: the block-entry states, whose rounding noise after the scan reached
+// 1e-12 on a stiff filter, profiles/r05a). For a fixed-point iteration contracting by rho per
+// pass, the distance of x_k from the fixed point is at most rho / (1 - rho) d_k; the channel
+// is converged when that bound is <= tol (1e-13), rho estimated on the device from the moves
+// (the larger of the last two ratios d_k / d_{k-1}). Ratios of moves at or below the rounding
+// noise (`noise` = tol) say nothing about the contraction, so there the last trusted ratio
+// stands in. A pass over which the channel does not contract (the geometric-mean contraction
+// of the last 4 passes >= 1), or contracts too slowly to meet the bound within the cap (>= 0.5
+// and the passes it would still need push it past the cap), counts towards `stall`; stall_max
+// such passes in a row, or a non-finite move after the first pass (the filter's own states are
+// not finite), hand the channel to the sequential kernel, as does the host's cap
+// (ekf_pit_passes). A pass costs ~1/1000 of the sequential kernel on one
+// 400k-sample channel, so the passes go on as long as the bound can still be met.
+struct PitRule {
+  double tol;
+  double noise;      // moves at or below this are rounding: their ratios are not trusted
+  int stall_max;
+  int cap;           // the host's pass cap (ekf_pit_passes)
+  int hist_n;        // moves recorded per channel into hist (0: none)
+  int measure;       // 0: the output snapshots' move (default); 1: the block-entry states' move
+};
+
+// A snapshot (fitters.py:305-307) written by this pass: its largest relative move since the
+// previous pass's value at the same place (the states buffer itself: zeros before the first
+// pass, whose move pit_decide ignores) into d.
+__device__ __forceinline__ void pit_snapshot(double* __restrict__ so, const double (&st)[5], double& d) {
+#pragma unroll
+  for (int c = 0; c < 5; ++c) {
+    const double m = fabs(st[c] - so[c]) / fmax(1.0, fabs(st[c]));
+    d = m <= d ? d : m;  // NaN propagates
+    so[c] = st[c];
+  }
+}
+
+__device__ __forceinline__ void pit_decide(PitChan& c, double d, const PitRule& ru, double* hist) {
+  const int pass = c.passes;
+  c.passes = pass + 1;
+  if (pass == 0) d = __builtin_nan("");  // no previous pass to have moved from
+  if (hist && pass < ru.hist_n) hist[pass] = d;
+  int status = 0;
+  const double dprev = c.dprev;
+  if (d == 0.0) {
+    status = 1;  // nothing moved at all: the fixed point itself
+  } else if (!(d <= 1.7976931348623157e308)) {
+    if (pass >= 1) status = 2;  // the filter's own states are not finite: the sequential kernel
+  } else {
+    // rho: the contraction of this pass, trusted when both moves stand above the rounding
+    // noise; the bound uses the larger of the last two trusted ratios (one move that happens
+    // to be small, e.g. a snapshot crossing its old value, does not end the passes)
+    double rho = -1.0;
+    if (dprev > 0.0 && dprev <= 1.7976931348623157e308) {
+      const double q = d / dprev;
+      if (dprev > ru.noise && d > ru.noise) {
+        rho = c.rho >= 0.0 ? fmax(q, c.rho) : q;
+        c.rho = q;
+      } else if (d > ru.noise) {
+        rho = q;  // out of the noise again: a real move
+      } else {
+        rho = c.rho;  // at the noise: the last trusted contraction stands
+      }
+    }
+    if (rho < 0.0) {
+      if (d <= ru.noise) status = 1;  // no ratio yet, the move itself at the rounding noise
+    } else if (rho < 1.0 && rho / (1.0 - rho) * d <= ru.tol) {
+      status = 1;
+    }
+    if (status == 0 && d > ru.noise) {
+      // not contracting, or too slowly to meet the bound within the cap: stall_max passes in
+      // a row of that hand the channel to the sequential kernel. The contraction here is the
+      // geometric mean over the last kPitTrend passes (a crawling start-up transient
+      // alternates good and bad single ratios)
+      int w = 0;
+      double dw = 0.0;
+#pragma unroll
+      for (int i = 0; i < kPitTrend; ++i)
+        if (c.dold[i] > 0.0 && c.dold[i] <= 1.7976931348623157e308) {
+          w = i + 1;
+          dw = c.dold[i];
+        }
+      if (w > 0) {
+        const double rt = pow(d / dw, 1.0 / w);
+        bool slow = rt >= 1.0;
+        if (!slow && rt >= 0.5) {
+          const double need = log(ru.tol * (1.0 - rt) / (rt * d)) / log(rt);
+          slow = pass + 1 + need > ru.cap;
+        }
+        c.stall = slow ? c.stall + 1 : 0;
+        if (c.stall >= ru.stall_max) status = 2;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = kPitTrend - 1; i > 0; --i) c.dold[i] = c.dold[i - 1];
+  c.dold[0] = d;
+  c.dprev = d;
+  c.status = status;
 }
 
 // a filtering element read through a strided pointer (global SoA or LDS)
@@ -416,16 +532,21 @@ __global__ __launch_bounds__(256) void ekf_pit_gather_kernel(const double* __res
                                                              const double* __restrict__ hst, int64_t T0, int64_t B,
                                                              int64_t nb, double w_m, double f_samp,
                                                              double* __restrict__ xt, double* __restrict__ wtt,
-                                                             double* __restrict__ xbar, int* __restrict__ flag,
+                                                             double* __restrict__ xbar, PitChan* __restrict__ ch,
                                                              double* __restrict__ conv, unsigned* __restrict__ done) {
   const int64_t r = blockIdx.y;
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // s = i nb + b
   const int64_t slots = B * nb;
   if (s == 0) {
-    flag[2 * r] = 0;      // converged
-    flag[2 * r + 1] = 0;  // passes run
-    conv[r] = 0.0;        // largest move of the pass (ekf_pit_blocks_kernel)
-    done[r] = 0;          // workgroups of the pass kernel finished (ekf_pit_pass_kernel)
+    PitChan c;
+    c.status = c.passes = c.stall = c.pad = 0;
+    c.dprev = __builtin_nan("");
+    c.rho = -1.0;
+#pragma unroll
+    for (int i = 0; i < kPitTrend; ++i) c.dold[i] = __builtin_nan("");
+    ch[r] = c;
+    conv[r] = 0.0;  // largest move of the pass (ekf_pit_blocks_kernel)
+    done[r] = 0;    // workgroups of the pass kernel finished (ekf_pit_pass_kernel)
   }
   if (s >= slots) return;
   const int64_t i = s / nb, b = s - i * nb;
@@ -519,10 +640,10 @@ __global__ __launch_bounds__(64) void ekf_pit_aggregate_kernel(const double* __r
                                                                const double* __restrict__ p0,
                                                                const double* __restrict__ qd,
                                                                const double* __restrict__ rv,
-                                                               const int* __restrict__ flag,
+                                                               const PitChan* __restrict__ ch,
                                                                double* __restrict__ agg, DfmiTrigK tk) {
   const int64_t r = blockIdx.y;
-  if (flag[2 * r]) return;
+  if (ch[r].status) return;
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= nb) return;
   const int64_t slots = B * nb;
@@ -596,10 +717,10 @@ __global__ __launch_bounds__(64) void ekf_pit_aggregate_kernel(const double* __r
 template <int WGE>
 __global__ __launch_bounds__(4 * WGE) void ekf_pit_scan_kernel(double* __restrict__ el, int64_t n_el, int64_t ld,
                                                                double* __restrict__ tot,
-                                                               const int* __restrict__ flag) {
+                                                               const PitChan* __restrict__ ch) {
   static_assert(WGE % 64 == 0, "whole waves per role");
   const int64_t r = blockIdx.y;
-  if (flag[2 * r]) return;
+  if (ch[r].status) return;
   __shared__ double s[kPitEl * WGE];
   const int t = threadIdx.x;
   const int w = t >> 6, role = w & 3, e = ((w >> 2) << 6) + (t & 63);
@@ -659,9 +780,9 @@ __global__ __launch_bounds__(4 * WGE) void ekf_pit_scan_kernel(double* __restric
 // are formed (pit_combine_state). One lane per element; the hierarchy is fixed top-down.
 __global__ __launch_bounds__(64) void ekf_pit_fixup_kernel(double* __restrict__ el, int64_t n_el,
                                                            const double* __restrict__ up, int64_t n_up,
-                                                           const int* __restrict__ flag) {
+                                                           const PitChan* __restrict__ ch) {
   const int64_t r = blockIdx.y;
-  if (flag[2 * r]) return;
+  if (ch[r].status) return;
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + kPitWg;  // the first workgroup is exact
   if (g >= n_el) return;
   double st[5], P[5][5];
@@ -727,11 +848,11 @@ __global__ __launch_bounds__(64) void ekf_pit_blocks_kernel(const double* __rest
                                                             const double* __restrict__ qd,
                                                             const double* __restrict__ rv,
                                                             const double* __restrict__ agg,
-                                                            const double* __restrict__ tot, const int* __restrict__ flag,
+                                                            const double* __restrict__ tot, const PitChan* __restrict__ ch,
                                                             double* __restrict__ conv, int R, int64_t nbuf,
-                                                            double* __restrict__ states, DfmiTrigK tk) {
+                                                            double* __restrict__ states, int measure, DfmiTrigK tk) {
   const int64_t r = blockIdx.y;
-  if (flag[2 * r]) return;
+  if (ch[r].status) return;
   const int64_t b0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = b0 < nb;  // lanes past the last block stay for the wave's max (no work)
   const int64_t b = live ? b0 : nb - 1;
@@ -741,7 +862,7 @@ __global__ __launch_bounds__(64) void ekf_pit_blocks_kernel(const double* __rest
   for (int i = 0; i < 5; ++i) Q[i] = qd[i];
   pit_entry(r, b, nb, x0, p0, agg, tot, st, P);
   const double Rv = rv[r];
-  double dmax = 0.0;
+  double dmax = 0.0, dsnap = 0.0;
   const int64_t kend = !live ? 0 : (b + 1) * B < n ? B : n - b * B;
   // inputs kPitG samples ahead (see ekf_pit_aggregate_kernel): y_k, w_m t_k and the xbar of
   // sample k + 1 this block overwrites
@@ -776,15 +897,13 @@ __global__ __launch_bounds__(64) void ekf_pit_blocks_kernel(const double* __rest
       }
       if ((k + 1) % R == 0) {
         const int64_t bi = (k + 1) / R - 1;
-        if (bi < nbuf) {
-#pragma unroll
-          for (int c = 0; c < 5; ++c) states[(r * nbuf + bi) * 5 + c] = st[c];
-        }
+        if (bi < nbuf) pit_snapshot(states + (r * nbuf + bi) * 5, st, dsnap);
       }
     }
 #pragma unroll
     for (int u = 0; u < kPitG; ++u) cur[u] = nxt[u];
   }
+  if (measure == 0) dmax = dsnap;
   // the channel's largest move: a non-negative double (or NaN, above every finite value
   // and inf) orders as its bits, so the wave's max goes to conv[r] by one integer atomic
   unsigned long long bits = __builtin_bit_cast(unsigned long long, dmax);
@@ -813,12 +932,12 @@ __global__ __launch_bounds__(64) void ekf_pit_pass_kernel(const double* __restri
                                                           const double* __restrict__ agg,
                                                           const double* __restrict__ tot,
                                                           double* __restrict__ agg_out, double* __restrict__ ent,
-                                                          int* __restrict__ flag, double* __restrict__ conv,
-                                                          unsigned* __restrict__ done, double tol, int R,
+                                                          PitChan* __restrict__ ch, double* __restrict__ conv,
+                                                          unsigned* __restrict__ done, PitRule rule, double* __restrict__ hist, int R,
                                                           int64_t nbuf, double* __restrict__ states,
                                                           DfmiTrigK tk) {
   const int64_t r = blockIdx.y;
-  if (flag[2 * r]) return;
+  if (ch[r].status) return;
   const int64_t b0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = b0 < nb;  // lanes past the last block stay for the wave's max (no work)
   const int64_t b = live ? b0 : nb - 1;
@@ -828,7 +947,7 @@ __global__ __launch_bounds__(64) void ekf_pit_pass_kernel(const double* __restri
   for (int i = 0; i < 5; ++i) Q[i] = qd[i];
   pit_entry(r, b, nb, x0, p0, agg, tot, st, P);
   double dmax = 0.0;
-  if (live) {
+  if (live && rule.measure == 1) {
 #pragma unroll
     for (int c = 0; c < 5; ++c) {
       double* pe = ent + (r * 5 + c) * nb + b;
@@ -839,6 +958,7 @@ __global__ __launch_bounds__(64) void ekf_pit_pass_kernel(const double* __restri
   }
   // the block's next aggregate: block 0 from the prior element, the others from the identity
   double A[25], bv[5], C[15], et[5], J[15];
+  double dsnap = 0.0;
   const bool first = b == 0;
 #pragma unroll
   for (int c = 0; c < 25; ++c) A[c] = (!first && c / 5 == c % 5) ? 1.0 : 0.0;
@@ -879,10 +999,7 @@ __global__ __launch_bounds__(64) void ekf_pit_pass_kernel(const double* __restri
       const int64_t k = b * B + i;
       if ((k + 1) % R == 0) {
         const int64_t bi = (k + 1) / R - 1;
-        if (bi < nbuf) {
-#pragma unroll
-          for (int c = 0; c < 5; ++c) states[(r * nbuf + bi) * 5 + c] = st[c];
-        }
+        if (bi < nbuf) pit_snapshot(states + (r * nbuf + bi) * 5, st, dsnap);
       }
     }
 #pragma unroll
@@ -906,6 +1023,7 @@ __global__ __launch_bounds__(64) void ekf_pit_pass_kernel(const double* __restri
       o[(kPitJ + c) * nb] = J[c];
     }
   }
+  if (rule.measure == 0) dmax = dsnap;
   unsigned long long bits = __builtin_bit_cast(unsigned long long, dmax);
 #pragma unroll
   for (int w = 32; w >= 1; w >>= 1) {
@@ -913,65 +1031,51 @@ __global__ __launch_bounds__(64) void ekf_pit_pass_kernel(const double* __restri
     bits = o > bits ? o : bits;
   }
   // the channel's check (ekf_pit_check_kernel's, without a launch): the last workgroup of
-  // the channel to finish (one wave each: lane 0 made the atomicMax) reads the max and sets
-  // the flag; every other workgroup of this launch had passed its flag test by then
+  // the channel to finish (one wave each: lane 0 made the atomicMax) reads the max and applies
+  // the stop rule; every other workgroup of this launch had passed its status test by then
   if (threadIdx.x == 0) {
     atomicMax((unsigned long long*)conv + r, bits);
     __threadfence();
     if (atomicAdd(done + r, 1u) == gridDim.x - 1) {
       __threadfence();
       const double c = __builtin_bit_cast(double, atomicAdd((unsigned long long*)conv + r, 0ull));
-      flag[2 * r + 1] += 1;
-      if (c <= tol) flag[2 * r] = 1;
+      pit_decide(ch[r], c, rule, hist ? hist + r * rule.hist_n : nullptr);
       atomicExch((unsigned long long*)conv + r, 0ull);
       atomicExch(done + r, 0u);
     }
   }
 }
 
-// One thread per channel: converged when no block moved xbar by more than tol (relative,
-// see ekf_pit_blocks_kernel); counts the passes that ran and clears conv for the next.
-__global__ __launch_bounds__(64) void ekf_pit_check_kernel(double* __restrict__ conv, int64_t nrec, double tol,
-                                                           int* __restrict__ flag) {
+// One thread per channel (the unfused path): the stop rule on the pass's largest move of xbar
+// (ekf_pit_blocks_kernel), then conv cleared for the next pass.
+__global__ __launch_bounds__(64) void ekf_pit_check_kernel(double* __restrict__ conv, int64_t nrec, PitRule rule,
+                                                           PitChan* __restrict__ ch, double* __restrict__ hist) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= nrec || flag[2 * r]) return;
-  flag[2 * r + 1] += 1;
-  if (conv[r] <= tol) flag[2 * r] = 1;
+  if (r >= nrec || ch[r].status) return;
+  pit_decide(ch[r], conv[r], rule, hist ? hist + r * rule.hist_n : nullptr);
   conv[r] = 0.0;
 }
 
-// A channel the passes left unconverged: the sequential EKF (ekf_kernel's loop) from x0.
-__global__ __launch_bounds__(64) void ekf_pit_fallback_kernel(const double* __restrict__ x, int64_t nrec, int64_t rs,
-                                                              int64_t n, const double* __restrict__ x0,
-                                                              const double* __restrict__ p0,
-                                                              const double* __restrict__ qd,
-                                                              const double* __restrict__ rv,
-                                                              const double* __restrict__ wt, int R, int64_t nbuf,
-                                                              double* __restrict__ states, int* __restrict__ flag,
-                                                              DfmiTrigK tk) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= nrec || flag[2 * r]) return;
-  flag[2 * r + 1] = -flag[2 * r + 1];  // reported as a negative pass count
-  const double* __restrict__ xr = x + r * rs;
-  double st[5], P[5][5], Q[5];
-#pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    st[i] = x0[r * 5 + i];
-    Q[i] = qd[i];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) P[i][j] = (i == j) ? p0[i] : 0.0;
-  }
-  const double Rv = rv[r];
-  for (int64_t k = 0; k < n; ++k) {
-    ekf_step(st, P, Q, Rv, xr[k], wt[k], tk);
-    if ((k + 1) % R == 0) {
-      const int64_t bi = (k + 1) / R - 1;
-      if (bi < nbuf) {
-#pragma unroll
-        for (int c = 0; c < 5; ++c) states[(r * nbuf + bi) * 5 + c] = st[c];
-      }
-    }
-  }
+// The channels the passes left to the sequential kernel (the host's list idx): their records,
+// x0 and R_val copied into compact arrays (grid.y = listed channel, x = samples) ...
+__global__ __launch_bounds__(256) void ekf_pit_pick_kernel(const double* __restrict__ x, int64_t rs, int64_t n,
+                                                           const double* __restrict__ x0,
+                                                           const double* __restrict__ rv,
+                                                           const int* __restrict__ idx, double* __restrict__ xs,
+                                                           double* __restrict__ x0s, double* __restrict__ rvs) {
+  const int64_t j = blockIdx.y, r = idx[j];
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) xs[j * n + k] = x[r * rs + k];
+  if (blockIdx.x == 0 && threadIdx.x < 5) x0s[j * 5 + threadIdx.x] = x0[r * 5 + threadIdx.x];
+  if (blockIdx.x == 0 && threadIdx.x == 5) rvs[j] = rv[r];
+}
+
+// ... and the sequential kernel's snapshots of them put back in place.
+__global__ __launch_bounds__(256) void ekf_pit_put_kernel(const double* __restrict__ ss, int64_t nbuf,
+                                                          const int* __restrict__ idx, double* __restrict__ states) {
+  const int64_t j = blockIdx.y, r = idx[j];
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < nbuf * 5) states[r * nbuf * 5 + k] = ss[j * nbuf * 5 + k];
 }
 
 }  // namespace dfmi

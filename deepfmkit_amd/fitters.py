@@ -21,6 +21,7 @@ Reference map:
 from __future__ import annotations
 
 import logging
+import time
 from abc import ABC, abstractmethod
 
 import numpy as np
@@ -33,6 +34,15 @@ from . import fit as _fit
 log = logging.getLogger(__name__)
 
 COLUMNS = ["amp", "m", "phi", "psi", "dc", "ssq", "fitok"]
+
+# Facade timing marks (scripts/profile_facade.py sets a list here): (label, perf_counter())
+# appended at each stage of DeepFitFramework.fit's NLS path; None = off (one test per mark).
+MARKS = None
+
+
+def mark(label):
+    if MARKS is not None:
+        MARKS.append((label, time.perf_counter()))
 
 
 def _calculate_fit_params(raw_obj, n):
@@ -98,11 +108,13 @@ def nls_records(records, f_samp, f_mod, R, nbuf, ndata=10, init_guess=(1.6, 6.0,
             raise ValueError("device records must be contiguous float64 rows")
         out = torch.empty((6, nseg), dtype=torch.float64, device=x.device)
         ok = torch.empty(nseg, dtype=torch.int32, device=x.device)
+        mark("alloc")
         with _on_device(x):
             rc = lib.dfmi_nls_record(x.data_ptr(), nrec, rec_stride, nbuf, R, ndata, w0, 0, _lib.ptr(g),
                                      1 if parallel else 0, max(nchunk, 1), cfg, out.data_ptr(), ok.data_ptr(),
                                      _lib.DFMI_MEM_DEVICE, _torch_stream(x.device))
         _lib.check(rc, "dfmi_nls_record")
+        mark("enqueue")
         return out, ok
     x = np.ascontiguousarray(x, dtype=np.float64)
     out = np.empty((6, nseg))
@@ -173,11 +185,17 @@ def frame_from(cols, fitok):
     float block as it is (pandas keeps a block as (columns, rows): the transpose is a view),
     instead of seven 1-D arrays consolidated into a new block (1.2 ms -> ~0.1 ms at 100k rows)."""
     if hasattr(cols, "cpu"):
+        if MARKS is not None:  # profiling: the wait for the kernels apart from the copy
+            import torch
+            torch.cuda.current_stream(cols.device).synchronize()
+            mark("gpu_done")
         cols = cols.cpu().numpy()
         fitok = fitok.cpu().numpy()
+        mark("d2h")
     cols = np.ascontiguousarray(cols, dtype=np.float64)
     df = pd.DataFrame(cols[:6].T, columns=COLUMNS[:6], copy=False)
     df["fitok"] = np.asarray(fitok).astype(np.int64)
+    mark("frame")
     return df
 
 
@@ -229,6 +247,7 @@ class StandardNLSFitter(BaseFitter):
             # (parallel=False, or the n_cores array_split chains) runs on the current GPU
             raise ValueError("devices= applies to parallel=True without n_cores (chunk size 1); "
                              f"got parallel={parallel}, n_cores={kwargs.get('n_cores')}")
+        mark("fitter_args")
         if devices is not None:
             cols, ok = nls_record_devices(x, main_raw.f_samp, main_raw.f_mod, R, nbuf, devices, ndata,
                                           (init_a, init_m, 0.0, init_psi))

@@ -128,8 +128,16 @@ int dfmi_nls_record(const double* x, int64_t nrec, int64_t rec_stride, int64_t n
  * dfmi_set_tuning "ekf_row" / "ekf_rot" select. Up to "ekf_pit" (1024) channels of at least
  * "ekf_pit_min" (4096) samples run parallel in time instead (ekf_pit.h): relinearization
  * passes of an associative linear Kalman scan over blocks, each ending in the true EKF per
- * block, until the trajectory stops moving (relative 1e-11), else the lane kernel; the same
- * states to rounding (~1e-13). x[r*rec_stride + k], k < n_samp. x0[r*5+i] initial state (dc included),
+ * block, until the output snapshots are within 1e-13 (relative to max(1, |x|)) of the
+ * iteration's fixed point by the bound rho / (1 - rho) x their last move between passes, rho
+ * the contraction measured per channel on the device; a channel that stops contracting (3
+ * passes in a row with rho >= 1, or too slow to meet the bound within the cap) or reaches the
+ * cap "ekf_pit_passes" (48) is re-run by the sequential kernel above; the same states to
+ * rounding (~1e-13). The parallel form reads how many channels still pass after
+ * "ekf_pit_first" (5) passes and then every "ekf_pit_every" (2): one stream
+ * synchronisation each, so a DFMI_MEM_DEVICE call on this path returns with its stream
+ * drained. The path depends on nrec and n_samp only (the sequential kernels run when the
+ * parallel form's scratch cannot be allocated). x[r*rec_stride + k], k < n_samp. x0[r*5+i] initial state (dc included),
  * p0_diag[5], q_diag[5], r_val[r] measurement variance, w_m = 2*pi*f_mod,
  * f_samp; snapshots every R samples into states[(r*nbuf + b)*5 + i]. */
 int dfmi_ekf(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_samp, const double* x0,
@@ -146,10 +154,17 @@ int dfmi_ekf_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t n_sa
                  int32_t R, int64_t nbuf, double* states, int32_t mem, void* stream);
 
 /* Passes the last dfmi_ekf / dfmi_ekf_fit call on this thread ran per channel (nrec as
- * that call's): 0 = sequential kernels, k > 0 = converged after k passes, -k = not
- * converged after k passes and re-run by the lane kernel. Synchronises the device; read it
- * before the next EKF call. */
+ * that call's): 0 = sequential kernels, k > 0 = converged after k passes, -k = stopped
+ * after k passes (not contracting, or the cap) and re-run by the sequential kernel. Copied
+ * to the host by that call itself: no device access here; valid until the next EKF call on
+ * this thread (a call that fails or takes the sequential path reports zeros). */
 int dfmi_ekf_pit_passes(int32_t* passes, int64_t nrec);
+
+/* Diagnostics of the stop rule: with dfmi_set_tuning("ekf_pit_trace", 1) during the last
+ * EKF call on this thread (parallel form), moves[r*max_pass + p] = channel r's largest
+ * relative move of its block-entry states in pass p (NaN for pass 0, whose previous entry
+ * does not exist, and for passes not run). DFMI_ERR_ARG when that call kept no trace. */
+int dfmi_ekf_pit_trace(double* moves, int64_t nrec, int32_t max_pass);
 
 /* np.mean / np.var of nrec float64 records x[r*rec_stride .. + n] (1 <= n < 2^31),
  * bit-exact with numpy's pairwise summation (numpy 2.x _methods._mean / _var); var
@@ -293,7 +308,13 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
  * to this many channels, default 1024; 0 = the sequential kernels always), "ekf_pit_min"
  * (samples per channel below which the sequential kernels run, default 4096),
  * "ekf_pit_block" (samples per block, 0 = ~n nrec^(2/3) / 16384, at least 16), "ekf_pit_passes"
- * (relinearization passes before the lane-kernel fallback, default 12), "ekf_pit_head"
+ * (pass cap before the sequential kernel, default 48), "ekf_pit_first" / "ekf_pit_every"
+ * (passes before the first / between later host reads of the channels still passing, 5 / 2),
+ * "ekf_pit_tol" (the stop rule's bound 10^-k, default 13), "ekf_pit_stall" (non-contracting
+ * passes in a row before the sequential kernel, default 3), "ekf_pit_measure" (0 [default]:
+ * the rule's move is the output snapshots'; 1, diagnostics: the block-entry states'), "ekf_pit_trace" (0 / 1,
+ * dfmi_ekf_pit_trace), "ekf_pit_seq" (1 [default]; 0, diagnostics only: an unconverged
+ * channel keeps its last pass's states instead of the sequential kernel's), "ekf_pit_head"
  * (samples the sequential EKF seeds the trajectory with, default 256), "ekf_pit_fused" (1
  * [default]: the EKF and the next pass's fold in one kernel per pass; 0: separate kernels),
  * "probe" (1 =

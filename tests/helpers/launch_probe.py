@@ -16,7 +16,7 @@ def main():
 
     import bench
     world = int(os.environ["WORLD_SIZE"])
-    dist.init_process_group("gloo")
+    bench.join_group(dist, "gloo", None, float(os.environ.get("PROBE_RDZV_TIMEOUT", "120")))
     ranks, backend = bench.rank_topology(dist, torch.device("cpu"), world)
     t = torch.tensor([float(dist.get_rank() + 1)])
     dist.all_reduce(t, op=dist.ReduceOp.MAX)

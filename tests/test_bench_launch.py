@@ -43,3 +43,46 @@ def test_world_size_mismatch_is_an_error():
                        text=True, timeout=120)
     assert p.returncode != 0
     assert "WORLD_SIZE=2" in p.stderr
+
+
+def test_rank_late_for_rendezvous_fails_fast_and_is_named(capfd):
+    """A rank that never reaches the rendezvous in time (rank 1 sleeps 60 s before joining,
+    the rendezvous timeout is 5 s): rank 0's init_process_group raises, the launcher takes
+    the job down, exits non-zero well inside the sleep and names rank 1 on stderr."""
+    import time
+
+    import bench
+    t0 = time.monotonic()
+    rc = bench.self_launch(2, [], script=os.path.join(ROOT, "tests", "helpers", "launch_probe.py"), timeout=120,
+                           env_extra={"DFMI_RDZV_DELAY": "1:60", "PROBE_RDZV_TIMEOUT": "5"})
+    dt = time.monotonic() - t0
+    err = capfd.readouterr().err
+    assert rc != 0 and dt < 45, (rc, dt)
+    assert "never reached the rendezvous: [1]" in err, err[-2000:]
+
+
+def test_launch_timeout_kills_and_names_the_ranks(capfd):
+    """The launcher's own bound: rank 0 stuck before the rendezvous, rank 1 waiting in it
+    (rendezvous timeout 120 s), both past the launch timeout of 8 s: killed, exit 124, rank 0
+    named as never arriving, both as not having joined."""
+    import time
+
+    import bench
+    t0 = time.monotonic()
+    rc = bench.self_launch(2, [], script=os.path.join(ROOT, "tests", "helpers", "launch_probe.py"), timeout=8,
+                           env_extra={"DFMI_RDZV_DELAY": "0:60", "PROBE_RDZV_TIMEOUT": "120"})
+    dt = time.monotonic() - t0
+    err = capfd.readouterr().err
+    assert rc == 124 and dt < 40, (rc, dt)
+    assert "launch timeout" in err and "never reached the rendezvous: [0];" in err, err[-2000:]
+    assert "did not complete it: [0, 1]" in err, err[-2000:]
+
+
+def test_launch_timeout_scales_with_the_work():
+    import argparse
+
+    import bench
+    a = argparse.Namespace(segments=None, steps=100, warmup=10, rdzv_timeout=120.0, no_extra=False)
+    t8 = bench.launch_timeout(a, 8)
+    a.steps = 1000
+    assert bench.launch_timeout(a, 8) > t8 > 600

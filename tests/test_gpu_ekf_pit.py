@@ -6,7 +6,8 @@ reference's own states by tests/test_oracle_golden.py::test_oracle_ekf_full_leng
 The parallel form is the sequential filter to rounding (every block runs the true EKF from
 an entry state the converged scan supplies), so it is held to the same 1e-12 of the C
 oracle as the sequential kernels; a channel that has not converged after the last pass is
-re-run by the lane kernel, bit for bit."""
+re-run by the sequential kernel (the row / lane kernel the sequential path would pick for that
+many channels), bit for bit."""
 import ctypes
 import os
 
@@ -49,7 +50,8 @@ def _c_ekf(x, init4, R, nbuf, qd=QD, r_val=None):
 class _tune:
     """dfmi_set_tuning for the duration of a block, restoring the defaults."""
     DEFAULTS = {"ekf_row": 1, "ekf_rot": 1, "ekf_pit": 1024, "ekf_pit_min": 4096, "ekf_pit_block": 0,
-                "ekf_pit_passes": 12, "ekf_pit_head": 256, "ekf_pit_fused": 1}
+                "ekf_pit_passes": 48, "ekf_pit_head": 256, "ekf_pit_fused": 1, "ekf_pit_first": 5,
+                "ekf_pit_every": 2, "ekf_pit_tol": 13, "ekf_pit_stall": 3, "ekf_pit_trace": 0, "ekf_pit_seq": 1}
 
     def __init__(self, lib, **kw):
         self.lib, self.kw = lib, kw
@@ -112,7 +114,7 @@ def test_pit_config5_default_path_matches_c_oracle(lib, c5, fused):
     with _tune(lib, ekf_pit_fused=fused):
         got, kname, passes = _ekf(lib, [c5], 4000, 100)
     assert kname.startswith("ekf_pit"), kname
-    assert 1 <= passes[0] <= 12, passes
+    assert 1 <= passes[0] <= 8, passes
     err = np.abs(got[0] - ref)
     print("pit passes", passes, "max |d state| vs C oracle", err.max())
     assert err.max() <= 1e-12, (err.max(), np.unravel_index(err.argmax(), err.shape))
@@ -164,17 +166,61 @@ def test_pit_channels_independent(lib):
 
 
 def test_pit_unconverged_falls_back_bit_exact(lib, c5):
-    """With one pass allowed the channel has not converged: it is re-run by the lane kernel
-    (ekf_pit_fallback_kernel = ekf_kernel's loop), reported as -1 pass, and its states equal
-    ekf_kernel's bit for bit."""
+    """With one pass allowed the channel has not converged: it is re-run by the sequential
+    kernel (ekf_rot_kernel for one channel at R = 4000, on the channel picked into a compact
+    buffer), reported as -1 pass, and its states equal that kernel's bit for bit."""
     x = c5[:100_000]
     with _tune(lib, ekf_pit_passes=1):
         got, kname, passes = _ekf(lib, [x], 4000, 25)
-    assert kname.startswith("ekf_pit") and passes == [-1], (kname, passes)
-    with _tune(lib, ekf_pit=0, ekf_row=0, ekf_rot=0):
-        lane, kl, _ = _ekf(lib, [x], 4000, 25)
-    assert kl == "ekf_kernel"
-    np.testing.assert_array_equal(got, lane)
+    assert kname.startswith("ekf_pit") and kname.endswith("+ ekf_rot_kernel x1") and passes == [-1], (kname, passes)
+    with _tune(lib, ekf_pit=0):
+        seq, kl, ps = _ekf(lib, [x], 4000, 25)
+    assert kl == "ekf_rot_kernel" and ps == [0]
+    np.testing.assert_array_equal(got, seq)
+
+
+def test_pit_fallback_only_for_unconverged_channels(lib):
+    """Three channels, one of them made to stall: with the pass cap at 2, every channel is
+    handed to the sequential kernel (passes -2); with the defaults, none is. In both, every
+    channel equals its own sequential run (the picked channels bit for bit, the converged ones
+    to the 1e-12 of the rule)."""
+    import deepfmkit_amd as dfm
+    xs = [_raw(dfm, 6.0, 0.1, 21), _raw(dfm, 4.3, 0.1, 22, psi=0.3, phi=0.7), _raw(dfm, 9.0, 0.1, 23, phi=1.3)]
+    with _tune(lib, ekf_pit=0):
+        seq, _, _ = _ekf(lib, xs, 4000, 5)
+    with _tune(lib, ekf_pit_passes=2):
+        got, kname, passes = _ekf(lib, xs, 4000, 5)
+    assert passes == [-2, -2, -2] and kname.endswith("+ ekf_rot_kernel x3"), (kname, passes)
+    np.testing.assert_array_equal(got, seq)
+    got, kname, passes = _ekf(lib, xs, 4000, 5)
+    assert all(p > 0 for p in passes) and "+" not in kname, (kname, passes)
+    assert np.abs(got - seq).max() <= 1e-12
+
+
+def test_pit_trace_and_passes_are_host_side(lib, c5):
+    """The pass counts and the per-pass moves are copied to the host by the EKF call itself
+    (dfmi_ekf_pit_passes reads no device memory): still readable after the workspaces are
+    released, cleared by the next EKF call (zeros after a sequential-path call), and the trace
+    ends at the converged pass with a move the rule accepts."""
+    import ctypes
+    from deepfmkit_amd import _lib
+    x = c5[:200_000]
+    with _tune(lib, ekf_pit_trace=1):
+        _, _, passes = _ekf(lib, [x], 4000, 50)
+    tr = np.empty(48)
+    _lib.check(lib.dfmi_ekf_pit_trace(tr.ctypes.data, 1, 48), "trace")
+    k = passes[0]
+    assert k > 1 and np.isnan(tr[0]) and np.isfinite(tr[1:k]).all() and np.isnan(tr[k:]).all(), (k, tr)
+    rho = tr[k - 1] / tr[k - 2]
+    assert tr[k - 1] == 0 or (rho < 1 and rho / (1 - rho) * tr[k - 1] <= 1e-13) or tr[k - 1] <= 1e-13, tr[:k]
+    _lib.check(lib.dfmi_release_workspaces(), "release")
+    p2 = (ctypes.c_int32 * 1)()
+    _lib.check(lib.dfmi_ekf_pit_passes(ctypes.cast(p2, ctypes.c_void_p), 1), "passes")
+    assert list(p2) == [k]
+    with _tune(lib, ekf_pit=0):
+        _, _, ps = _ekf(lib, [x], 4000, 50)
+    assert ps == [0]
+    assert lib.dfmi_ekf_pit_trace(tr.ctypes.data, 1, 48) != 0  # no trace kept by that call
 
 
 def test_pit_tuned_noise_matches_c_oracle(lib):

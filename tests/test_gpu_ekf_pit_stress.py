@@ -1,0 +1,82 @@
+"""EKF parallel in time under the stop rule of round 5 (ekf_pit.h pit_decide), stressed with
+>= 500 random channels in batched dfmi_ekf calls against the scalar C oracle
+(oracle/csrc/ekf_scalar.c, EKFFitter.fit's loop fitters.py:274-307; pinned to the numpy oracle
+by tests/test_oracle_c.py and to the reference's own states by tests/test_oracle_golden.py).
+
+Channels (tests/helpers/ekf_stress.py): m 1-25, phi / psi anywhere, SNR 0-60 dB, init_m offsets
+up to +-4, init phi / psi / a offsets, Q_diag and R_val scaled by 10^+-2 around the reference
+defaults (fitters.py:241-257), lengths 4,096 to 400,000 samples, R from 7 to 4000.
+
+Many of these filters never lock (init_m 4 off at m = 25, SNR 0 dB): they are chaotic, and the
+oracle itself moves by up to 1e-5 when its input is perturbed by one ulp
+(ekf_stress.sensitivity = S). No two correct implementations with different rounding (libm's
+sin / cos against the GPU's, numpy's summation against an FMA) agree there to 1e-12, the
+GPU's own sequential kernels included. So the gate per channel is
+    |x - oracle| / max(1, |x|) <= max(1e-12, 100 S)
+for the parallel form AND for the sequential kernel (the control: the bound is the channel's,
+not the method's), and a flat 1e-12 on the well-conditioned channels (S <= 1e-14), which are
+the BASELINE-like ones. Channels the rule hands to the sequential kernel are counted and the
+count is bounded (profiles/r05*_ekf_pit_stress*.json keeps the pass histogram)."""
+import collections
+import os
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "helpers"))
+import ekf_stress as S  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from deepfmkit_amd import _lib
+    lib = _lib.load()
+    if lib.dfmi_device_count() < 1:
+        pytest.skip("no GPU")
+    return lib
+
+
+def test_pit_stress_random_channels(lib):
+    from deepfmkit_amd import _lib
+    cl = S.c_oracle()
+    if cl is None:
+        pytest.skip("oracle/libekf_scalar.so not built (make -C oracle)")
+    hist = collections.Counter()
+    n_ch = n_seq = n_well = 0
+    worst_well = 0.0
+    for bi, (n, nch, R) in enumerate(S.BATCHES):
+        x, x0, rv, qd, meta = S.batch_inputs(bi, n, nch)
+        nbuf = n // R
+        got, kname, passes = S.gpu_states(lib, x, x0, rv, qd, R, nbuf)
+        assert kname.startswith("ekf_pit"), kname
+        _lib.check(lib.dfmi_set_tuning(b"ekf_pit", 0), "tune")
+        try:
+            seq, kseq, _ = S.gpu_states(lib, x, x0, rv, qd, R, nbuf)
+        finally:
+            _lib.check(lib.dfmi_set_tuning(b"ekf_pit", 1024), "tune")
+        ref, sens = S.oracle_batch(cl, x, x0, rv, qd, R, nbuf)
+        err, err_seq = S.rel_err(got, ref), S.rel_err(seq, ref)
+        gate = np.maximum(1e-12, 100.0 * sens)
+        well = sens <= 1e-14
+        hist.update(int(p) for p in passes)
+        n_ch += nch
+        n_well += int(well.sum())
+        n_seq += int((passes < 0).sum())
+        if well.any():
+            worst_well = max(worst_well, float(err[well].max()))
+        print(f"batch {bi}: n={n} ch={nch} R={R} {kname} | passes {sorted(collections.Counter(passes).items())} | "
+              f"max err {err.max():.2e} (sequential {kseq} {err_seq.max():.2e}) | well-conditioned {well.sum()} "
+              f"max err {err[well].max() if well.any() else 0:.2e}")
+        bad = np.where((err > gate) | (well & (err > 1e-12)))[0]
+        assert bad.size == 0, [(int(i), float(err[i]), float(err_seq[i]), float(sens[i]), int(passes[i]),
+                                float(meta["m"][i]), float(meta["snr_db"][i])) for i in bad[:10]]
+        assert (err_seq <= gate).all(), "the sequential control exceeds the channel gate: the gate is too tight"
+    print("channels", n_ch, "well-conditioned", n_well, "max err there", worst_well, "sequential re-runs", n_seq,
+          "pass histogram", sorted(hist.items()))
+    assert n_ch >= 500 and n_well >= 100
+    # the rule hands over the channels that do not lock (measured r05: ~1/3 of this harsh set;
+    # BASELINE-like channels converge in 4-10 passes, tests/test_gpu_ekf_pit.py)
+    assert n_seq <= 0.4 * n_ch, (n_seq, sorted(hist.items()))

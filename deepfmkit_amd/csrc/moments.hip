@@ -18,7 +18,13 @@ namespace dfmi {
 namespace {
 
 constexpr int kT = 256;
-constexpr int kTreeLds = 16384;  // nodes (2 per leaf) the tree kernel keeps in LDS: records up to ~1M samples
+// nodes (2 per leaf) the tree kernel keeps in static LDS: 16384 (128 KiB, records up to ~1M
+// samples) fits gfx950's 160 KiB; the Makefile sets a smaller count for a 64-KiB-LDS ARCH
+// (longer records then add the tree in the global node array)
+#ifndef DFMI_TREE_LDS_NODES
+#define DFMI_TREE_LDS_NODES 16384
+#endif
+constexpr int kTreeLds = DFMI_TREE_LDS_NODES;
 
 // leaf element: a_i, or (a_i - mean)^2 rounded as numpy's x = arr - mean; x * x
 template <bool SQ>

@@ -48,8 +48,6 @@ std::mutex g_mu;  // the device map, HIP initialisation and the tuning knobs
 struct Tuning {
   int demod_kernel = 1;  // 1: bin-in-LDS kernel where it applies, 0: cycle-aligned fold kernel
   int lm_general = 0;    // 1: force the two-pass (general) LM path for every ndata
-  int lm_finish = 0;     // 1: the register path's literal finisher (lm.h literal_finish) for descents that
-                         // ended on "no lambda improved" after a step of 1e-11 < |dp| < 1e-8
   int demod_spw = 2;     // bin kernels: grid sized for ~this many segments per wave (0: one persistent
                          // wave per slot); later workgroups go to the slots that free first
   int ekf_row = 1;       // EKF: ekf_row_kernel (4 channels per wave) up to ekf_row x 4 x 4 x CUs channels
@@ -393,10 +391,6 @@ int to_lmconst(const dfmi_lm_config* cfg, dfmi::LMConst* c) {
   grid_geometry(*cfg, &c->n_grid, &c->grid_delta);
   c->grid_min = cfg->m_grid_min;
   c->trig = dfmi_trig_k();
-  if (t_tune.lm_finish) {
-    c->fin_lo2 = 1e-22;  // (1e-11)^2
-    c->fin_hi2 = 1e-16;  // (1e-8)^2
-  }
   return DFMI_OK;
 }
 
@@ -890,7 +884,6 @@ const std::map<std::string, Knob>& knobs() {
   static const std::map<std::string, Knob> k = {
       {"demod_kernel", {&Tuning::demod_kernel, {0, 1}}},
       {"lm_general", {&Tuning::lm_general, {0, 1}}},
-      {"lm_finish", {&Tuning::lm_finish, {0, 1}}},
       {"demod_spw", {&Tuning::demod_spw, {}}},
       {"ekf_row", {&Tuning::ekf_row, {}}},
       {"ekf_rot", {&Tuning::ekf_rot, {0, 1}}},

@@ -54,17 +54,6 @@ struct LMConst {
   double grid_min;           // fit.py:12
   double grid_delta;         // (min + step) - min, numpy arange fill
   DfmiTrigK trig;            // dfmi_sincos_k's constants (in SGPRs as part of the kernel argument)
-  // literal finisher of the register path (fit_segment_t): a descent that ended on "no
-  // lambda improved" right after an accepted step with fin_lo2 < |dp|^2 < fin_hi2 goes on
-  // with the literal evaluation (eval_gen + damped_solve); fin_hi2 = 0: off
-  double fin_lo2, fin_hi2;
-};
-
-// How a descent ended: on "no lambda improved" (fit.py:246-247) or not, and the squared
-// norm of its last accepted step (0 if none).
-struct DescentEnd {
-  bool no_lambda = false;
-  double last2 = 0.0;
 };
 
 #define DFMI_HDI __host__ __device__ __forceinline__
@@ -659,9 +648,8 @@ DFMI_HDI bool norm_below(double ss, double thr) { return thr > 0.0 && ss < thr *
 // Ev: trial(p, t) -> ssqf at p; accept(p, t, e) -> coeffs at p from the trial's
 // state; solve(e, lambda, dp) -> msolve.
 template <typename Ev>
-DFMI_HDI double lm_descend_flat(Ev&& ev, double (&p)[4], const LMConst& c, DescentEnd* end = nullptr) {
+DFMI_HDI double lm_descend_flat(Ev&& ev, double (&p)[4], const LMConst& c) {
   Eval e;
-  double last2 = 0.0;
   {
     typename std::decay_t<Ev>::Trial t0;
     ev.trial(p, t0);
@@ -680,7 +668,6 @@ DFMI_HDI double lm_descend_flat(Ev&& ev, double (&p)[4], const LMConst& c, Desce
       if (ssq_try < e.ssq) {
         accepted = true;
         const double change2 = sumsq4(pt[0] - p[0], pt[1] - p[1], pt[2] - p[2], pt[3] - p[3]);
-        last2 = change2;
         p[0] = pt[0];
         p[1] = pt[1];
         p[2] = pt[2];
@@ -700,12 +687,8 @@ DFMI_HDI double lm_descend_flat(Ev&& ev, double (&p)[4], const LMConst& c, Desce
         }
       }
     }
-    if (!accepted && ++li >= c.n_lambda) {  // no lambda improved: fit.py:246-247
-      active = false;
-      if (end) end->no_lambda = true;
-    }
+    if (!accepted && ++li >= c.n_lambda) active = false;  // no lambda improved: fit.py:246-247
   }
-  if (end) end->last2 = last2;
   return e.ssq;
 }
 
@@ -771,9 +754,8 @@ struct SplitEval {  // NDMAX: a register-path variant tag (nd_cap / nd_exact)
 // check that the flattened descent takes the same path). p in/out; returns ssq0 at
 // the final p.
 template <typename Ev>
-DFMI_HDI double lm_descend(Ev&& ev, double (&p)[4], const LMConst& c, DescentEnd* end = nullptr) {
+DFMI_HDI double lm_descend(Ev&& ev, double (&p)[4], const LMConst& c) {
   Eval e;
-  double last2 = 0.0;
   {
     typename std::decay_t<Ev>::Trial t0;
     ev.trial(p, t0);
@@ -799,10 +781,7 @@ DFMI_HDI double lm_descend(Ev&& ev, double (&p)[4], const LMConst& c, DescentEnd
         break;
       }
     }
-    if (!found) {
-      if (end) end->no_lambda = true;
-      break;
-    }
+    if (!found) break;
     p[0] = pt[0];
     p[1] = pt[1];
     p[2] = pt[2];
@@ -810,10 +789,8 @@ DFMI_HDI double lm_descend(Ev&& ev, double (&p)[4], const LMConst& c, DescentEnd
     const double best_ssq = ssq_try;
     ev.accept(p, tt, e);  // coeffs(ndata, data, parm) at the accepted point (fit.py:251)
     const double change2 = sumsq4(p[0] - po0, p[1] - po1, p[2] - po2, p[3] - po3);
-    last2 = change2;
     if ((e.ssq - best_ssq) < c.conv_improve && norm_below(change2, c.conv_param_change)) break;
   }
-  if (end) end->last2 = last2;
   return e.ssq;
 }
 
@@ -853,8 +830,7 @@ constexpr int kLadderLanes = 8;  // lanes per segment of the parallel-ladder des
 // bits, LM 41-45 us against 36 us, removed)
 template <int LPS, typename Ev>
 __device__ __forceinline__ double lm_ladder_resume(Ev&& ev, double (&p)[4], const LMConst& c, Eval& e, int it,
-                                                   int base, bool live, DescentEnd* end = nullptr) {
-  double last2 = 0.0;
+                                                   int base, bool live) {
   using Trial = typename std::decay_t<Ev>::Trial;
   constexpr int NT = (int)(sizeof(Trial) / sizeof(double));
   static_assert(sizeof(Trial) == NT * sizeof(double), "trial state: doubles only");
@@ -886,7 +862,6 @@ __device__ __forceinline__ double lm_ladder_resume(Ev&& ev, double (&p)[4], cons
     if (active) {
       if (gm) {
         const double change2 = sumsq4(pt[0] - p[0], pt[1] - p[1], pt[2] - p[2], pt[3] - p[3]);
-        last2 = change2;
         p[0] = pt[0];
         p[1] = pt[1];
         p[2] = pt[2];
@@ -904,20 +879,15 @@ __device__ __forceinline__ double lm_ladder_resume(Ev&& ev, double (&p)[4], cons
         }
       } else {
         base += LPS;
-        if (base >= c.n_lambda) {  // no lambda improved: fit.py:246-247
-          active = false;
-          if (end) end->no_lambda = true;
-        }
+        if (base >= c.n_lambda) active = false;  // no lambda improved: fit.py:246-247
       }
     }
   }
-  if (end) end->last2 = last2;
   return e.ssq;
 }
 
 template <int LPS, typename Ev>
-__device__ __forceinline__ double lm_descend_ladder(Ev&& ev, double (&p)[4], const LMConst& c, bool live = true,
-                                                    DescentEnd* end = nullptr) {
+__device__ __forceinline__ double lm_descend_ladder(Ev&& ev, double (&p)[4], const LMConst& c, bool live = true) {
   using Trial = typename std::decay_t<Ev>::Trial;
   Eval e;
   {
@@ -925,7 +895,7 @@ __device__ __forceinline__ double lm_descend_ladder(Ev&& ev, double (&p)[4], con
     ev.trial(p, t0);
     ev.accept(p, t0, e);
   }
-  return lm_ladder_resume<LPS>(ev, p, c, e, 0, 0, live, end);
+  return lm_ladder_resume<LPS>(ev, p, c, e, 0, 0, live);
 }
 
 // fit.py:260-320 (_find_best_initial_guess). jtab: n_grid rows of J_1..J_ndata(mtry)
@@ -1007,42 +977,13 @@ DFMI_HDI void m_grid_seed(QF&& Q, int ndata, const double* __restrict__ jtab, co
 // (host build / equivalence tests). Q: QI accessor for the m-grid re-seed (runtime
 // harmonic index: memory, never a register array).
 template <int FLAT, typename Ev>
-DFMI_HDI double descend_t(Ev&& ev, double (&pp)[4], const LMConst& c, DescentEnd* end = nullptr) {
+DFMI_HDI double descend_t(Ev&& ev, double (&pp)[4], const LMConst& c) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (FLAT == 2) return lm_descend_ladder<kLadderLanes>(ev, pp, c, true, end);
+  if constexpr (FLAT == 2) return lm_descend_ladder<kLadderLanes>(ev, pp, c);
   else
 #endif
-  if constexpr (FLAT == 1) return lm_descend_flat(ev, pp, c, end);
-  else return lm_descend(ev, pp, c, end);
-}
-
-// The register path's literal finisher: where its descent ended on "no lambda improved" right
-// after an accepted step of fin_lo < |dp| < fin_hi (an ill-conditioned fit stopped at the
-// noise floor, ~1e-9 from the minimum along a weak direction of J^T J, where the accept test
-// ssq_try < ssq0 of fit.py:240 is decided by the last bits of ssq), the descent goes on with
-// the literal evaluation (eval_gen: the reference's per-residual Jacobian, damped_solve: dgesv
-// semantics) from that point, so the last sub-1e-9 decisions are taken with arithmetic
-// closer to the reference's. One lane per fit, out of line on the device (the
-// hot path keeps its register allocation; the lanes that need it are few).
-template <typename QM>
-#if defined(__HIP_DEVICE_COMPILE__)
-__device__ __attribute__((noinline))
-#else
-inline
-#endif
-double literal_finish(const QM& qm, int ndata, const LMConst& c, double* p4) {
-  double p[4] = {p4[0], p4[1], p4[2], p4[3]};
-  GenSplitEval<QM> gev{qm, ndata};
-  const double ssq = lm_descend_flat(gev, p, c);
-  p4[0] = p[0];
-  p4[1] = p[1];
-  p4[2] = p[2];
-  p4[3] = p[3];
-  return ssq;
-}
-
-DFMI_HDI bool finisher_wanted(const LMConst& c, const DescentEnd& end) {
-  return c.fin_hi2 > 0.0 && end.no_lambda && end.last2 > c.fin_lo2 && end.last2 < c.fin_hi2;
+  if constexpr (FLAT == 1) return lm_descend_flat(ev, pp, c);
+  else return lm_descend(ev, pp, c);
 }
 
 // fit.py:334-360 after the first descent (its result p, ssq): status, the m-grid re-seed
@@ -1083,15 +1024,10 @@ DFMI_HDI int fit_finish_t(Ev&& ev, QF&& Q, int ndata, const double* __restrict__
   return status;
 }
 
-// FIN: the register path's literal finisher (literal_finish) after the first descent.
-template <int FLAT = 1, bool FIN = false, typename Ev, typename QF>
+template <int FLAT = 1, typename Ev, typename QF>
 DFMI_HDI int fit_segment_t(Ev&& ev, QF&& Q, int ndata, const double* __restrict__ jtab, const LMConst& c,
                            double (&p)[4], double& ssq_out) {
-  DescentEnd end;
-  double ssq = descend_t<FLAT>(ev, p, c, &end);
-  if constexpr (FIN) {
-    if (finisher_wanted(c, end)) ssq = literal_finish<std::decay_t<QF>>(Q, ndata, c, p);
-  }
+  const double ssq = descend_t<FLAT>(ev, p, c);
   return fit_finish_t<FLAT>(ev, Q, ndata, jtab, c, p, ssq, ssq_out);
 }
 
@@ -1105,7 +1041,7 @@ __host__ __device__ __forceinline__ int fit_segment_q2(const QE& qe, const QM& q
                                                     double (&p)[4], double& ssq_out) {
   if constexpr (NDMAX > 0) {
     SplitEval<NDMAX, QE> ev{qe, ndata, c.trig};
-    return fit_segment_t<FLAT, true>(ev, qm, ndata, jtab, c, p, ssq_out);
+    return fit_segment_t<FLAT>(ev, qm, ndata, jtab, c, p, ssq_out);
   } else if constexpr (FLAT == 2) {  // lambda ladder: full trials (FullGenEval)
     FullGenEval<QE> ev{qe, ndata};
     return fit_segment_t<FLAT>(ev, qm, ndata, jtab, c, p, ssq_out);

@@ -1,4 +1,6 @@
-"""CPU study of the register path's literal finisher (lm.h literal_finish) on the random LM
+"""CPU study of the register path's literal finisher (lm.h literal_finish, in the tree of
+commit 9a49333 only: it never changed a result and was reverted; profiles/r05/
+lm_finisher_study.jsonl holds the output) on the random LM
 vectors of tests/test_gpu_lm_stress.py: the host build of the register path with the finisher
 off and on (tests/hostcheck hc_fit_segments_fin) and the literal general path, against the
 C restatement (oracle/csrc/nls_scalar.c) and, for every vector any of them puts beyond 5e-10

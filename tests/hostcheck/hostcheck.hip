@@ -89,57 +89,6 @@ void hc_ssq_points(const double* qi, int ndata, const double* p, long n, int reg
   }
 }
 
-// The register path with the literal finisher band (fin_lo, fin_hi on |dp|; fin_hi = 0: off):
-// as hc_fit_segments, plus per fit whether the first descent ended on "no lambda improved" (bit
-// 0) and whether the finisher ran (bit 1), and that descent's last accepted |dp| (last_dp).
-int hc_fit_segments_fin(const double* qi, long n, int ndata, const double* guess, const double* consts,
-                        const double* lambdas, int n_lambda, double fin_lo, double fin_hi, double* p_out,
-                        double* ssq_out, int* status_out, int* end_out, double* last_dp) {
-  dfmi::LMConst c{};
-  c.max_steps = (int)consts[0];
-  c.conv_improve = consts[1];
-  c.conv_param_change = consts[2];
-  c.fitok_threshold = consts[3];
-  const double gmin = consts[4], gmax = consts[5], gstep = consts[6];
-  c.bessel_amp_thr = consts[7];
-  c.sincos_amp_thr = consts[8];
-  c.min_step_norm = consts[9];
-  c.n_lambda = n_lambda;
-  for (int i = 0; i < n_lambda; ++i) c.lambdas[i] = lambdas[i];
-  const double stop = gmax + gstep;
-  const double len = ceil((stop - gmin) / gstep);
-  c.n_grid = len > 0 ? (int)len : 0;
-  c.grid_min = gmin;
-  c.grid_delta = (gmin + gstep) - gmin;
-  c.trig = dfmi_trig_k();
-  c.fin_lo2 = fin_lo * fin_lo;
-  c.fin_hi2 = fin_hi * fin_hi;
-  if (ndata > 12) return -1;
-  std::vector<double> tab((size_t)(c.n_grid > 0 ? c.n_grid : 1) * ndata);
-  std::vector<double> row(ndata + 2);
-  for (int g = 0; g < c.n_grid; ++g) {
-    dfmi_bessel_table(gmin + g * c.grid_delta, ndata, row.data());
-    for (int i = 0; i < ndata; ++i) tab[(size_t)g * ndata + i] = row[i + 1];
-  }
-  for (long s = 0; s < n; ++s) {
-    const dfmi::QGlobal qg{qi + s, n, ndata};
-    double p[4] = {guess[s * 4], guess[s * 4 + 1], guess[s * 4 + 2], guess[s * 4 + 3]};
-    {
-      double q[4] = {p[0], p[1], p[2], p[3]};
-      dfmi::SplitEval<12, dfmi::QGlobal> ev{qg, ndata, c.trig};
-      dfmi::DescentEnd end;
-      dfmi::lm_descend_flat(ev, q, c, &end);
-      end_out[s] = (end.no_lambda ? 1 : 0) | (dfmi::finisher_wanted(c, end) ? 2 : 0);
-      last_dp[s] = sqrt(end.last2);
-    }
-    double ssq;
-    status_out[s] = dfmi::fit_segment_q<12, dfmi::QGlobal>(qg, ndata, tab.data(), c, p, ssq);
-    for (int i = 0; i < 4; ++i) p_out[s * 4 + i] = p[i];
-    ssq_out[s] = ssq;
-  }
-  return 0;
-}
-
 // qi component-major (qi[c*n + s]); guess n x 4; constants in the reference order.
 int hc_fit_segments(const double* qi, long n, int ndata, const double* guess, const double* consts,
                     const double* lambdas, int n_lambda, double* p_out, double* ssq_out, int* status_out,

@@ -1,29 +1,28 @@
 """The GPU LM (dfmi_lm: fit.fit, fit.py:322-361, every vector its own guess) on 600,000
-random QI vectors against the scalar C restatement of fit.fit (oracle/csrc/nls_scalar.c
-lm_scalar_fit, which meets the reference's own LM vectors with the GPU's gates:
-tests/test_oracle_c.py), as a stress test across the parameter space the golden vectors
-sample only sparsely: ndata 5 / 10 / 16 (exact-ndata register path, masked register path,
-and the 16-harmonic variant), amplitude 0.2..3, m 1..25, any phi, psi in [-1, 1], noise from
-1e-7 to 1e-1 of the amplitude, guesses from near the truth to far off (m-grid re-seeds,
-status 1 / 2, sign normalisation, phi wrap).
+random QI vectors, screened against the scalar C restatement of fit.fit (oracle/csrc/nls_scalar.c
+lm_scalar_fit) and judged against the numpy oracle itself (oracle/nls_oracle.py = the
+reference's fit.fit, bit-exact on its golden vectors), as a stress test across the parameter
+space the golden vectors sample only sparsely: ndata 5 / 10 / 16 (exact-ndata register path,
+masked register path, and the 16-harmonic variant), amplitude 0.2..3, m 1..25, any phi, psi in
+[-1, 1], noise from 1e-7 to 1e-1 of the amplitude, guesses from near the truth to far off
+(m-grid re-seeds, status 1 / 2, sign normalisation, phi wrap).
 
-Gates: status equal on >= 99.9 % of the vectors; where both report status 0, every
-parameter within max(1e-9, the reference's resolution, conftest.resolution_tol) on
->= 99.9 % of them. Measured (profiles/r03q_lm_stress.log): status equal on all 600,000;
-beyond the resolution 79 / 161 k (ndata 5), 16 / 146 k (10), 14 / 139 k (16). Those are
-ill-conditioned, low-noise fits where the LM ends on "no lambda improved" about 1e-9 from
-the minimum, at a point set by the last bits of the Jacobian and of ssq: on 40 such ndata-5
-vectors the host build of the register path lands beyond the resolution from the numpy
-oracle (= the reference) on 31, and the literal C restatement itself on 7 — the
-reference's answer there is not determined to 1e-9 by its algorithm, only by its exact
-arithmetic (cos(fl(phi + j pi/2)), scipy's jv, BLAS summation order)."""
+Gates: status equal to the C port's on >= 99.9 % of the vectors. Where both report status 0,
+every vector the GPU puts more than 5e-10 from the C port is refitted by the numpy oracle;
+it must be within max(1e-9, the reference's resolution, conftest.resolution_tol) of the
+oracle's answer, or within 1.5x the oracle's OWN move when its QI moves by one ulp
+(tests/helpers/lm_oracle_check.py: there the reference's answer is set by its last bits, not
+by its algorithm). At most 1e-4 of the status-0 vectors may miss both (measured round 5 on
+the host build of the same arithmetic: the register path beyond the resolution on 35 of
+160,906 ndata-5 vectors, the literal C port on 25, the literal general path on 40; a literal
+"finisher" of the register path changed none of them, profiles/r05/lm_finisher_study.jsonl)."""
 import ctypes
 import os
 
 import numpy as np
 import pytest
 
-from conftest import resolution_tol, wrapped
+from conftest import wrapped
 
 pytestmark = pytest.mark.gpu
 
@@ -90,9 +89,21 @@ def test_gpu_lm_random_vectors_vs_c_restatement(nd):
     both0 = match & (rs == 0)
     d = np.stack([np.abs(gp[:, 0] - ref[:, 0]), np.abs(gp[:, 1] - ref[:, 1]), wrapped(gp[:, 2] - ref[:, 2]),
                   np.abs(gp[:, 3] - ref[:, 3])], axis=1)
-    cand = np.nonzero(both0 & (d.max(axis=1) > 1e-9))[0]
-    bad = [int(k) for k in cand if np.any(d[k] > resolution_tol(nd, qi[k], ref[k, :4]))]
-    frac_bad = len(bad) / max(1, int(both0.sum()))
-    print(f"ndata {nd}: status match {match.mean():.5f}, status-0 {both0.mean():.3f}, beyond 1e-9 {cand.size}, "
-          f"beyond resolution {len(bad)}")
-    assert frac_bad <= 1e-3, (len(bad), bad[:5], d[bad[:5]] if bad else None)
+    cand = np.nonzero(both0 & (d.max(axis=1) > 5e-10))[0]
+    import multiprocessing as mp
+    import sys
+    from concurrent.futures import ProcessPoolExecutor
+    sys.path.insert(0, os.path.join(ROOT, "tests", "helpers"))
+    import lm_oracle_check as LC
+    procs = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 8))
+    with ProcessPoolExecutor(procs, mp_context=mp.get_context("spawn")) as ex:
+        orc = list(ex.map(LC.oracle_fit, [(nd, qi[k], guess[k]) for k in cand], chunksize=32))
+        beyond = [(k, o) for k, o in zip(cand, orc) if o[0] == 0 and np.any(LC._dist(gp[k][None], o[1][None])[0] > o[2])]
+        spreads = list(ex.map(LC.oracle_spread, [(nd, qi[k], guess[k], o[1], 4) for k, o in beyond]))
+    unexplained = [int(k) for (k, o), sp in zip(beyond, spreads)
+                   if np.any(LC._dist(gp[k][None], o[1][None])[0] > np.maximum(o[2], 1.5 * sp))]
+    n0 = max(1, int(both0.sum()))
+    print(f"ndata {nd}: status match {match.mean():.5f}, status-0 {both0.mean():.3f}, beyond 5e-10 of the C port "
+          f"{cand.size}, beyond the resolution of the numpy oracle {len(beyond)}, of those beyond the oracle's own "
+          f"one-ulp spread {len(unexplained)} ({len(unexplained) / n0:.2e})")
+    assert len(unexplained) <= 1e-4 * n0, unexplained[:10]

@@ -15,6 +15,7 @@ import logging
 import time
 
 import numpy as np
+import pandas as pd
 import scipy.constants as sc
 
 from . import fitters as _fitters
@@ -22,6 +23,21 @@ from .data import DeepFitObject
 from .physics import DFMIObject, InterferometerConfig, SignalGenerator
 
 log = logging.getLogger(__name__)
+
+
+_time_axes = {}
+
+
+def _time_axis(nbuf, fs):
+    """core.py:515: np.arange(0, nbuf / fs, 1 / fs), formed once per (nbuf, fs) and handed out
+    as a fresh copy (the caller owns its array, as with the reference's)."""
+    key = (int(nbuf), float(fs))
+    t = _time_axes.get(key)
+    if t is None:
+        if len(_time_axes) > 64:
+            _time_axes.clear()
+        t = _time_axes[key] = np.arange(0, nbuf / fs, 1.0 / fs)
+    return t.copy()
 
 
 def vectorized_downsample(signal, R):
@@ -252,7 +268,13 @@ class DeepFitFramework:
 
     def _finish(self, fit_label, main_label, raw, method, df, n, R, fs, nbuf):
         if method in ("nls", "ekf"):
-            df["tau"] = df["m"] / (2 * np.pi * raw.sim.laser.df) if raw.sim else 0.0
+            # core.py:506-509: df['tau'] = df['m'] / (2 pi df) (0.0 without a sim). The column is
+            # appended by rebuilding the frame over the same column arrays (pandas' __setitem__
+            # would copy the array in), same columns, order and dtypes
+            cols = {k: df[k].to_numpy() for k in df.columns}
+            m = cols["m"]
+            cols["tau"] = m / (2 * np.pi * raw.sim.laser.df) if raw.sim else np.zeros(m.shape[0])
+            df = pd.DataFrame(cols, copy=False)
         _fitters.mark("tau")
         self.fits_df[fit_label] = df
         fit = DeepFitObject()
@@ -262,7 +284,7 @@ class DeepFitFramework:
         for k in ("ssq", "amp", "m", "tau", "phi", "psi", "dc"):
             setattr(fit, k, df[k].to_numpy())
         _fitters.mark("columns")
-        fit.time = np.arange(0, fit.ssq.shape[0] / fit.fs, 1.0 / fit.fs)
+        fit.time = _time_axis(fit.ssq.shape[0], fit.fs)
         fit.label = fit_label
         self.fits[fit_label] = fit
         _fitters.mark("fitobj")

@@ -16,7 +16,8 @@
 //
 // This replaces scipy.special.jv, the third-party Bessel the reference calls at
 // fit.py:106,108,160,275-276. Accuracy against the
-// scipy 1.15.3 table in tests/golden/bessel.npz: see tests/test_bessel_host.py.
+// scipy 1.15.3 table in tests/golden/bessel.npz: tests/test_host_numerics.py::test_bessel_vs_scipy_table
+// (host build) and tests/test_gpu_numerics.py (device).
 #pragma once
 #include <math.h>
 #include <stdint.h>

@@ -31,8 +31,21 @@ LAMBDA_LADDER = (0.0, 1e-7, 1e-5, 1e-3, 1e-1, 1.0, 10.0, 100.0)  # fit.py:222
 MIN_STEP_NORM = 1e-15  # fit.py:230
 
 
+_cfg_cache = {}
+
+
 def lm_config() -> _lib.LMConfig:
-    """dfmi_lm_config from the module globals as they are NOW."""
+    """dfmi_lm_config from the module globals as they are NOW (built once per distinct set of
+    values: a caller that changes a constant gets a new struct on its next call)."""
+    key = (MAX_LMA_STEPS, tuple(LAMBDA_LADDER), MIN_STEP_NORM, LMA_CONVERGENCE_IMPROVE, LMA_CONVERGENCE_PARAM_CHANGE,
+           FITOK_THRESHOLD, M_GRID_MIN, M_GRID_MAX, M_GRID_STEP, BESSEL_AMP_THRESHOLD, SINCOS_AMP_THRESHOLD)
+    cfg = _cfg_cache.get(key)
+    if cfg is None:
+        cfg = _cfg_cache[key] = _lm_config_build()
+    return cfg
+
+
+def _lm_config_build() -> _lib.LMConfig:
     cfg = _lib.LMConfig()
     cfg.max_lma_steps = int(MAX_LMA_STEPS)
     lad = tuple(LAMBDA_LADDER)

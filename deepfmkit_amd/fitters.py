@@ -106,7 +106,9 @@ def nls_records(records, f_samp, f_mod, R, nbuf, ndata=10, init_guess=(1.6, 6.0,
         import torch
         if x.dtype != torch.float64 or x.stride(-1) != 1:
             raise ValueError("device records must be contiguous float64 rows")
-        out = torch.empty((6, nseg), dtype=torch.float64, device=x.device)
+        # rows 0..5 of one (7, nseg) block: the six result columns; row 6 receives fitok as
+        # int64 (frame_from), so the whole result leaves the device in one copy
+        out = torch.empty((7, nseg), dtype=torch.float64, device=x.device)[:6]
         ok = torch.empty(nseg, dtype=torch.int32, device=x.device)
         mark("alloc")
         with _on_device(x):
@@ -181,20 +183,43 @@ def nls_record_devices(x, f_samp, f_mod, R, nbuf, devices, ndata=10, init_guess=
 
 def frame_from(cols, fitok):
     """DataFrame with the reference's column set and dtypes (fitters.py:55-58, 428): float64
-    amp, m, phi, psi, dc, ssq and int64 fitok. cols (6, n) in that order becomes the frame's
-    float block as it is (pandas keeps a block as (columns, rows): the transpose is a view),
-    instead of seven 1-D arrays consolidated into a new block (1.2 ms -> ~0.1 ms at 100k rows)."""
+    amp, m, phi, psi, dc, ssq and int64 fitok, one 1-D array per column (a dict frame built
+    with copy=False wraps them as they are: no consolidation copy).
+
+    Device results (nls_records' (6, n) rows of a (7, n) block and the int32 status): the status
+    is widened to int64 into the block's spare row on the device, the whole block goes to
+    pinned host memory in ONE asynchronous copy, and the frame is built over that memory while
+    the kernels and the copy run; one stream synchronisation, then the frame is returned. The
+    pinned block belongs to this frame's arrays (torch's caching host allocator reuses it once
+    they are gone)."""
     if hasattr(cols, "cpu"):
+        import torch
+        n = cols.shape[1]
+        base = cols
+        if cols.dim() == 2 and cols.shape[0] == 6 and cols.stride(0) == n and cols.stride(1) == 1 and \
+                cols.untyped_storage().nbytes() >= 7 * n * 8:
+            base = torch.as_strided(cols, (7, n), (n, 1))
+        else:  # a caller's own (6, n) tensors: same copy through a fresh block
+            base = torch.empty((7, n), dtype=torch.float64, device=cols.device)
+            base[:6].copy_(cols)
+        stream = torch.cuda.current_stream(cols.device)
+        base[6].view(torch.int64).copy_(fitok)
+        host = torch.empty((7, n), dtype=torch.float64, pin_memory=True)
+        host.copy_(base, non_blocking=True)
+        done = torch.cuda.Event()
+        done.record(stream)
+        h = host.numpy()
+        df = pd.DataFrame(dict(zip(COLUMNS, [h[0], h[1], h[2], h[3], h[4], h[5], h[6].view(np.int64)])), copy=False)
+        mark("frame_prebuilt")
         if MARKS is not None:  # profiling: the wait for the kernels apart from the copy
-            import torch
-            torch.cuda.current_stream(cols.device).synchronize()
+            stream.synchronize()
             mark("gpu_done")
-        cols = cols.cpu().numpy()
-        fitok = fitok.cpu().numpy()
+        done.synchronize()
         mark("d2h")
+        return df
     cols = np.ascontiguousarray(cols, dtype=np.float64)
-    df = pd.DataFrame(cols[:6].T, columns=COLUMNS[:6], copy=False)
-    df["fitok"] = np.asarray(fitok).astype(np.int64)
+    df = pd.DataFrame(dict(zip(COLUMNS, [cols[0], cols[1], cols[2], cols[3], cols[4], cols[5],
+                                         np.asarray(fitok).astype(np.int64)])), copy=False)
     mark("frame")
     return df
 

@@ -106,7 +106,7 @@ struct PitRule {
 // A snapshot (fitters.py:305-307) written by this pass: its largest relative move since the
 // previous pass's value at the same place (the states buffer itself: zeros before the first
 // pass, whose move pit_decide ignores) into d.
-__device__ __forceinline__ void pit_snapshot(double* __restrict__ so, const double (&st)[5], double& d) {
+__host__ __device__ __forceinline__ void pit_snapshot(double* __restrict__ so, const double (&st)[5], double& d) {
 #pragma unroll
   for (int c = 0; c < 5; ++c) {
     const double m = fabs(st[c] - so[c]) / fmax(1.0, fabs(st[c]));
@@ -115,7 +115,7 @@ __device__ __forceinline__ void pit_snapshot(double* __restrict__ so, const doub
   }
 }
 
-__device__ __forceinline__ void pit_decide(PitChan& c, double d, const PitRule& ru, double* hist) {
+__host__ __device__ __forceinline__ void pit_decide(PitChan& c, double d, const PitRule& ru, double* hist) {
   const int pass = c.passes;
   c.passes = pass + 1;
   if (pass == 0) d = __builtin_nan("");  // no previous pass to have moved from

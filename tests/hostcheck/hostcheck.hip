@@ -2,7 +2,8 @@
 //
 // Compiles deepfmkit_amd/csrc/dfmi_math.h and lm.h (whose numerics are
 // __host__ __device__) for the CPU so the CPU test suite can check the Bessel
-// walk and the per-segment LM against the golden vectors without a GPU. The
+// walk and the per-segment LM against the golden vectors without a GPU; also
+// the EKF parallel-in-time stop rule (ekf_pit.h pit_decide). The
 // product library never links this; the GPU parity tests (tests/test_gpu_*.py)
 // exercise the real kernels.
 #include <vector>
@@ -10,6 +11,7 @@
 #include "../../deepfmkit_amd/csrc/lm.h"
 #include "../../deepfmkit_amd/csrc/np_sum.h"
 #include "../../deepfmkit_amd/csrc/synth.h"
+#include "../../deepfmkit_amd/csrc/ekf_pit.h"
 
 namespace {
 struct HKey {
@@ -85,6 +87,31 @@ void hc_ssq_points(const double* qi, int ndata, const double* p, long n, int reg
       dfmi::Eval e;
       dfmi::eval_gen(qg, ndata, pp, e);
       out[i] = e.ssq;
+    }
+  }
+}
+
+// ekf_pit.h's stop rule fed a channel's move sequence (moves[0] is pass 0's, ignored as the
+// device ignores it): the pass after which the status left 0 (0: never) and that status.
+void hc_pit_decide(const double* moves, int n, double tol, int stall_max, int cap, int* passes_out,
+                   int* status_out) {
+  dfmi::PitChan c{};
+  c.dprev = __builtin_nan("");
+  c.rho = -1.0;
+  for (int i = 0; i < dfmi::kPitTrend; ++i) c.dold[i] = __builtin_nan("");
+  dfmi::PitRule ru{};
+  ru.tol = tol;
+  ru.noise = tol;
+  ru.stall_max = stall_max;
+  ru.cap = cap;
+  *passes_out = 0;
+  *status_out = 0;
+  for (int k = 0; k < n && k < cap; ++k) {
+    dfmi::pit_decide(c, moves[k], ru, nullptr);
+    if (c.status) {
+      *passes_out = c.passes;
+      *status_out = c.status;
+      return;
     }
   }
 }

@@ -260,18 +260,25 @@ class DeepFitFramework:
                 log.error(f"W-DFMI method '{method}' requires a valid 'witness_label'.")
                 return
             fitter_args["witness_raw"] = self.raws[witness_label]
-        df = fitter_map[method](fit_config).fit(**fitter_args, **kwargs)
+        fitter = fitter_map[method](fit_config)
+        df = fitter.fit(**fitter_args, **kwargs)
         if df is None or df.empty:
             log.error(f"{fitter_map[method].__name__} returned no results.")
             return None
-        return self._finish(fit_label, main_label, raw, method, df, n, R, fs, nbuf)
+        # the package's own NLS fitter returns frame_from's frame untouched: its column arrays
+        # can be used as they are (any other fitter's frame is read through pandas)
+        known = _fitters.frame_arrays(df) if type(fitter) is _fitters.StandardNLSFitter else None
+        return self._finish(fit_label, main_label, raw, method, df, n, R, fs, nbuf, known)
 
-    def _finish(self, fit_label, main_label, raw, method, df, n, R, fs, nbuf):
-        if method in ("nls", "ekf"):
+    def _finish(self, fit_label, main_label, raw, method, df, n, R, fs, nbuf, known=None):
+        arrays, with_tau = known if known is not None else (None, None)
+        cols = dict(arrays) if arrays is not None else {k: df[k].to_numpy() for k in df.columns}
+        if method == "nls" and with_tau is not None:
+            df, cols["tau"] = with_tau  # the same columns with tau, formed by the fitter (frame_from)
+        elif method in ("nls", "ekf"):
             # core.py:506-509: df['tau'] = df['m'] / (2 pi df) (0.0 without a sim). The column is
             # appended by rebuilding the frame over the same column arrays (pandas' __setitem__
             # would copy the array in), same columns, order and dtypes
-            cols = {k: df[k].to_numpy() for k in df.columns}
             m = cols["m"]
             cols["tau"] = m / (2 * np.pi * raw.sim.laser.df) if raw.sim else np.zeros(m.shape[0])
             df = pd.DataFrame(cols, copy=False)
@@ -282,7 +289,7 @@ class DeepFitFramework:
         fit.n, fit.R, fit.fs, fit.nbuf, fit.ndata, fit.init_a, fit.init_m = n, R, fs, nbuf, 0, 0, 0
         fit.t0, fit.f_samp, fit.f_mod = raw.t0, raw.f_samp, raw.f_mod
         for k in ("ssq", "amp", "m", "tau", "phi", "psi", "dc"):
-            setattr(fit, k, df[k].to_numpy())
+            setattr(fit, k, cols[k] if k in cols else df[k].to_numpy())
         _fitters.mark("columns")
         fit.time = _time_axis(fit.ssq.shape[0], fit.fs)
         fit.label = fit_label

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import logging
 import time
+import weakref
 from abc import ABC, abstractmethod
 
 import numpy as np
@@ -181,7 +182,36 @@ def nls_record_devices(x, f_samp, f_mod, R, nbuf, devices, ndata=10, init_guess=
     return np.concatenate(out_cols, axis=1), np.concatenate(out_ok)
 
 
-def frame_from(cols, fitok):
+# The 1-D column arrays a frame_from frame was built over, by id(frame) while the frame lives
+# (and, for the facade, the frame with core.py:506-509's tau column already appended): core's
+# _finish takes them from here for the package's own NLS fitter (a pandas column access costs
+# ~10 us each, a frame construction ~40 us) after checking the entry belongs to that frame.
+_FRAME_ARRAYS = {}
+NO_TAU = object()
+
+
+def _remember(df, arrays, with_tau=None):
+    key = id(df)
+    _FRAME_ARRAYS[key] = (weakref.ref(df), arrays, with_tau)
+    weakref.finalize(df, _FRAME_ARRAYS.pop, key, None)
+    return df
+
+
+def frame_arrays(df):
+    """The column arrays of a frame built by frame_from (dict name -> array) and, when frame_from
+    formed it, (the frame with tau appended, the tau array) (else None); None for other frames."""
+    e = _FRAME_ARRAYS.get(id(df))
+    if e is None or e[0]() is not df or list(df.columns) != list(e[1]):
+        return None
+    return e[1], e[2]
+
+
+def tau_divisor(raw):
+    """core.py:506-509: tau = m / (2 pi df), or 0.0 without a simulation object (None here)."""
+    return 2 * np.pi * raw.sim.laser.df if raw.sim else None
+
+
+def frame_from(cols, fitok, tau_div=NO_TAU):
     """DataFrame with the reference's column set and dtypes (fitters.py:55-58, 428): float64
     amp, m, phi, psi, dc, ssq and int64 fitok, one 1-D array per column (a dict frame built
     with copy=False wraps them as they are: no consolidation copy).
@@ -191,7 +221,9 @@ def frame_from(cols, fitok):
     pinned host memory in ONE asynchronous copy, and the frame is built over that memory while
     the kernels and the copy run; one stream synchronisation, then the frame is returned. The
     pinned block belongs to this frame's arrays (torch's caching host allocator reuses it once
-    they are gone)."""
+    they are gone). With tau_div (tau_divisor(raw), the facade's NLS path) the frame core's
+    _finish stores — the same columns plus tau = m / tau_div, numpy's division — is prebuilt
+    too, tau filled after the synchronisation."""
     if hasattr(cols, "cpu"):
         import torch
         n = cols.shape[1]
@@ -209,17 +241,25 @@ def frame_from(cols, fitok):
         done = torch.cuda.Event()
         done.record(stream)
         h = host.numpy()
-        df = pd.DataFrame(dict(zip(COLUMNS, [h[0], h[1], h[2], h[3], h[4], h[5], h[6].view(np.int64)])), copy=False)
+        arrays = dict(zip(COLUMNS, [h[0], h[1], h[2], h[3], h[4], h[5], h[6].view(np.int64)]))
+        with_tau = tau = None
+        if tau_div is not NO_TAU:
+            tau = np.empty(n) if tau_div is not None else np.zeros(n)
+            with_tau = pd.DataFrame({**arrays, "tau": tau}, copy=False)
+        df = _remember(pd.DataFrame(arrays, copy=False), arrays, None if with_tau is None else (with_tau, tau))
         mark("frame_prebuilt")
         if MARKS is not None:  # profiling: the wait for the kernels apart from the copy
             stream.synchronize()
             mark("gpu_done")
         done.synchronize()
         mark("d2h")
+        if tau is not None and tau_div is not None:
+            np.divide(h[1], tau_div, out=tau)
         return df
     cols = np.ascontiguousarray(cols, dtype=np.float64)
-    df = pd.DataFrame(dict(zip(COLUMNS, [cols[0], cols[1], cols[2], cols[3], cols[4], cols[5],
-                                         np.asarray(fitok).astype(np.int64)])), copy=False)
+    arrays = dict(zip(COLUMNS, [cols[0], cols[1], cols[2], cols[3], cols[4], cols[5],
+                                np.asarray(fitok).astype(np.int64)]))
+    df = _remember(pd.DataFrame(arrays, copy=False), arrays)
     mark("frame")
     return df
 
@@ -280,7 +320,7 @@ class StandardNLSFitter(BaseFitter):
         cols, ok = nls_records(x.reshape(1, N), main_raw.f_samp, main_raw.f_mod, R, nbuf, ndata,
                                (init_a, init_m, 0.0, init_psi), parallel=parallel,
                                n_cores=kwargs.get("n_cores") if parallel else None)
-        return frame_from(cols, ok)
+        return frame_from(cols, ok, tau_divisor(main_raw))
 
 
 class EKFFitter(BaseFitter):

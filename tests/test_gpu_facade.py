@@ -59,3 +59,22 @@ def test_device_frames_survive_later_fits(torch):
     t1 = fits[0].time
     t1[0] = -1.0  # every fit object owns its time axis (the cached one is handed out as a copy)
     assert fits[1].time[0] == 0.0
+
+
+def test_device_record_with_sim_tau_matches_host_and_reference(torch, manifest, records_npz):
+    """A simulated record (tau = m / (2 pi df), core.py:506-509, formed inside the fitter's
+    prebuilt frame for a device record) fitted from HBM and from host memory: the same frame
+    bit for bit, and tau equal to the reference's own facade output (tests/golden)."""
+    from conftest import make_record
+    e = next(r for r in manifest["records"] if r["name"] == "config1")
+    dff = make_record(e)
+    raw = dff.raws["config1"]
+    dff.fit("config1", n=e["n"], fit_label="host")
+    host_df = dff.fits_df["host"]
+    raw.data = torch.from_numpy(raw.samples().copy()).to("cuda")
+    fo = dff.fit("config1", n=e["n"], fit_label="dev")
+    dev_df = dff.fits_df["dev"]
+    assert list(dev_df.columns) == list(host_df.columns)
+    np.testing.assert_array_equal(dev_df.to_numpy(), host_df.to_numpy())
+    np.testing.assert_array_equal(fo.tau, dev_df["tau"].to_numpy())
+    np.testing.assert_allclose(fo.tau, records_npz["config1_facade_tau"], rtol=0, atol=1e-18)

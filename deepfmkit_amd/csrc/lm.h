@@ -1190,8 +1190,10 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
     }
     put(s0, st, ssq);
     out[4 * out_ld + s0] = dcv;
-    if (k == 0)  // segments before `first` (the seed buffer) are fitted elsewhere: carry their dc
-      for (int64_t t = r * nbuf; t < r * nbuf + first; ++t) out[4 * out_ld + t] = qi[t * qi_ld + dfmi_row_dc(ndata)];
+    // first == 1: the record's seed buffer was fitted elsewhere (the fused seed kernel): carry
+    // its dc. (A launch over a later slice of the buffers, first > 1, leaves the segments
+    // before it to the launch that fitted them: nls_record_hostout's tail.)
+    if (k == 0 && first == 1) out[4 * out_ld + r * nbuf] = qi[r * nbuf * qi_ld + dfmi_row_dc(ndata)];
   } else {
     auto one = [&](int64_t sidx) {
       double ssq;
@@ -1277,8 +1279,8 @@ __global__ __launch_bounds__(64) void lm_ladder_kernel(
     fit(q, s0);
     if (lead) {
       out[4 * out_ld + s0] = q.at(dfmi_row_dc(ndata));
-      if (k == 0)  // segments before `first` (the seed buffer) are fitted elsewhere: carry their dc
-        for (int64_t t = r * nbuf; t < r * nbuf + first; ++t) out[4 * out_ld + t] = qi[t * qi_ld + dfmi_row_dc(ndata)];
+      if (k == 0 && first == 1)  // the seed buffer was fitted elsewhere: carry its dc (lm_chunks_kernel)
+        out[4 * out_ld + r * nbuf] = qi[r * nbuf * qi_ld + dfmi_row_dc(ndata)];
     }
   } else if constexpr (kQReg && CHAIN) {
     // warm-start chain (sequential / n_cores). Every LPS fits the group stages the QI of

@@ -19,7 +19,6 @@ LIB_PATH = os.path.join(_HERE, "libdfmi.so")
 
 DFMI_MEM_HOST = 0
 DFMI_MEM_DEVICE = 1
-DFMI_MEM_OUT_HOST = 2  # dfmi_nls_record: | DFMI_MEM_DEVICE -> results into pinned host memory
 MAX_LAMBDA = 16
 
 SYMBOLS = ("dfmi_lm_config_default", "dfmi_demod", "dfmi_lm", "dfmi_nls_record", "dfmi_ekf",

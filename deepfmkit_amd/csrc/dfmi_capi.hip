@@ -60,7 +60,6 @@ struct Tuning {
                          // 0 = always one lane per chain / segment
   int ws_streams = 4;    // caller streams whose workspaces are kept; a call from one more stream first
                          // drains the DEVICE (hipDeviceSynchronize) and frees the least recently used set
-  int out_split = 1;     // DFMI_MEM_OUT_HOST: copy the first 4/5 of the results under the rest's demodulation
   int ekf_pit = 1024;    // EKF parallel in time (ekf_pit.h) for up to this many channels of at least
                          // ekf_pit_min samples (1,024 channels at 400k samples: 48 vs 71 ms for the row
                          // kernel, r04z); 0 = the sequential kernels always
@@ -152,8 +151,6 @@ struct DeviceState {
   std::vector<std::array<hipEvent_t, 3>> ev_steps;
   void* pin = nullptr;  // pinned host scratch for the EKF's pass control read-backs
   size_t pin_n = 0;
-  hipStream_t copy = nullptr;  // device-to-host copies of DFMI_MEM_OUT_HOST results
-  hipEvent_t ev_c0 = nullptr, ev_c1 = nullptr;
 };
 
 std::map<int, DeviceState> g_dev;
@@ -875,94 +872,6 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
                    jtab, out, out_ld, fitok, st, rows);
 }
 
-// DFMI_MEM_DEVICE | DFMI_MEM_OUT_HOST: the record on the device, the results into pinned host
-// memory in stream order. The results leave the device in two pieces so that the first
-// piece's copy runs under the demodulation of the second: [seeds + demodulation + LM of the
-// first (1 - out_tail) of the buffers] -> copy of their columns on the copy stream || [the
-// demodulation + LM of the rest] -> copy of the rest; the caller's stream then waits for the
-// copies. Exposed after the kernels: the rest's copy only (config 2: ~20 of ~105 us). Same
-// kernels and bits as nls_record_device's fused path (segments are independent once the
-// seed is known); any other case computes everything, then copies once.
-int nls_record_hostout(int dev, const double* x, int64_t nrec, int64_t rec_stride, int64_t nbuf, int R, int ndata,
-                       double w0, int period, const double* init_guess_host, int parallel, int64_t nchunk,
-                       const dfmi_lm_config& cfg, const dfmi::LMConst& c, double* out_host, int32_t* fitok_host,
-                       hipStream_t st) {
-  const int64_t nseg = nrec * nbuf;
-  DeviceState& ds = *t_ds;
-  void *dout, *dst;
-  int rc;
-  if ((rc = workspace(dev, "o_out", (size_t)6 * nseg * 8, &dout))) return rc;
-  if ((rc = workspace(dev, "o_status", (size_t)nseg * 4, &dst))) return rc;
-  if (!ds.copy) {
-    HIPCHK(hipStreamCreateWithFlags(&ds.copy, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&ds.ev_c0, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&ds.ev_c1, hipEventDisableTiming));
-  }
-  double* out = (double*)dout;
-  int32_t* fitok = (int32_t*)dst;
-  const int64_t out_ld = nseg;
-  // the columns of buffers [b0, b1) to the host on the copy stream, after `ev` on st
-  auto copy_out = [&](int64_t b0, int64_t b1) -> int {
-    HIPCHK(hipEventRecord(ds.ev_c0, st));
-    HIPCHK(hipStreamWaitEvent(ds.copy, ds.ev_c0, 0));
-    HIPCHK(hipMemcpy2DAsync(out_host + b0, nseg * sizeof(double), out + b0, nseg * sizeof(double),
-                            (size_t)(b1 - b0) * sizeof(double), 6, hipMemcpyDeviceToHost, ds.copy));
-    HIPCHK(hipMemcpyAsync(fitok_host + b0, fitok + b0, (size_t)(b1 - b0) * sizeof(int32_t), hipMemcpyDeviceToHost,
-                          ds.copy));
-    return DFMI_OK;
-  };
-  auto join = [&]() -> int {  // the caller's stream continues after the copies
-    HIPCHK(hipEventRecord(ds.ev_c1, ds.copy));
-    HIPCHK(hipStreamWaitEvent(st, ds.ev_c1, 0));
-    return DFMI_OK;
-  };
-  const double* jtab = nullptr;
-  if ((rc = grid_table(dev, ndata, cfg, &jtab))) return rc;
-  const int64_t qs = dfmi_row_stride(ndata);
-  int L = period;
-  if (L == 0) L = detect_period_impl(w0, R, ndata);
-  // the tail: a fifth of the buffers (its copy stays exposed; the head's copy, 4/5 of the
-  // bytes, runs under the tail's demodulation, 4x longer than that copy at config 2)
-  const int64_t tail = nbuf / 5;
-  const bool split = t_tune.out_split && nrec == 1 && parallel && nchunk >= nbuf - 1 && tail >= 256 &&
-                     rows_supported(dev, x, R, R, ndata, w0, period) && L > 0;
-  if (split) {
-    const int64_t nb1 = nbuf - tail;
-    const double* tab = nullptr;
-    if ((rc = basis_table(dev, L, ndata, w0, st, &tab))) return rc;
-    void* rw = nullptr;
-    if ((rc = workspace(dev, "qrow", (size_t)qs * nseg * sizeof(double), &rw))) return rc;
-    dfmi::GuessInline ginl;
-    memset(&ginl, 0, sizeof(ginl));
-    for (int i = 0; i < 4; ++i) ginl.v[0][i] = init_guess_host[i];
-    // the head: seed + demodulation of buffers [0, nb1) in one launch, then their LM
-    rc = fused_seed_demod(dev, x, 1, nb1, R, ndata, L, tab, (double*)rw, qs, nullptr, ginl, jtab, c, out, out_ld,
-                          fitok, st);
-    if (rc < 0) return rc;
-    if (rc == 0) {
-      if ((rc = lm_device(dev, (double*)rw, qs, ndata, 1, nbuf, 1, nb1 - 1, nb1 - 1, out, nbuf, out_ld, nullptr, c,
-                          jtab, out, out_ld, fitok, st, true)))
-        return rc;
-      if ((rc = copy_out(0, nb1))) return rc;
-      // the tail: demodulation and LM of buffers [nb1, nbuf), seeded from buffer 0 on the device
-      if ((rc = demod_device(dev, x + nb1 * (int64_t)R, tail, R, R, ndata, w0, period, (double*)rw + nb1 * qs, qs,
-                             nullptr, st, true)))
-        return rc;
-      if ((rc = lm_device(dev, (double*)rw, qs, ndata, 1, nbuf, nb1, tail, tail, out, nbuf, out_ld, nullptr, c, jtab,
-                          out, out_ld, fitok, st, true)))
-        return rc;
-      if ((rc = copy_out(nb1, nbuf))) return rc;
-      g_last_demod = "hostout split " + std::to_string(nb1) + "+" + std::to_string(tail);
-      return join();
-    }
-  }
-  if ((rc = nls_record_device(dev, x, nrec, rec_stride, nbuf, R, ndata, w0, period, init_guess_host, parallel, nchunk,
-                              cfg, c, out, fitok, st)))
-    return rc;
-  if ((rc = copy_out(0, nbuf))) return rc;
-  return join();
-}
-
 }  // namespace
 
 namespace {
@@ -981,7 +890,6 @@ const std::map<std::string, Knob>& knobs() {
       {"wdfmi_accel", {&Tuning::wdfmi_accel, {0, 1, 2, 3}}},
       {"lm_ladder", {&Tuning::lm_ladder, {}}},
       {"ws_streams", {&Tuning::ws_streams, {}}},
-      {"out_split", {&Tuning::out_split, {0, 1}}},
       {"ekf_pit", {&Tuning::ekf_pit, {}}},
       {"ekf_pit_min", {&Tuning::ekf_pit_min, {}}},
       {"ekf_pit_block", {&Tuning::ekf_pit_block, {}}},
@@ -1621,18 +1529,6 @@ int dfmi_nls_record(const double* x, int64_t nrec, int64_t rec_stride, int64_t n
   if (mem == DFMI_MEM_DEVICE)
     return nls_record_device(dev, x, nrec, rec_stride, nbuf, R, ndata, w0, period, init_guess, parallel, nchunk, *cfg,
                              c, out, fitok, st);
-  if (mem == (DFMI_MEM_DEVICE | DFMI_MEM_OUT_HOST)) {
-    for (const void* p : {(const void*)out, (const void*)fitok}) {
-      hipPointerAttribute_t a;
-      if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost) {
-        (void)hipGetLastError();
-        return fail(DFMI_ERR_ARG, "DFMI_MEM_OUT_HOST: out and fitok must be pinned host memory");
-      }
-    }
-    return nls_record_hostout(dev, x, nrec, rec_stride, nbuf, R, ndata, w0, period, init_guess, parallel, nchunk,
-                              *cfg, c, out, fitok, st);
-  }
-  if (mem != DFMI_MEM_HOST) return fail(DFMI_ERR_ARG, "mem: DFMI_MEM_HOST, DFMI_MEM_DEVICE or DFMI_MEM_DEVICE | DFMI_MEM_OUT_HOST");
   const int64_t rs = (nrec > 1) ? rec_stride : nbuf * (int64_t)R;
   const size_t xb = (size_t)((nrec - 1) * rs + nbuf * (int64_t)R) * 8;
   void *dx, *dout, *dst;

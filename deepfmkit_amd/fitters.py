@@ -264,48 +264,6 @@ def frame_from(cols, fitok, tau_div=NO_TAU):
     return df
 
 
-def nls_record_frame(x, f_samp, f_mod, R, nbuf, ndata, init_guess, tau_div=NO_TAU):
-    """StandardNLSFitter's parallel fit (chunk size 1) of ONE record already on the GPU, straight
-    into a DataFrame (the facade's device-resident path, fitters.py:395-428 + core.py:506-509):
-    dfmi_nls_record with DFMI_MEM_DEVICE | DFMI_MEM_OUT_HOST writes the six result columns and
-    the status into pinned host memory in stream order (the library copies the first 4/5 of
-    the buffers while it demodulates the rest); the frame (and core's frame with tau, for
-    tau_div) is built over that memory while the GPU works; one stream synchronisation, then
-    the status is widened to int64 and tau formed (numpy's m / tau_div). Same bits as
-    frame_from(*nls_records(...)). The pinned memory belongs to the frame's arrays."""
-    import torch
-    lib = _lib.load()
-    nseg = int(nbuf)
-    host = torch.empty((6, nseg), dtype=torch.float64, pin_memory=True)
-    st32 = torch.empty(nseg, dtype=torch.int32, pin_memory=True)
-    g = np.ascontiguousarray(init_guess, dtype=np.float64)
-    cfg = _fit.lm_config()
-    mark("alloc")
-    with _on_device(x):
-        stream = torch.cuda.current_stream(x.device)
-        rc = lib.dfmi_nls_record(x.data_ptr(), 1, nbuf * R, nbuf, R, ndata, w0_of(f_mod, f_samp), 0, _lib.ptr(g), 1,
-                                 max(nbuf - 1, 1), cfg, host.data_ptr(), st32.data_ptr(),
-                                 _lib.DFMI_MEM_DEVICE | _lib.DFMI_MEM_OUT_HOST, stream.cuda_stream)
-    _lib.check(rc, "dfmi_nls_record")
-    mark("enqueue")
-    h = host.numpy()
-    ok64 = np.empty(nseg, dtype=np.int64)
-    arrays = dict(zip(COLUMNS, [h[0], h[1], h[2], h[3], h[4], h[5], ok64]))
-    with_tau = tau = None
-    if tau_div is not NO_TAU:
-        tau = np.empty(nseg) if tau_div is not None else np.zeros(nseg)
-        with_tau = pd.DataFrame({**arrays, "tau": tau}, copy=False)
-    df = _remember(pd.DataFrame(arrays, copy=False), arrays, None if with_tau is None else (with_tau, tau))
-    mark("frame_prebuilt")
-    stream.synchronize()
-    mark("gpu_done")
-    np.copyto(ok64, st32.numpy())
-    if tau is not None and tau_div is not None:
-        np.divide(h[1], tau_div, out=tau)
-    mark("d2h")
-    return df
-
-
 class BaseFitter(ABC):
     """fitters.py:164-208."""
 
@@ -359,14 +317,9 @@ class StandardNLSFitter(BaseFitter):
             cols, ok = nls_record_devices(x, main_raw.f_samp, main_raw.f_mod, R, nbuf, devices, ndata,
                                           (init_a, init_m, 0.0, init_psi))
             return frame_from(cols, ok)
-        guess = (init_a, init_m, 0.0, init_psi)
-        if _is_device_tensor(x) and parallel and kwargs.get("n_cores") is None and nbuf > 1:
-            import torch
-            if x.dtype == torch.float64 and x.is_contiguous():
-                return nls_record_frame(x, main_raw.f_samp, main_raw.f_mod, R, nbuf, ndata, guess,
-                                        tau_divisor(main_raw))
-        cols, ok = nls_records(x.reshape(1, N), main_raw.f_samp, main_raw.f_mod, R, nbuf, ndata, guess,
-                               parallel=parallel, n_cores=kwargs.get("n_cores") if parallel else None)
+        cols, ok = nls_records(x.reshape(1, N), main_raw.f_samp, main_raw.f_mod, R, nbuf, ndata,
+                               (init_a, init_m, 0.0, init_psi), parallel=parallel,
+                               n_cores=kwargs.get("n_cores") if parallel else None)
         return frame_from(cols, ok, tau_divisor(main_raw))
 
 

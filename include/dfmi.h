@@ -49,11 +49,6 @@ extern "C" {
 
 #define DFMI_MEM_HOST 0
 #define DFMI_MEM_DEVICE 1
-/* dfmi_nls_record only: DFMI_MEM_DEVICE | DFMI_MEM_OUT_HOST = the record on the device, `out`
- * and `fitok` in PINNED host memory, written in stream order (valid once `stream` is
- * synchronised; the call returns at once, as with DFMI_MEM_DEVICE). The library copies the
- * first 4/5 of the buffers' results while the rest are demodulated (tuning key "out_split"). */
-#define DFMI_MEM_OUT_HOST 2
 
 #define DFMI_MAX_LAMBDA 16
 

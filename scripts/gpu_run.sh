@@ -10,6 +10,9 @@
 #   py=SCRIPT[,ARGS]   python -u SCRIPT ARGS > TAG_<script name>.jsonl
 #   prof=SCRIPT[,ARGS] rocprofv3 --kernel-trace --stats of python SCRIPT ARGS -> TAG_prof/
 #   pmc=COUNTERS=SCRIPT[,ARGS]  one rocprofv3 --pmc pass (COUNTERS space-free, '+'-joined)
+#   round              scripts/profile_round.sh (the judged profiles of the driver's bench
+#                      command: kernel trace + stats, PMC FETCH/WRITE, frac check) into
+#                      gpurun_out/prof_TAG
 # A step that fails stops the call: after a timeout (124/137), an abort (134) or a segfault
 # (139) nothing else touches the GPU; a pytest failure (rc 1) still lets later steps run.
 set -o pipefail
@@ -74,6 +77,11 @@ for step in "$@"; do
         -- python3 "${pargs[@]}" > gpurun_out/${TAG}_pmc.log 2>&1
       rc=$?
       tail -3 gpurun_out/${TAG}_pmc.log
+      ;;
+    round)
+      TAG=$TAG timeout -k 10 1500 bash scripts/profile_round.sh > gpurun_out/${TAG}_round.log 2>&1
+      rc=$?
+      tail -3 gpurun_out/${TAG}_round.log
       ;;
     *)
       echo "unknown step $step"

@@ -78,39 +78,3 @@ def test_device_record_with_sim_tau_matches_host_and_reference(torch, manifest, 
     np.testing.assert_array_equal(dev_df.to_numpy(), host_df.to_numpy())
     np.testing.assert_array_equal(fo.tau, dev_df["tau"].to_numpy())
     np.testing.assert_allclose(fo.tau, records_npz["config1_facade_tau"], rtol=0, atol=1e-18)
-
-
-@pytest.mark.parametrize("nbuf", [3000, 900, 5])
-def test_out_host_mode_equals_device_mode(torch, nbuf):
-    """dfmi_nls_record with DFMI_MEM_DEVICE | DFMI_MEM_OUT_HOST (results into pinned host memory,
-    the first 4/5 copied under the rest's demodulation; 900 and 5 buffers: a tail below 256
-    buffers, one copy at the end) equals DFMI_MEM_DEVICE bit for bit; pageable output is
-    refused."""
-    from deepfmkit_amd import _lib
-    from deepfmkit_amd import fit as F
-    from deepfmkit_amd.physics import SnrSpec, synth_snr
-    R = 4000
-    lib = _lib.load()
-    x = torch.empty(nbuf * R, dtype=torch.float64, device="cuda")
-    synth_snr(SnrSpec(seed=5, stream=1, f_samp=200000.0, f_mod=1000.0, m=7.5, snr_db=40.0), 0, nbuf * R, out=x)
-    g = np.array([1.6, 6.0, 0.0, 0.0])
-    w0 = 2.0 * np.pi * 1000.0 / 200000.0
-    st = torch.cuda.current_stream().cuda_stream
-    od = torch.empty((6, nbuf), dtype=torch.float64, device="cuda")
-    kd = torch.empty(nbuf, dtype=torch.int32, device="cuda")
-    _lib.check(lib.dfmi_nls_record(x.data_ptr(), 1, nbuf * R, nbuf, R, 10, w0, 0, _lib.ptr(g), 1, nbuf - 1,
-                                   F.lm_config(), od.data_ptr(), kd.data_ptr(), _lib.DFMI_MEM_DEVICE, st), "device")
-    oh = torch.empty((6, nbuf), dtype=torch.float64, pin_memory=True)
-    kh = torch.empty(nbuf, dtype=torch.int32, pin_memory=True)
-    _lib.check(lib.dfmi_nls_record(x.data_ptr(), 1, nbuf * R, nbuf, R, 10, w0, 0, _lib.ptr(g), 1, nbuf - 1,
-                                   F.lm_config(), oh.data_ptr(), kh.data_ptr(),
-                                   _lib.DFMI_MEM_DEVICE | _lib.DFMI_MEM_OUT_HOST, st), "out_host")
-    kname = lib.dfmi_last_demod_kernel().decode()
-    torch.cuda.synchronize()
-    np.testing.assert_array_equal(oh.numpy(), od.cpu().numpy())
-    np.testing.assert_array_equal(kh.numpy(), kd.cpu().numpy())
-    assert kname.startswith("hostout split") == (nbuf // 5 >= 256), kname
-    pageable = np.empty((6, nbuf))
-    rc = lib.dfmi_nls_record(x.data_ptr(), 1, nbuf * R, nbuf, R, 10, w0, 0, _lib.ptr(g), 1, nbuf - 1, F.lm_config(),
-                             _lib.ptr(pageable), kh.data_ptr(), _lib.DFMI_MEM_DEVICE | _lib.DFMI_MEM_OUT_HOST, st)
-    assert rc == -1 and b"pinned" in lib.dfmi_last_error()

@@ -110,6 +110,7 @@ def nls_records(records, f_samp, f_mod, R, nbuf, ndata=10, init_guess=(1.6, 6.0,
         # rows 0..5 of one (7, nseg) block: the six result columns; row 6 receives fitok as
         # int64 (frame_from), so the whole result leaves the device in one copy
         out = torch.empty((7, nseg), dtype=torch.float64, device=x.device)[:6]
+        out._dfmi_block = True  # frame_from may use row 6 (this function's own allocation)
         ok = torch.empty(nseg, dtype=torch.int32, device=x.device)
         mark("alloc")
         with _on_device(x):
@@ -227,9 +228,7 @@ def frame_from(cols, fitok, tau_div=NO_TAU):
     if hasattr(cols, "cpu"):
         import torch
         n = cols.shape[1]
-        base = cols
-        if cols.dim() == 2 and cols.shape[0] == 6 and cols.stride(0) == n and cols.stride(1) == 1 and \
-                cols.untyped_storage().nbytes() >= 7 * n * 8:
+        if getattr(cols, "_dfmi_block", False):  # nls_records' (7, n) block: row 6 is ours
             base = torch.as_strided(cols, (7, n), (n, 1))
         else:  # a caller's own (6, n) tensors: same copy through a fresh block
             base = torch.empty((7, n), dtype=torch.float64, device=cols.device)

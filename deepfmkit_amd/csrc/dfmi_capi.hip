@@ -66,8 +66,10 @@ struct Tuning {
   int ekf_pit_min = 4096;     // samples per channel below which the sequential kernels run (crossover
                               // ~3,000 samples: 2,000 0.8x, 4,000 1.45x the row kernel, r04r)
   int ekf_pit_block = 0;      // samples per block (0: ~n nrec^(2/3) / 16384, at least 16)
-  int ekf_pit_passes = 48;    // pass cap: a channel still passing then goes to the sequential kernel (a
-                              // pass of one 400k-sample channel is ~0.06 ms, the sequential kernel ~68 ms)
+  int ekf_pit_passes = 0;     // pass cap: a channel still passing then goes to the sequential kernel; 0 = by
+                              // length, n / 1600 within [48, 256] (a pass of one 400k-sample channel costs
+                              // ~0.1 ms against ~68 ms for the sequential kernel; 48 passes of a
+                              // 4,096-sample one cost about its ~0.7-ms sequential run)
   int ekf_pit_first = 5;      // passes enqueued before the host first reads how many channels still pass
                               // (then every ekf_pit_every); config 5's record converges in 5
   int ekf_pit_every = 2;
@@ -993,7 +995,9 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
   while (lsz.back() > dfmi::kPitWg) lsz.push_back((lsz.back() + dfmi::kPitWg - 1) / dfmi::kPitWg);
   const int L = (int)lsz.size() - 1;
   const int64_t T0 = std::min<int64_t>(std::max(t_tune.ekf_pit_head, 0), n);
-  const int hist_n = t_tune.ekf_pit_trace ? std::max(t_tune.ekf_pit_passes, 1) : 0;
+  const int cap = t_tune.ekf_pit_passes > 0 ? t_tune.ekf_pit_passes
+                                            : (int)std::min<int64_t>(256, std::max<int64_t>(48, n / 1600));
+  const int hist_n = t_tune.ekf_pit_trace ? cap : 0;
   void *xt, *wtt, *xbar, *conv, *chan, *hst, *done, *hs, *ent = nullptr, *hist = nullptr, *pin;
   std::vector<double*> lv[2];  // per aggregate buffer: level arrays [r][65][lsz[l]]
   // every allocation before the first launch: a failure leaves the sequential kernels to run
@@ -1033,7 +1037,7 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
   rule.tol = std::pow(10.0, -(double)t_tune.ekf_pit_tol);
   rule.noise = rule.tol;
   rule.stall_max = std::max(t_tune.ekf_pit_stall, 1);
-  rule.cap = std::max(t_tune.ekf_pit_passes, 1);
+  rule.cap = cap;
   rule.hist_n = hist_n;
   rule.measure = t_tune.ekf_pit_measure;
   if (hist_n) HIPCHK(hipMemsetAsync(hist, 0xFF, (size_t)nrec * hist_n * 8, st));  // NaN: pass not run
@@ -1056,7 +1060,6 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
                            0, st, a[l], lsz[l], (const double*)a[l + 1], lsz[l + 1], (const dfmi::PitChan*)ch);
   };
   const double* tops[2] = {L >= 1 ? lv[0][1] : nullptr, L >= 1 ? lv[1][1] : nullptr};
-  const int cap = std::max(t_tune.ekf_pit_passes, 1);
   const int every = std::max(t_tune.ekf_pit_every, 1);
   int next_check = std::min(std::max(t_tune.ekf_pit_first, 1), cap);
   if (t_tune.ekf_pit_fused) {

@@ -132,7 +132,7 @@ int dfmi_nls_record(const double* x, int64_t nrec, int64_t rec_stride, int64_t n
  * iteration's fixed point by the bound rho / (1 - rho) x their last move between passes, rho
  * the contraction measured per channel on the device; a channel that stops contracting (3
  * passes in a row with rho >= 1, or too slow to meet the bound within the cap) or reaches the
- * cap "ekf_pit_passes" (48) is re-run by the sequential kernel above; the same states to
+ * cap "ekf_pit_passes" (0 = by length: n / 1600 within [48, 256]) is re-run by the sequential kernel above; the same states to
  * rounding (~1e-13). The parallel form reads how many channels still pass after
  * "ekf_pit_first" (5) passes and then every "ekf_pit_every" (2): one stream
  * synchronisation each, so a DFMI_MEM_DEVICE call on this path returns with its stream
@@ -308,7 +308,7 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
  * to this many channels, default 1024; 0 = the sequential kernels always), "ekf_pit_min"
  * (samples per channel below which the sequential kernels run, default 4096),
  * "ekf_pit_block" (samples per block, 0 = ~n nrec^(2/3) / 16384, at least 16), "ekf_pit_passes"
- * (pass cap before the sequential kernel, default 48), "ekf_pit_first" / "ekf_pit_every"
+ * (pass cap before the sequential kernel, default 0 = n / 1600 within [48, 256]), "ekf_pit_first" / "ekf_pit_every"
  * (passes before the first / between later host reads of the channels still passing, 5 / 2),
  * "ekf_pit_tol" (the stop rule's bound 10^-k, default 13), "ekf_pit_stall" (non-contracting
  * passes in a row before the sequential kernel, default 3), "ekf_pit_measure" (0 [default]:

@@ -38,7 +38,7 @@ def tune(lib, **kw):
         _lib.check(lib.dfmi_set_tuning(k.encode(), int(v)), "tune " + k)
 
 
-DEFAULTS = dict(ekf_pit_passes=48, ekf_pit_first=5, ekf_pit_every=2, ekf_pit_tol=13, ekf_pit_stall=3,
+DEFAULTS = dict(ekf_pit_passes=0, ekf_pit_first=5, ekf_pit_every=2, ekf_pit_tol=13, ekf_pit_stall=3,
                 ekf_pit_trace=0, ekf_pit_seq=1, ekf_pit_block=0, ekf_pit_head=256, ekf_pit_measure=0)
 
 
@@ -81,7 +81,7 @@ def main():
         tune(lib, **DEFAULTS)
         tune(lib, ekf_pit_trace=1)
         got, kname, passes = S.gpu_states(lib, x[None, :], x0[None, :], rv, qd, R, nbuf)
-        trd = np.empty(DEFAULTS["ekf_pit_passes"])
+        trd = np.empty(256)
         _lib.check(lib.dfmi_ekf_pit_trace(trd.ctypes.data, 1, trd.size), "trace")
         tune(lib, ekf_pit_trace=0)
         ts = []
@@ -113,7 +113,7 @@ def main():
         t0 = time.perf_counter()
         got, kname, passes = S.gpu_states(lib, x, x0, rv, qd, R, nbuf)
         dt = time.perf_counter() - t0
-        tr = np.empty((nch, DEFAULTS["ekf_pit_passes"]))
+        tr = np.empty((nch, 256))
         _lib.check(lib.dfmi_ekf_pit_trace(tr.ctypes.data, nch, tr.shape[1]), "trace")
         tune(lib, ekf_pit_trace=0, ekf_pit=0)
         t0 = time.perf_counter()

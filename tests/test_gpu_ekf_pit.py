@@ -50,7 +50,7 @@ def _c_ekf(x, init4, R, nbuf, qd=QD, r_val=None):
 class _tune:
     """dfmi_set_tuning for the duration of a block, restoring the defaults."""
     DEFAULTS = {"ekf_row": 1, "ekf_rot": 1, "ekf_pit": 1024, "ekf_pit_min": 4096, "ekf_pit_block": 0,
-                "ekf_pit_passes": 48, "ekf_pit_head": 256, "ekf_pit_fused": 1, "ekf_pit_first": 5,
+                "ekf_pit_passes": 0, "ekf_pit_head": 256, "ekf_pit_fused": 1, "ekf_pit_first": 5,
                 "ekf_pit_every": 2, "ekf_pit_tol": 13, "ekf_pit_stall": 3, "ekf_pit_trace": 0, "ekf_pit_seq": 1}
 
     def __init__(self, lib, **kw):
@@ -235,3 +235,34 @@ def test_pit_tuned_noise_matches_c_oracle(lib):
     err = np.abs(got[0] - ref).max()
     print("tuned passes", passes, "err", err)
     assert err <= 1e-12, err
+
+
+def test_pit_nonfinite_channel_is_handed_over(lib):
+    """A NaN sample in one of two channels: that filter's states turn NaN from there on, its
+    moves are not finite, the rule hands it to the sequential kernel after the first finite-less
+    pass (status 2, negative passes) and its states equal the sequential kernel's (NaN where it
+    has NaN); the other channel converges as usual and is unaffected (bit-equal to its own run
+    at the same block size)."""
+    import deepfmkit_amd as dfm
+    a = _raw(dfm, 6.0, 0.1, 31)
+    b = _raw(dfm, 4.3, 0.1, 32, psi=0.3)
+    b_bad = b.copy()
+    b_bad[7000] = np.nan
+    with _tune(lib, ekf_pit_block=25):
+        got, kname, passes = _ekf(lib, [a, b_bad], 4000, 5)
+        one, _, _ = _ekf(lib, [a], 4000, 5)
+    assert passes[0] > 0 and passes[1] < 0, (kname, passes)
+    np.testing.assert_array_equal(got[0], one[0])
+    with _tune(lib, ekf_pit=0):
+        seq, _, _ = _ekf(lib, [a, b_bad], 4000, 5)
+    np.testing.assert_array_equal(got[1], seq[1])
+    assert np.isnan(got[1][-1]).any()
+
+
+def test_pit_record_without_snapshots(lib):
+    """n < R (no snapshot to write, nbuf = 0): the call succeeds, every channel reports a
+    positive pass count (nothing moves: converged) and nothing is written."""
+    import deepfmkit_amd as dfm
+    x = _raw(dfm, 6.0, 0.05, 33)[:6000]
+    st, kname, passes = _ekf(lib, [x, x], 8000, 0)
+    assert st.shape == (2, 0, 5) and kname.startswith("ekf_pit") and all(p > 0 for p in passes), (kname, passes)

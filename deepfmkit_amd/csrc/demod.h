@@ -564,6 +564,161 @@ __global__ __launch_bounds__(kBlockThreads) void demod_bins_kernel(
   bins_kernel_body<MAXSLOT, LOADS, ROWS, PFN>(x, nseg, seg_stride, R, L, ndata, tab, qi, qi_ld, dc, probe);
 }
 
+// Many harmonics (the bin kernel's LDS basis, 2·ndata·L doubles, no longer fits beside the
+// bins: ndata > 16 at L = 200). The fold is the bin kernel's (bins in LDS, flat 1-KB wave
+// loads), but each wave folds KSEG segments into KSEG bin sets before contracting them
+// together, with the lanes over the OUTPUTS instead of over the bins: lane l accumulates
+// outputs o = l + 64·i (i < NO) of the 2·ndata + 1 = [Q_1..Q_nd, I_1..I_nd, dc] over all L
+// bins, reading each bin pair as an LDS broadcast and each basis pair once per KSEG segments
+// from the transposed table tabT[(p/2)·64·NO + o] = (T[o][p], T[o][p+1]) (global, L2-resident:
+// 2·ndata·L·8 B = 198 KB at ndata 62; the dc row is all ones, rows past it zero). No cross-
+// lane reduction at all (the bin kernel's butterfly costs 17 shuffles per 16 sums), and the
+// basis is read L2-side once per KSEG segments instead of LDS-side once per segment.
+// Summation order: each output is a sequential fma chain over p = 0..L-1 (the bin kernel's is
+// a lane-partial tree) — the same QI to a few ulps, not the same bits; rows layout not
+// implemented (the record pipeline uses component-major QI at these ndata).
+// Segments: wave w of W owns the contiguous range [w·nseg/W, (w+1)·nseg/W) (balanced to
+// one segment), processed KSEG at a time. Preconditions (host-checked): 16-B aligned rows,
+// L even, 128 <= L <= 256, 2·ndata + 1 <= 64·NO.
+template <int LOADS, int PFN>
+__device__ __forceinline__ void wide_fold(const double* __restrict__ xs0, int R, int L, double* ybin, int lane,
+                                          double (*pf)[2], const double* __restrict__ next) {
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  const int nch = R >> 7;
+  const int tail = R - (nch << 7);
+  auto add_chunk = [&](int p0, const double (&v)[2]) {
+    int p = p0 + 2 * lane;
+    if (p >= L) p -= L;
+    d2v* yp = reinterpret_cast<d2v*>(ybin + p);
+    d2v t = *yp;
+    t.x += v[0];
+    t.y += v[1];
+    *yp = t;
+  };
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    if (2 * (lane + 64 * j) < L) *reinterpret_cast<d2v*>(ybin + 2 * (lane + 64 * j)) = d2v{0.0, 0.0};
+  const double* __restrict__ xs = xs0 + 2 * lane;
+  int p0 = 0;
+  int c = 0;
+  if constexpr (PFN > 0) {
+#pragma unroll
+    for (int u = 0; u < PFN; ++u) {
+      add_chunk(p0, pf[u]);
+      p0 += 128;
+      if (p0 >= L) p0 -= L;
+    }
+    c = PFN;
+  }
+  for (; c + LOADS <= nch; c += LOADS) {
+    double v[LOADS][2];
+#pragma unroll
+    for (int u = 0; u < LOADS; ++u) VecT<2>::load_nt(xs + (c + u) * 128, v[u]);
+#pragma unroll
+    for (int u = 0; u < LOADS; ++u) {
+      add_chunk(p0, v[u]);
+      p0 += 128;
+      if (p0 >= L) p0 -= L;
+    }
+  }
+  {
+    const int rem = nch - c;
+    double v[LOADS][2];
+#pragma unroll
+    for (int u = 0; u < LOADS; ++u)
+      if (u < rem) VecT<2>::load_nt(xs + (c + u) * 128, v[u]);
+    const int t0 = 2 * lane;
+    double tv0 = 0.0, tv1 = 0.0;
+    if (t0 < tail) tv0 = xs[nch * 128];
+    if (t0 + 1 < tail) tv1 = xs[nch * 128 + 1];
+#pragma unroll
+    for (int u = 0; u < LOADS; ++u) {
+      if (u < rem) {
+        add_chunk(p0, v[u]);
+        p0 += 128;
+        if (p0 >= L) p0 -= L;
+      }
+    }
+    if (tail) {
+      int p = p0 + t0;
+      if (p >= L) p -= L;
+      if (t0 < tail) ybin[p] += tv0;
+      if (t0 + 1 < tail) ybin[p + 1] += tv1;
+    }
+  }
+  if constexpr (PFN > 0) {
+    if (next) {
+      const double* __restrict__ xn = next + 2 * lane;
+#pragma unroll
+      for (int u = 0; u < PFN; ++u) VecT<2>::load_nt(xn + u * 128, pf[u]);
+    }
+  }
+}
+
+template <int NO, int KSEG, int LOADS, int PFN>
+__global__ __launch_bounds__(kBlockThreads) void demod_wide_kernel(
+    const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
+    const double* __restrict__ tabT, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc) {
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  double* ybase = lds_dyn + (size_t)wave * KSEG * L;  // this wave's KSEG bin sets
+  const int64_t nw = (int64_t)gridDim.x * kWavesPerBlock;
+  const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  const int64_t sbeg = w * nseg / nw, send = (w + 1) * nseg / nw;
+  const int nout = 2 * ndata + 1;
+  const bool pfok = PFN > 0 && (R >> 7) >= PFN;
+  double pf[PFN > 0 ? PFN : 1][2];
+  if (pfok && sbeg < send) {
+    const double* __restrict__ x0 = x + sbeg * seg_stride + 2 * lane;
+#pragma unroll
+    for (int u = 0; u < (PFN > 0 ? PFN : 1); ++u) VecT<2>::load_nt(x0 + u * 128, pf[u]);
+  }
+  const d2v* __restrict__ T2 = reinterpret_cast<const d2v*>(tabT);
+  for (int64_t s0 = sbeg; s0 < send; s0 += KSEG) {
+    const int nk = (int)(send - s0 < KSEG ? send - s0 : KSEG);
+    for (int k = 0; k < nk; ++k) {
+      const int64_t s = s0 + k;
+      const double* nx = s + 1 < send ? x + (s + 1) * seg_stride : nullptr;
+      if (pfok) wide_fold<LOADS, PFN>(x + s * seg_stride, R, L, ybase + k * L, lane, pf, nx);
+      else wide_fold<LOADS, 0>(x + s * seg_stride, R, L, ybase + k * L, lane, pf, nullptr);
+    }
+    double acc[KSEG][NO];
+#pragma unroll
+    for (int k = 0; k < KSEG; ++k)
+#pragma unroll
+      for (int i = 0; i < NO; ++i) acc[k][i] = 0.0;
+#pragma unroll 2
+    for (int pp = 0; pp < (L >> 1); ++pp) {
+      d2v t[NO];
+#pragma unroll
+      for (int i = 0; i < NO; ++i) t[i] = T2[(size_t)pp * 64 * NO + lane + 64 * i];
+#pragma unroll
+      for (int k = 0; k < KSEG; ++k) {
+        const d2v y = *reinterpret_cast<const d2v*>(ybase + k * L + 2 * pp);  // LDS broadcast
+#pragma unroll
+        for (int i = 0; i < NO; ++i) {
+          acc[k][i] = fma(y.x, t[i].x, acc[k][i]);
+          acc[k][i] = fma(y.y, t[i].y, acc[k][i]);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KSEG; ++k) {
+      if (k < nk) {
+#pragma unroll
+        for (int i = 0; i < NO; ++i) {
+          const int o = lane + 64 * i;
+          const double v = acc[k][i] / (double)R;  // numpy mean: sum / count
+          if (o < nout - 1) qi[(int64_t)o * qi_ld + s0 + k] = v;
+          else if (o == nout - 1) dc[s0 + k] = v;
+        }
+      }
+    }
+  }
+}
+
 // Fallback when no short integer period exists: per-sample angles
 // fl(fl(h·w0)·t) exactly as fit.py:55-64 forms them, sincos on the device.
 // VALU-bound; only used for unusual f_samp/f_mod ratios.

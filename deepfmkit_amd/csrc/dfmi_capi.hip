@@ -50,6 +50,11 @@ struct Tuning {
   int lm_general = 0;    // 1: force the two-pass (general) LM path for every ndata
   int demod_spw = 2;     // bin kernels: grid sized for ~this many segments per wave (0: one persistent
                          // wave per slot); later workgroups go to the slots that free first
+  int demod_wide = 1;    // component-major QI where the bin kernel's LDS basis does not fit: 1 the
+                         // many-harmonic kernel (demod_wide_kernel), 0 the fold kernel; 2 (A/B) the
+                         // many-harmonic kernel wherever its geometry applies
+  int demod_wide_grid = 1;  // demod_wide_kernel: 1 one group of KSEG segments per wave (the dispatcher
+                            // balances), 0 one persistent wave per slot with a contiguous range
   int ekf_row = 1;       // EKF: ekf_row_kernel (4 channels per wave) up to ekf_row x 4 x 4 x CUs channels
                          // (past one wave per SIMD the issue-bound rows share a SIMD, and one lane per
                          // channel carries 16x the channels per instruction); 0 = ekf_kernel only
@@ -138,7 +143,7 @@ struct DeviceState {
   size_t lds_per_block = 0;
   std::map<uintptr_t, StreamWs> ws;                                  // caller stream -> workspaces
   uint64_t ws_clock = 0;
-  std::map<std::tuple<int, int, uint64_t>, DevBuf> basis;            // (L, ndata, w0 bits)
+  std::map<std::tuple<int, int, uint64_t>, DevBuf> basis;            // (L, ndata, w0 bits); (L, -(8 ndata + no), w0 bits): wide
   std::map<std::tuple<int, uint64_t, uint64_t, uint64_t>, DevBuf> gridtab;  // (ndata, min, max, step)
   std::map<int64_t, DevBuf> pwplan;                                 // n -> numpy pairwise-sum plan
   std::map<std::pair<const void*, int>, int> occupancy;              // (kernel, LDS bytes) -> blocks per CU
@@ -340,6 +345,34 @@ int basis_table(int dev, int L, int ndata, double w0, hipStream_t st, const doub
   return DFMI_OK;
 }
 
+// The basis transposed for demod_wide_kernel: pairs (T[o][p], T[o][p+1]) at
+// [(p/2)·64·no + o], o over [cos rows | sin rows | ones (dc) | zeros up to 64·no]; the
+// values are basis_table's.
+int basis_table_wide(int dev, int L, int ndata, double w0, int no, const double** out) {
+  auto key = std::make_tuple(L, -(ndata * 8 + no), bits(w0));
+  DevBuf& b = t_ds->basis[key];
+  if (!b.p) {
+    const int w = 64 * no;
+    std::vector<double> h((size_t)(L / 2) * w * 2, 0.0);
+    auto put = [&](int o, int p, double v) { h[((size_t)(p / 2) * w + o) * 2 + (p & 1)] = v; };
+    for (int c = 0; c < ndata; ++c) {
+      const double wh = (double)(c + 1) * w0;
+      for (int p = 0; p < L; ++p) {
+        const double ang = wh * (double)p;
+        put(c, p, cos(ang));
+        put(ndata + c, p, sin(ang));
+      }
+    }
+    for (int p = 0; p < L; ++p) put(2 * ndata, p, 1.0);
+    HIPCHK(hipMalloc(&b.p, h.size() * 8));
+    b.n = h.size() * 8;
+    HIPCHK(hipMemcpy(b.p, h.data(), b.n, hipMemcpyHostToDevice));
+  }
+  (void)dev;
+  *out = (const double*)b.p;
+  return DFMI_OK;
+}
+
 // numpy.arange(min, max + step, step): length ceil((stop - start)/step),
 // values start + i*((start + step) - start).
 void grid_geometry(const dfmi_lm_config& c, int* n, double* delta) {
@@ -523,6 +556,45 @@ int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, i
   return DFMI_OK;
 }
 
+// demod_wide_kernel (component-major QI at many harmonics): KSEG = 8 bin sets per wave while
+// 4 waves' sets fit in 52 KB (3 workgroups per CU), else 4.
+bool wide_geometry(bool vec2, int L, int ndata) {
+  return vec2 && !(L & 1) && L >= 128 && L <= 256 && 2 * ndata + 1 <= 64 * 4;
+}
+
+template <int NO, int KSEG>
+int launch_wide_t(const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tabT,
+                  double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu) {
+  auto kern = dfmi::demod_wide_kernel<NO, KSEG, 8, 4>;
+  const size_t lds = (size_t)dfmi::kWavesPerBlock * KSEG * L * sizeof(double);
+  int per_cu = 0;
+  if (int orc = occupancy(kern, dfmi::kBlockThreads, lds, &per_cu)) return orc;
+  if (per_cu < 1) per_cu = 1;
+  const int64_t per_block = (int64_t)dfmi::kWavesPerBlock * KSEG;
+  const int64_t groups = (nseg + per_block - 1) / per_block;
+  const int64_t grid = t_tune.demod_wide_grid ? groups : persistent_grid(n_cu, per_cu, groups);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(dfmi::kBlockThreads), lds, st, x, nseg, stride, R, L, ndata,
+                     tabT, qi, qi_ld, dc);
+  HIPCHK(hipGetLastError());
+  g_last_demod = "demod_wide_kernel<" + std::to_string(NO) + "," + std::to_string(KSEG) + ",8,4>";
+  return DFMI_OK;
+}
+
+int launch_wide(int dev, const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, double w0,
+                double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu) {
+  const int no = 2 * ndata + 1 <= 64 ? 1 : 2 * ndata + 1 <= 128 ? 2 : 4;
+  const double* tabT = nullptr;
+  if (int rc = basis_table_wide(dev, L, ndata, w0, no, &tabT)) return rc;
+  const bool k8 = (size_t)dfmi::kWavesPerBlock * 8 * L * sizeof(double) <= 52 * 1024;
+#define DFMI_WIDE(NO_)                                                                                   \
+  return k8 ? launch_wide_t<NO_, 8>(x, nseg, stride, R, L, ndata, tabT, qi, qi_ld, dc, st, n_cu)          \
+            : launch_wide_t<NO_, 4>(x, nseg, stride, R, L, ndata, tabT, qi, qi_ld, dc, st, n_cu)
+  if (no == 1) DFMI_WIDE(1);
+  if (no == 2) DFMI_WIDE(2);
+  DFMI_WIDE(4);
+#undef DFMI_WIDE
+}
+
 // Geometry the LDS bin fold needs (bin kernels, seed kernels): 16-B rows, an even basis
 // period 128 <= L <= 1024, and a basis + `nbins` bin sets that fit in LDS.
 bool bins_geometry(bool vec2, int L, int ndata, size_t lds_cap, int nbins) {
@@ -586,9 +658,13 @@ int demod_device(int dev, const double* x, int64_t nseg, int64_t stride, int R, 
       if (rc) return rc;
       const size_t lds = (size_t)2 * ndata * L * sizeof(double);
       const bool use_lds = lds <= 64 * 1024 && lds <= lds_cap;
+      if (!rows && t_tune.demod_wide == 2 && wide_geometry(vec2, L, ndata))
+        return launch_wide(dev, x, nseg, stride, R, L, ndata, w0, qi, qi_ld, dc, st, n_cu);
       rc = try_bins(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, vec2, lds_cap, rows);
       if (rc <= 0) return rc;
       if (rows) return fail(DFMI_ERR_UNSUPPORTED, "row layout needs the bin-in-LDS demodulation kernel");
+      if (t_tune.demod_wide && t_tune.demod_kernel == 1 && wide_geometry(vec2, L, ndata))
+        return launch_wide(dev, x, nseg, stride, R, L, ndata, w0, qi, qi_ld, dc, st, n_cu);
       if (vec2) {
         return use_lds ? launch_fold_ms<2, true>(ms, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu)
                        : launch_fold_ms<2, false>(ms, x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu);
@@ -887,6 +963,8 @@ const std::map<std::string, Knob>& knobs() {
       {"demod_kernel", {&Tuning::demod_kernel, {0, 1}}},
       {"lm_general", {&Tuning::lm_general, {0, 1}}},
       {"demod_spw", {&Tuning::demod_spw, {}}},
+      {"demod_wide", {&Tuning::demod_wide, {0, 1, 2}}},
+      {"demod_wide_grid", {&Tuning::demod_wide_grid, {0, 1}}},
       {"ekf_row", {&Tuning::ekf_row, {}}},
       {"ekf_rot", {&Tuning::ekf_rot, {0, 1}}},
       {"wdfmi_accel", {&Tuning::wdfmi_accel, {0, 1, 2, 3}}},

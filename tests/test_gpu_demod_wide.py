@@ -1,0 +1,120 @@
+"""The many-harmonic demodulation (demod.h demod_wide_kernel: ndata beyond the bin kernel's
+LDS basis, component-major QI) against the fold / bin kernels and a torch fp64 restatement
+of calculate_quadratures (fit.py:18-66: mean(x cos((n+1) w0 t)), mean(x sin(...)), and
+fitters.py:57's dc = mean(x)), on ragged shapes: segment counts that leave partial groups,
+R with a partial last chunk, basis periods 128..256 (KSEG 8 and 4), 1..3 output slices."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def env():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from deepfmkit_amd import _lib
+    return torch, _lib, _lib.load()
+
+
+def _demod(env, x, nseg, R, nd, w0, **tune):
+    torch, _lib, lib = env
+    for k, v in tune.items():
+        _lib.check(lib.dfmi_set_tuning(k.encode(), v), "tune")
+    try:
+        qi = torch.full((2 * nd, nseg), float("nan"), dtype=torch.float64, device="cuda")
+        dc = torch.full((nseg,), float("nan"), dtype=torch.float64, device="cuda")
+        _lib.check(lib.dfmi_demod(x.data_ptr(), nseg, R, R, nd, w0, 0, qi.data_ptr(), dc.data_ptr(),
+                                  _lib.DFMI_MEM_DEVICE, torch.cuda.current_stream().cuda_stream), "dfmi_demod")
+        torch.cuda.synchronize()
+        return qi.cpu().numpy(), dc.cpu().numpy(), lib.dfmi_last_demod_kernel().decode()
+    finally:
+        for k in tune:
+            _lib.check(lib.dfmi_set_tuning(k.encode(), {"demod_wide": 1, "demod_wide_grid": 1}[k]), "tune")
+
+
+def _torch_ref(torch, x, nseg, R, nd, w0, take):
+    """fit.py:18-66 in torch fp64 on the device: the reference's angle fl(fl(h w0) t)."""
+    xs = x.view(nseg, R)[take]
+    t = torch.arange(R, dtype=torch.float64, device="cuda")
+    q, i = [], []
+    for h in range(1, nd + 1):
+        ang = (h * w0) * t
+        q.append((xs * torch.cos(ang)).mean(dim=1))
+        i.append((xs * torch.sin(ang)).mean(dim=1))
+    return torch.stack(q + i).cpu().numpy(), xs.mean(dim=1).cpu().numpy()
+
+
+@pytest.mark.parametrize("nd,f_samp,nseg,R", [
+    (20, 200000.0, 3001, 4000),   # L 200, one output slice, KSEG 8, partial groups
+    (30, 200000.0, 517, 4000),
+    (62, 200000.0, 1029, 4000),   # two slices (125 outputs)
+    (100, 200000.0, 131, 4000),   # four slices
+    (40, 250000.0, 700, 5000),    # L 250: KSEG 4
+    (40, 128000.0, 33, 3968),     # L 128, R = 31 chunks exactly
+    (20, 200000.0, 5, 4000),      # fewer segments than one group
+    (20, 200000.0, 1, 334),       # one segment, shorter than one basis period
+])
+def test_wide_matches_fold_and_torch_reference(env, nd, f_samp, nseg, R):
+    torch = env[0]
+    w0 = 2 * np.pi * 1000.0 / f_samp
+    g = torch.Generator(device="cuda")
+    g.manual_seed(nd * 7919 + nseg)
+    x = torch.randn(nseg * R, dtype=torch.float64, device="cuda", generator=g) + 0.25
+    qw, dw, kw = _demod(env, x, nseg, R, nd, w0)
+    assert kw.startswith("demod_wide_kernel"), kw
+    qf, df, kf = _demod(env, x, nseg, R, nd, w0, demod_wide=0)
+    assert not kf.startswith("demod_wide"), kf
+    scale = np.abs(qf).max()
+    assert np.isfinite(qw).all() and np.isfinite(dw).all()
+    assert np.abs(qw - qf).max() <= 1e-13 * max(scale, 1.0), np.abs(qw - qf).max()
+    assert np.abs(dw - df).max() <= 1e-14 * max(np.abs(df).max(), 1.0)
+    take = torch.arange(0, nseg, max(1, nseg // 24), device="cuda")
+    rq, rd = _torch_ref(torch, x, nseg, R, nd, w0, take)
+    idx = take.cpu().numpy()
+    assert np.abs(qw[:, idx] - rq).max() <= 1e-12, np.abs(qw[:, idx] - rq).max()
+    assert np.abs(dw[idx] - rd).max() <= 1e-13
+    # the persistent grid (contiguous ranges) gives the same bits: a segment's result does
+    # not depend on the group it is contracted in
+    qp, dp, _ = _demod(env, x, nseg, R, nd, w0, demod_wide_grid=0)
+    np.testing.assert_array_equal(qp, qw)
+    np.testing.assert_array_equal(dp, dw)
+
+
+@pytest.mark.parametrize("nd", [10, 16])
+def test_wide_forced_at_bin_kernel_ndata(env, nd):
+    """demod_wide = 2 runs the many-harmonic kernel where the bin kernel also applies (A/B):
+    the same QI within a few ulps."""
+    torch = env[0]
+    w0 = 2 * np.pi * 1000.0 / 200000.0
+    g = torch.Generator(device="cuda")
+    g.manual_seed(nd)
+    nseg, R = 2049, 4000
+    x = torch.randn(nseg * R, dtype=torch.float64, device="cuda", generator=g) - 0.5
+    qb, db, kb = _demod(env, x, nseg, R, nd, w0)
+    assert kb.startswith("demod_bins_kernel"), kb
+    qw, dw, kw = _demod(env, x, nseg, R, nd, w0, demod_wide=2)
+    assert kw.startswith("demod_wide_kernel"), kw
+    assert np.abs(qw - qb).max() <= 1e-13 * max(np.abs(qb).max(), 1.0)
+    assert np.abs(dw - db).max() <= 1e-14
+
+
+def test_record_pipeline_at_many_harmonics(env):
+    """dfmi_nls_record at ndata 30 (the quickstart's m = 31.4 setting) on a
+    noiseless m = 12, psi = 0.2 record seeded near psi (from psi = 0 the LM settles in a local
+    minimum at m = 11.2 whichever demodulation runs): every segment recovers the parameters,
+    through the many-harmonic demodulation."""
+    torch, _lib, lib = env
+    from deepfmkit_amd.fitters import nls_records
+    nseg, R = 4000, 4000
+    t = torch.arange(R, dtype=torch.float64, device="cuda") / 200000.0
+    seg_phi = torch.linspace(-0.4, 0.4, nseg, dtype=torch.float64, device="cuda")
+    x = (1.0 + torch.cos(seg_phi[:, None] + 12.0 * torch.cos(2 * np.pi * 1000.0 * t[None, :] + 0.2))).reshape(1, -1)
+    cols, ok = nls_records(x, 200000.0, 1000.0, R, nseg, 30, init_guess=(1.6, 12.0, 0.0, 0.2))
+    assert lib.dfmi_last_demod_kernel().decode().startswith("demod_wide_kernel")
+    cols, ok = cols.cpu().numpy(), ok.cpu().numpy()
+    assert (ok == 0).all()
+    assert np.abs(cols[0] - 1.0).max() < 1e-9
+    assert np.abs(cols[1] - 12.0).max() < 1e-9
+    assert np.abs(cols[3] - 0.2).max() < 1e-9

@@ -566,20 +566,33 @@ __global__ __launch_bounds__(kBlockThreads) void demod_bins_kernel(
 
 // Many harmonics (the bin kernel's LDS basis, 2·ndata·L doubles, no longer fits beside the
 // bins: ndata > 16 at L = 200). The fold is the bin kernel's (bins in LDS, flat 1-KB wave
-// loads), but each wave folds KSEG segments into KSEG bin sets before contracting them
-// together, with the lanes over the OUTPUTS instead of over the bins: lane l accumulates
-// outputs o = l + 64·i (i < NO) of the 2·ndata + 1 = [Q_1..Q_nd, I_1..I_nd, dc] over all L
-// bins, reading each bin pair as an LDS broadcast and each basis pair once per KSEG segments
-// from the transposed table tabT[(p/2)·64·NO + o] = (T[o][p], T[o][p+1]) (global, L2-resident:
-// 2·ndata·L·8 B = 198 KB at ndata 62; the dc row is all ones, rows past it zero). No cross-
-// lane reduction at all (the bin kernel's butterfly costs 17 shuffles per 16 sums), and the
-// basis is read L2-side once per KSEG segments instead of LDS-side once per segment.
-// Summation order: each output is a sequential fma chain over p = 0..L-1 (the bin kernel's is
-// a lane-partial tree) — the same QI to a few ulps, not the same bits; rows layout not
-// implemented (the record pipeline uses component-major QI at these ndata).
-// Segments: wave w of W owns the contiguous range [w·nseg/W, (w+1)·nseg/W) (balanced to
-// one segment), processed KSEG at a time. Preconditions (host-checked): 16-B aligned rows,
-// L even, 128 <= L <= 256, 2·ndata + 1 <= 64·NO.
+// loads); each wave folds KSEG consecutive segments into KSEG bin sets and then contracts
+// them together, with the lanes over the OUTPUTS instead of over the bins: lane l accumulates
+// outputs o = l + 64·i (i < NO) of [Q_1..Q_nd, I_1..I_nd, dc] (2·ndata + 1), with no cross-lane
+// reduction (the bin kernel's butterfly costs 17 shuffles per 16 sums).
+// Half-period symmetry: with L·w0 = 2π·k, cos(h w0 (L-p)) = cos(h w0 p) and sin(h w0 (L-p)) =
+// -sin(h w0 p), so each segment's bins are first paired in place, y+[p] = y[p] + y[L-p] and
+// y-[p] = y[p] - y[L-p] for 0 < p < L/2 (y±[0] = y[0], y±[L/2] = y[L/2]), and the cos / dc
+// lanes contract y+ and the sin lanes y- over p = 0..L/2 only: half the LDS reads and FMAs.
+// The basis values at L-p are taken equal to those at p: the host's cos / sin of the
+// reference's angles fl(fl(h w0) p) differ from them by the angle rounding, ~h·L·w0·eps
+// (4e-14 at h = 62, L = 200), inside the periodicity error the fold itself accepts
+// (dfmi_detect_period: 1e-11 rad over the record); so QI agree with the bin / fold kernels to
+// ~1e-14 relative, not bit for bit (tests/test_gpu_demod_wide.py).
+// Basis: tabT[pp·64·NO + o] = (T[o][2pp], T[o][2pp+1]) for p <= L/2 (zero beyond), o over
+// [cos rows | sin rows | ones | zeros], global (L2-resident: 51 KB at ndata 62), TD pairs
+// in flight.
+// Work: workgroup b owns segments [b·4·KSEG, +4·KSEG), its wave w the KSEG from b·4·KSEG +
+// w·KSEG (one group per wave: the dispatcher balances the tail). The waves' results meet in
+// LDS and the workgroup stores each output row's 4·KSEG consecutive segments as one run
+// (8-B stores one line per lane cost 0.09 ms of 0.65 at ndata 30, r05s).
+// Preconditions (host-checked): 16-B aligned rows, L even, 128 <= L <= 256, 2·ndata + 1 <=
+// 64·NO; dynamic LDS 4·KSEG·wide_set(L, NO, KSEG) doubles.
+__host__ __device__ constexpr int wide_set(int L, int NO, int KSEG) {
+  // per-set doubles: the bins (L) + 4 for the paired layout (ym + 2·npair <= L + 4), or this wave's share of the
+  // result tile (64·NO rows x (KSEG + 1) pitch), whichever is larger
+  return (L + 4 > (64 * NO * (KSEG + 1) + KSEG - 1) / KSEG) ? L + 4 : (64 * NO * (KSEG + 1) + KSEG - 1) / KSEG;
+}
 template <int LOADS, int PFN>
 __device__ __forceinline__ void wide_fold(const double* __restrict__ xs0, int R, int L, double* ybin, int lane,
                                           double (*pf)[2], const double* __restrict__ next) {
@@ -655,66 +668,126 @@ __device__ __forceinline__ void wide_fold(const double* __restrict__ xs0, int R,
   }
 }
 
-template <int NO, int KSEG, int LOADS, int PFN>
-__global__ __launch_bounds__(kBlockThreads) void demod_wide_kernel(
+template <int NO, int KSEG, int LOADS, int PFN, int TD = (NO >= 4 ? 2 : 8 / NO)>
+__global__ __launch_bounds__(kBlockThreads, 3) void demod_wide_kernel(  // 3 waves per SIMD: <= 168 VGPRs
     const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
-    const double* __restrict__ tabT, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc) {
+    const double* __restrict__ tabT, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc, int dbg) {
+  // dbg (diagnostics, demod_wide_dbg): bit 0 skips the contraction (acc = one bin), bit 1
+  // the stores (kept alive by a never-true NaN test) — fold / contraction / store split
   typedef double d2v __attribute__((ext_vector_type(2)));
   extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  double* ybase = lds_dyn + (size_t)wave * KSEG * L;  // this wave's KSEG bin sets
-  const int64_t nw = (int64_t)gridDim.x * kWavesPerBlock;
-  const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + wave;
-  const int64_t sbeg = w * nseg / nw, send = (w + 1) * nseg / nw;
+  const int ws = wide_set(L, NO, KSEG);
+  double* ybase = lds_dyn + (size_t)wave * KSEG * ws;  // this wave's KSEG bin sets
+  const int64_t b0 = (int64_t)blockIdx.x * kWavesPerBlock * KSEG;
+  const int64_t sbeg = b0 + (int64_t)wave * KSEG;
+  const int64_t send = sbeg + KSEG < nseg ? sbeg + KSEG : nseg;
+  const int nk = sbeg < send ? (int)(send - sbeg) : 0;
   const int nout = 2 * ndata + 1;
+  const int half = L >> 1;
+  const int npair = (half + 2) >> 1;  // basis pairs covering p = 0..half
+  const int ym = (half + 2) & ~1;     // start of y- in a set
   const bool pfok = PFN > 0 && (R >> 7) >= PFN;
   double pf[PFN > 0 ? PFN : 1][2];
-  if (pfok && sbeg < send) {
+  if (pfok && nk > 0) {
     const double* __restrict__ x0 = x + sbeg * seg_stride + 2 * lane;
 #pragma unroll
     for (int u = 0; u < (PFN > 0 ? PFN : 1); ++u) VecT<2>::load_nt(x0 + u * 128, pf[u]);
   }
+  for (int k = 0; k < nk; ++k) {
+    const int64_t s = sbeg + k;
+    double* yb = ybase + k * ws;
+    const double* nx = s + 1 < send ? x + (s + 1) * seg_stride : nullptr;
+    if (pfok) wide_fold<LOADS, PFN>(x + s * seg_stride, R, L, yb, lane, pf, nx);
+    else wide_fold<LOADS, 0>(x + s * seg_stride, R, L, yb, lane, pf, nullptr);
+    // pair the bins in place: y+ at [0, 2 npp), y- at [ym, ym + 2 npp) (ym even: 16-B aligned
+    // pair reads), zero past half; every lane reads all its inputs before any lane writes
+    // (one wave: its LDS operations execute in order)
+    double a[3], bb[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int p = lane + 64 * u;
+      a[u] = p <= half ? yb[p] : 0.0;
+      bb[u] = (p > 0 && p < half) ? yb[L - p] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int p = lane + 64 * u;
+      if (p < 2 * npair) {
+        const bool self = p == 0 || p == half;
+        yb[p] = self ? a[u] : a[u] + bb[u];
+        yb[ym + p] = self ? a[u] : a[u] - bb[u];
+      }
+    }
+  }
+  double acc[KSEG][NO];
+#pragma unroll
+  for (int k = 0; k < KSEG; ++k)
+#pragma unroll
+    for (int i = 0; i < NO; ++i) acc[k][i] = 0.0;
+  // lanes of sin rows read y-, the others y+ (two addresses per lane group: no conflict)
+  int yoff[NO];
+#pragma unroll
+  for (int i = 0; i < NO; ++i) {
+    const int o = lane + 64 * i;
+    yoff[i] = (o >= ndata && o < 2 * ndata) ? ym : 0;
+  }
+  const int npp = (dbg & 1) || nk == 0 ? 0 : npair;
+  if (dbg & 1)
+#pragma unroll
+    for (int k = 0; k < KSEG; ++k) acc[k][0] = ybase[k * ws + lane];
   const d2v* __restrict__ T2 = reinterpret_cast<const d2v*>(tabT);
-  for (int64_t s0 = sbeg; s0 < send; s0 += KSEG) {
-    const int nk = (int)(send - s0 < KSEG ? send - s0 : KSEG);
-    for (int k = 0; k < nk; ++k) {
-      const int64_t s = s0 + k;
-      const double* nx = s + 1 < send ? x + (s + 1) * seg_stride : nullptr;
-      if (pfok) wide_fold<LOADS, PFN>(x + s * seg_stride, R, L, ybase + k * L, lane, pf, nx);
-      else wide_fold<LOADS, 0>(x + s * seg_stride, R, L, ybase + k * L, lane, pf, nullptr);
-    }
-    double acc[KSEG][NO];
+  d2v tb[TD][NO];
 #pragma unroll
-    for (int k = 0; k < KSEG; ++k)
+  for (int u = 0; u < TD; ++u)
 #pragma unroll
-      for (int i = 0; i < NO; ++i) acc[k][i] = 0.0;
-#pragma unroll 2
-    for (int pp = 0; pp < (L >> 1); ++pp) {
-      d2v t[NO];
+    for (int i = 0; i < NO; ++i)
+      if (u < npp) tb[u][i] = T2[(size_t)u * 64 * NO + lane + 64 * i];
+  for (int pp0 = 0; pp0 < npp; pp0 += TD) {
 #pragma unroll
-      for (int i = 0; i < NO; ++i) t[i] = T2[(size_t)pp * 64 * NO + lane + 64 * i];
-#pragma unroll
-      for (int k = 0; k < KSEG; ++k) {
-        const d2v y = *reinterpret_cast<const d2v*>(ybase + k * L + 2 * pp);  // LDS broadcast
+    for (int u = 0; u < TD; ++u) {
+      const int pp = pp0 + u;
+      if (pp < npp) {
+        d2v t[NO];
 #pragma unroll
         for (int i = 0; i < NO; ++i) {
-          acc[k][i] = fma(y.x, t[i].x, acc[k][i]);
-          acc[k][i] = fma(y.y, t[i].y, acc[k][i]);
+          t[i] = tb[u][i];
+          if (pp + TD < npp) tb[u][i] = T2[(size_t)(pp + TD) * 64 * NO + lane + 64 * i];
+        }
+#pragma unroll
+        for (int k = 0; k < KSEG; ++k) {
+#pragma unroll
+          for (int i = 0; i < NO; ++i) {
+            const d2v y = *reinterpret_cast<const d2v*>(ybase + k * ws + yoff[i] + 2 * pp);
+            acc[k][i] = fma(y.x, t[i].x, acc[k][i]);
+            acc[k][i] = fma(y.y, t[i].y, acc[k][i]);
+          }
         }
       }
     }
+  }
+  // results to LDS (this wave's share of the tile: [o][KSEG + 1] in its own sets), then the
+  // workgroup writes each output row's 4·KSEG consecutive segments as one run. The stores
+  // are what this kernel pays beyond its fold (0.463 ms at config 2): +0.087 ms at ndata 30
+  // for 48.8 MB (TCC_EA0_WRREQ_64B: exactly the bytes), the same for a segment-major order
+  // (one contiguous run per workgroup), with plain stores, or with XCD-contiguous ranges,
+  // and +0.008 ms for one store per wave — the write bytes themselves, in a saturated read
+  // stream (profiles/r05/wide_demod_ab.jsonl)
+  constexpr int KP = KSEG + 1;
 #pragma unroll
-    for (int k = 0; k < KSEG; ++k) {
-      if (k < nk) {
+  for (int k = 0; k < KSEG; ++k)
 #pragma unroll
-        for (int i = 0; i < NO; ++i) {
-          const int o = lane + 64 * i;
-          const double v = acc[k][i] / (double)R;  // numpy mean: sum / count
-          if (o < nout - 1) qi[(int64_t)o * qi_ld + s0 + k] = v;
-          else if (o == nout - 1) dc[s0 + k] = v;
-        }
-      }
+    for (int i = 0; i < NO; ++i) ybase[(lane + 64 * i) * KP + k] = acc[k][i] / (double)R;  // mean: sum / count
+  __syncthreads();
+  constexpr int SEGS = kWavesPerBlock * KSEG;  // consecutive segments per output row
+  for (int e = threadIdx.x; e < nout * SEGS; e += kBlockThreads) {
+    const int o = e / SEGS, c = e - o * SEGS;
+    const int64_t s = b0 + c;
+    if (s < nseg) {
+      const double v = lds_dyn[(size_t)(c / KSEG) * KSEG * ws + o * KP + (c % KSEG)];
+      if ((dbg & 2) && v == v) continue;
+      __builtin_nontemporal_store(v, o < nout - 1 ? qi + (int64_t)o * qi_ld + s : dc + s);
     }
   }
 }

@@ -53,8 +53,8 @@ struct Tuning {
   int demod_wide = 1;    // component-major QI where the bin kernel's LDS basis does not fit: 1 the
                          // many-harmonic kernel (demod_wide_kernel), 0 the fold kernel; 2 (A/B) the
                          // many-harmonic kernel wherever its geometry applies
-  int demod_wide_grid = 1;  // demod_wide_kernel: 1 one group of KSEG segments per wave (the dispatcher
-                            // balances), 0 one persistent wave per slot with a contiguous range
+  int demod_wide_dbg = 0;   // diagnostics: demod_wide_kernel without its contraction (1) / stores (2)
+  int demod_wide_k = 0;     // demod_wide_kernel segments per wave (KSEG): 0 = 4 (8 beyond 31 harmonics); 2 / 4 / 8 (A/B)
   int ekf_row = 1;       // EKF: ekf_row_kernel (4 channels per wave) up to ekf_row x 4 x 4 x CUs channels
                          // (past one wave per SIMD the issue-bound rows share a SIMD, and one lane per
                          // channel carries 16x the channels per instruction); 0 = ekf_kernel only
@@ -345,25 +345,26 @@ int basis_table(int dev, int L, int ndata, double w0, hipStream_t st, const doub
   return DFMI_OK;
 }
 
-// The basis transposed for demod_wide_kernel: pairs (T[o][p], T[o][p+1]) at
-// [(p/2)·64·no + o], o over [cos rows | sin rows | ones (dc) | zeros up to 64·no]; the
+// The basis for demod_wide_kernel: pairs (T[o][p], T[o][p+1]) at [(p/2)·64·no + o] for
+// p = 0..L/2 (zero beyond), o over [cos rows | sin rows | ones (dc) | zeros up to 64·no]; the
 // values are basis_table's.
 int basis_table_wide(int dev, int L, int ndata, double w0, int no, const double** out) {
   auto key = std::make_tuple(L, -(ndata * 8 + no), bits(w0));
   DevBuf& b = t_ds->basis[key];
   if (!b.p) {
     const int w = 64 * no;
-    std::vector<double> h((size_t)(L / 2) * w * 2, 0.0);
+    const int npp = (L / 2 + 2) / 2;
+    std::vector<double> h((size_t)npp * w * 2, 0.0);
     auto put = [&](int o, int p, double v) { h[((size_t)(p / 2) * w + o) * 2 + (p & 1)] = v; };
     for (int c = 0; c < ndata; ++c) {
       const double wh = (double)(c + 1) * w0;
-      for (int p = 0; p < L; ++p) {
+      for (int p = 0; p <= L / 2; ++p) {
         const double ang = wh * (double)p;
         put(c, p, cos(ang));
         put(ndata + c, p, sin(ang));
       }
     }
-    for (int p = 0; p < L; ++p) put(2 * ndata, p, 1.0);
+    for (int p = 0; p <= L / 2; ++p) put(2 * ndata, p, 1.0);
     HIPCHK(hipMalloc(&b.p, h.size() * 8));
     b.n = h.size() * 8;
     HIPCHK(hipMemcpy(b.p, h.data(), b.n, hipMemcpyHostToDevice));
@@ -440,6 +441,9 @@ constexpr int kMaxSlotCap = 8;
 #endif
 #ifndef DFMI_BINS_PFN
 #define DFMI_BINS_PFN 4       // next segment's chunks prefetched during the contraction (L <= 256)
+#endif
+#ifndef DFMI_WIDE_LOADS
+#define DFMI_WIDE_LOADS 10    // demod_wide_kernel: 1-KB chunk loads in flight per wave
 #endif
 #ifndef DFMI_BINS_LDS_PAD
 #define DFMI_BINS_LDS_PAD 0   // extra dynamic LDS bytes per workgroup (occupancy experiments)
@@ -556,8 +560,8 @@ int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, i
   return DFMI_OK;
 }
 
-// demod_wide_kernel (component-major QI at many harmonics): KSEG = 8 bin sets per wave while
-// 4 waves' sets fit in 52 KB (3 workgroups per CU), else 4.
+// demod_wide_kernel (component-major QI at many harmonics): its geometry (16-B rows, an even
+// basis period 128..256, at most 127 harmonics).
 bool wide_geometry(bool vec2, int L, int ndata) {
   return vec2 && !(L & 1) && L >= 128 && L <= 256 && 2 * ndata + 1 <= 64 * 4;
 }
@@ -565,18 +569,16 @@ bool wide_geometry(bool vec2, int L, int ndata) {
 template <int NO, int KSEG>
 int launch_wide_t(const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tabT,
                   double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu) {
-  auto kern = dfmi::demod_wide_kernel<NO, KSEG, 8, 4>;
-  const size_t lds = (size_t)dfmi::kWavesPerBlock * KSEG * L * sizeof(double);
-  int per_cu = 0;
-  if (int orc = occupancy(kern, dfmi::kBlockThreads, lds, &per_cu)) return orc;
-  if (per_cu < 1) per_cu = 1;
+  auto kern = dfmi::demod_wide_kernel<NO, KSEG, DFMI_WIDE_LOADS, 4>;
+  const size_t lds = (size_t)dfmi::kWavesPerBlock * KSEG * dfmi::wide_set(L, NO, KSEG) * sizeof(double);
+  (void)n_cu;
   const int64_t per_block = (int64_t)dfmi::kWavesPerBlock * KSEG;
-  const int64_t groups = (nseg + per_block - 1) / per_block;
-  const int64_t grid = t_tune.demod_wide_grid ? groups : persistent_grid(n_cu, per_cu, groups);
+  const int64_t grid = (nseg + per_block - 1) / per_block;  // one group of KSEG segments per wave
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(dfmi::kBlockThreads), lds, st, x, nseg, stride, R, L, ndata,
-                     tabT, qi, qi_ld, dc);
+                     tabT, qi, qi_ld, dc, t_tune.demod_wide_dbg);
   HIPCHK(hipGetLastError());
-  g_last_demod = "demod_wide_kernel<" + std::to_string(NO) + "," + std::to_string(KSEG) + ",8,4>";
+  g_last_demod = "demod_wide_kernel<" + std::to_string(NO) + "," + std::to_string(KSEG) + "," +
+                 std::to_string(DFMI_WIDE_LOADS) + ",4>";
   return DFMI_OK;
 }
 
@@ -585,10 +587,12 @@ int launch_wide(int dev, const double* x, int64_t nseg, int64_t stride, int R, i
   const int no = 2 * ndata + 1 <= 64 ? 1 : 2 * ndata + 1 <= 128 ? 2 : 4;
   const double* tabT = nullptr;
   if (int rc = basis_table_wide(dev, L, ndata, w0, no, &tabT)) return rc;
-  const bool k8 = (size_t)dfmi::kWavesPerBlock * 8 * L * sizeof(double) <= 52 * 1024;
+  int k = t_tune.demod_wide_k;
+  if (k == 0) k = no >= 2 ? 8 : 4;  // r05t-x: 0.578 / 0.576 ms at ndata 30, 0.631 / 0.617 at 62
 #define DFMI_WIDE(NO_)                                                                                   \
-  return k8 ? launch_wide_t<NO_, 8>(x, nseg, stride, R, L, ndata, tabT, qi, qi_ld, dc, st, n_cu)          \
-            : launch_wide_t<NO_, 4>(x, nseg, stride, R, L, ndata, tabT, qi, qi_ld, dc, st, n_cu)
+  return k == 8 ? launch_wide_t<NO_, 8>(x, nseg, stride, R, L, ndata, tabT, qi, qi_ld, dc, st, n_cu)      \
+         : k == 4 ? launch_wide_t<NO_, 4>(x, nseg, stride, R, L, ndata, tabT, qi, qi_ld, dc, st, n_cu)    \
+                  : launch_wide_t<NO_, 2>(x, nseg, stride, R, L, ndata, tabT, qi, qi_ld, dc, st, n_cu)
   if (no == 1) DFMI_WIDE(1);
   if (no == 2) DFMI_WIDE(2);
   DFMI_WIDE(4);
@@ -964,7 +968,8 @@ const std::map<std::string, Knob>& knobs() {
       {"lm_general", {&Tuning::lm_general, {0, 1}}},
       {"demod_spw", {&Tuning::demod_spw, {}}},
       {"demod_wide", {&Tuning::demod_wide, {0, 1, 2}}},
-      {"demod_wide_grid", {&Tuning::demod_wide_grid, {0, 1}}},
+      {"demod_wide_k", {&Tuning::demod_wide_k, {0, 2, 4, 8}}},
+      {"demod_wide_dbg", {&Tuning::demod_wide_dbg, {0, 1, 2, 3}}},
       {"ekf_row", {&Tuning::ekf_row, {}}},
       {"ekf_rot", {&Tuning::ekf_rot, {0, 1}}},
       {"wdfmi_accel", {&Tuning::wdfmi_accel, {0, 1, 2, 3}}},

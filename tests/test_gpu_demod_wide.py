@@ -31,7 +31,7 @@ def _demod(env, x, nseg, R, nd, w0, **tune):
         return qi.cpu().numpy(), dc.cpu().numpy(), lib.dfmi_last_demod_kernel().decode()
     finally:
         for k in tune:
-            _lib.check(lib.dfmi_set_tuning(k.encode(), {"demod_wide": 1, "demod_wide_grid": 1}[k]), "tune")
+            _lib.check(lib.dfmi_set_tuning(k.encode(), {"demod_wide": 1, "demod_wide_k": 0}[k]), "tune")
 
 
 def _torch_ref(torch, x, nseg, R, nd, w0, take):
@@ -68,6 +68,7 @@ def test_wide_matches_fold_and_torch_reference(env, nd, f_samp, nseg, R):
     assert not kf.startswith("demod_wide"), kf
     scale = np.abs(qf).max()
     assert np.isfinite(qw).all() and np.isfinite(dw).all()
+    # half-period pairing: the basis at L - p taken equal to that at p (~h L w0 eps apart)
     assert np.abs(qw - qf).max() <= 1e-13 * max(scale, 1.0), np.abs(qw - qf).max()
     assert np.abs(dw - df).max() <= 1e-14 * max(np.abs(df).max(), 1.0)
     take = torch.arange(0, nseg, max(1, nseg // 24), device="cuda")
@@ -75,11 +76,12 @@ def test_wide_matches_fold_and_torch_reference(env, nd, f_samp, nseg, R):
     idx = take.cpu().numpy()
     assert np.abs(qw[:, idx] - rq).max() <= 1e-12, np.abs(qw[:, idx] - rq).max()
     assert np.abs(dw[idx] - rd).max() <= 1e-13
-    # the persistent grid (contiguous ranges) gives the same bits: a segment's result does
-    # not depend on the group it is contracted in
-    qp, dp, _ = _demod(env, x, nseg, R, nd, w0, demod_wide_grid=0)
-    np.testing.assert_array_equal(qp, qw)
-    np.testing.assert_array_equal(dp, dw)
+    # other group sizes give the same bits: a segment's result does not depend on the group
+    # it is contracted in
+    for k in (2, 8):
+        qp, dp, _ = _demod(env, x, nseg, R, nd, w0, demod_wide_k=k)
+        np.testing.assert_array_equal(qp, qw)
+        np.testing.assert_array_equal(dp, dw)
 
 
 @pytest.mark.parametrize("nd", [10, 16])

@@ -578,6 +578,34 @@ def extra_configs(torch, dev, lib, _lib, stream, cfg, cpu_leg):
     out["config2_sequential"] = {"workload": "100,000 segments (config 2's record), parallel=False: one warm-start "
                                              "chain", "value": round(nb2 / t2, 1), "unit": "segments/s",
                                  "s_per_record": round(t2, 4), "status0_frac": float(np.mean(k4.cpu().numpy() == 0))}
+    # ---- config 2 at more harmonics ("for ndata >= 20 the demodulation
+    # crosses the ridge; report that separately"): the record pipeline's step and the
+    # demodulation alone (component-major QI: demod_wide_kernel beyond 16 harmonics)
+    sweep = []
+    for nd in (16, 20, 30, 62):
+        def stepn():
+            _lib.check(lib.dfmi_nls_record(x.data_ptr(), 1, nb2 * R, nb2, R, nd, w0, 0, _lib.ptr(g1), 1, nb2 - 1, cfg,
+                                           o4.data_ptr(), k4.data_ptr(), _lib.DFMI_MEM_DEVICE, stream.cuda_stream),
+                       "dfmi_nls_record")
+        tn = _timed_steps(torch, stepn, 20, 5)
+        kstep = lib.dfmi_last_demod_kernel().decode()
+        okn = float(np.mean(k4.cpu().numpy() == 0))
+        qn = torch.empty((2 * nd, nb2), dtype=torch.float64, device=dev)
+        dn = torch.empty(nb2, dtype=torch.float64, device=dev)
+
+        def demn():
+            _lib.check(lib.dfmi_demod(x.data_ptr(), nb2, R, R, nd, w0, 0, qn.data_ptr(), dn.data_ptr(),
+                                      _lib.DFMI_MEM_DEVICE, stream.cuda_stream), "dfmi_demod")
+        td = _timed_steps(torch, demn, 20, 5)
+        sweep.append({"ndata": nd, "value": round(nb2 / tn, 1), "unit": "segments/s", "ms_per_step": round(tn * 1e3, 4),
+                      "step_demod_kernel": kstep, "status0_frac": okn,
+                      "demod_component_major_ms": round(td * 1e3, 4),
+                      "demod_kernel": lib.dfmi_last_demod_kernel().decode(),
+                      "demod_hbm_frac": round(nb2 * (8 * R + 8 * (2 * nd + 1)) / td / 1e9 / HBM_PEAK_GBS, 4),
+                      "hbm_frac_end_to_end": round(nb2 * (8 * R + 56) / tn / 1e9 / HBM_PEAK_GBS, 4)})
+        del qn, dn
+    out["config2_ndata_sweep"] = {"workload": "config 2 (100,000 x R=4000, 40 dB) at ndata 16 / 20 / 30 / 62, "
+                                              "dfmi_nls_record parallel", "points": sweep}
     del x, o4, k4
     torch.cuda.empty_cache()
     # ---- config 4's per-GPU shard on this one GPU: the same-workload N = 1 point of the

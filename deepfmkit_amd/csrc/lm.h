@@ -499,21 +499,88 @@ DFMI_HDI void harmonic_walk(int ndata, double m, double psi, Body&& body) {
   }
 }
 
+constexpr int kQPre = 4;
+
+// harmonic_walk handing the body its harmonic's QI as well (body(j, J_{j-1}, J_j, J_{j+1},
+// cos j psi, sin j psi, Q_j, I_j)). On the Miller branch (every ordinary m) the QI of
+// harmonic j - kQPre is loaded while harmonic j is evaluated, kQPre pairs in registers: the
+// walk is otherwise one L2 round trip per harmonic (QI from global memory, ~60 per evaluation
+// at ndata 62). The same values in the same operations: the same bits.
+// Only lm_chunks_kernel's chunk-size-1 path prefetches (QGlobalT<kQPre>: 196 -> 256 VGPRs, still
+// two waves per SIMD); elsewhere the registers cost occupancy or spills (the warm-start chain
+// kernel one wave per SIMD, the ladder 50 spilled values, the fused seed + demodulation
+// kernel 229), so QGlobal, QRow and QRegs keep kPre = 0 (plain loads).
+template <typename QF, typename Body>
+DFMI_HDI void harmonic_walk_q(int ndata, double m, double psi, const QF& q, Body&& body) {
+  const double am = fabs(m);
+  if (QF::kPre == 0 || m == 0.0 || am < DFMI_BES_TINY || !(am < 1.0e5) || dfmi_bessel_use_large(am, ndata + 1)) {
+    harmonic_walk(ndata, m, psi, [&](int j, double jm1, double j0, double jp1, double cj, double sj) {
+      body(j, jm1, j0, jp1, cj, sj, q.qc(j - 1), q.qs(j - 1));
+    });
+    return;
+  }
+  double s1, c1;
+  sincos(psi, &s1, &c1);
+  double sj, cj;
+  sincos((double)ndata * psi, &sj, &cj);
+  const int M = dfmi_bessel_start(ndata + 1, am);
+  int ef = 0;
+  const double S = dfmi_bessel_norm(am, M, &ef);
+  DfmiBesselWalk w;
+  w.init(m, M, S, ef);
+  double bq[kQPre], bs[kQPre];  // slot u: harmonic j - u of the block starting at j
+#pragma unroll
+  for (int u = 0; u < kQPre; ++u) {
+    const int h = ndata - 1 - u > 0 ? ndata - 1 - u : 0;
+    bq[u] = q.qc(h);
+    bs[u] = q.qs(h);
+  }
+  double jp1, j0, jm1;
+  for (int k = M; k > ndata; --k) w.step(&jp1, &j0, &jm1);
+  auto one = [&](int j, double qcv, double qsv) {
+    w.step(&jp1, &j0, &jm1);
+    body(j, jm1, j0, jp1, cj, sj, qcv, qsv);
+    const double cn = fma(cj, c1, sj * s1);     // cos((j-1) psi)
+    const double sn = fma(sj, c1, -(cj * s1));  // sin((j-1) psi)
+    cj = cn;
+    sj = sn;
+  };
+  int j = ndata;
+  for (; j >= kQPre; j -= kQPre) {
+#pragma unroll
+    for (int u = 0; u < kQPre; ++u) {
+      const double qcv = bq[u], qsv = bs[u];
+      const int h = j - 1 - u - kQPre > 0 ? j - 1 - u - kQPre : 0;  // next block's slot u (clamped)
+      bq[u] = q.qc(h);
+      bs[u] = q.qs(h);
+      one(j - u, qcv, qsv);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kQPre; ++u)
+    if (u < j) one(j - u, bq[u], bs[u]);
+}
+
 // QI accessors. qc(h) = Q_{h+1} (cos), qs(h) = I_{h+1} (sin), dc() = the segment mean.
 //  QGlobal: component-major qi[c·ld + s] (dfmi_demod's layout; dc lives elsewhere).
 //  QRow<STRIDE>: one demodulation row per segment (demod.h qi_row_pos): blocks of
 //  16 doubles [cos h0..7 | sin h0..7] per 8 harmonics, dc in a spare slot;
 //  STRIDE = 1 for a row in global memory, 65 for a wave's rows transposed into LDS.
-struct QGlobal {
+//  kPre: QI pairs harmonic_walk_q keeps in flight for the accessor (0: plain loads).
+template <int PRE = 0>
+struct QGlobalT {
+  static constexpr int kPre = PRE;
   const double* __restrict__ p;
   int64_t ld;
   int nd;
   DFMI_HDI double qc(int h) const { return p[(int64_t)h * ld]; }
   DFMI_HDI double qs(int h) const { return p[(int64_t)(nd + h) * ld]; }
 };
+using QGlobal = QGlobalT<>;
 
 template <int STRIDE>
 struct QRow {
+  static constexpr int kPre = 0;
   const double* __restrict__ p;
   DFMI_HDI double qc(int h) const { return p[((h >> 3) * 16 + (h & 7)) * STRIDE]; }
   DFMI_HDI double qs(int h) const { return p[((h >> 3) * 16 + 8 + (h & 7)) * STRIDE]; }
@@ -524,6 +591,7 @@ struct QRow {
 // the register path's evaluations then index it with compile-time harmonics only.
 template <int N>
 struct QRegs {
+  static constexpr int kPre = 0;
   double c[N], s[N];
   template <typename QF>
   DFMI_HDI void load(const QF& q) {
@@ -544,8 +612,9 @@ DFMI_HDI void eval_gen(const QF& q, int nd, const double (&p)[4], Eval& e) {
   sincos(phi, &sph, &cph);
   const bool a_nz = (a != 0.0);
   eval_zero(e);
-  harmonic_walk(nd, m, psi, [&](int j, double Jm1, double J0, double Jp1, double cj, double sj) {
-    harmonic_term(e, j, a, a_nz, cph, sph, Jm1, J0, Jp1, cj, sj, q.qc(j - 1), q.qs(j - 1));
+  harmonic_walk_q(nd, m, psi, q, [&](int j, double Jm1, double J0, double Jp1, double cj, double sj, double qc,
+                                     double qs) {
+    harmonic_term(e, j, a, a_nz, cph, sph, Jm1, J0, Jp1, cj, sj, qc, qs);
   });
 }
 
@@ -558,11 +627,11 @@ DFMI_HDI double ssq_gen(const QF& q, int nd, const double (&p)[4]) {
   double sph, cph;
   sincos(phi, &sph, &cph);
   double ssq = 0.0;
-  harmonic_walk(nd, m, psi, [&](int j, double, double J0, double, double cj, double sj) {
+  harmonic_walk_q(nd, m, psi, q, [&](int j, double, double J0, double, double cj, double sj, double qc, double qs) {
     const double pt = quarter_turn(j, cph, sph);
     const double common = a * pt * J0;
-    const double rq = fma(-common, cj, q.qc(j - 1));
-    const double ri = fma(common, sj, q.qs(j - 1));
+    const double rq = fma(-common, cj, qc);
+    const double ri = fma(common, sj, qs);
     ssq = fma(rq, rq, ssq);
     ssq = fma(ri, ri, ssq);
   });
@@ -1060,12 +1129,12 @@ __host__ __device__ __forceinline__ int fit_segment_q(const QF& q, int ndata, co
 // Component-major QI (qi[c·ld + s], qptr = qi + s). QI is re-read per evaluation
 // through the vector L1 (64 segments x 2·ndata doubles = 10 KB per wave): keeping
 // it in registers costs 2·NDMAX VGPRs and with them the second wave per SIMD.
-template <int NDMAX, int FLAT = 1>
+template <int NDMAX, int FLAT = 1, int PRE = 0>
 __host__ __device__ __forceinline__ int fit_segment(const double* __restrict__ qptr, int64_t ld, int ndata,
                                                  const double* __restrict__ jtab, const LMConst& c, double (&p)[4],
                                                  double& ssq_out) {
-  const QGlobal qg{qptr, ld, ndata};
-  return fit_segment_q<NDMAX, QGlobal, FLAT>(qg, ndata, jtab, c, p, ssq_out);
+  const QGlobalT<PRE> qg{qptr, ld, ndata};
+  return fit_segment_q<NDMAX, QGlobalT<PRE>, FLAT>(qg, ndata, jtab, c, p, ssq_out);
 }
 
 // Seeds of up to 8 records passed by value (read with constant offsets only).
@@ -1204,7 +1273,7 @@ __global__ __launch_bounds__(64) void lm_chunks_kernel(
         qr.load(qg);
         st = fit_segment_q2<NDMAX, QRegs<nd_cap(NDMAX)>, QGlobal, 1>(qr, qg, ndata, jtab, c, p, ssq);
       } else {
-        st = fit_segment<NDMAX>(qi + sidx, qi_ld, ndata, jtab, c, p, ssq);
+        st = fit_segment<NDMAX, 1, CHAIN ? 0 : kQPre>(qi + sidx, qi_ld, ndata, jtab, c, p, ssq);
       }
       put(sidx, st, ssq);
     };

@@ -31,7 +31,8 @@ def _demod(env, x, nseg, R, nd, w0, **tune):
         return qi.cpu().numpy(), dc.cpu().numpy(), lib.dfmi_last_demod_kernel().decode()
     finally:
         for k in tune:
-            _lib.check(lib.dfmi_set_tuning(k.encode(), {"demod_wide": 1, "demod_wide_k": 0}[k]), "tune")
+            _lib.check(lib.dfmi_set_tuning(k.encode(), {"demod_wide": 1, "demod_wide_k": 0, "demod_wide_from": 13}[k]),
+                       "tune")
 
 
 def _torch_ref(torch, x, nseg, R, nd, w0, take):
@@ -84,22 +85,49 @@ def test_wide_matches_fold_and_torch_reference(env, nd, f_samp, nseg, R):
         np.testing.assert_array_equal(dp, dw)
 
 
-@pytest.mark.parametrize("nd", [10, 16])
+@pytest.mark.parametrize("nd", [10, 12, 16])
 def test_wide_forced_at_bin_kernel_ndata(env, nd):
-    """demod_wide = 2 runs the many-harmonic kernel where the bin kernel also applies (A/B):
-    the same QI within a few ulps."""
+    """demod_wide = 2 runs the many-harmonic kernel where the bin kernel also applies (A/B; by
+    default it takes over from 13 harmonics): the same QI within a few ulps."""
     torch = env[0]
     w0 = 2 * np.pi * 1000.0 / 200000.0
     g = torch.Generator(device="cuda")
     g.manual_seed(nd)
     nseg, R = 2049, 4000
     x = torch.randn(nseg * R, dtype=torch.float64, device="cuda", generator=g) - 0.5
-    qb, db, kb = _demod(env, x, nseg, R, nd, w0)
+    qb, db, kb = _demod(env, x, nseg, R, nd, w0, demod_wide=0)
     assert kb.startswith("demod_bins_kernel"), kb
     qw, dw, kw = _demod(env, x, nseg, R, nd, w0, demod_wide=2)
     assert kw.startswith("demod_wide_kernel"), kw
     assert np.abs(qw - qb).max() <= 1e-13 * max(np.abs(qb).max(), 1.0)
     assert np.abs(dw - db).max() <= 1e-14
+
+
+@pytest.mark.parametrize("nd", [12, 13, 16])
+def test_record_pipeline_switches_layout_at_wide_from(env, nd):
+    """ndata >= demod_wide_from (13): the record pipeline leaves the row layout and the fused
+    seed launch for component-major QI through demod_wide_kernel (seed on the side stream);
+    below it the fused bin kernel stays. Noiseless m = 6 segments are recovered either way,
+    and the two layouts agree to the parity tolerance."""
+    torch, _lib, lib = env
+    from deepfmkit_amd.fitters import nls_records
+    nseg, R = 3000, 4000
+    t = torch.arange(R, dtype=torch.float64, device="cuda") / 200000.0
+    seg_phi = torch.linspace(-0.4, 0.4, nseg, dtype=torch.float64, device="cuda")
+    x = (1.0 + torch.cos(seg_phi[:, None] + 6.0 * torch.cos(2 * np.pi * 1000.0 * t[None, :] + 0.1))).reshape(1, -1)
+    cols, ok = nls_records(x, 200000.0, 1000.0, R, nseg, nd)
+    k = lib.dfmi_last_demod_kernel().decode()
+    assert k.startswith("demod_wide_kernel" if nd >= 13 else "demod_seed_bins_kernel"), (nd, k)
+    _lib.check(lib.dfmi_set_tuning(b"demod_wide_from", 1000), "tune")
+    try:
+        cols2, ok2 = nls_records(x, 200000.0, 1000.0, R, nseg, nd)
+        assert lib.dfmi_last_demod_kernel().decode().startswith("demod_seed_bins_kernel")
+    finally:
+        _lib.check(lib.dfmi_set_tuning(b"demod_wide_from", 13), "tune")
+    cols, ok, cols2, ok2 = (a.cpu().numpy() for a in (cols, ok, cols2, ok2))
+    assert (ok == 0).all() and (ok2 == 0).all()
+    assert np.abs(cols[1] - 6.0).max() < 1e-9
+    assert np.abs(cols[:4] - cols2[:4]).max() < 1e-9
 
 
 def test_record_pipeline_at_many_harmonics(env):

@@ -460,15 +460,22 @@ def _demod_both(x, nseg, R, nd, w0):
 @pytest.mark.parametrize("nd", [10, 3, 8, 16])
 def test_demod_rows_bit_identical_to_component_major(nd):
     """The record pipeline's row layout (full-line stores, dc inside the row) carries
-    exactly the values of dfmi_demod; unused slots are 0. ndata 8/16 have no spare
-    slot (dc in an 8-double tail)."""
+    exactly the values of dfmi_demod's bin kernel; unused slots are 0. ndata 8/16 have no
+    spare slot (dc in an 8-double tail). (From 13 harmonics dfmi_demod runs
+    demod_wide_kernel by default, tests/test_gpu_demod_wide.py; demod_wide = 0 here.)"""
     import torch
+    from deepfmkit_amd import _lib
     from deepfmkit_amd.fitters import w0_of
+    lib = _lib.load()
     nseg, R = 3001, 4000
     g = torch.Generator(device="cuda")
     g.manual_seed(nd)
     x = torch.randn(nseg * R, dtype=torch.float64, device="cuda", generator=g) + 0.25
-    qi, dc, rows, qs, dpos = _demod_both(x, nseg, R, nd, w0_of(1000.0, 200000.0))
+    _lib.check(lib.dfmi_set_tuning(b"demod_wide", 0), "tune")
+    try:
+        qi, dc, rows, qs, dpos = _demod_both(x, nseg, R, nd, w0_of(1000.0, 200000.0))
+    finally:
+        _lib.check(lib.dfmi_set_tuning(b"demod_wide", 1), "tune")
     nblk = (nd + 7) // 8
     assert qs == 16 * nblk + (0 if nd % 8 else 8)
     used = np.zeros(qs, bool)

@@ -591,7 +591,8 @@ __global__ __launch_bounds__(kBlockThreads) void demod_bins_kernel(
 __host__ __device__ constexpr int wide_set(int L, int NO, int KSEG) {
   // per-set doubles: the bins (L) + 4 for the paired layout (ym + 2·npair <= L + 4), or this wave's share of the
   // result tile (64·NO rows x (KSEG + 1) pitch), whichever is larger
-  return (L + 4 > (64 * NO * (KSEG + 1) + KSEG - 1) / KSEG) ? L + 4 : (64 * NO * (KSEG + 1) + KSEG - 1) / KSEG;
+  // (even: the sets' pair loads / stores stay 16-B aligned)
+  return (((L + 4 > (64 * NO * (KSEG + 1) + KSEG - 1) / KSEG) ? L + 4 : (64 * NO * (KSEG + 1) + KSEG - 1) / KSEG) + 1) & ~1;
 }
 template <int LOADS, int PFN>
 __device__ __forceinline__ void wide_fold(const double* __restrict__ xs0, int R, int L, double* ybin, int lane,
@@ -668,12 +669,71 @@ __device__ __forceinline__ void wide_fold(const double* __restrict__ xs0, int R,
   }
 }
 
+// The fold of a workgroup-wave's nk CONTIGUOUS segments (seg_stride == R) as one flat stream of
+// nk·R samples: 1-KB chunk loads, LOADS in flight, with no restart at segment boundaries (a
+// short segment, R = 200, is otherwise one exposed memory round trip of 1.6 KB: 0.1 of peak,
+// r05ad). Lane l's two samples of a chunk sit in one segment (R even), at position t, bin p;
+// (k, t, p) advance by 128 samples a chunk (p -= R mod L at each segment wrap).
+template <int LOADS>
+__device__ __forceinline__ void wide_fold_flat(const double* __restrict__ xg, int nk, int R, int L, double* ybase,
+                                               int ws, int lane) {
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  for (int k = 0; k < nk; ++k)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (2 * (lane + 64 * j) < L) *reinterpret_cast<d2v*>(ybase + k * ws + 2 * (lane + 64 * j)) = d2v{0.0, 0.0};
+  const int64_t total = (int64_t)nk * R;
+  const int64_t nch = total >> 7;
+  const int tail = (int)(total - (nch << 7));
+  const int rL = R % L;
+  int k = (2 * lane) / R, t = 2 * lane - k * R, p = t % L;
+  auto add = [&](const d2v v) {
+    d2v* yp = reinterpret_cast<d2v*>(ybase + k * ws + p);
+    d2v y = *yp;
+    y.x += v.x;
+    y.y += v.y;
+    *yp = y;
+    t += 128;
+    p += 128;
+    if (p >= L) p -= L;
+    while (t >= R) {
+      t -= R;
+      ++k;
+      p -= rL;
+      if (p < 0) p += L;
+    }
+  };
+  const d2v* __restrict__ xv = reinterpret_cast<const d2v*>(xg) + lane;
+  int64_t c = 0;
+  for (; c + LOADS <= nch; c += LOADS) {
+    d2v v[LOADS];
+#pragma unroll
+    for (int u = 0; u < LOADS; ++u) v[u] = __builtin_nontemporal_load(xv + (c + u) * 64);
+#pragma unroll
+    for (int u = 0; u < LOADS; ++u) add(v[u]);
+  }
+  {
+    const int rem = (int)(nch - c);
+    d2v v[LOADS];
+#pragma unroll
+    for (int u = 0; u < LOADS; ++u)
+      if (u < rem) v[u] = __builtin_nontemporal_load(xv + (c + u) * 64);
+    d2v tv = d2v{0.0, 0.0};
+    if (2 * lane < tail) tv = xv[nch * 64];  // partial last chunk (tail even: both samples or none)
+#pragma unroll
+    for (int u = 0; u < LOADS; ++u)
+      if (u < rem) add(v[u]);
+    if (2 * lane < tail) add(tv);
+  }
+}
+
 template <int NO, int KSEG, int LOADS, int PFN, int TD = (NO >= 4 ? 2 : 8 / NO)>
 __global__ __launch_bounds__(kBlockThreads, 3) void demod_wide_kernel(  // 3 waves per SIMD: <= 168 VGPRs
     const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
     const double* __restrict__ tabT, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc, int dbg) {
   // dbg (diagnostics, demod_wide_dbg): bit 0 skips the contraction (acc = one bin), bit 1
-  // the stores (kept alive by a never-true NaN test) — fold / contraction / store split
+  // the stores (kept alive by a never-true NaN test) — fold / contraction / store split;
+  // bit 2 folds contiguous segments one by one (the strided-record path) instead of flat
   typedef double d2v __attribute__((ext_vector_type(2)));
   extern __shared__ __attribute__((aligned(16))) double lds_dyn[];
   const int lane = threadIdx.x & 63;
@@ -690,17 +750,23 @@ __global__ __launch_bounds__(kBlockThreads, 3) void demod_wide_kernel(  // 3 wav
   const int ym = (half + 2) & ~1;     // start of y- in a set
   const bool pfok = PFN > 0 && (R >> 7) >= PFN;
   double pf[PFN > 0 ? PFN : 1][2];
-  if (pfok && nk > 0) {
+  if (pfok && nk > 0 && !(seg_stride == R && !(dbg & 4))) {
     const double* __restrict__ x0 = x + sbeg * seg_stride + 2 * lane;
 #pragma unroll
     for (int u = 0; u < (PFN > 0 ? PFN : 1); ++u) VecT<2>::load_nt(x0 + u * 128, pf[u]);
   }
+  const bool flat = seg_stride == R && !(dbg & 4);  // contiguous segments: one flat stream per wave
+  if (flat && nk > 0) wide_fold_flat<LOADS>(x + sbeg * seg_stride, nk, R, L, ybase, ws, lane);
   for (int k = 0; k < nk; ++k) {
     const int64_t s = sbeg + k;
     double* yb = ybase + k * ws;
     const double* nx = s + 1 < send ? x + (s + 1) * seg_stride : nullptr;
-    if (pfok) wide_fold<LOADS, PFN>(x + s * seg_stride, R, L, yb, lane, pf, nx);
-    else wide_fold<LOADS, 0>(x + s * seg_stride, R, L, yb, lane, pf, nullptr);
+    if (flat) {
+    } else if (pfok) {
+      wide_fold<LOADS, PFN>(x + s * seg_stride, R, L, yb, lane, pf, nx);
+    } else {
+      wide_fold<LOADS, 0>(x + s * seg_stride, R, L, yb, lane, pf, nullptr);
+    }
     // pair the bins in place: y+ at [0, 2 npp), y- at [ym, ym + 2 npp) (ym even: 16-B aligned
     // pair reads), zero past half; every lane reads all its inputs before any lane writes
     // (one wave: its LDS operations execute in order)

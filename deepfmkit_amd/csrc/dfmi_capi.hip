@@ -55,6 +55,7 @@ struct Tuning {
                          // many-harmonic kernel wherever its geometry applies
   int demod_wide_from = 13;  // ndata from which demod_wide_kernel (component-major) goes ahead of the bin
                              // kernel, and the record pipeline leaves the row layout for it
+  int demod_wide_rmax = 2000;  // segments shorter than this go through demod_wide_kernel too
   int demod_wide_dbg = 0;   // diagnostics: demod_wide_kernel without its contraction (1) / stores (2)
   int demod_wide_k = 0;     // demod_wide_kernel segments per wave (KSEG): 0 = 4 (8 beyond 31 harmonics); 2 / 4 / 8 (A/B)
   int ekf_row = 1;       // EKF: ekf_row_kernel (4 channels per wave) up to ekf_row x 4 x 4 x CUs channels
@@ -564,10 +565,15 @@ int launch_bins_t(const double* x, int64_t nseg, int64_t stride, int R, int L, i
 
 // Component-major QI through demod_wide_kernel ahead of the bin kernel: from
 // demod_wide_from harmonics on (the bin kernel's LDS basis costs it occupancy from 13: 0.624
-// vs ~0.55 ms at ndata 16, bench r05z), or everywhere with demod_wide = 2 (A/B).
-bool wide_first(int ndata) {
+// vs ~0.55 ms at ndata 16, bench r05z), for segments shorter than demod_wide_rmax samples
+// (the bin kernel's per-segment contraction and butterfly dominate there: the record step at
+// R = 200 / 400 / 1000, ndata 10, 1.69 / 0.96 / 0.43 ms against 0.95 / 0.58 / 0.34 through
+// demod_wide_kernel, 0.233 against 0.265 at R = 4000: profiles/r05/short_segments.jsonl), or
+// everywhere with demod_wide = 2 (A/B).
+bool wide_first(int ndata, int R) {
   return t_tune.demod_kernel == 1 &&
-         (t_tune.demod_wide == 2 || (t_tune.demod_wide == 1 && ndata >= t_tune.demod_wide_from));
+         (t_tune.demod_wide == 2 ||
+          (t_tune.demod_wide == 1 && (ndata >= t_tune.demod_wide_from || R < t_tune.demod_wide_rmax)));
 }
 
 // demod_wide_kernel (component-major QI at many harmonics): its geometry (16-B rows, an even
@@ -672,7 +678,7 @@ int demod_device(int dev, const double* x, int64_t nseg, int64_t stride, int R, 
       if (rc) return rc;
       const size_t lds = (size_t)2 * ndata * L * sizeof(double);
       const bool use_lds = lds <= 64 * 1024 && lds <= lds_cap;
-      if (!rows && wide_first(ndata) && wide_geometry(vec2, L, ndata))
+      if (!rows && wide_first(ndata, R) && wide_geometry(vec2, L, ndata))
         return launch_wide(dev, x, nseg, stride, R, L, ndata, w0, qi, qi_ld, dc, st, n_cu);
       rc = try_bins(x, nseg, stride, R, L, ndata, tab, qi, qi_ld, dc, st, n_cu, vec2, lds_cap, rows);
       if (rc <= 0) return rc;
@@ -896,7 +902,7 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
   int L = period;
   if (L == 0) L = detect_period_impl(w0, R, ndata);
   const bool even_recs = nrec == 1 || (rec_stride % 2) == 0;
-  const bool wide = L > 0 && even_recs && wide_first(ndata) && wide_geometry(vec2_ok(x, R, L), L, ndata);
+  const bool wide = L > 0 && even_recs && wide_first(ndata, R) && wide_geometry(vec2_ok(x, R, L), L, ndata);
   const bool rows = parallel && (nbuf <= 1 || nchunk >= nbuf - 1) && even_recs && !wide &&
                     rows_supported(dev, x, R, R, ndata, w0, period);
   const int64_t qs = rows ? dfmi_row_stride(ndata) : 0;
@@ -983,7 +989,8 @@ const std::map<std::string, Knob>& knobs() {
       {"demod_wide", {&Tuning::demod_wide, {0, 1, 2}}},
       {"demod_wide_k", {&Tuning::demod_wide_k, {0, 2, 4, 8}}},
       {"demod_wide_from", {&Tuning::demod_wide_from, {}}},
-      {"demod_wide_dbg", {&Tuning::demod_wide_dbg, {0, 1, 2, 3}}},
+      {"demod_wide_rmax", {&Tuning::demod_wide_rmax, {}}},
+      {"demod_wide_dbg", {&Tuning::demod_wide_dbg, {0, 1, 2, 3, 4, 5, 6, 7}}},
       {"ekf_row", {&Tuning::ekf_row, {}}},
       {"ekf_rot", {&Tuning::ekf_rot, {0, 1}}},
       {"wdfmi_accel", {&Tuning::wdfmi_accel, {0, 1, 2, 3}}},

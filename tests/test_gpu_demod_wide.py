@@ -2,7 +2,8 @@
 LDS basis, component-major QI) against the fold / bin kernels and a torch fp64 restatement
 of calculate_quadratures (fit.py:18-66: mean(x cos((n+1) w0 t)), mean(x sin(...)), and
 fitters.py:57's dc = mean(x)), on ragged shapes: segment counts that leave partial groups,
-R with a partial last chunk, basis periods 128..256 (KSEG 8 and 4), 1..3 output slices."""
+R with a partial last chunk, basis periods 128..256 (KSEG 8 and 4), 1..3 output slices, and
+the flat multi-segment fold of contiguous short segments."""
 import numpy as np
 import pytest
 
@@ -31,8 +32,8 @@ def _demod(env, x, nseg, R, nd, w0, **tune):
         return qi.cpu().numpy(), dc.cpu().numpy(), lib.dfmi_last_demod_kernel().decode()
     finally:
         for k in tune:
-            _lib.check(lib.dfmi_set_tuning(k.encode(), {"demod_wide": 1, "demod_wide_k": 0, "demod_wide_from": 13}[k]),
-                       "tune")
+            _lib.check(lib.dfmi_set_tuning(k.encode(), {"demod_wide": 1, "demod_wide_k": 0, "demod_wide_from": 13,
+                                                         "demod_wide_dbg": 0}[k]), "tune")
 
 
 def _torch_ref(torch, x, nseg, R, nd, w0, take):
@@ -83,6 +84,30 @@ def test_wide_matches_fold_and_torch_reference(env, nd, f_samp, nseg, R):
         qp, dp, _ = _demod(env, x, nseg, R, nd, w0, demod_wide_k=k)
         np.testing.assert_array_equal(qp, qw)
         np.testing.assert_array_equal(dp, dw)
+
+
+@pytest.mark.parametrize("nd,R,nseg", [(10, 200, 4099), (20, 300, 777), (20, 100, 1001), (30, 1000, 513),
+                                        (15, 4000, 67)])
+def test_flat_fold_equals_per_segment_fold(env, nd, R, nseg):
+    """Contiguous segments are folded as one flat stream per wave (demod_wide_fold_flat):
+    the same bits as the segment-by-segment fold (demod_wide_dbg bit 2), for segments
+    shorter than a chunk (R = 100), not a whole number of periods (R = 300, L = 200), and
+    long; and the reference's quadratures."""
+    torch = env[0]
+    w0 = 2 * np.pi * 1000.0 / 200000.0
+    g = torch.Generator(device="cuda")
+    g.manual_seed(R + nd)
+    x = torch.randn(nseg * R, dtype=torch.float64, device="cuda", generator=g) + 0.5
+    qf, df, kf = _demod(env, x, nseg, R, nd, w0)
+    assert kf.startswith("demod_wide_kernel"), kf  # R < 2000 or ndata >= 13
+    qs, ds, _ = _demod(env, x, nseg, R, nd, w0, demod_wide_dbg=4)
+    np.testing.assert_array_equal(qf, qs)
+    np.testing.assert_array_equal(df, ds)
+    take = torch.arange(0, nseg, max(1, nseg // 16), device="cuda")
+    rq, rd = _torch_ref(torch, x, nseg, R, nd, w0, take)
+    idx = take.cpu().numpy()
+    assert np.abs(qf[:, idx] - rq).max() <= 1e-12
+    assert np.abs(df[idx] - rd).max() <= 1e-13
 
 
 @pytest.mark.parametrize("nd", [10, 12, 16])

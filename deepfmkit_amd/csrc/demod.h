@@ -727,7 +727,9 @@ __device__ __forceinline__ void wide_fold_flat(const double* __restrict__ xg, in
   }
 }
 
-template <int NO, int KSEG, int LOADS, int PFN, int TD = (NO >= 4 ? 2 : 8 / NO)>
+// HALF (NO = 1, 2·ndata + 1 <= 32): the two half-waves contract different segments (lanes
+// 0..31 the even k, 32..63 the odd), halving the contraction's instructions per segment.
+template <int NO, int KSEG, int LOADS, int PFN, int HALF = 0, int TD = (NO >= 4 ? 2 : 8 / NO)>
 __global__ __launch_bounds__(kBlockThreads, 3) void demod_wide_kernel(  // 3 waves per SIMD: <= 168 VGPRs
     const double* __restrict__ x, int64_t nseg, int64_t seg_stride, int R, int L, int ndata,
     const double* __restrict__ tabT, double* __restrict__ qi, int64_t qi_ld, double* __restrict__ dc, int dbg) {
@@ -787,29 +789,33 @@ __global__ __launch_bounds__(kBlockThreads, 3) void demod_wide_kernel(  // 3 wav
       }
     }
   }
-  double acc[KSEG][NO];
+  static_assert(!HALF || (NO == 1 && KSEG % 2 == 0), "half-wave contraction: one output slice, even KSEG");
+  constexpr int KH = HALF ? KSEG / 2 : KSEG;  // segments contracted per lane
+  const int grp = HALF ? lane >> 5 : 0;       // half-wave: which segments (k = 2 j + grp)
+  const int ol = HALF ? lane & 31 : lane;     // output lane
+  double acc[KH][NO];
 #pragma unroll
-  for (int k = 0; k < KSEG; ++k)
+  for (int j = 0; j < KH; ++j)
 #pragma unroll
-    for (int i = 0; i < NO; ++i) acc[k][i] = 0.0;
+    for (int i = 0; i < NO; ++i) acc[j][i] = 0.0;
   // lanes of sin rows read y-, the others y+ (two addresses per lane group: no conflict)
   int yoff[NO];
 #pragma unroll
   for (int i = 0; i < NO; ++i) {
-    const int o = lane + 64 * i;
+    const int o = ol + 64 * i;
     yoff[i] = (o >= ndata && o < 2 * ndata) ? ym : 0;
   }
   const int npp = (dbg & 1) || nk == 0 ? 0 : npair;
   if (dbg & 1)
 #pragma unroll
-    for (int k = 0; k < KSEG; ++k) acc[k][0] = ybase[k * ws + lane];
+    for (int j = 0; j < KH; ++j) acc[j][0] = ybase[(HALF ? 2 * j + grp : j) * ws + lane];
   const d2v* __restrict__ T2 = reinterpret_cast<const d2v*>(tabT);
   d2v tb[TD][NO];
 #pragma unroll
   for (int u = 0; u < TD; ++u)
 #pragma unroll
     for (int i = 0; i < NO; ++i)
-      if (u < npp) tb[u][i] = T2[(size_t)u * 64 * NO + lane + 64 * i];
+      if (u < npp) tb[u][i] = T2[(size_t)u * 64 * NO + ol + 64 * i];
   for (int pp0 = 0; pp0 < npp; pp0 += TD) {
 #pragma unroll
     for (int u = 0; u < TD; ++u) {
@@ -819,15 +825,16 @@ __global__ __launch_bounds__(kBlockThreads, 3) void demod_wide_kernel(  // 3 wav
 #pragma unroll
         for (int i = 0; i < NO; ++i) {
           t[i] = tb[u][i];
-          if (pp + TD < npp) tb[u][i] = T2[(size_t)(pp + TD) * 64 * NO + lane + 64 * i];
+          if (pp + TD < npp) tb[u][i] = T2[(size_t)(pp + TD) * 64 * NO + ol + 64 * i];
         }
 #pragma unroll
-        for (int k = 0; k < KSEG; ++k) {
+        for (int j = 0; j < KH; ++j) {
+          const int k = HALF ? 2 * j + grp : j;
 #pragma unroll
           for (int i = 0; i < NO; ++i) {
             const d2v y = *reinterpret_cast<const d2v*>(ybase + k * ws + yoff[i] + 2 * pp);
-            acc[k][i] = fma(y.x, t[i].x, acc[k][i]);
-            acc[k][i] = fma(y.y, t[i].y, acc[k][i]);
+            acc[j][i] = fma(y.x, t[i].x, acc[j][i]);
+            acc[j][i] = fma(y.y, t[i].y, acc[j][i]);
           }
         }
       }
@@ -842,9 +849,10 @@ __global__ __launch_bounds__(kBlockThreads, 3) void demod_wide_kernel(  // 3 wav
   // stream (profiles/r05/wide_demod_ab.jsonl)
   constexpr int KP = KSEG + 1;
 #pragma unroll
-  for (int k = 0; k < KSEG; ++k)
+  for (int j = 0; j < KH; ++j)
 #pragma unroll
-    for (int i = 0; i < NO; ++i) ybase[(lane + 64 * i) * KP + k] = acc[k][i] / (double)R;  // mean: sum / count
+    for (int i = 0; i < NO; ++i)  // mean: sum / count
+      ybase[(ol + 64 * i) * KP + (HALF ? 2 * j + grp : j)] = acc[j][i] / (double)R;
   __syncthreads();
   constexpr int SEGS = kWavesPerBlock * KSEG;  // consecutive segments per output row
   for (int e = threadIdx.x; e < nout * SEGS; e += kBlockThreads) {

@@ -56,8 +56,9 @@ struct Tuning {
   int demod_wide_from = 13;  // ndata from which demod_wide_kernel (component-major) goes ahead of the bin
                              // kernel, and the record pipeline leaves the row layout for it
   int demod_wide_rmax = 2000;  // segments shorter than this go through demod_wide_kernel too
+  int demod_wide_half = 1;  // demod_wide_kernel: half-wave contraction at 2·ndata + 1 <= 32 (0: off, A/B)
   int demod_wide_dbg = 0;   // diagnostics: demod_wide_kernel without its contraction (1) / stores (2)
-  int demod_wide_k = 0;     // demod_wide_kernel segments per wave (KSEG): 0 = 4 (8 beyond 31 harmonics); 2 / 4 / 8 (A/B)
+  int demod_wide_k = 0;     // demod_wide_kernel segments per wave (KSEG): 0 = 8; 2 / 4 / 8 (A/B)
   int ekf_row = 1;       // EKF: ekf_row_kernel (4 channels per wave) up to ekf_row x 4 x 4 x CUs channels
                          // (past one wave per SIMD the issue-bound rows share a SIMD, and one lane per
                          // channel carries 16x the channels per instruction); 0 = ekf_kernel only
@@ -585,7 +586,10 @@ bool wide_geometry(bool vec2, int L, int ndata) {
 template <int NO, int KSEG>
 int launch_wide_t(const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, const double* tabT,
                   double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu) {
-  auto kern = dfmi::demod_wide_kernel<NO, KSEG, DFMI_WIDE_LOADS, 4>;
+  // half-wave contraction where the outputs fit 32 lanes (2·ndata + 1 <= 32)
+  const bool half = NO == 1 && 2 * ndata + 1 <= 32 && t_tune.demod_wide_half;
+  auto kern = half ? dfmi::demod_wide_kernel<NO, KSEG, DFMI_WIDE_LOADS, 4, (NO == 1 && KSEG % 2 == 0) ? 1 : 0>
+                   : dfmi::demod_wide_kernel<NO, KSEG, DFMI_WIDE_LOADS, 4, 0>;
   const size_t lds = (size_t)dfmi::kWavesPerBlock * KSEG * dfmi::wide_set(L, NO, KSEG) * sizeof(double);
   (void)n_cu;
   const int64_t per_block = (int64_t)dfmi::kWavesPerBlock * KSEG;
@@ -594,7 +598,7 @@ int launch_wide_t(const double* x, int64_t nseg, int64_t stride, int R, int L, i
                      tabT, qi, qi_ld, dc, t_tune.demod_wide_dbg);
   HIPCHK(hipGetLastError());
   g_last_demod = "demod_wide_kernel<" + std::to_string(NO) + "," + std::to_string(KSEG) + "," +
-                 std::to_string(DFMI_WIDE_LOADS) + ",4>";
+                 std::to_string(DFMI_WIDE_LOADS) + ",4," + (half && KSEG % 2 == 0 ? "1" : "0") + ">";
   return DFMI_OK;
 }
 
@@ -604,7 +608,10 @@ int launch_wide(int dev, const double* x, int64_t nseg, int64_t stride, int R, i
   const double* tabT = nullptr;
   if (int rc = basis_table_wide(dev, L, ndata, w0, no, &tabT)) return rc;
   int k = t_tune.demod_wide_k;
-  if (k == 0) k = no >= 2 ? 8 : 4;  // r05t-x: 0.578 / 0.576 ms at ndata 30, 0.631 / 0.617 at 62
+  // KSEG 8: level with 4 at R = 4000 (0.578 / 0.576 ms at ndata 30, r05t-x), ahead at 62 (0.631 /
+  // 0.617) and for short segments, where the contraction dominates (R = 200, ndata 10: 0.768 /
+  // 0.684 ms; R = 400: 0.471 / 0.423; profiles/r05/short_segments_split.jsonl)
+  if (k == 0) k = 8;
 #define DFMI_WIDE(NO_)                                                                                   \
   return k == 8 ? launch_wide_t<NO_, 8>(x, nseg, stride, R, L, ndata, tabT, qi, qi_ld, dc, st, n_cu)      \
          : k == 4 ? launch_wide_t<NO_, 4>(x, nseg, stride, R, L, ndata, tabT, qi, qi_ld, dc, st, n_cu)    \
@@ -990,6 +997,7 @@ const std::map<std::string, Knob>& knobs() {
       {"demod_wide_k", {&Tuning::demod_wide_k, {0, 2, 4, 8}}},
       {"demod_wide_from", {&Tuning::demod_wide_from, {}}},
       {"demod_wide_rmax", {&Tuning::demod_wide_rmax, {}}},
+      {"demod_wide_half", {&Tuning::demod_wide_half, {0, 1}}},
       {"demod_wide_dbg", {&Tuning::demod_wide_dbg, {0, 1, 2, 3, 4, 5, 6, 7}}},
       {"ekf_row", {&Tuning::ekf_row, {}}},
       {"ekf_rot", {&Tuning::ekf_rot, {0, 1}}},

@@ -55,13 +55,42 @@ def main():
             ms = ev0.elapsed_time(ev1) / 10
             k = ok.cpu().numpy()
             m = out[1].cpu().numpy()
+            # the demodulation alone (component-major QI) and the LM alone over it
+            qi = torch.empty((2 * nd, nseg), dtype=torch.float64, device=dev)
+            dcb = torch.empty(nseg, dtype=torch.float64, device=dev)
+            lo = torch.empty((4, nseg), dtype=torch.float64, device=dev)
+            ls = torch.empty(nseg, dtype=torch.float64, device=dev)
+            lk = torch.empty(nseg, dtype=torch.int32, device=dev)
+            gd = torch.tensor([1.6, 6.0, 0.0, 0.0], dtype=torch.float64, device=dev)
+
+            def dem():
+                _lib.check(lib.dfmi_demod(x.data_ptr(), nseg, R, R, nd, w0, 0, qi.data_ptr(), dcb.data_ptr(),
+                                          _lib.DFMI_MEM_DEVICE, st.cuda_stream), "dfmi_demod")
+
+            def lmf():
+                _lib.check(lib.dfmi_lm(qi.data_ptr(), nseg, nd, gd.data_ptr(), 0, nseg, cfg, lo.data_ptr(),
+                                       ls.data_ptr(), lk.data_ptr(), _lib.DFMI_MEM_DEVICE, st.cuda_stream), "dfmi_lm")
+            res = {}
+            for name, fn in (("demod_ms", dem), ("lm_ms", lmf)):
+                for _ in range(2):
+                    fn()
+                ev0.record(st)
+                for _ in range(10):
+                    fn()
+                ev1.record(st)
+                ev1.synchronize()
+                res[name] = round(ev0.elapsed_time(ev1) / 10, 4)
+            res["demod_alone_kernel"] = lib.dfmi_last_demod_kernel().decode()
+            del qi, dcb, lo, ls, lk
             for kk in tune:
-                _lib.check(lib.dfmi_set_tuning(kk.encode(), {"demod_wide": 1, "demod_wide_dbg": 0}[kk]), "tune")
+                _lib.check(lib.dfmi_set_tuning(kk.encode(), {"demod_wide": 1, "demod_wide_dbg": 0, "demod_wide_k": 0,
+                                                             "demod_wide_half": 1}[kk]), "tune")
             print(json.dumps({"tune": tune, "cycles_per_segment": ncyc, "R": R, "ndata": nd, "segments": nseg, "ms_per_step": round(ms, 4),
                               "segments_per_s": round(nseg / ms * 1e3, 1),
                               "hbm_frac_end_to_end": round(nseg * (8 * R + 56) / (ms * 1e-3) / 8e12, 4),
                               "demod_kernel": lib.dfmi_last_demod_kernel().decode(),
-                              "status0_frac": float(np.mean(k == 0)), "mean_m": float(np.mean(m[k == 0]))}), flush=True)
+                              "status0_frac": float(np.mean(k == 0)), "mean_m": float(np.mean(m[k == 0])), **res}),
+                  flush=True)
         del out, ok
 
 

@@ -33,7 +33,7 @@ def _demod(env, x, nseg, R, nd, w0, **tune):
     finally:
         for k in tune:
             _lib.check(lib.dfmi_set_tuning(k.encode(), {"demod_wide": 1, "demod_wide_k": 0, "demod_wide_from": 13,
-                                                         "demod_wide_dbg": 0}[k]), "tune")
+                                                         "demod_wide_dbg": 0, "demod_wide_half": 1}[k]), "tune")
 
 
 def _torch_ref(torch, x, nseg, R, nd, w0, take):
@@ -103,6 +103,12 @@ def test_flat_fold_equals_per_segment_fold(env, nd, R, nseg):
     qs, ds, _ = _demod(env, x, nseg, R, nd, w0, demod_wide_dbg=4)
     np.testing.assert_array_equal(qf, qs)
     np.testing.assert_array_equal(df, ds)
+    # the half-wave contraction (2 ndata + 1 <= 32: each half-wave its own segments) is the
+    # same fma chain per output: the same bits with it off
+    qh, dh, kh = _demod(env, x, nseg, R, nd, w0, demod_wide_half=0)
+    assert kf.endswith(",1>") == (2 * nd + 1 <= 32) and kh.endswith(",0>"), (kf, kh)
+    np.testing.assert_array_equal(qf, qh)
+    np.testing.assert_array_equal(df, dh)
     take = torch.arange(0, nseg, max(1, nseg // 16), device="cuda")
     rq, rd = _torch_ref(torch, x, nseg, R, nd, w0, take)
     idx = take.cpu().numpy()

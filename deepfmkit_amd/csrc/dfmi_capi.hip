@@ -1120,7 +1120,8 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
     };
     ws("p_xt", (size_t)(nrec * slots) * 8, &xt);
     ws("p_wt", (size_t)slots * 8, &wtt);
-    ws("p_xbar", (size_t)(nrec * 5 * slots) * 8, &xbar);
+    xbar = nullptr;  // the unfused path's trajectory; the fused first pass reads the head directly
+    if (!t_tune.ekf_pit_fused) ws("p_xbar", (size_t)(nrec * 5 * slots) * 8, &xbar);
     for (int bf = 0; bf < 2 && !rc; ++bf)
       for (int l = 0; l <= L && !rc; ++l) {
         void* a = nullptr;
@@ -1155,9 +1156,14 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
   if (hist_n) HIPCHK(hipMemsetAsync(hist, 0xFF, (size_t)nrec * hist_n * 8, st));  // NaN: pass not run
   hipLaunchKernelGGL(dfmi::ekf_pit_head_kernel, dim3((unsigned)((nrec + 3) / 4)), dim3(64), 0, st, dx, nrec, rs, T0,
                      dx0, dp0, dq, dr, wt, (double*)hs, (double*)hst, tk);
-  hipLaunchKernelGGL(dfmi::ekf_pit_gather_kernel, dim3((unsigned)((slots + 255) / 256), nr), dim3(256), 0, st, dx, rs,
-                     n, (const double*)hs, (const double*)hst, T0, B, nb, w_m, f_samp, (double*)xt, (double*)wtt,
-                     (double*)xbar, ch, (double*)conv, (unsigned*)done);
+  if (xbar)  // the unfused path: the trajectory buffer too
+    hipLaunchKernelGGL(dfmi::ekf_pit_gather_kernel, dim3((unsigned)((slots + 255) / 256), nr), dim3(256), 0, st, dx,
+                       rs, n, (const double*)hs, (const double*)hst, T0, B, nb, w_m, f_samp, (double*)xt,
+                       (double*)wtt, (double*)xbar, ch, (double*)conv, (unsigned*)done);
+  else
+    hipLaunchKernelGGL(dfmi::ekf_pit_gather_tiled_kernel, dim3((unsigned)((B + 31) / 32), (unsigned)((nb + 63) / 64), nr),
+                       dim3(256), 0, st, dx, rs, n, B, nb, w_m, f_samp, (double*)xt, (double*)wtt, ch,
+                       (double*)conv, (unsigned*)done);
   const dim3 lanes((unsigned)((nb + 63) / 64), nr);
   // scan of one buffer's hierarchy: every level bottom-up, then the fix-ups top-down; the
   // pass kernels read level 0 (prefixes within workgroups) and level 1 (true prefixes)
@@ -1180,7 +1186,8 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
     // of the new aggregates
     if (ent) HIPCHK(hipMemsetAsync(ent, 0xFF, (size_t)(nrec * 5 * nb) * 8, st));  // NaN: no previous entry
     hipLaunchKernelGGL(dfmi::ekf_pit_aggregate_kernel, lanes, dim3(64), 0, st, (const double*)xt, (const double*)wtt,
-                       (const double*)xbar, n, B, nb, dx0, dp0, dq, dr, (const dfmi::PitChan*)ch, lv[0][0], tk);
+                       (const double*)nullptr, n, B, nb, dx0, dp0, dq, dr, (const dfmi::PitChan*)ch, lv[0][0], tk,
+                       (const double*)hs, (const double*)hst, T0);
     scan(lv[0]);
   }
   int cur = 0;
@@ -1194,7 +1201,8 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
     } else {
       hipLaunchKernelGGL(dfmi::ekf_pit_aggregate_kernel, lanes, dim3(64), 0, st, (const double*)xt,
                          (const double*)wtt, (const double*)xbar, n, B, nb, dx0, dp0, dq, dr,
-                         (const dfmi::PitChan*)ch, lv[0][0], tk);
+                         (const dfmi::PitChan*)ch, lv[0][0], tk, (const double*)nullptr, (const double*)nullptr,
+                         (int64_t)0);
       scan(lv[0]);
       hipLaunchKernelGGL(dfmi::ekf_pit_blocks_kernel, lanes, dim3(64), 0, st, (const double*)xt, (const double*)wtt,
                          (double*)xbar, n, B, nb, dx0, dp0, dq, dr, (const double*)lv[0][0], tops[0],

@@ -39,7 +39,8 @@
 // converged.
 //
 // Layouts (all channel-major, blocks fastest so lane b of a wave reads address b):
-//   xt[r][i][b], wtt[i][b] (sample k = b B + i), xbar[r][c][i][b] (the seeded trajectory),
+//   xt[r][i][b], wtt[i][b] (sample k = b B + i), xbar[r][c][i][b] (the seeded trajectory:
+//   the unfused path only; the fused first pass reads the head's states directly),
 //   scan level l: [r][65][n_l] with n_0 = nb, n_{l+1} = ceil(n_l / 64), two buffers (a pass
 //   reads one and writes the other), ent[r][c][b] (the previous pass's entry states).
 // Element components: A 0..24 (row-major), b 25..29, C 30..44 (upper triangle, row-major),
@@ -553,9 +554,62 @@ __global__ __launch_bounds__(256) void ekf_pit_gather_kernel(const double* __res
   const int64_t k = b * B + i;
   xt[r * slots + s] = k < n ? x[r * rs + k] : 0.0;
   if (r == 0) wtt[s] = w_m * ((double)k / f_samp);
-  const double* src = k < T0 ? hs + (r * T0 + k) * 5 : hst + r * 5;
+  if (xbar) {  // the unfused path's trajectory buffer (the fused first pass reads the head itself)
+    const double* src = k < T0 ? hs + (r * T0 + k) * 5 : hst + r * 5;
 #pragma unroll
-  for (int c = 0; c < 5; ++c) xbar[(r * 5 + c) * slots + s] = src[c];
+    for (int c = 0; c < 5; ++c) xbar[(r * 5 + c) * slots + s] = src[c];
+  }
+}
+
+// The fused path's gather (no xbar): the channel data into blocks through an LDS tile of 64
+// blocks x 32 samples — each block's 32 samples read as one contiguous run, each sample slot's
+// 64 blocks written as one — where ekf_pit_gather_kernel reads with a stride of B samples
+// (1.8 TB/s at 1,024 x 400,000 samples, B = 2,481: 3.7 ms). Also w_m t_k (z = 0) and the
+// per-channel control blocks (the tile at x = y = 0). Grid (ceil(B / 32), ceil(nb / 64), nrec).
+__global__ __launch_bounds__(256) void ekf_pit_gather_tiled_kernel(const double* __restrict__ x, int64_t rs,
+                                                                   int64_t n, int64_t B, int64_t nb, double w_m,
+                                                                   double f_samp, double* __restrict__ xt,
+                                                                   double* __restrict__ wtt, PitChan* __restrict__ ch,
+                                                                   double* __restrict__ conv,
+                                                                   unsigned* __restrict__ done) {
+  __shared__ double tile[64][33];
+  const int64_t r = blockIdx.z;
+  const int64_t i0 = (int64_t)blockIdx.x * 32, b0 = (int64_t)blockIdx.y * 64;
+  const int t = threadIdx.x;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && t == 0) {
+    PitChan c;
+    c.status = c.passes = c.stall = c.pad = 0;
+    c.dprev = __builtin_nan("");
+    c.rho = -1.0;
+#pragma unroll
+    for (int i = 0; i < kPitTrend; ++i) c.dold[i] = __builtin_nan("");
+    ch[r] = c;
+    conv[r] = 0.0;
+    done[r] = 0;
+  }
+  {  // read: thread t -> block b0 + t / 4, samples i0 + 8 (t % 4) .. + 7
+    const int bl = t >> 2, il = (t & 3) * 8;
+    const int64_t b = b0 + bl;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t i = i0 + il + u;
+      const int64_t k = b * B + i;
+      tile[bl][il + u] = (b < nb && i < B && k < n) ? x[r * rs + k] : 0.0;
+    }
+  }
+  __syncthreads();
+  const int64_t slots = B * nb;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {  // write: 8 sample slots x 64 blocks per pass of 256 threads
+    const int e = t + 256 * u;
+    const int il = e >> 6, bl = e & 63;
+    const int64_t i = i0 + il, b = b0 + bl;
+    if (i < B && b < nb) {
+      const int64_t s = i * nb + b;
+      xt[r * slots + s] = tile[bl][il];
+      if (r == 0) wtt[s] = w_m * ((double)(b * B + i) / f_samp);
+    }
+  }
 }
 
 // Fold one sample's element (h, eps = e - h.b) into the running aggregate (see
@@ -615,12 +669,24 @@ struct PitSamp {
 };
 constexpr int kPitG = 4;  // samples per prefetch group
 // sample i of block b (clamped into the block: the padded slots are allocated)
+// xbar == nullptr: the seeded trajectory straight from the head (ekf_pit_gather_kernel's values:
+// the head's predicted state for k < T0, the state entering T0 beyond), no [r][5][slots] buffer
+// (16 GB written and read at 1,024 x 400,000 samples).
 __device__ __forceinline__ void pit_load_agg(PitSamp& d, const double* __restrict__ xt, const double* __restrict__ wtt,
                                              const double* __restrict__ xbar, int64_t r, int64_t slots, int64_t nb,
-                                             int64_t B, int64_t b, int64_t i) {
-  const int64_t s = (i < B ? i : B - 1) * nb + b;
+                                             int64_t B, int64_t b, int64_t i, const double* __restrict__ hs,
+                                             const double* __restrict__ hst, int64_t T0) {
+  const int64_t ii = i < B ? i : B - 1;
+  const int64_t s = ii * nb + b;
+  if (xbar) {
 #pragma unroll
-  for (int c = 0; c < 5; ++c) d.xb[c] = xbar[(r * 5 + c) * slots + s];
+    for (int c = 0; c < 5; ++c) d.xb[c] = xbar[(r * 5 + c) * slots + s];
+  } else {
+    const int64_t k = b * B + ii;
+    const double* src = k < T0 ? hs + (r * T0 + k) * 5 : hst + r * 5;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) d.xb[c] = src[c];
+  }
   d.w = wtt[s];
   d.y = xt[r * slots + s];
 }
@@ -641,7 +707,9 @@ __global__ __launch_bounds__(64) void ekf_pit_aggregate_kernel(const double* __r
                                                                const double* __restrict__ qd,
                                                                const double* __restrict__ rv,
                                                                const PitChan* __restrict__ ch,
-                                                               double* __restrict__ agg, DfmiTrigK tk) {
+                                                               double* __restrict__ agg, DfmiTrigK tk,
+                                                               const double* __restrict__ hs,
+                                                               const double* __restrict__ hst, int64_t T0) {
   const int64_t r = blockIdx.y;
   if (ch[r].status) return;
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -666,10 +734,11 @@ __global__ __launch_bounds__(64) void ekf_pit_aggregate_kernel(const double* __r
   // (one wave per SIMD: nothing else hides a load's latency)
   PitSamp cur[kPitG], nxt[kPitG];
 #pragma unroll
-  for (int u = 0; u < kPitG; ++u) pit_load_agg(cur[u], xt, wtt, xbar, r, slots, nb, B, b, u);
+  for (int u = 0; u < kPitG; ++u) pit_load_agg(cur[u], xt, wtt, xbar, r, slots, nb, B, b, u, hs, hst, T0);
   for (int64_t i0 = 0; i0 < kend; i0 += kPitG) {
 #pragma unroll
-    for (int u = 0; u < kPitG; ++u) pit_load_agg(nxt[u], xt, wtt, xbar, r, slots, nb, B, b, i0 + kPitG + u);
+    for (int u = 0; u < kPitG; ++u)
+      pit_load_agg(nxt[u], xt, wtt, xbar, r, slots, nb, B, b, i0 + kPitG + u, hs, hst, T0);
 #pragma unroll
     for (int u = 0; u < kPitG; ++u) {
       if (i0 + u >= kend) break;

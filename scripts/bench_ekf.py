@@ -25,7 +25,7 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=2.0)
-    ap.add_argument("--channels", default="1,64,1024")
+    ap.add_argument("--channels", default="1,64,1024", help="comma- or colon-separated channel counts")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cpu-seconds", type=float, default=0.1, help="oracle sample length (s of signal)")
     args = ap.parse_args()
@@ -89,7 +89,7 @@ def main():
     p0 = torch.ones(5, dtype=torch.float64, device=dev)
     qd = torch.tensor([1e-8, 1e-8, 1e-6, 1e-6, 1e-8], dtype=torch.float64, device=dev)
     init4 = torch.tensor([1.6, 6.0, 0.0, 0.0], dtype=torch.float64, device=dev)
-    for nch in [int(v) for v in args.channels.split(",")]:
+    for nch in [int(v) for v in args.channels.replace(":", ",").split(",")]:
         x = torch.from_numpy(x1).to(dev).reshape(1, -1).expand(nch, -1).contiguous()
         states = torch.empty((nch, nbuf, 5), dtype=torch.float64, device=dev)
 

@@ -293,7 +293,14 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
  * start. Results are unaffected (ekf_rot, ekf_pit*: rounding only). Keys: "demod_kernel" (1 phase bins in LDS where they
  * apply [default], 0 cycle-aligned fold), "lm_general" (1 = two-pass general LM path
  * for every ndata), "demod_spw" (segments per wave the bin grid is sized for; 0 =
- * persistent), "ekf_row" (EKF row kernel up to ekf_row x 16 x CUs channels, 0 = lane
+ * persistent), "demod_wide" (1 [default]: component-major QI through the many-harmonic
+ * kernel demod_wide_kernel from "demod_wide_from" (13) harmonics or below "demod_wide_rmax"
+ * (2000) samples per segment — the record pipeline then leaves its fused row layout; 0: the
+ * bin / fold kernels; 2: demod_wide_kernel wherever its geometry applies; QI within ~1e-14
+ * relative of the bin kernel's), "demod_wide_k" (segments per wave, 0 = 8; 2 / 4 / 8),
+ * "demod_wide_half" (1 [default]: half-wave contraction at 2 ndata + 1 <= 32; same bits),
+ * "demod_wide_dbg" (diagnostics: bit 0 no contraction, bit 1 no stores, bit 2 segment-by-segment
+ * fold — results invalid with bits 0 / 1), "ekf_row" (EKF row kernel up to ekf_row x 16 x CUs channels, 0 = lane
  * kernel only), "ekf_rot" (1 [default]: the row kernel takes sin / cos by rotation between
  * anchors of 16 (8, 4) samples where R % 4 == 0, ekf_rot_kernel; rounding only),
  * "wdfmi_accel" (bit 0: W-DFMI time axis without division, bit 1: template slopes in

@@ -1160,8 +1160,16 @@ struct GuessInline {
 // into registers once (QRegs) instead of re-read from LDS / L1 at every evaluation
 // (ndata 10: 248 VGPRs, still 2 waves per SIMD; step 0.5558 -> 0.5507 ms,
 // profiles/r02m_tune_lm_spec3.log). Same bits either way.
+// Waves per SIMD the chunk-size-1 12-harmonic variant is compiled for: 2 (280 -> 256 VGPRs, 29
+// spilled) runs dfmi_lm at ndata 12 in 0.047 ms per 100k segments against 0.055 at one wave;
+// the 16-harmonic variant spills ~240 values at 2 and runs 2.5x slower (0.171 vs 0.068 ms,
+// r05as), so it keeps its allocation.
+template <int NDMAX, bool CHAIN>
+constexpr int lm_waves() {
+  return (!CHAIN && NDMAX == 12) ? 2 : 1;
+}
 template <int NDMAX, bool CHAIN, bool ROWS = false, bool QREG = false>
-__global__ __launch_bounds__(64) void lm_chunks_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(lm_waves<NDMAX, CHAIN>()))) void lm_chunks_kernel(
     const double* __restrict__ qi, int64_t qi_ld, int ndata, int64_t nrec, int64_t nbuf, int64_t first,
     int64_t nitems, int64_t nchunk, const double* __restrict__ guess, int64_t g_rec, int64_t g_comp,
     GuessInline ginl, int use_inline, const double* __restrict__ jtab, LMConst c, double* __restrict__ out,

@@ -179,3 +179,39 @@ def test_record_pipeline_at_many_harmonics(env):
     assert np.abs(cols[0] - 1.0).max() < 1e-9
     assert np.abs(cols[1] - 12.0).max() < 1e-9
     assert np.abs(cols[3] - 0.2).max() < 1e-9
+
+
+@pytest.mark.parametrize("nd,R", [(20, 4000), (10, 200), (15, 400)])
+def test_nonfinite_samples_through_the_wide_path(env, nd, R):
+    """Erasures in the many-harmonic / short-segment record path: a NaN or inf sample poisons
+    exactly its own segment (every QI of it, through the bins' half-period pairing and the
+    flat multi-segment fold) as it does on the bin / fold kernels: status and every finite
+    result agree with demod_wide = 0 (parity 1e-9), the neighbours untouched."""
+    torch, _lib, lib = env
+    from deepfmkit_amd.fitters import nls_records
+    nseg = 2000
+    t = torch.arange(R, dtype=torch.float64, device="cuda") / 200000.0
+    seg_phi = torch.linspace(-0.3, 0.3, nseg, dtype=torch.float64, device="cuda")
+    x = 1.0 + torch.cos(seg_phi[:, None] + 6.0 * torch.cos(2 * np.pi * 1000.0 * t[None, :] + 0.1))
+    g = torch.Generator(device="cuda")
+    g.manual_seed(R + nd)
+    x = (x + 1e-3 * torch.randn(x.shape, dtype=torch.float64, device="cuda", generator=g)).reshape(1, -1)
+    bad = {17: float("nan"), 555: float("inf"), 1999: float("-inf")}
+    for s_, v in bad.items():
+        x[0, s_ * R + R // 3] = v
+    cols, ok = nls_records(x, 200000.0, 1000.0, R, nseg, nd)
+    k = lib.dfmi_last_demod_kernel().decode()
+    assert k.startswith("demod_wide_kernel"), k
+    _lib.check(lib.dfmi_set_tuning(b"demod_wide", 0), "tune")
+    try:
+        cols0, ok0 = nls_records(x, 200000.0, 1000.0, R, nseg, nd)
+        assert not lib.dfmi_last_demod_kernel().decode().startswith("demod_wide")
+    finally:
+        _lib.check(lib.dfmi_set_tuning(b"demod_wide", 1), "tune")
+    cols, ok, cols0, ok0 = (a.cpu().numpy() for a in (cols, ok, cols0, ok0))
+    np.testing.assert_array_equal(ok, ok0)
+    for s_ in bad:
+        assert not np.isfinite(cols[4, s_])  # dc of the poisoned segment
+    good = np.array([i for i in range(nseg) if i not in bad])
+    assert (ok[good] == 0).all()
+    assert np.abs(cols[:4, good] - cols0[:4, good]).max() < 1e-9

@@ -215,3 +215,38 @@ def test_nonfinite_samples_through_the_wide_path(env, nd, R):
     good = np.array([i for i in range(nseg) if i not in bad])
     assert (ok[good] == 0).all()
     assert np.abs(cols[:4, good] - cols0[:4, good]).max() < 1e-9
+
+
+@pytest.mark.parametrize("parallel", [False, True])
+def test_crlb_notebook_call_shape_vs_oracle(env, parallel):
+    """notebooks/1.1_CRLB-test's fitter call, StandardNLSFitter({'n': 1, 'ndata': 15}).fit(raw,
+    parallel=False) (1-cycle segments, 15 harmonics: demod_wide_kernel and the 16-harmonic LM),
+    and its parallel form, on a 40 dB snr-mode record of 0.1 s (100 segments) against the numpy
+    oracle (fitters.py:370-393 sequential / 395-428 parallel with chunk size 1): status equal,
+    parameters within 1e-9 (a warm-start chain carries each fit into the next one's seed)."""
+    import deepfmkit_amd as dfm
+    from deepfmkit_amd.fitters import StandardNLSFitter
+    from oracle import nls_oracle as O
+    laser, ifo = dfm.LaserConfig(), dfm.InterferometerConfig()
+    dfm.set_laser_df_for_effect(laser, ifo, 6.0)
+    dff = dfm.DeepFitFramework()
+    dff.load_sim(dfm.DFMIObject("crlb", laser, ifo, f_samp=200000.0))
+    dff.simulate("crlb", n_seconds=0.1, mode="snr", snr_db=40.0, trial_num=3)
+    raw = dff.raws["crlb"]
+    x = np.ascontiguousarray(raw.samples(), dtype=np.float64)
+    df = StandardNLSFitter({"n": 1, "ndata": 15}).fit(raw, parallel=parallel)
+    if parallel:  # _fit_parallel with chunk size 1, in this process (no Pool from a GPU process)
+        R = x.size // 100
+        first = O.fit_record_sequential(x[:R], raw.f_samp, raw.f_mod, 1, ndata=15)
+        seed = [float(v) for v in first[0, :4]]
+        bufs = x.reshape(-1, R)
+        ref = np.concatenate([first] + [O.fit_chunk((bufs[b:b + 1], seed, 15, raw.f_mod, raw.f_samp, dict(O.C0)))
+                                        for b in range(1, 100)], axis=0)
+    else:
+        ref = O.fit_record_sequential(x, raw.f_samp, raw.f_mod, 1, ndata=15)
+    assert len(df) == ref.shape[0] == 100
+    np.testing.assert_array_equal(df["fitok"].to_numpy(), ref[:, 6].astype(int))
+    got = np.stack([df[c].to_numpy() for c in ("amp", "m", "phi", "psi")], axis=1)
+    d = np.abs(got - ref[:, :4])
+    d[:, 2] = np.abs((got[:, 2] - ref[:, 2] + np.pi) % (2 * np.pi) - np.pi)
+    assert d.max() <= 1e-9, (int(np.argmax(d.max(axis=1))), d.max(axis=0))

@@ -55,6 +55,8 @@ struct Tuning {
                          // many-harmonic kernel wherever its geometry applies
   int demod_wide_from = 13;  // ndata from which demod_wide_kernel (component-major) goes ahead of the bin
                              // kernel, and the record pipeline leaves the row layout for it
+  int lm_onepass = 1;           // LM general path: one Bessel walk per evaluation with the values in LDS
+                                // (1: where 8 waves per CU still fit, 2: always, 0: never)
   int demod_wide_rmax = 2000;  // segments shorter than this go through demod_wide_kernel too
   int demod_wide_half = 1;  // demod_wide_kernel: half-wave contraction at 2·ndata + 1 <= 32 (0: off, A/B)
   int demod_wide_dbg = 0;   // diagnostics: demod_wide_kernel without its contraction (1) / stores (2)
@@ -782,6 +784,13 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
   auto kern = chain ? lm_kernel<true, false>(nd_sel) : rows ? lm_kernel<false, true>(nd_sel)
                                                             : lm_kernel<false, false>(nd_sel);
   if (rows && nd_sel <= 16) lds = (size_t)qi_ld * 65 * sizeof(double);  // the wave's rows, transposed
+  // the general path's one-pass Bessel walk: the lane's recurrence values in LDS, while 8
+  // waves per CU still fit (ndata + 2 <= 40: 160 KB)
+  if (!chain && !rows && nd_sel > 16 && t_tune.lm_onepass &&
+      (t_tune.lm_onepass == 2 || (size_t)64 * (ndata + 2) * 8 * 8 <= t_ds->lds_per_block)) {
+    kern = dfmi::lm_chunks_kernel<0, false, false, false, true>;
+    lds = (size_t)64 * (ndata + 2) * sizeof(double);
+  }
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(block), lds, st, qi, qi_ld, ndata, nrec, nbuf, first, nitems,
                      nchunk, guess_dev, g_rec, g_comp, ginl, use_inline, jtab, c, out, out_ld, status);
   HIPCHK(hipGetLastError());
@@ -997,6 +1006,7 @@ const std::map<std::string, Knob>& knobs() {
       {"demod_wide_k", {&Tuning::demod_wide_k, {0, 2, 4, 8}}},
       {"demod_wide_from", {&Tuning::demod_wide_from, {}}},
       {"demod_wide_rmax", {&Tuning::demod_wide_rmax, {}}},
+      {"lm_onepass", {&Tuning::lm_onepass, {0, 1, 2}}},
       {"demod_wide_half", {&Tuning::demod_wide_half, {0, 1}}},
       {"demod_wide_dbg", {&Tuning::demod_wide_dbg, {0, 1, 2, 3, 4, 5, 6, 7}}},
       {"ekf_row", {&Tuning::ekf_row, {}}},

@@ -81,6 +81,36 @@ DFMI_HD double dfmi_bessel_norm(double ax, int M, int* e_final) {
   return S;
 }
 
+// Pass 1 that also keeps the raw values f_0..f_nmax (store[k * stride], as formed): when no
+// rescale happened (*e_final == 0) they are exactly the values pass 2 would form again, so
+// J_k = f_k * (1 / S) can be read back instead of walking a second time (lm.h
+// harmonic_walk_q); with a rescale the caller walks as usual.
+DFMI_HD double dfmi_bessel_norm_store(double ax, int M, int* e_final, double* store, int stride, int nmax) {
+  const double two_over_x = 2.0 / ax;
+  const double big = ldexp(1.0, DFMI_BES_BIG_EXP);
+  double fp1 = 0.0, f = 1.0, S = 0.0;
+  int e = 0;
+  S = 2.0 * f;
+  for (int k = M; k >= 1; --k) {
+    double fm1 = fma((double)k * two_over_x, f, -fp1);  // f_{k-1}
+    if (fabs(fm1) > big) {
+      fm1 = ldexp(fm1, -DFMI_BES_BIG_EXP);
+      f = ldexp(f, -DFMI_BES_BIG_EXP);
+      S = ldexp(S, -DFMI_BES_BIG_EXP);
+      ++e;
+    }
+    const int km1 = k - 1;
+    if (km1 == nmax) store[(k) * stride] = f;  // f_{nmax + 1}
+    if (km1 <= nmax) store[km1 * stride] = fm1;
+    if (km1 == 0) S += fm1;
+    else if ((km1 & 1) == 0) S += 2.0 * fm1;
+    fp1 = f;
+    f = fm1;
+  }
+  *e_final = e;
+  return S;
+}
+
 // Pass 2: walk k = M..1; at each k the caller gets J_{k+1}, J_k, J_{k-1}.
 struct DfmiBesselWalk {
   double two_over_x, big, invS, fp1, f;

@@ -500,6 +500,18 @@ DFMI_HDI void harmonic_walk(int ndata, double m, double psi, Body&& body) {
 }
 
 constexpr int kQPre = 4;
+template <typename QF, typename = void>
+struct QfBes {
+  static constexpr bool value = false;
+};
+template <typename QF>
+struct QfBes<QF, std::void_t<decltype(QF::kBes)>> {
+  static constexpr bool value = QF::kBes;
+};
+template <typename QF>
+constexpr bool qf_bes() {
+  return QfBes<QF>::value;
+}
 
 // harmonic_walk handing the body its harmonic's QI as well (body(j, J_{j-1}, J_j, J_{j+1},
 // cos j psi, sin j psi, Q_j, I_j)). On the Miller branch (every ordinary m) the QI of
@@ -525,7 +537,49 @@ DFMI_HDI void harmonic_walk_q(int ndata, double m, double psi, const QF& q, Body
   sincos((double)ndata * psi, &sj, &cj);
   const int M = dfmi_bessel_start(ndata + 1, am);
   int ef = 0;
-  const double S = dfmi_bessel_norm(am, M, &ef);
+  double S;
+  if constexpr (qf_bes<QF>()) {
+    S = dfmi_bessel_norm_store(am, M, &ef, q.bes, 64, ndata);
+    if (ef == 0) {  // no rescale: the stored values are pass 2's, J_k = f_k / S
+      const double invS = 1.0 / S;
+      const bool neg = m < 0.0;
+      auto jv = [&](int k) {
+        const double v = q.bes[k * 64] * invS;
+        return (neg && (k & 1)) ? -v : v;  // J_n(-x) = (-1)^n J_n(x)
+      };
+      double bq[kQPre], bs[kQPre];
+#pragma unroll
+      for (int u = 0; u < kQPre; ++u) {
+        const int h = ndata - 1 - u > 0 ? ndata - 1 - u : 0;
+        bq[u] = q.qc(h);
+        bs[u] = q.qs(h);
+      }
+      auto one = [&](int j, double qcv, double qsv) {
+        body(j, jv(j - 1), jv(j), jv(j + 1), cj, sj, qcv, qsv);
+        const double cn = fma(cj, c1, sj * s1);
+        const double sn = fma(sj, c1, -(cj * s1));
+        cj = cn;
+        sj = sn;
+      };
+      int j = ndata;
+      for (; j >= kQPre; j -= kQPre) {
+#pragma unroll
+        for (int u = 0; u < kQPre; ++u) {
+          const double qcv = bq[u], qsv = bs[u];
+          const int h = j - 1 - u - kQPre > 0 ? j - 1 - u - kQPre : 0;
+          bq[u] = q.qc(h);
+          bs[u] = q.qs(h);
+          one(j - u, qcv, qsv);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kQPre; ++u)
+        if (u < j) one(j - u, bq[u], bs[u]);
+      return;
+    }
+  } else {
+    S = dfmi_bessel_norm(am, M, &ef);
+  }
   DfmiBesselWalk w;
   w.init(m, M, S, ef);
   double bq[kQPre], bs[kQPre];  // slot u: harmonic j - u of the block starting at j
@@ -567,12 +621,16 @@ DFMI_HDI void harmonic_walk_q(int ndata, double m, double psi, const QF& q, Body
 //  16 doubles [cos h0..7 | sin h0..7] per 8 harmonics, dc in a spare slot;
 //  STRIDE = 1 for a row in global memory, 65 for a wave's rows transposed into LDS.
 //  kPre: QI pairs harmonic_walk_q keeps in flight for the accessor (0: plain loads).
-template <int PRE = 0>
+//  BES: harmonic_walk_q may keep the lane's Bessel recurrence values in `bes` (LDS, stride 64:
+//  ndata + 2 doubles) and walk once instead of twice.
+template <int PRE = 0, bool BES = false>
 struct QGlobalT {
   static constexpr int kPre = PRE;
+  static constexpr bool kBes = BES;
   const double* __restrict__ p;
   int64_t ld;
   int nd;
+  double* bes = nullptr;
   DFMI_HDI double qc(int h) const { return p[(int64_t)h * ld]; }
   DFMI_HDI double qs(int h) const { return p[(int64_t)(nd + h) * ld]; }
 };
@@ -1164,12 +1222,15 @@ struct GuessInline {
 // spilled) runs dfmi_lm at ndata 12 in 0.047 ms per 100k segments against 0.055 at one wave;
 // the 16-harmonic variant spills ~240 values at 2 and runs 2.5x slower (0.171 vs 0.068 ms,
 // r05as), so it keeps its allocation.
-template <int NDMAX, bool CHAIN>
+template <int NDMAX, bool CHAIN, bool ONEPASS = false>
 constexpr int lm_waves() {
-  return (!CHAIN && NDMAX == 12) ? 2 : 1;
+  return (!CHAIN && (NDMAX == 12 || ONEPASS)) ? 2 : 1;  // ONEPASS: 259 VGPRs unbounded
 }
-template <int NDMAX, bool CHAIN, bool ROWS = false, bool QREG = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(lm_waves<NDMAX, CHAIN>()))) void lm_chunks_kernel(
+// ONEPASS (general path, chunk size 1, component-major): each lane keeps its Bessel recurrence
+// values in dynamic LDS (64 x (ndata + 2) doubles per wave) and walks once per evaluation
+// (harmonic_walk_q); same bits.
+template <int NDMAX, bool CHAIN, bool ROWS = false, bool QREG = false, bool ONEPASS = false>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(lm_waves<NDMAX, CHAIN, ONEPASS>()))) void lm_chunks_kernel(
     const double* __restrict__ qi, int64_t qi_ld, int ndata, int64_t nrec, int64_t nbuf, int64_t first,
     int64_t nitems, int64_t nchunk, const double* __restrict__ guess, int64_t g_rec, int64_t g_comp,
     GuessInline ginl, int use_inline, const double* __restrict__ jtab, LMConst c, double* __restrict__ out,
@@ -1280,6 +1341,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(lm_waves<NDM
         QRegs<nd_cap(NDMAX)> qr;
         qr.load(qg);
         st = fit_segment_q2<NDMAX, QRegs<nd_cap(NDMAX)>, QGlobal, 1>(qr, qg, ndata, jtab, c, p, ssq);
+      } else if constexpr (ONEPASS && NDMAX == 0 && !CHAIN && !ROWS) {
+        const QGlobalT<kQPre, true> qg{qi + sidx, qi_ld, ndata, lds_q + threadIdx.x};
+        st = fit_segment_q<NDMAX, QGlobalT<kQPre, true>, 1>(qg, ndata, jtab, c, p, ssq);
       } else {
         st = fit_segment<NDMAX, 1, CHAIN ? 0 : kQPre>(qi + sidx, qi_ld, ndata, jtab, c, p, ssq);
       }

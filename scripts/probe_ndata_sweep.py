@@ -29,6 +29,9 @@ def main():
     dev = torch.device("cuda", 0)
     R = 4000
     nseg = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
+    tune = dict(kv.split("=") for kv in sys.argv[2].split("+")) if len(sys.argv) > 2 and sys.argv[2] else {}
+    for k, v in tune.items():  # e.g. lm_onepass=0
+        _lib.check(lib.dfmi_set_tuning(k.encode(), int(v)), "tune")
     x = torch.empty(nseg * R, dtype=torch.float64, device=dev)
     bench.gen_shard(torch, dev, 0, nseg, R, seed=bench.SEED, out=x)
     w0 = w0_of(1000.0, 200000.0)
@@ -90,7 +93,7 @@ def main():
         lm_ms = timed(lm, 60)
         bytes_seg = 8 * R + 8 * (2 * nd + 1)
         print(json.dumps({
-            "ndata": nd, "segments": nseg, "R": R,
+            "ndata": nd, "segments": nseg, "R": R, "tune": tune,
             "step_ms": round(step_ms, 4), "segments_per_s": round(nseg / step_ms * 1e3, 1),
             "step_demod_kernel": step_kernel, "demod_layout": layout, "demod_ms": round(demod_ms, 4), "demod_kernel": demod_kernel,
             "demod_hbm_frac": round(nseg * bytes_seg / (demod_ms * 1e-3) / 8e12, 4),

@@ -266,3 +266,37 @@ def test_device_bessel_large_argument(method, nmax):
     d = np.load(os.path.join(GOLDEN, "bessel_large.npz"))
     x, jv = d["x"], d["jv"][: nmax + 1]
     assert np.abs(_bessel(x, nmax, method) - jv).max() <= 1e-14
+
+
+@pytest.mark.parametrize("nd", [20, 30, 38, 62])
+def test_lm_one_pass_bessel_walk_bit_identical(nd):
+    """The general path's one-pass Bessel walk (lm_onepass: the lane's recurrence values kept
+    in LDS, lm.h harmonic_walk_q) against the two-pass walk on the same QI: the same bits
+    (the stored values are the ones the second pass would form again), for noiseless and
+    noisy segments, m small enough to rescale the recurrence (the two-pass fallback) and
+    negative m seeds."""
+    import torch
+    from deepfmkit_amd import _lib
+    from deepfmkit_amd import fit as F
+    lib = _lib.load()
+    from scipy.special import jv
+    rng = np.random.default_rng(nd)
+    n = 4096
+    j = np.arange(1, nd + 1)
+    a = rng.uniform(0.3, 2.0, n)[:, None]
+    m = rng.uniform(0.05, 25.0, n)[:, None]
+    phi = rng.uniform(-np.pi, np.pi, n)[:, None]
+    psi = rng.uniform(-0.5, 0.5, n)[:, None]
+    c = a * np.cos(phi + j * np.pi / 2) * jv(j, m)  # the model's QI (fit.py:110-114)
+    qi = np.concatenate([c * np.cos(j * psi), -c * np.sin(j * psi)], axis=1)
+    qi += rng.normal(size=qi.shape) * 10 ** rng.uniform(-6, -1, (n, 1))
+    guess = np.column_stack([np.full(n, 1.6), rng.uniform(-8.0, 30.0, n), np.zeros(n), np.zeros(n)])
+    res = {}
+    for mode in (2, 0):
+        _lib.check(lib.dfmi_set_tuning(b"lm_onepass", mode), "tune")
+        try:
+            res[mode] = F.fit_batch(nd, qi, guess)
+        finally:
+            _lib.check(lib.dfmi_set_tuning(b"lm_onepass", 1), "tune")
+    for a, b in zip(res[2], res[0]):
+        np.testing.assert_array_equal(a, b)

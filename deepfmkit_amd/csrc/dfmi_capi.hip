@@ -56,7 +56,7 @@ struct Tuning {
   int demod_wide_from = 13;  // ndata from which demod_wide_kernel (component-major) goes ahead of the bin
                              // kernel, and the record pipeline leaves the row layout for it
   int lm_onepass = 1;           // LM general path: one Bessel walk per evaluation with the values in LDS
-                                // (1: where 8 waves per CU still fit, 2: always, 0: never)
+                                // (1: where 7 waves per CU still fit, 2: always, 0: never)
   int demod_wide_rmax = 2000;  // segments shorter than this go through demod_wide_kernel too
   int demod_wide_half = 1;  // demod_wide_kernel: half-wave contraction at 2·ndata + 1 <= 32 (0: off, A/B)
   int demod_wide_dbg = 0;   // diagnostics: demod_wide_kernel without its contraction (1) / stores (2)
@@ -784,10 +784,11 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
   auto kern = chain ? lm_kernel<true, false>(nd_sel) : rows ? lm_kernel<false, true>(nd_sel)
                                                             : lm_kernel<false, false>(nd_sel);
   if (rows && nd_sel <= 16) lds = (size_t)qi_ld * 65 * sizeof(double);  // the wave's rows, transposed
-  // the general path's one-pass Bessel walk: the lane's recurrence values in LDS, while 8
-  // waves per CU still fit (ndata + 2 <= 40: 160 KB)
+  // the general path's one-pass Bessel walk: the lane's recurrence values in LDS, while 7
+  // waves per CU still fit (ndata + 2 <= 45): ndata 40 0.276 -> 0.264 ms per 100k; at 62 (5
+  // waves per CU) 0.384 -> 0.663, r05ax
   if (!chain && !rows && nd_sel > 16 && t_tune.lm_onepass &&
-      (t_tune.lm_onepass == 2 || (size_t)64 * (ndata + 2) * 8 * 8 <= t_ds->lds_per_block)) {
+      (t_tune.lm_onepass == 2 || (size_t)64 * (ndata + 2) * 8 * 7 <= t_ds->lds_per_block)) {
     kern = dfmi::lm_chunks_kernel<0, false, false, false, true>;
     lds = (size_t)64 * (ndata + 2) * sizeof(double);
   }

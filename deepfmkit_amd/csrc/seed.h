@@ -45,6 +45,13 @@ __global__ __launch_bounds__(64) void seed_kernel(const double* __restrict__ x, 
   if (L > 0) fold_segment<1, 16>(xs, R, L, ndata, tab, lane, qis, nrec, r, dcs);
   else direct_segment(xs, R, ndata, w0, lane, qis, nrec, r, dcs);
   __syncthreads();  // QI of this record (global, same workgroup) visible to the wave
+  // ... and into LDS for the fit: its evaluations read every QI value once per harmonic, and
+  // from global memory each read waited a round trip under the bulk demodulation's load
+  // (the kernel took 0.36 / 0.47 / 0.61 ms at ndata 20 / 30 / 62, longer than the bulk
+  // demodulation at 62; profiles/r05/ndata_sweep_kernel_stats.csv). Same values: same fit.
+  __shared__ double qsh[2 * 128];
+  for (int i = lane; i < 2 * ndata && i < 2 * 128; i += 64) qsh[i] = qis[(int64_t)i * nrec + r];
+  __syncthreads();
   double p[4] = {0.0, 0.0, 0.0, 0.0};
   if (use_inline) {
 #pragma unroll
@@ -59,7 +66,8 @@ __global__ __launch_bounds__(64) void seed_kernel(const double* __restrict__ x, 
     for (int i = 0; i < 4; ++i) p[i] = guess[r * 4 + i];
   }
   double ssq;
-  const int st = fit_segment<kSeedPath, kSeedFlat>(qis + r, nrec, ndata, jtab, c, p, ssq);
+  const QGlobal qs{ndata <= 128 ? qsh : qis + r, ndata <= 128 ? 1 : nrec, ndata};
+  const int st = fit_segment_q<kSeedPath, QGlobal, kSeedFlat>(qs, ndata, jtab, c, p, ssq);
   if (lane != 0) return;
   const int64_t sidx = r * nbuf;
   out[0 * out_ld + sidx] = p[0];

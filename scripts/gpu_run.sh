@@ -64,7 +64,7 @@ for step in "$@"; do
       ;;
     prof)
       IFS=',' read -ra pargs <<< "$arg"
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run -- python3 "${pargs[@]}" \
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- python3 "${pargs[@]}" \
         > gpurun_out/${TAG}_prof.log 2>&1
       rc=$?
       tail -5 gpurun_out/${TAG}_prof.log

@@ -866,6 +866,55 @@ __global__ __launch_bounds__(kBlockThreads, 3) void demod_wide_kernel(  // 3 wav
   }
 }
 
+// One segment the many-harmonic way, by one wave (the seed step beyond the bin kernel's LDS
+// basis, seed.h seed_kernel): wide_fold into the wave's LDS bins (ybin, L + 4 doubles), the
+// half-period pairing and the lanes-over-outputs contraction of demod_wide_kernel, the same
+// operations in the same order — the segment's QI and dc are bit-identical to what the bulk
+// demod_wide_kernel gives it; written component-major to qi[o * qi_ld + col] / dc[col].
+__device__ __forceinline__ void wide_seed_segment(const double* __restrict__ xs, int R, int L, int ndata,
+                                                  const double* __restrict__ tabT, int no, double* ybin, int lane,
+                                                  double* __restrict__ qi, int64_t qi_ld, int64_t col,
+                                                  double* __restrict__ dc) {
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  double pf[1][2];
+  wide_fold<10, 0>(xs, R, L, ybin, lane, pf, nullptr);
+  const int half = L >> 1;
+  const int npair = (half + 2) >> 1;
+  const int ym = (half + 2) & ~1;
+  double a[3], bb[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int p = lane + 64 * u;
+    a[u] = p <= half ? ybin[p] : 0.0;
+    bb[u] = (p > 0 && p < half) ? ybin[L - p] : 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int p = lane + 64 * u;
+    if (p < 2 * npair) {
+      const bool self = p == 0 || p == half;
+      ybin[p] = self ? a[u] : a[u] + bb[u];
+      ybin[ym + p] = self ? a[u] : a[u] - bb[u];
+    }
+  }
+  const d2v* __restrict__ T2 = reinterpret_cast<const d2v*>(tabT);
+  const int nout = 2 * ndata + 1;
+  for (int i = 0; i < no; ++i) {
+    const int o = lane + 64 * i;
+    const int yoff = (o >= ndata && o < 2 * ndata) ? ym : 0;
+    double acc = 0.0;
+    for (int pp = 0; pp < npair; ++pp) {
+      const d2v t = T2[(size_t)pp * 64 * no + o];
+      const d2v y = *reinterpret_cast<const d2v*>(ybin + yoff + 2 * pp);
+      acc = fma(y.x, t.x, acc);
+      acc = fma(y.y, t.y, acc);
+    }
+    const double v = acc / (double)R;
+    if (o < nout - 1) qi[(int64_t)o * qi_ld + col] = v;
+    else if (o == nout - 1) dc[col] = v;
+  }
+}
+
 // Fallback when no short integer period exists: per-sample angles
 // fl(fl(h·w0)·t) exactly as fit.py:55-64 forms them, sincos on the device.
 // VALU-bound; only used for unusual f_samp/f_mod ratios.

@@ -878,8 +878,19 @@ int seed_launch(int dev, const double* x, int64_t nrec, int64_t rec_stride, int 
     if ((rc = workspace(dev, "qi_seed", (size_t)2 * ndata * nrec * 8, &qs))) return rc;
     if ((rc = workspace(dev, "dc_seed", (size_t)nrec * 8, &ds_))) return rc;
     auto sk = ndata <= 12 ? dfmi::seed_kernel<12> : ndata <= 16 ? dfmi::seed_kernel<16> : dfmi::seed_kernel<0>;
-    hipLaunchKernelGGL(sk, dim3((unsigned)nrec), dim3(64), 0, sst, x, rec_stride, R, L, ndata, w0, tab, (double*)qs,
-                       (double*)ds_, nrec, gdev, ginl, gdev ? 0 : 1, jtab, c, out, out_ld, nbuf, fitok);
+    // the many-harmonic demodulation where its geometry holds (16-B rows, 128 <= L <= 256):
+    // the bulk's own QI for buffer 0, and a fold with 10 wave loads in flight instead of the
+    // cycle-aligned scalar fold against a global basis
+    const double* tabT = nullptr;
+    int no = 0;
+    if (L > 0 && wide_geometry(vec2, L, ndata)) {
+      no = 2 * ndata + 1 <= 64 ? 1 : 2 * ndata + 1 <= 128 ? 2 : 4;
+      if ((rc = basis_table_wide(dev, L, ndata, w0, no, &tabT))) return rc;
+    }
+    const size_t lds = tabT ? (size_t)(L + 4) * sizeof(double) : 0;
+    hipLaunchKernelGGL(sk, dim3((unsigned)nrec), dim3(64), lds, sst, x, rec_stride, R, L, ndata, w0, tab,
+                       (double*)qs, (double*)ds_, nrec, gdev, ginl, gdev ? 0 : 1, jtab, c, out, out_ld, nbuf, fitok,
+                       tabT, no);
   }
   HIPCHK(hipGetLastError());
   return DFMI_OK;

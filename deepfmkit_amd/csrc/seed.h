@@ -31,6 +31,9 @@ constexpr int kSeedPath = 0;
 // passes, so it stays hidden under (or close to) the bulk demodulation.
 constexpr int kSeedFlat = 2;
 
+// tabT (not null): the many-harmonic demodulation (demod.h wide_seed_segment, basis_table_wide
+// with `no` output slices; dynamic LDS L + 4 doubles): the record's buffer 0 gets the QI the
+// bulk demod_wide_kernel would give it.
 template <int NDMAX>
 __global__ __launch_bounds__(64) void seed_kernel(const double* __restrict__ x, int64_t rec_stride, int R, int L,
                                                   int ndata, double w0, const double* __restrict__ tab,
@@ -38,11 +41,14 @@ __global__ __launch_bounds__(64) void seed_kernel(const double* __restrict__ x, 
                                                   const double* __restrict__ guess, GuessInline ginl, int use_inline,
                                                   const double* __restrict__ jtab, LMConst c,
                                                   double* __restrict__ out, int64_t out_ld, int64_t nbuf,
-                                                  int32_t* __restrict__ status) {
+                                                  int32_t* __restrict__ status, const double* __restrict__ tabT,
+                                                  int no) {
+  extern __shared__ __attribute__((aligned(16))) double ybin_dyn[];
   const int64_t r = blockIdx.x;
   const int lane = threadIdx.x;
   const double* __restrict__ xs = x + r * rec_stride;
-  if (L > 0) fold_segment<1, 16>(xs, R, L, ndata, tab, lane, qis, nrec, r, dcs);
+  if (tabT) wide_seed_segment(xs, R, L, ndata, tabT, no, ybin_dyn, lane, qis, nrec, r, dcs);
+  else if (L > 0) fold_segment<1, 16>(xs, R, L, ndata, tab, lane, qis, nrec, r, dcs);
   else direct_segment(xs, R, ndata, w0, lane, qis, nrec, r, dcs);
   __syncthreads();  // QI of this record (global, same workgroup) visible to the wave
   // ... and into LDS for the fit: its evaluations read every QI value once per harmonic, and

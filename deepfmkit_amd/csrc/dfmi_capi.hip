@@ -5,6 +5,7 @@
 // launch geometry. No torch, no Python.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <unistd.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -24,6 +25,7 @@
 #include "lm.h"
 #include "seed.h"
 #include "np_sum.h"
+#include "fork_guard.h"
 #include "moments.h"
 #include "synth.h"
 #include "wdfmi.h"
@@ -168,6 +170,7 @@ struct DeviceState {
 
 std::map<int, DeviceState> g_dev;
 int g_ndev = -1;
+long g_init_pid = 0;  // the process that first initialised HIP through this library (fork_guard.h)
 
 thread_local DeviceState* t_ds = nullptr;  // the device of the current call
 
@@ -189,7 +192,12 @@ int ensure_init(int* dev_out) {
 }
 
 int ensure_init_locked(int* dev_out) {
+  // fork_guard.h: a process forked after this library initialised HIP gets an error
+  // before any runtime call (the pid is recorded at the first initialisation attempt)
+  const std::string forked = dfmi_fork_guard(g_init_pid, (long)getpid());
+  if (!forked.empty()) return fail(DFMI_ERR_HIP, forked);
   if (g_ndev < 0) {
+    g_init_pid = (long)getpid();
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess || n == 0) {

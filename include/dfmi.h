@@ -8,7 +8,13 @@
  * hipStream_t or NULL for the null stream, and returns without synchronising).
  * The library keeps no caller pointer after a call returns. HIP is initialised
  * lazily on the first call (never at load time), so the .so is safe to load in
- * a process that later forks (fitters.py:422 / experiments.py:381 Pools).
+ * a process that later forks (fitters.py:422 / experiments.py:381 Pools): a child
+ * forked BEFORE the parent's first GPU call initialises HIP for itself. The library
+ * records the pid of the process whose call first initialised HIP; a call from any
+ * other pid — a child forked AFTER that point, which inherits HIP state it cannot
+ * use — returns DFMI_ERR_HIP before touching the HIP runtime, and dfmi_last_error()
+ * names both pids (fork first, or use the 'spawn' start method;
+ * deepfmkit_amd/csrc/fork_guard.h).
  *
  * Return value: 0 on success, a negative DFMI_ERR_* code otherwise; the
  * message is in dfmi_last_error(). Numerical non-convergence is NOT an error:

@@ -12,6 +12,7 @@
 #include "../../deepfmkit_amd/csrc/np_sum.h"
 #include "../../deepfmkit_amd/csrc/synth.h"
 #include "../../deepfmkit_amd/csrc/ekf_pit.h"
+#include "../../deepfmkit_amd/csrc/fork_guard.h"
 
 namespace {
 struct HKey {
@@ -25,6 +26,14 @@ struct HVec {
 }  // namespace
 
 extern "C" {
+
+// fork_guard.h: the message libdfmi.so returns (DFMI_ERR_HIP) to a process forked after
+// it initialised HIP; "" when `cur_pid` may call in. Returns the message length.
+int hc_fork_guard(long init_pid, long cur_pid, char* buf, int cap) {
+  const std::string m = dfmi_fork_guard(init_pid, cur_pid);
+  snprintf(buf, cap, "%s", m.c_str());
+  return (int)m.size();
+}
 
 // numpy summation order (np_sum.h): the plan the W-DFMI kernels run for their means.
 double hc_np_sum(const double* a, int n) { return dfmi_plan_sum_host(a, n); }

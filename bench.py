@@ -100,6 +100,37 @@ def shard_plan(rank, world, nseg):
     return rank * nseg, nseg + 1, True
 
 
+def plan_workload(world, segments=None, channels=1):
+    """What one rank of `bench.py --gpus world` fits, and how its line names it. Config 4
+    (BASELINE.json): ONE 10,000,000-segment record split over the ranks (total work fixed:
+    strong scaling; 1.25 M segments = 40 GB per GPU at 8); config 2: 100,000 segments on one
+    GPU; an explicit --segments is per GPU (weak scaling). The workload string names the
+    per-GPU shard only, so the N = 1 scaling anchor (config 4's 8-way shard on one GPU) and
+    rank 0 at N = 8 carry the same string (tests/test_bench_launch.py)."""
+    R = int(F_SAMP / F_MOD * N_CYC)
+    config4 = world > 1 and segments is None
+    if config4:
+        if CONFIG4_SEGMENTS % world:
+            raise SystemExit(f"config 4: {CONFIG4_SEGMENTS} segments do not split over {world} ranks")
+        nseg = CONFIG4_SEGMENTS // world
+    else:
+        nseg = segments if segments is not None else 100_000
+    nrec = max(1, channels) if world == 1 else 1
+    if config4:
+        name = "config4"
+    elif nrec == 2:
+        name = "config3"
+    else:
+        name = {100_000: "config2", 1_250_000: "config4 shard"}.get(nseg, "config2-shape")
+    workload = (f"{name}: {nseg} segments/GPU x R={R} @200 kS/s, ndata={NDATA}, {nrec} channel"
+                f"{'s' if nrec > 1 else ''}, _fit_parallel chunk size 1")
+    return {"name": name, "config4": config4, "nseg": nseg, "nrec": nrec, "R": R, "workload": workload,
+            "record_segments": CONFIG4_SEGMENTS if config4 else nseg * nrec, "scaling": "strong" if config4 else "weak"}
+
+
+ANCHOR_WORLD = 8  # the driver's largest scaling point: config 4's shard at N = 8 is the N = 1 anchor
+
+
 def cpu_share():
     """The host CPUs this process may use: affinity, capped by a cgroup CPU quota
     (a GPU box's share is far below os.cpu_count(), which counts the whole machine)."""
@@ -582,7 +613,15 @@ def extra_configs(torch, dev, lib, _lib, stream, cfg, cpu_leg):
     # crosses the ridge; report that separately"): the record pipeline's step and the
     # demodulation alone (component-major QI: demod_wide_kernel beyond 16 harmonics)
     sweep = []
-    for nd in (16, 20, 30, 62):
+    # (ndata, m): config 2's record at more harmonics, and the reference quickstart's own
+    # setting (notebooks/0.0_quickstart.ipynb: m_target = 10*3.14, ndata = int(2*m_target) = 62,
+    # and ndata 30) on a 100,000-segment record of m = 31.4, buffer 0 through the m-grid seed
+    m_rec = M_TRUE
+    for nd, m in ((16, M_TRUE), (20, M_TRUE), (30, M_TRUE), (62, M_TRUE), (30, 31.4), (62, 31.4)):
+        if m != m_rec:
+            gen_shard(torch, dev, 0, nb2, R, seed=SEED, m_true=m, out=x)
+            m_rec = m
+
         def stepn():
             _lib.check(lib.dfmi_nls_record(x.data_ptr(), 1, nb2 * R, nb2, R, nd, w0, 0, _lib.ptr(g1), 1, nb2 - 1, cfg,
                                            o4.data_ptr(), k4.data_ptr(), _lib.DFMI_MEM_DEVICE, stream.cuda_stream),
@@ -590,6 +629,7 @@ def extra_configs(torch, dev, lib, _lib, stream, cfg, cpu_leg):
         tn = _timed_steps(torch, stepn, 20, 5)
         kstep = lib.dfmi_last_demod_kernel().decode()
         okn = float(np.mean(k4.cpu().numpy() == 0))
+        m_fit = float(o4[1].mean().item())
         qn = torch.empty((2 * nd, nb2), dtype=torch.float64, device=dev)
         dn = torch.empty(nb2, dtype=torch.float64, device=dev)
 
@@ -597,47 +637,62 @@ def extra_configs(torch, dev, lib, _lib, stream, cfg, cpu_leg):
             _lib.check(lib.dfmi_demod(x.data_ptr(), nb2, R, R, nd, w0, 0, qn.data_ptr(), dn.data_ptr(),
                                       _lib.DFMI_MEM_DEVICE, stream.cuda_stream), "dfmi_demod")
         td = _timed_steps(torch, demn, 20, 5)
-        sweep.append({"ndata": nd, "value": round(nb2 / tn, 1), "unit": "segments/s", "ms_per_step": round(tn * 1e3, 4),
-                      "step_demod_kernel": kstep, "status0_frac": okn,
-                      "demod_component_major_ms": round(td * 1e3, 4),
-                      "demod_kernel": lib.dfmi_last_demod_kernel().decode(),
+        lo = torch.empty((4, nb2), dtype=torch.float64, device=dev)
+        ls = torch.empty(nb2, dtype=torch.float64, device=dev)
+        lk = torch.empty(nb2, dtype=torch.int32, device=dev)
+        gm = torch.tensor([1.0, m, 0.0, 0.0], dtype=torch.float64, device=dev)
+
+        def lmn():  # the LM alone over these QI, every segment seeded near its m (chunk size 1)
+            _lib.check(lib.dfmi_lm(qn.data_ptr(), nb2, nd, gm.data_ptr(), 0, nb2, cfg, lo.data_ptr(), ls.data_ptr(),
+                                   lk.data_ptr(), _lib.DFMI_MEM_DEVICE, stream.cuda_stream), "dfmi_lm")
+        tl = _timed_steps(torch, lmn, 20, 5)
+        sweep.append({"ndata": nd, "m": m, "value": round(nb2 / tn, 1), "unit": "segments/s",
+                      "ms_per_step": round(tn * 1e3, 4), "step_demod_kernel": kstep, "status0_frac": okn,
+                      "mean_m": m_fit, "demod_component_major_ms": round(td * 1e3, 4),
+                      "demod_kernel": lib.dfmi_last_demod_kernel().decode(), "lm_alone_ms": round(tl * 1e3, 4),
                       "demod_hbm_frac": round(nb2 * (8 * R + 8 * (2 * nd + 1)) / td / 1e9 / HBM_PEAK_GBS, 4),
                       "hbm_frac_end_to_end": round(nb2 * (8 * R + 56) / tn / 1e9 / HBM_PEAK_GBS, 4)})
-        del qn, dn
-    out["config2_ndata_sweep"] = {"workload": "config 2 (100,000 x R=4000, 40 dB) at ndata 16 / 20 / 30 / 62, "
+        del qn, dn, lo, ls, lk
+    out["config2_ndata_sweep"] = {"workload": "config 2 (100,000 x R=4000, 40 dB) at ndata 16 / 20 / 30 / 62 (m = 6), "
+                                              "and the reference quickstart's m = 31.4 at ndata 30 / 62; "
                                               "dfmi_nls_record parallel", "points": sweep}
     del x, o4, k4
     torch.cuda.empty_cache()
-    # ---- config 4's per-GPU shard on this one GPU: the same-workload N = 1 point of the
-    # driver's 1 -> 8 curve (each of 8 ranks fits 1.25 M segments = 40 GB of config 4)
-    out["config4_shard_1gpu"] = config4_shard_point(torch, dev, lib, _lib, stream, cfg)
     return out
 
 
-def config4_shard_point(torch, dev, lib, _lib, stream, cfg, steps=20, warmup=5):
-    """bench.py's step over CONFIG4_SEGMENTS / 8 segments on one GPU: rank 0's shard of the
-    10M-segment record at N = 8 (global segments [0, 1.25 M), buffer 0 first)."""
+def scaling_anchor(torch, dev, lib, _lib, stream, cfg, steps, warmup):
+    """The N = 1 anchor of the driver's strong-scaling curve: bench.py's step
+    and timed window (W warmup steps, synchronize, exactly K steps, synchronize) over the shard
+    rank 0 fits at N = ANCHOR_WORLD = 8 (global segments [0, 1.25 M) of the 10M-segment record,
+    40 GB resident, buffer 0 first), on this one GPU. At N ranks each GPU fits 10M / N segments,
+    and a rank's per-segment cost is flat in its shard size from ~10^5 segments up, so
+    value_N / (N x this value) is the scaling efficiency of the curve's N-th point; the headline
+    stays config 2."""
     from deepfmkit_amd.fitters import w0_of
-    R = int(F_SAMP / F_MOD * N_CYC)
-    nseg = CONFIG4_SEGMENTS // 8
-    x = torch.empty(nseg * R, dtype=torch.float64, device=dev)
-    gen_shard(torch, dev, 0, nseg, R, seed=SEED, out=x)
+    plan = plan_workload(ANCHOR_WORLD)
+    R, nseg = plan["R"], plan["nseg"]
+    seg0, nbuf, prepend = shard_plan(0, ANCHOR_WORLD, nseg)
+    x = torch.empty(nbuf * R, dtype=torch.float64, device=dev)
+    gen_shard(torch, dev, seg0, nseg, R, seed=SEED, out=x)
     g = np.array([1.6, 6.0, 0.0, 0.0])
-    o = torch.empty((6, nseg), dtype=torch.float64, device=dev)
-    k = torch.empty(nseg, dtype=torch.int32, device=dev)
+    o = torch.empty((6, nbuf), dtype=torch.float64, device=dev)
+    k = torch.empty(nbuf, dtype=torch.int32, device=dev)
     w0 = w0_of(F_MOD, F_SAMP)
 
     def step():
-        _lib.check(lib.dfmi_nls_record(x.data_ptr(), 1, nseg * R, nseg, R, NDATA, w0, 0, _lib.ptr(g), 1, nseg - 1, cfg,
+        _lib.check(lib.dfmi_nls_record(x.data_ptr(), 1, nbuf * R, nbuf, R, NDATA, w0, 0, _lib.ptr(g), 1, nbuf - 1, cfg,
                                        o.data_ptr(), k.data_ptr(), _lib.DFMI_MEM_DEVICE, stream.cuda_stream),
                    "dfmi_nls_record")
 
     t = _timed_steps(torch, step, steps, warmup)
     st = k.cpu().numpy()
-    res = {"workload": f"config 4 per-GPU shard: {nseg} segments (40 GB resident) x R={R}, one record, chunk size 1",
+    res = {"workload": plan["workload"], "n_gpus": 1, "of_world": ANCHOR_WORLD, "record_segments": CONFIG4_SEGMENTS,
            "value": round(nseg / t, 1), "unit": "segments/s", "ms_per_step": round(t * 1e3, 4), "steps": steps,
            "warmup": warmup, "status0_frac": float(np.mean(st == 0)),
-           "hbm_frac_end_to_end": round(nseg * (8 * R + 56) / t / 1e9 / HBM_PEAK_GBS, 4)}
+           "hbm_frac_end_to_end": round(nseg * (8 * R + 56) / t / 1e9 / HBM_PEAK_GBS, 4),
+           "note": "rank 0's shard of config 4 at N = 8, timed on one GPU: the curve's N-th point has "
+                   "efficiency value_N / (N x value)"}
     del x, o, k
     torch.cuda.empty_cache()
     return res
@@ -688,18 +743,8 @@ def main():
     for kv in filter(None, args.tune.split(",")):
         k, v = kv.split("=")
         _lib.check(lib.dfmi_set_tuning(k.encode(), int(v)), "dfmi_set_tuning")
-    R = int(F_SAMP / F_MOD * N_CYC)
-    # config 4 (BASELINE.json): ONE 10,000,000-segment record split over the ranks
-    # (total work fixed: strong scaling); config 2: 100,000 segments on one GPU;
-    # an explicit --segments is per GPU (weak scaling)
-    config4 = world > 1 and args.segments is None
-    if config4:
-        if CONFIG4_SEGMENTS % world:
-            raise SystemExit(f"config 4: {CONFIG4_SEGMENTS} segments do not split over {world} ranks")
-        nseg = CONFIG4_SEGMENTS // world
-    else:
-        nseg = args.segments if args.segments is not None else 100_000
-    nrec = max(1, args.channels) if world == 1 else 1
+    plan = plan_workload(world, args.segments, args.channels)
+    R, nseg, nrec, config4 = plan["R"], plan["nseg"], plan["nrec"], plan["config4"]
     if nrec > 1:  # config 3: channels as records of one batch (fit_many), each with its own seed
         if nseg % nrec:
             raise SystemExit("--segments must be a multiple of --channels")
@@ -835,15 +880,6 @@ def main():
     ms = el / args.steps * 1e3
     total_segments = nseg * world  # units of work; the seed replicas on ranks > 0 are not counted
     value = total_segments * args.steps / el
-    # BASELINE.json configs: 2 = 100k segments on one GPU, 3 = two channels,
-    # 4 = 10M over the ranks (1.25M per GPU at 8)
-    if config4:
-        cfg_name = "config4"
-    elif nrec == 2:
-        cfg_name = "config3"
-    else:
-        cfg_name = {100_000: "config2", 1_250_000: "config4 shard"}.get(nseg, "config2-shape")
-
     bytes_per_seg = 8 * R + 8 * (2 * NDATA + 1)  # read the segment, write QI + dc
     achieved = nall * bytes_per_seg / (demod_ms * 1e-3) / 1e9
     family = kname.split("<")[0]
@@ -879,14 +915,11 @@ def main():
 
     line = {"metric": METRIC, "value": round(value, 1), "unit": "segments/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
-            "scaling": "strong" if config4 else "weak", "vs_baseline": None, "dtype": "f64",
+            "scaling": plan["scaling"], "vs_baseline": None, "dtype": "f64",
             "data": "synthetic snr-mode DFMI (m=6, 40 dB white noise) generated on device by the counter-based "
                     "dfmi_synth_snr (Philox4x32-10 keyed by (seed, sample index): every rank regenerates buffer 0 "
                     "bit for bit)",
-            "config": {"workload": f"{cfg_name}: {nseg} segments/GPU"
-                                   + (f" ({nseg * world} total, one record)" if world > 1 else "")
-                                   + f" x R={R} @200 kS/s, ndata={NDATA}, "
-                                   f"{nrec} channel{'s' if nrec > 1 else ''}, _fit_parallel chunk size 1",
+            "config": {"workload": plan["workload"], "record_segments": plan["record_segments"],
                        "segments_per_gpu": nseg, "channels": nrec, "R": R, "ndata": NDATA,
                        "parallelism": f"shard{world}"},
             "world": {"size": world, "backend": backend, "ranks": ranks,
@@ -901,6 +934,11 @@ def main():
             "batch_m_mean": float(res[1].mean())}
     if args.tune:
         line["tuning"] = args.tune
+    if world == 1 and nrec == 1 and args.segments is None:
+        # the N = 1 point of the driver's 1 -> 8 curve, on the workload rank 0 fits at N = 8
+        del x, out, ok, qi, dcb, rows, lm_out, lm_ssq, lm_st
+        torch.cuda.empty_cache()
+        line["scaling_anchor"] = scaling_anchor(torch, dev, lib, _lib, stream, cfg, args.steps, args.warmup)
     if world == 1 and not args.no_extra and nrec == 1 and args.segments is None:
         line["extra_configs"] = extra_configs(torch, dev, lib, _lib, stream, cfg, want_base)
     if pre is not None:

@@ -57,6 +57,8 @@ struct Tuning {
                          // many-harmonic kernel wherever its geometry applies
   int demod_wide_from = 13;  // ndata from which demod_wide_kernel (component-major) goes ahead of the bin
                              // kernel, and the record pipeline leaves the row layout for it
+  int lm_wide = 1;              // ndata > 16: the many-harmonic LM path (lm.h kWideNd: closed-form sums over a
+                                // lean Miller walk); 0 = the literal general path (lm_general = 1 forces it too)
   int lm_onepass = 1;           // LM general path: one Bessel walk per evaluation with the values in LDS
                                 // (1: where 7 waves per CU still fit, 2: always, 0: never)
   int demod_wide_rmax = 2000;  // segments shorter than this go through demod_wide_kernel too
@@ -166,6 +168,10 @@ struct DeviceState {
   std::vector<std::array<hipEvent_t, 3>> ev_steps;
   void* pin = nullptr;  // pinned host scratch for the EKF's pass control read-backs
   size_t pin_n = 0;
+  // the EKF parallel in time's hand-over stream: sequential re-runs of channels that stopped
+  // contracting run here beside the remaining passes (created on first use)
+  hipStream_t ekf_side = nullptr;
+  hipEvent_t ev_ekf_in = nullptr, ev_ekf_out = nullptr;
 };
 
 std::map<int, DeviceState> g_dev;
@@ -587,10 +593,23 @@ bool wide_first(int ndata, int R) {
           (t_tune.demod_wide == 1 && (ndata >= t_tune.demod_wide_from || R < t_tune.demod_wide_rmax)));
 }
 
+int wide_no(int ndata) { return 2 * ndata + 1 <= 64 ? 1 : 2 * ndata + 1 <= 128 ? 2 : 4; }
+
+// Segments per wave demod_wide_kernel runs with: the requested KSEG (demod_wide_k, 0 = 8),
+// halved until the workgroup's dynamic LDS (kWavesPerBlock·KSEG·wide_set doubles: 66,560 B at
+// L = 256, KSEG 8) fits this device's LDS per workgroup; 0 when not even KSEG 2 fits.
+int wide_kseg(int L, int ndata) {
+  const int no = wide_no(ndata);
+  for (int k = t_tune.demod_wide_k ? t_tune.demod_wide_k : 8; k >= 2; k >>= 1)
+    if ((size_t)dfmi::kWavesPerBlock * k * dfmi::wide_set(L, no, k) * sizeof(double) <= t_ds->lds_per_block) return k;
+  return 0;
+}
+
 // demod_wide_kernel (component-major QI at many harmonics): its geometry (16-B rows, an even
-// basis period 128..256, at most 127 harmonics).
+// basis period 128..256, at most 127 harmonics) and an LDS footprint this device holds
+// (otherwise the bin / fold kernels run).
 bool wide_geometry(bool vec2, int L, int ndata) {
-  return vec2 && !(L & 1) && L >= 128 && L <= 256 && 2 * ndata + 1 <= 64 * 4;
+  return vec2 && !(L & 1) && L >= 128 && L <= 256 && 2 * ndata + 1 <= 64 * 4 && wide_kseg(L, ndata) > 0;
 }
 
 template <int NO, int KSEG>
@@ -614,14 +633,15 @@ int launch_wide_t(const double* x, int64_t nseg, int64_t stride, int R, int L, i
 
 int launch_wide(int dev, const double* x, int64_t nseg, int64_t stride, int R, int L, int ndata, double w0,
                 double* qi, int64_t qi_ld, double* dc, hipStream_t st, int n_cu) {
-  const int no = 2 * ndata + 1 <= 64 ? 1 : 2 * ndata + 1 <= 128 ? 2 : 4;
+  const int no = wide_no(ndata);
   const double* tabT = nullptr;
   if (int rc = basis_table_wide(dev, L, ndata, w0, no, &tabT)) return rc;
-  int k = t_tune.demod_wide_k;
   // KSEG 8: level with 4 at R = 4000 (0.578 / 0.576 ms at ndata 30, r05t-x), ahead at 62 (0.631 /
   // 0.617) and for short segments, where the contraction dominates (R = 200, ndata 10: 0.768 /
-  // 0.684 ms; R = 400: 0.471 / 0.423; profiles/r05/short_segments_split.jsonl)
-  if (k == 0) k = 8;
+  // 0.684 ms; R = 400: 0.471 / 0.423; profiles/r05/short_segments_split.jsonl); fewer where the
+  // device's LDS per workgroup cannot hold 8 (wide_kseg; callers checked wide_geometry)
+  const int k = wide_kseg(L, ndata);
+  if (k == 0) return fail(DFMI_ERR_UNSUPPORTED, "demod_wide_kernel: LDS per workgroup too small");
 #define DFMI_WIDE(NO_)                                                                                   \
   return k == 8 ? launch_wide_t<NO_, 8>(x, nseg, stride, R, L, ndata, tabT, qi, qi_ld, dc, st, n_cu)      \
          : k == 4 ? launch_wide_t<NO_, 4>(x, nseg, stride, R, L, ndata, tabT, qi, qi_ld, dc, st, n_cu)    \
@@ -725,18 +745,23 @@ int demod_device(int dev, const double* x, int64_t nseg, int64_t stride, int R, 
 // LM kernel selection: the register path (ndata <= 16; the exact-ndata variant with QI
 // in registers for the reference default ndata = 10) or the general path (any ndata,
 // or lm_general = 1). CHAIN: warm-start chains (sequential / n_cores chunks).
+// nd_sel: ndata, or 1000 for the literal general path (lm_general = 1); beyond 16 harmonics
+// the many-harmonic path (lm.h kWideNd) on component-major QI, "lm_wide" = 0 the literal one.
 template <bool CHAIN, bool ROWS>
 auto lm_kernel(int nd_sel) {
   constexpr int kNd10 = dfmi::kExactNd | 10;
+  const bool wide = nd_sel > 16 && nd_sel < 1000 && t_tune.lm_wide && !ROWS;
   if constexpr (CHAIN) {
     return nd_sel == 10   ? dfmi::lm_chunks_kernel<kNd10, true>
            : nd_sel <= 12 ? dfmi::lm_chunks_kernel<12, true>
            : nd_sel <= 16 ? dfmi::lm_chunks_kernel<16, true>
+           : wide         ? dfmi::lm_chunks_kernel<dfmi::kWideNd, true>
                           : dfmi::lm_chunks_kernel<0, true>;
   } else {
     return nd_sel == 10   ? dfmi::lm_chunks_kernel<kNd10, false, ROWS, true>
            : nd_sel <= 12 ? dfmi::lm_chunks_kernel<12, false, ROWS>
            : nd_sel <= 16 ? dfmi::lm_chunks_kernel<16, false, ROWS>
+           : wide         ? dfmi::lm_chunks_kernel<dfmi::kWideNd, false, false>
                           : dfmi::lm_chunks_kernel<0, false, ROWS>;
   }
 }
@@ -795,7 +820,7 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
   // the general path's one-pass Bessel walk: the lane's recurrence values in LDS, while 7
   // waves per CU still fit (ndata + 2 <= 45): ndata 40 0.276 -> 0.264 ms per 100k; at 62 (5
   // waves per CU) 0.384 -> 0.663, r05ax
-  if (!chain && !rows && nd_sel > 16 && t_tune.lm_onepass &&
+  if (!chain && !rows && nd_sel > 16 && !(t_tune.lm_wide && nd_sel < 1000) && t_tune.lm_onepass &&
       (t_tune.lm_onepass == 2 || (size_t)64 * (ndata + 2) * 8 * 7 <= t_ds->lds_per_block)) {
     kern = dfmi::lm_chunks_kernel<0, false, false, false, true>;
     lds = (size_t)64 * (ndata + 2) * sizeof(double);
@@ -864,7 +889,7 @@ int fused_seed_demod(int dev, const double* x, int64_t nrec, int64_t nbuf, int R
 // so both paths give the same bits — the global fold / direct kernel otherwise.
 int seed_launch(int dev, const double* x, int64_t nrec, int64_t rec_stride, int R, int ndata, double w0, int L,
                 const double* gdev, const dfmi::GuessInline& ginl, const double* jtab, const dfmi::LMConst& c,
-                double* out, int64_t out_ld, int64_t nbuf, int32_t* fitok, hipStream_t sst) {
+                double* out, int64_t out_ld, int64_t nbuf, int32_t* fitok, hipStream_t sst, bool seed_dc) {
   int rc;
   if (L > 64 * 16) L = 0;  // no table: the direct kernel's per-sample sincos
   const double* tab = nullptr;
@@ -880,7 +905,7 @@ int seed_launch(int dev, const double* x, int64_t nrec, int64_t rec_stride, int 
                           : (nslot <= 2 ? dfmi::seed_bins_kernel<0, 2> : nslot <= 4 ? dfmi::seed_bins_kernel<0, 4>
                                                                                   : dfmi::seed_bins_kernel<0, 8>);
     hipLaunchKernelGGL(sk, dim3((unsigned)nrec), dim3(64), blds, sst, x, rec_stride, R, L, ndata, tab, gdev, ginl,
-                       gdev ? 0 : 1, jtab, c, out, out_ld, nbuf, fitok, t_ds->probe);
+                       gdev ? 0 : 1, jtab, c, out, out_ld, nbuf, fitok, t_ds->probe, seed_dc ? 1 : 0);
   } else {
     void *qs, *ds_;
     if ((rc = workspace(dev, "qi_seed", (size_t)2 * ndata * nrec * 8, &qs))) return rc;
@@ -892,7 +917,7 @@ int seed_launch(int dev, const double* x, int64_t nrec, int64_t rec_stride, int 
     const double* tabT = nullptr;
     int no = 0;
     if (L > 0 && wide_geometry(vec2, L, ndata)) {
-      no = 2 * ndata + 1 <= 64 ? 1 : 2 * ndata + 1 <= 128 ? 2 : 4;
+      no = wide_no(ndata);
       if ((rc = basis_table_wide(dev, L, ndata, w0, no, &tabT))) return rc;
     }
     const size_t lds = tabT ? (size_t)(L + 4) * sizeof(double) : 0;
@@ -968,8 +993,10 @@ int nls_record_device(int dev, const double* x, int64_t nrec, int64_t rec_stride
   if (parallel) {  // the seed beside the bulk demodulation (side stream, event)
     HIPCHK(hipEventRecord(ds.ev_in, st));
     HIPCHK(hipStreamWaitEvent(ds.side, ds.ev_in, 0));
+    // buffer 0's dc: the bulk demodulation writes it on the component-major path (beside the
+    // seed, unordered: one writer only); on the row path the LM skips buffer 0, so the seed does
     if ((rc = seed_launch(dev, x, nrec, rec_stride, R, ndata, w0, L, gdev, ginl, jtab, c, out, out_ld, nbuf, fitok,
-                          ds.side)))
+                          ds.side, rows)))
       return rc;
     HIPCHK(hipEventRecord(ds.ev_seed, ds.side));
   }
@@ -1027,6 +1054,7 @@ const std::map<std::string, Knob>& knobs() {
       {"demod_wide_from", {&Tuning::demod_wide_from, {}}},
       {"demod_wide_rmax", {&Tuning::demod_wide_rmax, {}}},
       {"lm_onepass", {&Tuning::lm_onepass, {0, 1, 2}}},
+      {"lm_wide", {&Tuning::lm_wide, {0, 1}}},
       {"demod_wide_half", {&Tuning::demod_wide_half, {0, 1}}},
       {"demod_wide_dbg", {&Tuning::demod_wide_dbg, {0, 1, 2, 3, 4, 5, 6, 7}}},
       {"ekf_row", {&Tuning::ekf_row, {}}},
@@ -1090,14 +1118,14 @@ int pinned(size_t bytes, void** out) {
 // ekf_kernel, 16x the channels per instruction). Returns the variant's name in *name.
 int ekf_seq_launch(const double* dx, int64_t nrec, int64_t rs, int64_t n, const double* dx0, const double* dp0,
                    const double* dq, const double* dr, const double* wt, int32_t R, int64_t nbuf, double* dstates,
-                   hipStream_t st, const char** name) {
+                   hipStream_t st, const char** name, const int* idx = nullptr) {
   const int block = 64;
   const bool row = t_tune.ekf_row && nrec <= (int64_t)t_tune.ekf_row * t_ds->n_cu * 16;
   const int64_t grid = row ? (nrec + 3) / 4 : (nrec + block - 1) / block;
   // rotation between anchors: groups of 16 (8, 4) samples whose ends carry the snapshots
   const bool rot = t_tune.ekf_rot && R % 4 == 0;
   using EK = void (*)(const double*, int64_t, int64_t, int64_t, const double*, const double*, const double*,
-                      const double*, const double*, int, int64_t, double*, DfmiTrigK);
+                      const double*, const double*, int, int64_t, double*, DfmiTrigK, const int*);
   EK ek;
   if (row)
     ek = !rot ? dfmi::ekf_row_kernel<DFMI_EKF_SPLIT != 0>
@@ -1107,7 +1135,7 @@ int ekf_seq_launch(const double* dx, int64_t nrec, int64_t rs, int64_t n, const 
   else
     ek = !rot ? dfmi::ekf_kernel : R % 8 == 0 ? dfmi::ekf_lane_rot_kernel<8> : dfmi::ekf_lane_rot_kernel<4>;
   hipLaunchKernelGGL(ek, dim3((unsigned)grid), dim3(block), 0, st, dx, nrec, rs, n, dx0, dp0, dq, dr, wt, (int)R, nbuf,
-                     dstates, dfmi_trig_k());
+                     dstates, dfmi_trig_k(), idx);
   HIPCHK(hipGetLastError());
   *name = row ? (rot ? "ekf_rot_kernel" : "ekf_row_kernel") : (rot ? "ekf_lane_rot_kernel" : "ekf_kernel");
   return DFMI_OK;
@@ -1141,6 +1169,7 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
                                             : (int)std::min<int64_t>(256, std::max<int64_t>(48, n / 1600));
   const int hist_n = t_tune.ekf_pit_trace ? cap : 0;
   void *xt, *wtt, *xbar, *conv, *chan, *hst, *done, *hs, *ent = nullptr, *hist = nullptr, *pin;
+  void *sidx = nullptr, *handed = nullptr;
   std::vector<double*> lv[2];  // per aggregate buffer: level arrays [r][65][lsz[l]]
   // every allocation before the first launch: a failure leaves the sequential kernels to run
   {
@@ -1166,6 +1195,10 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
     ws("p_hs", (size_t)(nrec * (T0 > 0 ? T0 : 1) * 5) * 8, &hs);
     if (t_tune.ekf_pit_fused && t_tune.ekf_pit_measure == 1) ws("p_ent", (size_t)(nrec * 5 * nb) * 8, &ent);
     if (hist_n) ws("p_hist", (size_t)nrec * hist_n * 8, &hist);
+    if (t_tune.ekf_pit_seq) {  // the hand-over list (sequential re-runs read the records in place)
+      ws("p_sidx", (size_t)nrec * sizeof(int), &sidx);
+      ws("p_handed", (size_t)nrec * sizeof(unsigned), &handed);
+    }
     if (!rc) rc = pinned((size_t)nrec * sizeof(dfmi::PitChan) + 64, &pin);
     if (rc) {
       (void)hipGetLastError();  // clear the failed allocation
@@ -1220,6 +1253,47 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
                        (const double*)hs, (const double*)hst, T0);
     scan(lv[0]);
   }
+  // Hand-over: channels the stop rule gave up on (status 2; at the end every channel not
+  // converged) are re-run by the sequential kernel as soon as a host check sees them, on the
+  // device's hand-over stream beside the passes the other channels still run (a pass kernel
+  // returns at once for a channel whose status is set, so the two never write the same
+  // states). The list is built on the device (ekf_pit_handover_kernel); the host only counts.
+  std::vector<char> host_handed((size_t)nrec, 0);
+  int64_t nh = 0;
+  bool side_used = false;
+  std::string seq_name;
+  if (handed) HIPCHK(hipMemsetAsync(handed, 0, (size_t)nrec * sizeof(unsigned), st));
+  auto hand_over = [&](const dfmi::PitChan* hc, bool final_) -> int {
+    if (!t_tune.ekf_pit_seq) return DFMI_OK;
+    int64_t cnt = 0;
+    for (int64_t r = 0; r < nrec; ++r)
+      if (!host_handed[r] && (hc[r].status == 2 || (final_ && hc[r].status != 1))) {
+        host_handed[r] = 1;
+        ++cnt;
+      }
+    if (cnt == 0) return DFMI_OK;
+    DeviceState& d = *t_ds;
+    if (!d.ekf_side) {
+      int lo = 0, hi = 0;
+      HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIPCHK(hipStreamCreateWithPriority(&d.ekf_side, hipStreamNonBlocking, hi));
+      HIPCHK(hipEventCreateWithFlags(&d.ev_ekf_in, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&d.ev_ekf_out, hipEventDisableTiming));
+    }
+    hipLaunchKernelGGL(dfmi::ekf_pit_handover_kernel, dim3(1), dim3(64), 0, st, (const dfmi::PitChan*)ch, nrec,
+                       (unsigned*)handed, (int*)sidx + nh, final_ ? 1 : 0);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(d.ev_ekf_in, st));
+    HIPCHK(hipStreamWaitEvent(d.ekf_side, d.ev_ekf_in, 0));
+    const char* kname;
+    if (int rc = ekf_seq_launch(dx, cnt, rs, n, dx0, dp0, dq, dr, wt, R, nbuf, dstates, d.ekf_side, &kname,
+                                (const int*)sidx + nh))
+      return rc;
+    seq_name = kname;
+    nh += cnt;
+    side_used = true;
+    return DFMI_OK;
+  };
   int cur = 0;
   bool fresh = false;  // pin holds the channels' final control blocks
   for (int pass = 1;; ++pass) {
@@ -1254,6 +1328,7 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
         fresh = true;
         break;
       }
+      if (int rc = hand_over(hc, false)) return rc;  // beside the passes still to come
       next_check = std::min(pass + every, cap);
     }
     if (t_tune.ekf_pit_fused) {
@@ -1270,34 +1345,14 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
   }
   if (!fresh || hist_n) HIPCHK(hipStreamSynchronize(st));
   const dfmi::PitChan* hc = (const dfmi::PitChan*)pin;
-  std::vector<int> seq;
   g_pit_passes.assign((size_t)nrec, 0);
-  for (int64_t r = 0; r < nrec; ++r) {
-    g_pit_passes[r] = hc[r].status == 1 ? hc[r].passes : -hc[r].passes;
-    if (hc[r].status != 1) seq.push_back((int)r);
-  }
+  for (int64_t r = 0; r < nrec; ++r) g_pit_passes[r] = hc[r].status == 1 ? hc[r].passes : -hc[r].passes;
   g_last_demod = "ekf_pit (B=" + std::to_string(B) + ", nb=" + std::to_string(nb) + ")";
-  if (!seq.empty() && t_tune.ekf_pit_seq) {
-    const int64_t ns = (int64_t)seq.size();
-    void *idx, *xs, *x0s, *rvs, *ss;
-    int rc;
-    if ((rc = workspace(dev, "p_sidx", (size_t)ns * sizeof(int), &idx))) return rc;
-    if ((rc = workspace(dev, "p_sx", (size_t)(ns * n) * 8, &xs))) return rc;
-    if ((rc = workspace(dev, "p_sx0", (size_t)ns * 5 * 8, &x0s))) return rc;
-    if ((rc = workspace(dev, "p_srv", (size_t)ns * 8, &rvs))) return rc;
-    if ((rc = workspace(dev, "p_sst", (size_t)(ns * (nbuf > 0 ? nbuf : 1) * 5) * 8, &ss))) return rc;
-    HIPCHK(hipMemcpy(idx, seq.data(), (size_t)ns * sizeof(int), hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(dfmi::ekf_pit_pick_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)ns), dim3(256), 0, st,
-                       dx, rs, n, dx0, dr, (const int*)idx, (double*)xs, (double*)x0s, (double*)rvs);
-    const char* kname;
-    if ((rc = ekf_seq_launch((const double*)xs, ns, n, n, (const double*)x0s, dp0, dq, (const double*)rvs, wt, R, nbuf,
-                             (double*)ss, st, &kname)))
-      return rc;
-    if (nbuf > 0)
-      hipLaunchKernelGGL(dfmi::ekf_pit_put_kernel, dim3((unsigned)((nbuf * 5 + 255) / 256), (unsigned)ns), dim3(256),
-                         0, st, (const double*)ss, nbuf, (const int*)idx, dstates);
-    HIPCHK(hipGetLastError());
-    g_last_demod += std::string(" + ") + kname + " x" + std::to_string(ns);
+  if (int rc = hand_over(hc, true)) return rc;  // every channel still not converged
+  if (side_used) {  // join: the caller's stream sees the re-run states
+    HIPCHK(hipEventRecord(t_ds->ev_ekf_out, t_ds->ekf_side));
+    HIPCHK(hipStreamWaitEvent(st, t_ds->ev_ekf_out, 0));
+    g_last_demod += std::string(" + ") + seq_name + " x" + std::to_string(nh);
   }
   return DFMI_OK;
 }

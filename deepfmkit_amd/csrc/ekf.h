@@ -114,21 +114,24 @@ __global__ __launch_bounds__(64) void ekf_kernel(const double* __restrict__ x, i
                                                   int64_t n_samp, const double* __restrict__ x0,
                                                   const double* __restrict__ p0, const double* __restrict__ qd,
                                                   const double* __restrict__ rv, const double* __restrict__ wt, int R,
-                                                  int64_t nbuf, double* __restrict__ states, DfmiTrigK tk) {
+                                                  int64_t nbuf, double* __restrict__ states, DfmiTrigK tk,
+    const int* __restrict__ idx) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= nrec) return;
-  const double* __restrict__ xr = x + r * rec_stride;
+  // idx (optional): channel r of this launch is record idx[r] of the caller's arrays
+  const int64_t rid = idx ? (int64_t)idx[r] : r;
+  const double* __restrict__ xr = x + rid * rec_stride;
   double st[5];
   double P[5][5];
   double Q[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
-    st[i] = x0[r * 5 + i];
+    st[i] = x0[rid * 5 + i];
     Q[i] = qd[i];
 #pragma unroll
     for (int j = 0; j < 5; ++j) P[i][j] = (i == j) ? p0[i] : 0.0;
   }
-  const double Rv = rv[r];
+  const double Rv = rv[rid];
   // the snapshot test counts down (wave-uniform) instead of a 64-bit modulo per sample
   int64_t to_snap = R;
   auto snap = [&](int64_t k) {
@@ -137,7 +140,7 @@ __global__ __launch_bounds__(64) void ekf_kernel(const double* __restrict__ x, i
       const int64_t b = (k + 1) / R - 1;
       if (b < nbuf) {
 #pragma unroll
-        for (int i = 0; i < 5; ++i) states[(r * nbuf + b) * 5 + i] = st[i];
+        for (int i = 0; i < 5; ++i) states[(rid * nbuf + b) * 5 + i] = st[i];
       }
     }
   };
@@ -305,22 +308,25 @@ __global__ __launch_bounds__(64) void ekf_row_kernel(const double* __restrict__ 
                                                       const double* __restrict__ p0, const double* __restrict__ qd,
                                                       const double* __restrict__ rv, const double* __restrict__ wt,
                                                       int R, int64_t nbuf, double* __restrict__ states,
-                                                      DfmiTrigK tk) {
+                                                      DfmiTrigK tk,
+    const int* __restrict__ idx) {
   const int lane = threadIdx.x & 63;
   const int64_t r0 = (int64_t)blockIdx.x * 4 + (lane >> 4);
   const bool live = r0 < nrec;
   const int64_t r = live ? r0 : nrec - 1;  // rows past the end shadow the last channel (no stores)
   int j = lane & 15;
   if (j > 4) j = 4;
-  const double* __restrict__ xr = x + r * rec_stride;
+  // idx (optional): channel r of this launch is record idx[r] of the caller's arrays
+  const int64_t rid = idx ? (int64_t)idx[r] : r;
+  const double* __restrict__ xr = x + rid * rec_stride;
   double st[5], Pc[5], qv[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
-    st[i] = x0[r * 5 + i];
+    st[i] = x0[rid * 5 + i];
     Pc[i] = (i == j) ? p0[i] : 0.0;
     qv[i] = (i == j) ? qd[i] : 0.0;
   }
-  const double Rv = rv[r];
+  const double Rv = rv[rid];
   const bool writer = live && (lane & 15) == 0;
   int64_t to_snap = R;
   auto snap = [&](int64_t k) {
@@ -329,7 +335,7 @@ __global__ __launch_bounds__(64) void ekf_row_kernel(const double* __restrict__ 
       const int64_t b = (k + 1) / R - 1;
       if (b < nbuf && writer) {
 #pragma unroll
-        for (int i = 0; i < 5; ++i) states[(r * nbuf + b) * 5 + i] = st[i];
+        for (int i = 0; i < 5; ++i) states[(rid * nbuf + b) * 5 + i] = st[i];
       }
     }
   };
@@ -522,22 +528,25 @@ __global__ __launch_bounds__(64) void ekf_rot_kernel(const double* __restrict__ 
                                                       const double* __restrict__ p0, const double* __restrict__ qd,
                                                       const double* __restrict__ rv, const double* __restrict__ wt,
                                                       int R, int64_t nbuf, double* __restrict__ states,
-                                                      DfmiTrigK tk) {
+                                                      DfmiTrigK tk,
+    const int* __restrict__ idx) {
   const int lane = threadIdx.x & 63;
   const int64_t r0 = (int64_t)blockIdx.x * 4 + (lane >> 4);
   const bool live = r0 < nrec;
   const int64_t r = live ? r0 : nrec - 1;
   int j = lane & 15;
   if (j > 4) j = 4;
-  const double* __restrict__ xr = x + r * rec_stride;
+  // idx (optional): channel r of this launch is record idx[r] of the caller's arrays
+  const int64_t rid = idx ? (int64_t)idx[r] : r;
+  const double* __restrict__ xr = x + rid * rec_stride;
   double st[5], Pc[5], qv[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
-    st[i] = x0[r * 5 + i];
+    st[i] = x0[rid * 5 + i];
     Pc[i] = (i == j) ? p0[i] : 0.0;
     qv[i] = (i == j) ? qd[i] : 0.0;
   }
-  const double Rv = rv[r];
+  const double Rv = rv[rid];
   const bool writer = live && (lane & 15) == 0;
   const bool odd = lane & 1;
   const RowSplitCoef rc = row_split_coef(tk, odd);
@@ -591,7 +600,7 @@ __global__ __launch_bounds__(64) void ekf_rot_kernel(const double* __restrict__ 
       const int64_t b = (k + G) / R - 1;
       if (b < nbuf && writer) {
 #pragma unroll
-        for (int i = 0; i < 5; ++i) states[(r * nbuf + b) * 5 + i] = st[i];
+        for (int i = 0; i < 5; ++i) states[(rid * nbuf + b) * 5 + i] = st[i];
       }
     }
 #pragma unroll
@@ -684,19 +693,22 @@ __global__ __launch_bounds__(64) void ekf_lane_rot_kernel(const double* __restri
                                                            const double* __restrict__ x0, const double* __restrict__ p0,
                                                            const double* __restrict__ qd, const double* __restrict__ rv,
                                                            const double* __restrict__ wt, int R, int64_t nbuf,
-                                                           double* __restrict__ states, DfmiTrigK tk) {
+                                                           double* __restrict__ states, DfmiTrigK tk,
+    const int* __restrict__ idx) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= nrec) return;
-  const double* __restrict__ xr = x + r * rec_stride;
+  // idx (optional): channel r of this launch is record idx[r] of the caller's arrays
+  const int64_t rid = idx ? (int64_t)idx[r] : r;
+  const double* __restrict__ xr = x + rid * rec_stride;
   double st[5], P[5][5], Q[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
-    st[i] = x0[r * 5 + i];
+    st[i] = x0[rid * 5 + i];
     Q[i] = qd[i];
 #pragma unroll
     for (int j = 0; j < 5; ++j) P[i][j] = (i == j) ? p0[i] : 0.0;
   }
-  const double Rv = rv[r];
+  const double Rv = rv[rid];
   LaneRot lr{0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   double dmax = 0.0;
   int64_t k = 0;
@@ -747,7 +759,7 @@ __global__ __launch_bounds__(64) void ekf_lane_rot_kernel(const double* __restri
       const int64_t b = (k + G) / R - 1;
       if (b < nbuf) {
 #pragma unroll
-        for (int i = 0; i < 5; ++i) states[(r * nbuf + b) * 5 + i] = st[i];
+        for (int i = 0; i < 5; ++i) states[(rid * nbuf + b) * 5 + i] = st[i];
       }
     }
 #pragma unroll

@@ -34,9 +34,10 @@
 // converged channel's later kernels return at once (status per channel); the host reads the
 // count of channels still passing after the first ekf_pit_first passes and then every
 // ekf_pit_every, and stops when none is left. A channel that stops contracting (or reaches
-// the pass cap) is re-run by the sequential row / lane kernel (ekf_pit_pick_kernel /
-// ekf_pit_put_kernel around it), so the result never depends on the iteration having
-// converged.
+// the pass cap) is re-run by the sequential row / lane kernel, launched at the host check
+// that first sees it handed over, on a stream of its own beside the remaining passes and
+// reading the record in place (ekf_pit_handover_kernel's index list), so the result never
+// depends on the iteration having converged.
 //
 // Layouts (all channel-major, blocks fastest so lane b of a wave reads address b):
 //   xt[r][i][b], wtt[i][b] (sample k = b B + i), xbar[r][c][i][b] (the seeded trajectory:
@@ -1125,26 +1126,30 @@ __global__ __launch_bounds__(64) void ekf_pit_check_kernel(double* __restrict__ 
   conv[r] = 0.0;
 }
 
-// The channels the passes left to the sequential kernel (the host's list idx): their records,
-// x0 and R_val copied into compact arrays (grid.y = listed channel, x = samples) ...
-__global__ __launch_bounds__(256) void ekf_pit_pick_kernel(const double* __restrict__ x, int64_t rs, int64_t n,
-                                                           const double* __restrict__ x0,
-                                                           const double* __restrict__ rv,
-                                                           const int* __restrict__ idx, double* __restrict__ xs,
-                                                           double* __restrict__ x0s, double* __restrict__ rvs) {
-  const int64_t j = blockIdx.y, r = idx[j];
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < n) xs[j * n + k] = x[r * rs + k];
-  if (blockIdx.x == 0 && threadIdx.x < 5) x0s[j * 5 + threadIdx.x] = x0[r * 5 + threadIdx.x];
-  if (blockIdx.x == 0 && threadIdx.x == 5) rvs[j] = rv[r];
-}
-
-// ... and the sequential kernel's snapshots of them put back in place.
-__global__ __launch_bounds__(256) void ekf_pit_put_kernel(const double* __restrict__ ss, int64_t nbuf,
-                                                          const int* __restrict__ idx, double* __restrict__ states) {
-  const int64_t j = blockIdx.y, r = idx[j];
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < nbuf * 5) states[r * nbuf * 5 + k] = ss[j * nbuf * 5 + k];
+// Channels the passes handed to the sequential kernel since the previous call: status 2 (with
+// final != 0: every channel not converged, status 0 at the pass cap included) and not yet flagged
+// in `handed`, appended to idx[0..] in channel order (ballot prefix: one wave, no atomics). The
+// sequential kernels then read those records in place through idx (no copy of the samples), on
+// a stream of their own while the other channels keep passing (dfmi_capi.hip ekf_pit_run).
+__global__ __launch_bounds__(64) void ekf_pit_handover_kernel(const PitChan* __restrict__ ch, int64_t nrec,
+                                                              unsigned* __restrict__ handed, int* __restrict__ idx,
+                                                              int final_) {
+  const int lane = threadIdx.x;
+  int base = 0;
+  for (int64_t r0 = 0; r0 < nrec; r0 += 64) {
+    const int64_t r = r0 + lane;
+    bool take = false;
+    if (r < nrec) {
+      const int s = ch[r].status;
+      take = handed[r] == 0u && (s == 2 || (final_ && s != 1));
+    }
+    const uint64_t m = __ballot(take);
+    if (take) {
+      idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (int)r;
+      handed[r] = 1u;
+    }
+    base += __popcll(m);
+  }
 }
 
 }  // namespace dfmi

@@ -877,6 +877,225 @@ struct SplitEval {  // NDMAX: a register-path variant tag (nd_cap / nd_exact)
   DFMI_HDI static double ssq_of(const Trial& t) { return t.ssq; }
 };
 
+// ---------------------------------------------------------------------------
+// Many-harmonic path (ndata > 16): the register path's structured evaluation over a lean
+// Miller walk.
+//
+// The general path above spends ~71k VALU instructions per wave of 64 fits at ndata 62
+// (config-2 QI; profiles/r06/lm_general_pmc_before.txt): each harmonic of a full evaluation
+// is ~85 instructions (the literal per-residual Jacobian, quarter_turn selects on a runtime
+// j, 64-bit QI addressing) and each step of the two Miller passes ~10 more (the per-step
+// overflow test and the rescale bookkeeping of dfmi_math.h). A wave issues those back to back
+// (fp64 chains are issue-bound, dfmi_math.h dfmi_sincos_k), so the LM's time is its
+// instruction count. Here:
+//  * the two Miller passes without per-step tests where no rescale can happen: |f_{k-1}| <=
+//    (2k/x + 1) |f_k|, so M log2(2M/x + 1) < 590 keeps every f below 2^600 (the walk's rescale
+//    threshold) and the values are bit for bit those of the checked walk (same fma sequence);
+//    otherwise (tiny / huge / negative m, or a bound that does not hold) the checked walk of
+//    harmonic_walk;
+//  * harmonics in blocks of four with j = 4b - u, so cos(phi + j pi/2) is a signed (a cos phi,
+//    a sin phi) without a select;
+//  * the closed-form J^T J / J^T r of eval_reg_accept (psi column orthogonal: block-diagonal
+//    J^T J, damped_solve_block) and ssqf-only trials as on the register path;
+//  * QI through QCol: a uniform column base plus a 32-bit per-lane offset (no 64-bit address
+//    arithmetic per load), the next block's four QI pairs loaded while this block is evaluated.
+// Not bit-identical to the literal general path (lm_general = 1 keeps that one); parity with
+// the reference is gated at full scale (tests/test_gpu_full_scale.py ndata 16..62,
+// tests/test_gpu_quickstart.py).
+// ---------------------------------------------------------------------------
+constexpr int kWideNd = 1 << 9;  // NDMAX tag of the many-harmonic path
+
+// Component-major QI with the column base uniform across the wave (qi, harmonic h) and the
+// segment index per lane.
+struct QCol {
+  static constexpr int kPre = 0;
+  const double* __restrict__ base;
+  uint32_t off;
+  int64_t ld;
+  int nd;
+  DFMI_HDI double qc(int h) const { return (base + (int64_t)h * ld)[off]; }
+  DFMI_HDI double qs(int h) const { return (base + (int64_t)(nd + h) * ld)[off]; }
+};
+
+// Harmonics j = nd .. 1 in descending order: body(j, J_{j-1}, J_j, J_{j+1}, cos j psi, sin j psi,
+// Q_j, I_j). (c1, s1) = (cos, sin) psi, (cn, sn) = (cos, sin)(nd psi).
+template <typename QF, typename Body>
+DFMI_HDI void wide_walk(const QF& q, int nd, double m, double psi, double c1, double s1, double cn, double sn,
+                        Body&& body) {
+  const int M = dfmi_bessel_start(nd + 1, m);
+  const bool fast = m > 0.0 && m >= DFMI_BES_TINY && m < 1.0e5 && !dfmi_bessel_use_large(m, nd + 1) &&
+                    (float)M * log2f((float)(2.0 * M / m + 1.0)) < (float)(DFMI_BES_BIG_EXP - 10);
+  if (!fast) {
+    harmonic_walk(nd, m, psi, [&](int j, double jm1, double j0, double jp1, double cj, double sj) {
+      body(j, jm1, j0, jp1, cj, sj, q.qc(j - 1), q.qs(j - 1));
+    });
+    return;
+  }
+  const double tox = 2.0 / m;
+  // pass 1: S = f_0 + 2 sum f_2k (M even; dfmi_bessel_norm without its rescale test)
+  double fp1 = 0.0, f = 1.0, S = 2.0;
+  double kd = (double)M;
+  for (int k = M; k > 2; k -= 2) {
+    double fm1 = fma(kd * tox, f, -fp1);
+    fp1 = f;
+    f = fm1;
+    kd -= 1.0;
+    fm1 = fma(kd * tox, f, -fp1);
+    fp1 = f;
+    f = fm1;
+    kd -= 1.0;
+    S += 2.0 * f;  // f_{k-2}, an even order > 0
+  }
+  {
+    double fm1 = fma(kd * tox, f, -fp1);  // f_1
+    fp1 = f;
+    f = fm1;
+    kd -= 1.0;
+    fm1 = fma(kd * tox, f, -fp1);  // f_0
+    S += fm1;
+  }
+  const double invS = 1.0 / S;
+  // pass 2: down to f_{nd+1}, then one step per harmonic
+  fp1 = 0.0;
+  f = 1.0;
+  kd = (double)M;
+  for (int k = M; k > nd + 1; --k) {
+    const double fm1 = fma(kd * tox, f, -fp1);
+    fp1 = f;
+    f = fm1;
+    kd -= 1.0;
+  }
+  // f = f_{nd+1}, fp1 = f_{nd+2}, kd = nd + 1
+  double Jp1 = f * invS;
+  {
+    const double fm1 = fma(kd * tox, f, -fp1);  // f_nd
+    fp1 = f;
+    f = fm1;
+    kd -= 1.0;
+  }
+  double J0 = f * invS;
+  double cj = cn, sj = sn;
+  auto one = [&](int j, double Q, double I) {
+    const double fm1 = fma(kd * tox, f, -fp1);  // f_{j-1}
+    fp1 = f;
+    f = fm1;
+    kd -= 1.0;
+    const double Jm1 = fm1 * invS;
+    body(j, Jm1, J0, Jp1, cj, sj, Q, I);
+    Jp1 = J0;
+    J0 = Jm1;
+    const double c2 = fma(cj, c1, sj * s1);     // cos((j-1) psi)
+    const double s2 = fma(sj, c1, -(cj * s1));  // sin((j-1) psi)
+    cj = c2;
+    sj = s2;
+  };
+  int j = nd;
+  for (; (j & 3) != 0; --j) one(j, q.qc(j - 1), q.qs(j - 1));
+  // blocks of four from a multiple of four: j & 3 is known at compile time in each body
+  const int nb = j >> 2;
+  if (nb > 0) {
+    double bq[4], bs[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      bq[u] = q.qc(4 * nb - 1 - u);
+      bs[u] = q.qs(4 * nb - 1 - u);
+    }
+    for (int b = nb; b >= 1; --b) {
+      const int jb = b << 2;
+      double cq[4], cs[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        cq[u] = bq[u];
+        cs[u] = bs[u];
+        const int h = b > 1 ? jb - 5 - u : 0;  // the next block's QI (clamped on the last)
+        bq[u] = q.qc(h);
+        bs[u] = q.qs(h);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) one(jb - u, cq[u], cs[u]);
+    }
+  }
+}
+
+struct WideTrial {
+  double ssq, cph, sph, c1, s1, cn, sn;
+};
+
+// ssqf (fit.py:152-167) at p on the many-harmonic path; keeps the point's trig in t.
+template <typename QF>
+DFMI_HDI double wide_trial(const QF& q, int nd, const double (&p)[4], WideTrial& t, const DfmiTrigK& k) {
+  dfmi_sincos_auto(p[2], k, &t.sph, &t.cph);
+  dfmi_sincos_auto(p[3], k, &t.s1, &t.c1);
+  dfmi_sincos_auto((double)nd * p[3], k, &t.sn, &t.cn);
+  const double ac = p[0] * t.cph, as = p[0] * t.sph;
+  double so = 0.0, se = 0.0;
+  wide_walk(q, nd, p[1], p[3], t.c1, t.s1, t.cn, t.sn,
+            [&](int j, double, double J0, double, double cj, double sj, double Q, double I) {
+              const double c = quarter_turn(j, ac, as) * J0;  // a cos(phi + j pi/2) J_j
+              const double rq = fma(-c, cj, Q);
+              const double ri = fma(c, sj, I);
+              if (j & 1) {
+                so = fma(rq, rq, so);
+                so = fma(ri, ri, so);
+              } else {
+                se = fma(rq, rq, se);
+                se = fma(ri, ri, se);
+              }
+            });
+  t.ssq = so + se;
+  return t.ssq;
+}
+
+// coeffs (fit.py:68-150) at an accepted trial point: eval_reg_accept's closed form over the
+// many-harmonic walk; e.ssq is the trial's.
+template <typename QF>
+DFMI_HDI void wide_accept(const QF& q, int nd, const double (&p)[4], const WideTrial& t, Eval& e) {
+  const double a = p[0];
+  const double ac = a * t.cph, as = a * t.sph;
+  const double cph0 = (a != 0.0) ? t.cph : 0.0, sph0 = (a != 0.0) ? t.sph : 0.0;
+  double a00 = 0.0, a01 = 0.0, a02 = 0.0, a11 = 0.0, a12 = 0.0, a22 = 0.0, a33 = 0.0;
+  double g0 = 0.0, g1 = 0.0, g2 = 0.0, g3 = 0.0;
+  wide_walk(q, nd, p[1], p[3], t.c1, t.s1, t.cn, t.sn,
+            [&](int j, double Jm1, double Jj, double Jp1, double cj, double sj, double Q, double I) {
+              const double aP = quarter_turn(j, ac, as), aD = quarter_turn(j + 1, ac, as);
+              const double c = aP * Jj;
+              const double u0 = quarter_turn(j, cph0, sph0) * Jj;
+              const double u1 = aP * (0.5 * (Jm1 - Jp1));
+              const double u2 = aD * Jj;
+              const double rq = fma(-c, cj, Q);
+              const double ri = fma(c, sj, I);
+              const double A = fma(cj, rq, -(sj * ri));
+              const double B = fma(sj, rq, cj * ri);
+              const double w = fma(cj, cj, sj * sj);
+              const double v0 = u0 * w, v1 = u1 * w, v2 = u2 * w;
+              a00 = fma(v0, u0, a00);
+              a01 = fma(v0, u1, a01);
+              a02 = fma(v0, u2, a02);
+              a11 = fma(v1, u1, a11);
+              a12 = fma(v1, u2, a12);
+              a22 = fma(v2, u2, a22);
+              const double jc = (double)j * c;
+              a33 = fma(jc * w, jc, a33);
+              g0 = fma(u0, A, g0);
+              g1 = fma(u1, A, g1);
+              g2 = fma(u2, A, g2);
+              g3 = fma(-jc, B, g3);
+            });
+  e = Eval{t.ssq, a00, a01, a02, 0.0, a11, a12, 0.0, a22, 0.0, a33, g0, g1, g2, g3};
+}
+
+template <typename QF>
+struct WideEval {
+  const QF& q;
+  int nd;
+  const DfmiTrigK& k;
+  using Trial = WideTrial;
+  DFMI_HDI double trial(const double (&p)[4], Trial& t) { return wide_trial(q, nd, p, t, k); }
+  DFMI_HDI void accept(const double (&p)[4], const Trial& t, Eval& e) { wide_accept(q, nd, p, t, e); }
+  DFMI_HDI void solve(const Eval& e, double lam, double (&dp)[4]) { damped_solve_block(e, lam, dp); }
+  DFMI_HDI static double ssq_of(const Trial& t) { return t.ssq; }
+};
+
 // fit.py:208-258 (_run_lma_fit), nested form (one lane at a time: the host build's
 // check that the flattened descent takes the same path). p in/out; returns ssq0 at
 // the final p.
@@ -1166,7 +1385,10 @@ template <int NDMAX, typename QE, typename QM, int FLAT = 1>
 __host__ __device__ __forceinline__ int fit_segment_q2(const QE& qe, const QM& qm, int ndata,
                                                     const double* __restrict__ jtab, const LMConst& c,
                                                     double (&p)[4], double& ssq_out) {
-  if constexpr (NDMAX > 0) {
+  if constexpr (NDMAX == kWideNd) {  // many harmonics: closed form over the lean Miller walk
+    WideEval<QE> ev{qe, ndata, c.trig};
+    return fit_segment_t<FLAT>(ev, qm, ndata, jtab, c, p, ssq_out);
+  } else if constexpr (NDMAX > 0) {
     SplitEval<NDMAX, QE> ev{qe, ndata, c.trig};
     return fit_segment_t<FLAT>(ev, qm, ndata, jtab, c, p, ssq_out);
   } else if constexpr (FLAT == 2) {  // lambda ladder: full trials (FullGenEval)
@@ -1224,7 +1446,7 @@ struct GuessInline {
 // r05as), so it keeps its allocation.
 template <int NDMAX, bool CHAIN, bool ONEPASS = false>
 constexpr int lm_waves() {
-  return (!CHAIN && (NDMAX == 12 || ONEPASS)) ? 2 : 1;  // ONEPASS: 259 VGPRs unbounded
+  return (!CHAIN && (NDMAX == 12 || ONEPASS || NDMAX == kWideNd)) ? 2 : 1;  // ONEPASS: 259 VGPRs unbounded
 }
 // ONEPASS (general path, chunk size 1, component-major): each lane keeps its Bessel recurrence
 // values in dynamic LDS (64 x (ndata + 2) doubles per wave) and walks once per evaluation
@@ -1336,7 +1558,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(lm_waves<NDM
     auto one = [&](int64_t sidx) {
       double ssq;
       int st;
-      if constexpr (kQReg) {
+      if constexpr (NDMAX == kWideNd) {
+        const QCol qg{qi, (uint32_t)sidx, qi_ld, ndata};
+        st = fit_segment_q<kWideNd, QCol, 1>(qg, ndata, jtab, c, p, ssq);
+      } else if constexpr (kQReg) {
         const QGlobal qg{qi + sidx, qi_ld, ndata};
         QRegs<nd_cap(NDMAX)> qr;
         qr.load(qg);

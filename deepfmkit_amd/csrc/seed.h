@@ -98,9 +98,12 @@ __global__ __launch_bounds__(64) void seed_bins_kernel(const double* __restrict_
                                                        const double* __restrict__ guess, GuessInline ginl,
                                                        int use_inline, const double* __restrict__ jtab, LMConst c,
                                                        double* __restrict__ out, int64_t out_ld, int64_t nbuf,
-                                                       int32_t* __restrict__ status, uint64_t* __restrict__ probe) {
+                                                       int32_t* __restrict__ status, uint64_t* __restrict__ probe,
+                                                       int write_dc) {
   // probe (diagnostics, may be null): s_memrealtime (100 MHz) at entry, after the
-  // fold, after the fit, written by record 0
+  // fold, after the fit, written by record 0. write_dc = 0: the bulk demodulation beside this
+  // kernel writes buffer 0's dc itself (component-major QI + dc), so this kernel leaves it
+  // alone — one writer, the same bits every run
   const uint64_t t_in = __builtin_amdgcn_s_memrealtime();
   extern __shared__ __attribute__((aligned(16))) double sh[];  // basis | bins [L] | row
   const int64_t r = blockIdx.x;
@@ -166,7 +169,7 @@ __global__ __launch_bounds__(64) void seed_bins_kernel(const double* __restrict_
   out[1 * out_ld + sidx] = p[1];
   out[2 * out_ld + sidx] = p[2];
   out[3 * out_ld + sidx] = p[3];
-  out[4 * out_ld + sidx] = q.at(dfmi_row_dc(ndata));
+  if (write_dc) out[4 * out_ld + sidx] = q.at(dfmi_row_dc(ndata));
   out[5 * out_ld + sidx] = ssq;
   status[sidx] = st;
   if (probe && r == 0) {

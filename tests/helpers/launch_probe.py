@@ -20,9 +20,14 @@ def main():
     ranks, backend = bench.rank_topology(dist, torch.device("cpu"), world)
     t = torch.tensor([float(dist.get_rank() + 1)])
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    # what this rank of `bench.py --gpus world` fits (no --segments; config 4 splits 10M evenly)
+    plan = bench.plan_workload(world) if bench.CONFIG4_SEGMENTS % world == 0 else {"workload": None,
+                                                                                   "record_segments": None}
     if dist.get_rank() == 0:
         print(json.dumps({"n_gpus": world, "world": {"size": world, "backend": backend, "ranks": ranks},
-                          "max_over_ranks": float(t.item()), "argv": sys.argv[1:]}), flush=True)
+                          "max_over_ranks": float(t.item()), "argv": sys.argv[1:],
+                          "config": {"workload": plan["workload"], "record_segments": plan["record_segments"]}}),
+              flush=True)
     dist.barrier()
     dist.destroy_process_group()
 

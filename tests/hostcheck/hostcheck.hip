@@ -155,7 +155,10 @@ int hc_fit_segments(const double* qi, long n, int ndata, const double* guess, co
   for (long s = 0; s < n; ++s) {
     double p[4] = {guess[s * 4], guess[s * 4 + 1], guess[s * 4 + 2], guess[s * 4 + 3]};
     double ssq;
-    if (force_general == 2 && ndata <= 12) {  // nested (one-lane) descent: must equal the flattened one
+    if (force_general == 3) {  // the many-harmonic path (lm.h kWideNd), any ndata
+      const dfmi::QCol qc{qi, (uint32_t)s, n, ndata};
+      status_out[s] = dfmi::fit_segment_q<dfmi::kWideNd, dfmi::QCol>(qc, ndata, tab.data(), c, p, ssq);
+    } else if (force_general == 2 && ndata <= 12) {  // nested (one-lane) descent: must equal the flattened one
       const dfmi::QGlobal qg{qi + s, n, ndata};
       status_out[s] = dfmi::fit_segment_q<12, dfmi::QGlobal, false>(qg, ndata, tab.data(), c, p, ssq);
     } else if (force_general)

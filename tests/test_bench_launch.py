@@ -31,6 +31,22 @@ def test_self_launch_gathers_every_rank(capfd, n):
     assert line["argv"] == ["--gpus", str(n)]
 
 
+def test_scaling_anchor_names_rank0_workload_at_8(capfd):
+    """The N = 1 line's scaling_anchor (bench.scaling_anchor) fits config 4's shard of rank 0 at
+    N = 8: eight gloo ranks launched like `bench.py --gpus 8`, rank 0's workload string equals
+    the anchor's, and it is the 10M-segment record's 1/8."""
+    import bench
+    rc = bench.self_launch(8, ["--gpus", "8"], script=os.path.join(ROOT, "tests", "helpers", "launch_probe.py"),
+                           timeout=180)
+    assert rc == 0
+    lines = [json.loads(v) for v in capfd.readouterr().out.strip().splitlines() if v.startswith("{")]
+    assert len(lines) == 1 and lines[0]["n_gpus"] == 8
+    anchor = bench.plan_workload(bench.ANCHOR_WORLD)
+    assert lines[0]["config"]["workload"] == anchor["workload"]
+    assert anchor["nseg"] * 8 == lines[0]["config"]["record_segments"] == bench.CONFIG4_SEGMENTS
+    assert bench.plan_workload(1)["workload"].startswith("config2: 100000 segments/GPU")
+
+
 def test_self_launch_failing_rank_fails_the_job():
     import bench
     rc = bench.self_launch(2, [], script=os.path.join(ROOT, "tests", "helpers", "no_such_script.py"), timeout=60)

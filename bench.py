@@ -569,6 +569,7 @@ def extra_configs(torch, dev, lib, _lib, stream, cfg, cpu_leg):
                                                             "(gcc -O2, libm), the numpy loop's operation order"}
             c5["max_abs_dstate_gpu_vs_cpu"] = float(np.max(np.abs(s1 - cst)))
     out["config5"] = c5
+    out["config5_handover"] = ekf_handover_point(torch, dev, lib, _lib, stream)
     # ---- config 1 through the sequential path (one warm-start chain, fitters.py:370-393)
     nb1 = 500
     x1r = torch.empty(nb1 * R, dtype=torch.float64, device=dev)
@@ -659,6 +660,77 @@ def extra_configs(torch, dev, lib, _lib, stream, cfg, cpu_leg):
     del x, o4, k4
     torch.cuda.empty_cache()
     return out
+
+
+def ekf_handover_point(torch, dev, lib, _lib, stream, ns=400_000, nch=1024, n_bad=64):
+    """The EKF parallel in time's hand-over (dfmi_capi.hip ekf_pit_run, round 6): channels whose
+    iteration does not lock (here m = 20 records fitted from init_m = 6: the filter never
+    locks, moves O(1) every pass) are re-run by the sequential kernel, launched at the host
+    check that first sees them on a stream of their own while the other channels keep passing.
+    One such channel alone: its time against the sequential kernel's alone (the passes before
+    the hand-over are the overhead). A batch of nch config-5 channels with n_bad of those among
+    them: its time against the passes alone (the same batch with the re-run switched off,
+    ekf_pit_seq 0: diagnostics) and the n_bad channels' sequential run alone."""
+    from deepfmkit_amd.physics import SnrSpec, synth_snr
+    R = int(F_SAMP / F_MOD * N_CYC)
+    nb5 = ns // R
+    init4 = torch.tensor([1.6, 6.0, 0.0, 0.0], dtype=torch.float64, device=dev)
+    p0d = torch.ones(5, dtype=torch.float64, device=dev)
+    qdd = torch.tensor([1e-8, 1e-8, 1e-6, 1e-6, 1e-8], dtype=torch.float64, device=dev)
+
+    def records(ms):
+        xe = torch.empty(len(ms) * ns, dtype=torch.float64, device=dev)
+        for c, m in enumerate(ms):
+            synth_snr(SnrSpec(seed=SEED, stream=300 + c, f_samp=F_SAMP, f_mod=F_MOD, m=m, snr_db=SNR_DB), 0, ns,
+                      out=xe[c * ns:(c + 1) * ns])
+        return xe
+
+    def run(xe, n, tune=None, reps=3):
+        stt = torch.empty((n, nb5, 5), dtype=torch.float64, device=dev)
+        for k, v in (tune or {}).items():
+            _lib.check(lib.dfmi_set_tuning(k.encode(), v), "tune")
+
+        def ekf():
+            _lib.check(lib.dfmi_ekf_fit(xe.data_ptr(), n, ns, ns, init4.data_ptr(), p0d.data_ptr(), qdd.data_ptr(),
+                                        None, 2 * np.pi * F_MOD, F_SAMP, R, nb5, stt.data_ptr(), _lib.DFMI_MEM_DEVICE,
+                                        stream.cuda_stream), "dfmi_ekf_fit")
+        try:
+            t = _timed_steps(torch, ekf, reps, 1)
+            kname = lib.dfmi_last_demod_kernel().decode()
+            passes = (ctypes.c_int32 * n)()
+            _lib.check(lib.dfmi_ekf_pit_passes(ctypes.cast(passes, ctypes.c_void_p), n), "passes")
+        finally:
+            for k in (tune or {}):
+                _lib.check(lib.dfmi_set_tuning(k.encode(), {"ekf_pit": 1024, "ekf_pit_seq": 1}[k]), "tune")
+        return t, kname, np.array(list(passes)), stt
+    bad = records([20.0])
+    t1, k1, p1, s1 = run(bad, 1)
+    ts1, ks1, _, q1 = run(bad, 1, {"ekf_pit": 0})
+    one = {"channels": 1, "record": "m = 20 fitted from init_m = 6 (never locks)", "ms": round(t1 * 1e3, 3),
+           "passes": int(p1[0]), "kernel": k1, "sequential_alone_ms": round(ts1 * 1e3, 3),
+           "overhead_ms": round((t1 - ts1) * 1e3, 3),
+           "bit_identical_to_sequential": bool(torch.equal(s1, q1))}
+    del bad, s1, q1
+    ms = [M_TRUE] * nch
+    for i in range(n_bad):  # spread over the batch
+        ms[(i * nch) // n_bad + 3] = 20.0
+    xe = records(ms)
+    tb, kb, pb, sb = run(xe, nch, reps=2)
+    tp, _, _, _ = run(xe, nch, {"ekf_pit_seq": 0}, reps=2)
+    idx = [i for i, m in enumerate(ms) if m != M_TRUE]
+    xs = torch.stack([xe[i * ns:(i + 1) * ns] for i in idx]).reshape(-1).contiguous()
+    del xe
+    tsq, ksq, _, ss = run(xs, n_bad, {"ekf_pit": 0}, reps=2)
+    handed = int(np.sum(pb < 0))
+    batch = {"channels": nch, "samples_per_channel": ns, "non_locking": n_bad, "handed_over": handed,
+             "ms": round(tb * 1e3, 3), "kernel": kb, "passes_alone_ms": round(tp * 1e3, 3),
+             "sequential_alone_ms": round(tsq * 1e3, 3), "sequential_kernel": ksq,
+             "ratio_to_max_of_parts": round(tb / max(tp, tsq), 4),
+             "handed_states_bit_identical_to_sequential": bool(torch.equal(sb[idx], ss))}
+    del sb, ss, xs
+    torch.cuda.empty_cache()
+    return {"workload": f"EKFFitter.fit hand-over: {ns} samples per channel, m = 20 channels from init_m = 6",
+            "one_channel": one, "batch": batch}
 
 
 def scaling_anchor(torch, dev, lib, _lib, stream, cfg, steps, warmup):

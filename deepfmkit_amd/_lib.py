@@ -108,6 +108,35 @@ def _torch_hip_runtime():
     return p if os.path.exists(p) else None
 
 
+def _elf_dynamic_strings(path, tag):
+    """The DT_SONAME (tag 14) or DT_NEEDED (tag 1) strings of a 64-bit little-endian ELF
+    shared object, read from its section headers (no tool, no import); [] if unreadable."""
+    import struct
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return []
+    if data[:4] != b"\x7fELF" or data[4] != 2 or data[5] != 1:
+        return []
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum = struct.unpack_from("<HH", data, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", data, shoff + i * shentsize) for i in range(shnum)]
+    out = []
+    for sec in secs:
+        if sec[1] != 6:  # SHT_DYNAMIC
+            continue
+        strtab = secs[sec[6]]  # sh_link: its string table
+        for off in range(sec[4], sec[4] + sec[5], 16):
+            d_tag, d_val = struct.unpack_from("<qQ", data, off)
+            if d_tag == 0:
+                break
+            if d_tag == tag:
+                s = strtab[4] + d_val
+                out.append(data[s:data.index(b"\0", s)].decode())
+    return out
+
+
 def _bind_runtime():
     """Pick the HIP runtime libdfmi.so binds to, before loading it.
 
@@ -133,6 +162,16 @@ def _bind_runtime():
         return RUNTIME
     p = _torch_hip_runtime()
     if p is None:
+        return None
+    # preload torch's runtime only when it is the one libdfmi.so asks for: its soname must be
+    # libdfmi.so's DT_NEEDED HIP runtime (a torch built against another ROCm major ships another
+    # soname; preloading it would map a second runtime, the failure this avoids)
+    need = [n for n in _elf_dynamic_strings(LIB_PATH, 1) if n.startswith("libamdhip64")]
+    have = _elf_dynamic_strings(p, 14)
+    if not need or not have or have[0] not in need:
+        import warnings
+        warnings.warn(f"deepfmkit_amd: torch's HIP runtime {p} (soname {have}) is not the one libdfmi.so needs "
+                      f"({need}); using the system runtime — import torch only if it binds the same one")
         return None
     try:
         ctypes.CDLL(p)

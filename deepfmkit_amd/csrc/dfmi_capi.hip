@@ -59,6 +59,12 @@ struct Tuning {
                              // kernel, and the record pipeline leaves the row layout for it
   int lm_wide = 1;              // ndata > 16: the many-harmonic LM path (lm.h kWideNd: closed-form sums over a
                                 // lean Miller walk); 0 = the literal general path (lm_general = 1 forces it too)
+  int lm_wide_lds = 20;         // many-harmonic LM: QI staged in LDS per lane up to this ndata (0: never): while 8
+                                // waves per CU still fit (20 KB per wave); ndata 20 0.076 vs 0.088 ms per 100k
+                                // segments, but 30 / 40 0.151 / 0.179 vs 0.118 / 0.149 at 5 / 3 waves per CU (r06g)
+  int lm_split = 0;             // many-harmonic LM with this many lanes per segment (2 / 4; 0 = one lane): measured
+  int lm_split_from = 41;       // slower everywhere (ndata 30 / 62: 0.195 / 0.432 ms at 2 lanes, 0.260 / 0.420 at 4,
+                                // against 0.118 / 0.215 for one lane; r06g), kept for A/B
   int lm_onepass = 1;           // LM general path: one Bessel walk per evaluation with the values in LDS
                                 // (1: where 7 waves per CU still fit, 2: always, 0: never)
   int demod_wide_rmax = 2000;  // segments shorter than this go through demod_wide_kernel too
@@ -89,6 +95,7 @@ struct Tuning {
                               // (then every ekf_pit_every); config 5's record converges in 5
   int ekf_pit_every = 2;
   int ekf_pit_tol = 13;       // stop rule: distance from the fixed point bounded by 10^-ekf_pit_tol (pit_decide)
+  int ekf_pit_slow_from = 16; // pass from which "too slow to meet the bound within the cap" counts (pit_decide)
   int ekf_pit_stall = 3;      // passes in a row not contracting fast enough to meet the bound within the cap
                               // before the sequential kernel (pit_decide)
   int ekf_pit_trace = 0;      // 1: record every pass's move per channel (dfmi_ekf_pit_trace)
@@ -798,15 +805,20 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
                         int64_t, int64_t, dfmi::GuessInline, int, const double*, dfmi::LMConst, double*, int64_t,
                         int32_t*);
     LK lk;
+    // beyond 16 harmonics the many-harmonic evaluation as in the one-lane kernels (same bits as
+    // lm_chunks_kernel<kWideNd>: the ladder only tries the rungs in parallel)
+    const bool wide = nd_sel > 16 && nd_sel < 1000 && t_tune.lm_wide;
     if (rows)
       lk = nd_sel == 10 ? dfmi::lm_ladder_kernel<kNd10, false, true> : nd_sel <= 12 ? dfmi::lm_ladder_kernel<12, false, true>
            : nd_sel <= 16 ? dfmi::lm_ladder_kernel<16, false, true> : dfmi::lm_ladder_kernel<0, false, true>;
     else if (chain)
       lk = nd_sel == 10 ? dfmi::lm_ladder_kernel<kNd10, true, false> : nd_sel <= 12 ? dfmi::lm_ladder_kernel<12, true, false>
-           : nd_sel <= 16 ? dfmi::lm_ladder_kernel<16, true, false> : dfmi::lm_ladder_kernel<0, true, false>;
+           : nd_sel <= 16 ? dfmi::lm_ladder_kernel<16, true, false>
+           : wide ? dfmi::lm_ladder_kernel<dfmi::kWideNd, true, false> : dfmi::lm_ladder_kernel<0, true, false>;
     else
       lk = nd_sel == 10 ? dfmi::lm_ladder_kernel<kNd10, false, false> : nd_sel <= 12 ? dfmi::lm_ladder_kernel<12, false, false>
-           : nd_sel <= 16 ? dfmi::lm_ladder_kernel<16, false, false> : dfmi::lm_ladder_kernel<0, false, false>;
+           : nd_sel <= 16 ? dfmi::lm_ladder_kernel<16, false, false>
+           : wide ? dfmi::lm_ladder_kernel<dfmi::kWideNd, false, false> : dfmi::lm_ladder_kernel<0, false, false>;
     const int64_t lgrid = (lanes * dfmi::kLadderLanes + block - 1) / block;
     hipLaunchKernelGGL(lk, dim3((unsigned)lgrid), dim3(block), 0, st, qi, qi_ld, ndata, nrec, nbuf, first, nitems,
                        nchunk, guess_dev, g_rec, g_comp, ginl, use_inline, jtab, c, out, out_ld, status);
@@ -820,6 +832,26 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
   // the general path's one-pass Bessel walk: the lane's recurrence values in LDS, while 7
   // waves per CU still fit (ndata + 2 <= 45): ndata 40 0.276 -> 0.264 ms per 100k; at 62 (5
   // waves per CU) 0.384 -> 0.663, r05ax
+  // many harmonics, P lanes per segment (lm.h lm_split_kernel: QI in a per-wave LDS tile of
+  // 64 / P segments) from "lm_split_from" harmonics on ("lm_split" = P, 0 = never)
+  const int sp = t_tune.lm_split;
+  if (!chain && !rows && nd_sel > 16 && nd_sel < 1000 && t_tune.lm_wide && sp > 1 && ndata >= t_tune.lm_split_from &&
+      (size_t)2 * ndata * (64 / sp) * sizeof(double) <= t_ds->lds_per_block) {
+    const size_t slds = (size_t)2 * ndata * (64 / sp) * sizeof(double);
+    const int64_t sgrid = (nrec * nitems + 64 / sp - 1) / (64 / sp);
+    auto sk = sp == 4 ? dfmi::lm_split_kernel<4> : dfmi::lm_split_kernel<2>;
+    hipLaunchKernelGGL(sk, dim3((unsigned)sgrid), dim3(64), slds, st, qi, qi_ld, ndata, nrec, nbuf, first, nitems,
+                       guess_dev, g_rec, g_comp, ginl, use_inline, jtab, c, out, out_ld, status);
+    HIPCHK(hipGetLastError());
+    return DFMI_OK;
+  }
+  // many harmonics with QI staged in LDS per lane (lm.h QLds) while 2 ndata x 64 x 8 B per wave
+  // leaves 8 waves per CU ("lm_wide_lds": the largest ndata staged, default 20 = 20 KB)
+  if (!chain && !rows && nd_sel > 16 && nd_sel < 1000 && t_tune.lm_wide && ndata <= t_tune.lm_wide_lds &&
+      (size_t)2 * ndata * 64 * sizeof(double) <= t_ds->lds_per_block) {
+    kern = dfmi::lm_chunks_kernel<dfmi::kWideNd, false, false, true>;
+    lds = (size_t)2 * ndata * 64 * sizeof(double);
+  }
   if (!chain && !rows && nd_sel > 16 && !(t_tune.lm_wide && nd_sel < 1000) && t_tune.lm_onepass &&
       (t_tune.lm_onepass == 2 || (size_t)64 * (ndata + 2) * 8 * 7 <= t_ds->lds_per_block)) {
     kern = dfmi::lm_chunks_kernel<0, false, false, false, true>;
@@ -1055,6 +1087,9 @@ const std::map<std::string, Knob>& knobs() {
       {"demod_wide_rmax", {&Tuning::demod_wide_rmax, {}}},
       {"lm_onepass", {&Tuning::lm_onepass, {0, 1, 2}}},
       {"lm_wide", {&Tuning::lm_wide, {0, 1}}},
+      {"lm_wide_lds", {&Tuning::lm_wide_lds, {}}},
+      {"lm_split", {&Tuning::lm_split, {0, 2, 4}}},
+      {"lm_split_from", {&Tuning::lm_split_from, {}}},
       {"demod_wide_half", {&Tuning::demod_wide_half, {0, 1}}},
       {"demod_wide_dbg", {&Tuning::demod_wide_dbg, {0, 1, 2, 3, 4, 5, 6, 7}}},
       {"ekf_row", {&Tuning::ekf_row, {}}},
@@ -1070,6 +1105,7 @@ const std::map<std::string, Knob>& knobs() {
       {"ekf_pit_every", {&Tuning::ekf_pit_every, {}}},
       {"ekf_pit_tol", {&Tuning::ekf_pit_tol, {}}},
       {"ekf_pit_stall", {&Tuning::ekf_pit_stall, {}}},
+      {"ekf_pit_slow_from", {&Tuning::ekf_pit_slow_from, {}}},
       {"ekf_pit_trace", {&Tuning::ekf_pit_trace, {0, 1}}},
       {"ekf_pit_seq", {&Tuning::ekf_pit_seq, {0, 1}}},
       {"ekf_pit_measure", {&Tuning::ekf_pit_measure, {0, 1}}},
@@ -1214,6 +1250,7 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
   rule.noise = rule.tol;
   rule.stall_max = std::max(t_tune.ekf_pit_stall, 1);
   rule.cap = cap;
+  rule.slow_from = t_tune.ekf_pit_slow_from;
   rule.hist_n = hist_n;
   rule.measure = t_tune.ekf_pit_measure;
   if (hist_n) HIPCHK(hipMemsetAsync(hist, 0xFF, (size_t)nrec * hist_n * 8, st));  // NaN: pass not run

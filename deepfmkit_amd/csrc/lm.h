@@ -917,21 +917,47 @@ struct QCol {
   DFMI_HDI double qs(int h) const { return (base + (int64_t)(nd + h) * ld)[off]; }
 };
 
+// The lane's own QI staged in LDS by lm_chunks_kernel (column c of the lane at p[c * 64]): every
+// evaluation of a fit reads each value again, and from L2 / the MALL the wave waited on those
+// loads for half its lifetime (profiles/r06/lm_general_pmc_after.txt).
+struct QLds {
+  static constexpr int kPre = 0;
+  const double* p;
+  int nd;
+  DFMI_HDI double qc(int h) const { return p[h * 64]; }
+  DFMI_HDI double qs(int h) const { return p[(nd + h) * 64]; }
+};
+
 // Harmonics j = nd .. 1 in descending order: body(j, J_{j-1}, J_j, J_{j+1}, cos j psi, sin j psi,
 // Q_j, I_j). (c1, s1) = (cos, sin) psi, (cn, sn) = (cos, sin)(nd psi).
 template <typename QF, typename Body>
 DFMI_HDI void wide_walk(const QF& q, int nd, double m, double psi, double c1, double s1, double cn, double sn,
                         Body&& body) {
   const int M = dfmi_bessel_start(nd + 1, m);
+  const double tox = 2.0 / m;
   const bool fast = m > 0.0 && m >= DFMI_BES_TINY && m < 1.0e5 && !dfmi_bessel_use_large(m, nd + 1) &&
-                    (float)M * log2f((float)(2.0 * M / m + 1.0)) < (float)(DFMI_BES_BIG_EXP - 10);
+                    (float)M * log2f((float)fma((double)M, tox, 1.0)) < (float)(DFMI_BES_BIG_EXP - 10);
   if (!fast) {
     harmonic_walk(nd, m, psi, [&](int j, double jm1, double j0, double jp1, double cj, double sj) {
       body(j, jm1, j0, jp1, cj, sj, q.qc(j - 1), q.qs(j - 1));
     });
     return;
   }
-  const double tox = 2.0 / m;
+  // the QI of the first two blocks of four, issued before the Miller passes (which need none)
+  // so that their latency hides behind them; each later block is loaded two blocks (8
+  // harmonics) ahead of its use. (Four blocks ahead, 64 more VGPRs, took the kernel past 256
+  // VGPRs into scratch: 0.29 ms at ndata 62 against 0.22, r06e.)
+  const int top = nd & 3, nb = nd >> 2;
+  double bq[2][4], bs[2][4];  // ring of two blocks: slot i holds block nb - i
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int blk = nb - i;
+      const int h = blk >= 1 ? 4 * blk - 1 - u : 0;
+      bq[i][u] = q.qc(h);
+      bs[i][u] = q.qs(h);
+    }
   // pass 1: S = f_0 + 2 sum f_2k (M even; dfmi_bessel_norm without its rescale test)
   double fp1 = 0.0, f = 1.0, S = 2.0;
   double kd = (double)M;
@@ -989,32 +1015,29 @@ DFMI_HDI void wide_walk(const QF& q, int nd, double m, double psi, double c1, do
     cj = c2;
     sj = s2;
   };
-  int j = nd;
-  for (; (j & 3) != 0; --j) one(j, q.qc(j - 1), q.qs(j - 1));
-  // blocks of four from a multiple of four: j & 3 is known at compile time in each body
-  const int nb = j >> 2;
-  if (nb > 0) {
-    double bq[4], bs[4];
+  for (int u = 0; u < top; ++u) one(nd - u, q.qc(nd - 1 - u), q.qs(nd - 1 - u));
+  // blocks of four from a multiple of four (j = 4 blk - u: j & 3 known at compile time), each
+  // block's QI loaded two blocks (8 harmonics) ahead of its use
+  auto block = [&](int slot, int blk) {
+    double cq[4], cs[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      bq[u] = q.qc(4 * nb - 1 - u);
-      bs[u] = q.qs(4 * nb - 1 - u);
+      cq[u] = bq[slot][u];
+      cs[u] = bs[slot][u];
+      const int h = blk - 2 >= 1 ? 4 * (blk - 2) - 1 - u : 0;  // two blocks ahead (clamped)
+      bq[slot][u] = q.qc(h);
+      bs[slot][u] = q.qs(h);
     }
-    for (int b = nb; b >= 1; --b) {
-      const int jb = b << 2;
-      double cq[4], cs[4];
+    const int jb = blk << 2;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        cq[u] = bq[u];
-        cs[u] = bs[u];
-        const int h = b > 1 ? jb - 5 - u : 0;  // the next block's QI (clamped on the last)
-        bq[u] = q.qc(h);
-        bs[u] = q.qs(h);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) one(jb - u, cq[u], cs[u]);
-    }
+    for (int u = 0; u < 4; ++u) one(jb - u, cq[u], cs[u]);
+  };
+  int b = nb;
+  for (; b >= 2; b -= 2) {
+    block(0, b);
+    block(1, b - 1);
   }
+  if (b == 1) block(0, 1);
 }
 
 struct WideTrial {
@@ -1066,16 +1089,16 @@ DFMI_HDI void wide_accept(const QF& q, int nd, const double (&p)[4], const WideT
               const double ri = fma(c, sj, I);
               const double A = fma(cj, rq, -(sj * ri));
               const double B = fma(sj, rq, cj * ri);
-              const double w = fma(cj, cj, sj * sj);
-              const double v0 = u0 * w, v1 = u1 * w, v2 = u2 * w;
-              a00 = fma(v0, u0, a00);
-              a01 = fma(v0, u1, a01);
-              a02 = fma(v0, u2, a02);
-              a11 = fma(v1, u1, a11);
-              a12 = fma(v1, u2, a12);
-              a22 = fma(v2, u2, a22);
+              // cos^2 + sin^2 of the rotation taken as 1 (it is to ~1e-14 after 62 rotations):
+              // J^T J moves by that much relative, the step direction with it, ssq not at all
+              a00 = fma(u0, u0, a00);
+              a01 = fma(u0, u1, a01);
+              a02 = fma(u0, u2, a02);
+              a11 = fma(u1, u1, a11);
+              a12 = fma(u1, u2, a12);
+              a22 = fma(u2, u2, a22);
               const double jc = (double)j * c;
-              a33 = fma(jc * w, jc, a33);
+              a33 = fma(jc, jc, a33);
               g0 = fma(u0, A, g0);
               g1 = fma(u1, A, g1);
               g2 = fma(u2, A, g2);
@@ -1094,6 +1117,192 @@ struct WideEval {
   DFMI_HDI void accept(const double (&p)[4], const Trial& t, Eval& e) { wide_accept(q, nd, p, t, e); }
   DFMI_HDI void solve(const Eval& e, double lam, double (&dp)[4]) { damped_solve_block(e, lam, dp); }
   DFMI_HDI static double ssq_of(const Trial& t) { return t.ssq; }
+};
+
+// ---------------------------------------------------------------------------
+// Many harmonics, P lanes per segment (lm_split_kernel). A wave fits 64 / P segments; lane r
+// of a segment's group walks a contiguous share of the harmonics (r = 0 the top nd / P), its
+// own Miller recurrence down to that share (pass 1 in full on every lane) and rotation start
+// (cos, sin)(hi psi); the harmonic sums are partial per lane and reduced over the group by an
+// xor butterfly within the quad (DPP): every lane of the group ends with the same bits, so the
+// group takes the LM's decisions together (one control flow per segment). QI are staged in
+// LDS by the kernel: 64 / P segments x 2 ndata doubles per wave (31 KB at ndata 62, P = 2).
+// ---------------------------------------------------------------------------
+template <int S>
+struct QLdsG {  // QI of one segment in a wave's LDS tile [component][S segments]
+  static constexpr int kPre = 0;
+  const double* p;
+  int nd;
+  DFMI_HDI double qc(int h) const { return p[h * S]; }
+  DFMI_HDI double qs(int h) const { return p[(nd + h) * S]; }
+};
+
+// sum of v over the P lanes of a group (P = 1, 2, 4: lanes r = lane % P), the same bits on
+// every lane of the group (each butterfly level adds two commuted operands)
+template <int P>
+__device__ __forceinline__ double group_sum(double v) {
+  if constexpr (P >= 2) {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = (int)b, hi = (int)(b >> 32);
+    const int lo1 = __builtin_amdgcn_update_dpp(0, lo, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    const int hi1 = __builtin_amdgcn_update_dpp(0, hi, 0xB1, 0xF, 0xF, false);
+    v += __builtin_bit_cast(double, ((long long)hi1 << 32) | (unsigned)lo1);
+  }
+  if constexpr (P >= 4) {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = (int)b, hi = (int)(b >> 32);
+    const int lo2 = __builtin_amdgcn_update_dpp(0, lo, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    const int hi2 = __builtin_amdgcn_update_dpp(0, hi, 0x4E, 0xF, 0xF, false);
+    v += __builtin_bit_cast(double, ((long long)hi2 << 32) | (unsigned)lo2);
+  }
+  static_assert(P == 1 || P == 2 || P == 4, "P");
+  return v;
+}
+
+// wide_walk over lane r's share of the harmonics: j = hi .. lo with hi = nd - r ceil(nd / P).
+template <int P, typename QF, typename Body>
+__device__ __forceinline__ void wide_walk_part(const QF& q, int nd, double m, double psi, double c1, double s1,
+                                               const DfmiTrigK& tk, int r, Body&& body) {
+  const int len = (nd + P - 1) / P;
+  const int hi = nd - r * len;
+  const int lo = hi - len + 1 > 1 ? hi - len + 1 : 1;
+  const int M = dfmi_bessel_start(nd + 1, m);
+  const double tox = 2.0 / m;
+  const bool fast = m > 0.0 && m >= DFMI_BES_TINY && m < 1.0e5 && !dfmi_bessel_use_large(m, nd + 1) &&
+                    (float)M * log2f((float)fma((double)M, tox, 1.0)) < (float)(DFMI_BES_BIG_EXP - 10);
+  if (!fast) {  // the checked walk of every harmonic, this lane's share accumulated
+    harmonic_walk(nd, m, psi, [&](int j, double jm1, double j0, double jp1, double cj, double sj) {
+      if (j <= hi && j >= lo) body(j, jm1, j0, jp1, cj, sj, q.qc(j - 1), q.qs(j - 1));
+    });
+    return;
+  }
+  if (hi < 1) return;  // no share (nd < P)
+  double sn, cn;
+  dfmi_sincos_auto((double)hi * psi, tk, &sn, &cn);
+  double nq = q.qc(hi - 1), ni = q.qs(hi - 1);
+  // pass 1 (as wide_walk)
+  double fp1 = 0.0, f = 1.0, S = 2.0;
+  double kd = (double)M;
+  for (int k = M; k > 2; k -= 2) {
+    double fm1 = fma(kd * tox, f, -fp1);
+    fp1 = f;
+    f = fm1;
+    kd -= 1.0;
+    fm1 = fma(kd * tox, f, -fp1);
+    fp1 = f;
+    f = fm1;
+    kd -= 1.0;
+    S += 2.0 * f;
+  }
+  {
+    double fm1 = fma(kd * tox, f, -fp1);
+    fp1 = f;
+    f = fm1;
+    kd -= 1.0;
+    fm1 = fma(kd * tox, f, -fp1);
+    S += fm1;
+  }
+  const double invS = 1.0 / S;
+  // pass 2 down to this lane's share (a per-lane trip count)
+  fp1 = 0.0;
+  f = 1.0;
+  kd = (double)M;
+  for (int k = M; k > hi + 1; --k) {
+    const double fm1 = fma(kd * tox, f, -fp1);
+    fp1 = f;
+    f = fm1;
+    kd -= 1.0;
+  }
+  double Jp1 = f * invS;
+  {
+    const double fm1 = fma(kd * tox, f, -fp1);  // f_hi
+    fp1 = f;
+    f = fm1;
+    kd -= 1.0;
+  }
+  double J0 = f * invS;
+  double cj = cn, sj = sn;
+  for (int j = hi; j >= lo; --j) {
+    const double Q = nq, I = ni;
+    const int h = j > lo ? j - 2 : j - 1;  // the next harmonic's QI (LDS)
+    nq = q.qc(h);
+    ni = q.qs(h);
+    const double fm1 = fma(kd * tox, f, -fp1);  // f_{j-1}
+    fp1 = f;
+    f = fm1;
+    kd -= 1.0;
+    const double Jm1 = fm1 * invS;
+    body(j, Jm1, J0, Jp1, cj, sj, Q, I);
+    Jp1 = J0;
+    J0 = Jm1;
+    const double c2 = fma(cj, c1, sj * s1);
+    const double s2 = fma(sj, c1, -(cj * s1));
+    cj = c2;
+    sj = s2;
+  }
+}
+
+template <int P, typename QF>
+struct PartEval {
+  const QF& q;
+  int nd;
+  const DfmiTrigK& k;
+  int r;  // this lane's place in its segment's group
+  using Trial = WideTrial;
+  __device__ __forceinline__ double trial(const double (&p)[4], Trial& t) {
+    dfmi_sincos_auto(p[2], k, &t.sph, &t.cph);
+    dfmi_sincos_auto(p[3], k, &t.s1, &t.c1);
+    const double ac = p[0] * t.cph, as = p[0] * t.sph;
+    double so = 0.0, se = 0.0;
+    wide_walk_part<P>(q, nd, p[1], p[3], t.c1, t.s1, k, r,
+                      [&](int j, double, double J0, double, double cj, double sj, double Q, double I) {
+                        const double c = quarter_turn(j, ac, as) * J0;
+                        const double rq = fma(-c, cj, Q);
+                        const double ri = fma(c, sj, I);
+                        so = fma(rq, rq, so);
+                        se = fma(ri, ri, se);
+                      });
+    t.ssq = group_sum<P>(so + se);
+    return t.ssq;
+  }
+  __device__ __forceinline__ void accept(const double (&p)[4], const Trial& t, Eval& e) {
+    const double a = p[0];
+    const double ac = a * t.cph, as = a * t.sph;
+    const double cph0 = (a != 0.0) ? t.cph : 0.0, sph0 = (a != 0.0) ? t.sph : 0.0;
+    double a00 = 0.0, a01 = 0.0, a02 = 0.0, a11 = 0.0, a12 = 0.0, a22 = 0.0, a33 = 0.0;
+    double g0 = 0.0, g1 = 0.0, g2 = 0.0, g3 = 0.0;
+    wide_walk_part<P>(q, nd, p[1], p[3], t.c1, t.s1, k, r,
+                      [&](int j, double Jm1, double Jj, double Jp1, double cj, double sj, double Q, double I) {
+                        const double aP = quarter_turn(j, ac, as), aD = quarter_turn(j + 1, ac, as);
+                        const double c = aP * Jj;
+                        const double u0 = quarter_turn(j, cph0, sph0) * Jj;
+                        const double u1 = aP * (0.5 * (Jm1 - Jp1));
+                        const double u2 = aD * Jj;
+                        const double rq = fma(-c, cj, Q);
+                        const double ri = fma(c, sj, I);
+                        const double A = fma(cj, rq, -(sj * ri));
+                        const double B = fma(sj, rq, cj * ri);
+                        const double w = fma(cj, cj, sj * sj);
+                        const double v0 = u0 * w, v1 = u1 * w, v2 = u2 * w;
+                        a00 = fma(v0, u0, a00);
+                        a01 = fma(v0, u1, a01);
+                        a02 = fma(v0, u2, a02);
+                        a11 = fma(v1, u1, a11);
+                        a12 = fma(v1, u2, a12);
+                        a22 = fma(v2, u2, a22);
+                        const double jc = (double)j * c;
+                        a33 = fma(jc * w, jc, a33);
+                        g0 = fma(u0, A, g0);
+                        g1 = fma(u1, A, g1);
+                        g2 = fma(u2, A, g2);
+                        g3 = fma(-jc, B, g3);
+                      });
+    e = Eval{t.ssq, group_sum<P>(a00), group_sum<P>(a01), group_sum<P>(a02), 0.0, group_sum<P>(a11),
+             group_sum<P>(a12), 0.0, group_sum<P>(a22), 0.0, group_sum<P>(a33), group_sum<P>(g0), group_sum<P>(g1),
+             group_sum<P>(g2), group_sum<P>(g3)};
+  }
+  __device__ __forceinline__ void solve(const Eval& e, double lam, double (&dp)[4]) { damped_solve_block(e, lam, dp); }
+  __device__ __forceinline__ static double ssq_of(const Trial& t) { return t.ssq; }
 };
 
 // fit.py:208-258 (_run_lma_fit), nested form (one lane at a time: the host build's
@@ -1558,7 +1767,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(lm_waves<NDM
     auto one = [&](int64_t sidx) {
       double ssq;
       int st;
-      if constexpr (NDMAX == kWideNd) {
+      if constexpr (NDMAX == kWideNd && QREG && !CHAIN) {
+        // the lane's 2 ndata QI into its own LDS column (no other lane reads it: no barrier),
+        // 16 loads in flight
+        double* col = lds_q + threadIdx.x;
+        const double* __restrict__ src = qi + sidx;
+        const int nc = 2 * ndata;
+        for (int c0 = 0; c0 < nc; c0 += 16) {
+          double v[16];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) v[u] = c0 + u < nc ? src[(int64_t)(c0 + u) * qi_ld] : 0.0;
+#pragma unroll
+          for (int u = 0; u < 16; ++u)
+            if (c0 + u < nc) col[(c0 + u) * 64] = v[u];
+        }
+        const QLds ql{col, ndata};
+        st = fit_segment_q<kWideNd, QLds, 1>(ql, ndata, jtab, c, p, ssq);
+      } else if constexpr (NDMAX == kWideNd) {
         const QCol qg{qi, (uint32_t)sidx, qi_ld, ndata};
         st = fit_segment_q<kWideNd, QCol, 1>(qg, ndata, jtab, c, p, ssq);
       } else if constexpr (kQReg) {
@@ -1580,6 +1805,64 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(lm_waves<NDM
       for (int64_t t = 0; t < len; ++t) one(s0 + t);  // warm-start chain (sequential / n_cores)
     }
   }
+}
+
+// Many harmonics with P lanes per segment (PartEval): chunk size 1 (every segment its own
+// chunk, seeded by its record's guess), component-major QI staged into a per-wave LDS tile
+// [2 ndata][64 / P] (dynamic LDS), lane r = threadIdx.x % P of each group writing nothing but
+// its share of the sums, lane 0 the results. Items and guesses as lm_chunks_kernel.
+template <int P>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void lm_split_kernel(
+    const double* __restrict__ qi, int64_t qi_ld, int ndata, int64_t nrec, int64_t nbuf, int64_t first,
+    int64_t nitems, const double* __restrict__ guess, int64_t g_rec, int64_t g_comp, GuessInline ginl, int use_inline,
+    const double* __restrict__ jtab, LMConst c, double* __restrict__ out, int64_t out_ld, int32_t* __restrict__ status) {
+  extern __shared__ double lds_q[];
+  constexpr int G = 64 / P;  // segments per wave
+  const int lane = threadIdx.x, gi = lane / P, r = lane % P;
+  const int64_t id = (int64_t)blockIdx.x * G + gi;
+  const bool valid = id < nrec * nitems;
+  const int64_t idc = valid ? id : 0;
+  const int64_t rec = idc / nitems;
+  const int64_t sidx = rec * nbuf + first + (idc - rec * nitems);
+  double* col = lds_q + gi;
+  const int nc = 2 * ndata;
+  if (valid) {  // the group's P lanes load the segment's components r, r + P, ... (8 in flight)
+    const double* __restrict__ src = qi + sidx;
+    for (int c0 = r; c0 < nc; c0 += 8 * P) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = c0 + u * P < nc ? src[(int64_t)(c0 + u * P) * qi_ld] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (c0 + u * P < nc) col[(c0 + u * P) * G] = v[u];
+    }
+  }
+  __syncthreads();  // one wave: the tile is read by every lane of a group
+  if (!valid) return;  // a group is valid or not as a whole
+  double p[4] = {0.0, 0.0, 0.0, 0.0};
+  if (use_inline) {
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) {
+      if (rec == rr) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) p[i] = ginl.v[rr][i];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) p[i] = guess[rec * g_rec + i * g_comp];
+  }
+  const QLdsG<G> q{col, ndata};
+  PartEval<P, QLdsG<G>> ev{q, ndata, c.trig, r};
+  double ssq;
+  const int st = fit_segment_t<1>(ev, q, ndata, jtab, c, p, ssq);
+  if (r != 0) return;
+  out[0 * out_ld + sidx] = p[0];
+  out[1 * out_ld + sidx] = p[1];
+  out[2 * out_ld + sidx] = p[2];
+  out[3 * out_ld + sidx] = p[3];
+  out[5 * out_ld + sidx] = ssq;
+  status[sidx] = st;
 }
 
 // Latency-bound fits (few chains or few segments): kLadderLanes lanes per item, the

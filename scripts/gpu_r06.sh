@@ -20,6 +20,10 @@ for step in "$@"; do
     wdfmi) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$O/wdfmi_prof" -o wd -- python3 scripts/bench_wdfmi.py > $O/wdfmi.jsonl 2> $O/wdfmi.err || exit 17 ;;
     sweep) timeout -k 10 300 python -u scripts/probe_ndata_sweep.py 100000 > $O/sweep.jsonl 2> $O/sweep.err || exit 18
            timeout -k 10 300 python -u scripts/probe_ndata_sweep.py 100000 lm_wide=0 > $O/sweep_literal.jsonl 2>> $O/sweep.err || exit 18 ;;
+    sweepnolds) timeout -k 10 300 python -u scripts/probe_ndata_sweep.py 100000 lm_wide_lds=0 > $O/sweep_nolds.jsonl 2>> $O/sweep.err || exit 21 ;;
+    sweepx) for spec in $SWEEPS; do  # SWEEPS="name:key=v+key=v ..."
+              timeout -k 10 300 python -u scripts/probe_ndata_sweep.py 100000 "${spec#*:}" > $O/sweep_${spec%%:*}.jsonl 2>> $O/sweep.err || exit 22
+            done ;;
     lmvec) timeout -k 10 600 $PYT tests/test_gpu_lm_stress.py tests/test_gpu_parity.py tests/test_gpu_numerics.py > $O/lmvec.log 2>&1 || exit 19 ;;
     pitmoves) timeout -k 10 300 python -u scripts/probe_pit_moves.py > $O/pit_moves.jsonl 2> $O/pit_moves.err || exit 20 ;;
     *) echo "unknown step $step"; exit 2 ;;

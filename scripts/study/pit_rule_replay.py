@@ -16,8 +16,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 BIG = 1.7976931348623157e308
 
 
-def decide(moves, tol=1e-13, stall_max=3, cap=48, trend=4, min_pass=0, slow_floor=0.5):
-    """pit_decide over a channel's move sequence: (passes when the status left 0, status)."""
+def fmax(a, b):
+    """C fmax: a NaN operand is ignored."""
+    if a != a:
+        return b
+    if b != b:
+        return a
+    return max(a, b)
+
+
+def decide(moves, tol=1e-13, stall_max=3, cap=48, trend=4, min_pass=0, slow_floor=0.5, slow_from=16, env=True):
+    """pit_decide over a channel's move sequence: (passes when the status left 0, status).
+    slow_from / env: round 6's transient grace and envelope test (slow_from=0, env=False: the
+    round-5 rule)."""
     dprev, rho_c, stall = math.nan, -1.0, 0
     dold = [math.nan] * trend
     for pass_ in range(min(cap, len(moves))):
@@ -46,6 +57,12 @@ def decide(moves, tol=1e-13, stall_max=3, cap=48, trend=4, min_pass=0, slow_floo
                     status = 1
             elif rho < 1.0 and rho / (1.0 - rho) * d <= tol:
                 status = 1
+            if env and status == 0 and pass_ >= 3:
+                dk, dk2 = fmax(d, dold[0]), fmax(dold[1], dold[2])
+                if 0.0 < dk <= BIG and 0.0 < dk2 <= BIG:
+                    r = math.sqrt(dk / dk2)
+                    if r < 1.0 and 2.0 * dk * r / (1.0 - r) <= tol:
+                        status = 1
             if status == 0 and d > tol:
                 w, dw = 0, 0.0
                 for i in range(trend):
@@ -54,7 +71,7 @@ def decide(moves, tol=1e-13, stall_max=3, cap=48, trend=4, min_pass=0, slow_floo
                 if w > 0:
                     rt = (d / dw) ** (1.0 / w)
                     slow = rt >= 1.0
-                    if not slow and rt >= slow_floor:
+                    if not slow and rt >= slow_floor and pass_ + 1 >= slow_from:
                         need = math.log(tol * (1.0 - rt) / (rt * d)) / math.log(rt)
                         slow = pass_ + 1 + need > cap
                     stall = stall + 1 if slow else 0
@@ -72,8 +89,8 @@ def main():
     hc = ctypes.CDLL(os.path.join(ROOT, "tests", "hostcheck", "libhostcheck.so"))
     hc.hc_pit_decide.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_void_p, ctypes.c_void_p]
-    variants = [dict(), dict(stall_max=5), dict(min_pass=8), dict(min_pass=12), dict(stall_max=6, min_pass=10),
-                dict(trend=6), dict(stall_max=4, trend=6, min_pass=8)]
+    variants = [dict(), dict(slow_from=0, env=False), dict(env=False), dict(slow_from=0), dict(slow_from=20),
+                dict(slow_from=24)]
     for v in variants:
         tot = dict(ch=0, conv=0, seq=0, seq_well=0, well=0, passes_conv=0, seq_pass=[])
         for r in rows:

@@ -113,6 +113,7 @@ void hc_pit_decide(const double* moves, int n, double tol, int stall_max, int ca
   ru.noise = tol;
   ru.stall_max = stall_max;
   ru.cap = cap;
+  ru.slow_from = 16;
   *passes_out = 0;
   *status_out = 0;
   for (int k = 0; k < n && k < cap; ++k) {

@@ -73,3 +73,29 @@ def test_torch_first_shares_its_runtime(torch_hip):
     r = _child(torch_first=True, import_after=False, DFMI_HIP_RUNTIME="")
     assert r["runtime"] == torch_hip
     assert len(r["hip_final"]) == 1 and len(r["hsa_final"]) == 1, r
+
+
+def test_soname_check_reads_the_elf_dynamic_section(torch_hip):
+    """The preload happens only when torch's runtime carries the soname libdfmi.so needs
+    (_lib._elf_dynamic_strings: DT_SONAME / DT_NEEDED from the section headers)."""
+    from deepfmkit_amd import _lib
+    need = [n for n in _lib._elf_dynamic_strings(_lib.LIB_PATH, 1) if n.startswith("libamdhip64")]
+    assert need == ["libamdhip64.so.7"]
+    assert _lib._elf_dynamic_strings(torch_hip, 14) == need
+    assert _lib._elf_dynamic_strings(__file__, 14) == []  # not an ELF file
+
+
+def test_mismatched_torch_runtime_is_not_preloaded(torch_hip, tmp_path, monkeypatch):
+    """A torch whose runtime has another soname (e.g. a ROCm 6 build): no preload, a warning,
+    the system runtime."""
+    import warnings
+    from deepfmkit_amd import _lib
+    fake = tmp_path / "libamdhip64.so"
+    fake.write_bytes(b"not an ELF")
+    monkeypatch.setattr(_lib, "_torch_hip_runtime", lambda: str(fake))
+    monkeypatch.setitem(os.environ, "DFMI_HIP_RUNTIME", "")
+    monkeypatch.delitem(sys.modules, "torch", raising=False)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        assert _lib._bind_runtime() is None
+    assert any("not the one libdfmi.so needs" in str(x.message) for x in w)

@@ -95,6 +95,8 @@ struct Tuning {
                               // (then every ekf_pit_every); config 5's record converges in 5
   int ekf_pit_every = 2;
   int ekf_pit_tol = 13;       // stop rule: distance from the fixed point bounded by 10^-ekf_pit_tol (pit_decide)
+  int ekf_pit_overlap = 2;    // sequential re-runs of handed-over channels: 2 at each host check on a high-priority
+                              // stream beside the passes, 1 the same on a default-priority stream, 0 after the passes
   int ekf_pit_slow_from = 16; // pass from which "too slow to meet the bound within the cap" counts (pit_decide)
   int ekf_pit_stall = 3;      // passes in a row not contracting fast enough to meet the bound within the cap
                               // before the sequential kernel (pit_decide)
@@ -177,7 +179,7 @@ struct DeviceState {
   size_t pin_n = 0;
   // the EKF parallel in time's hand-over stream: sequential re-runs of channels that stopped
   // contracting run here beside the remaining passes (created on first use)
-  hipStream_t ekf_side = nullptr;
+  hipStream_t ekf_side = nullptr, ekf_side_lo = nullptr;  // high / default priority (ekf_pit_overlap 2 / 1)
   hipEvent_t ev_ekf_in = nullptr, ev_ekf_out = nullptr;
 };
 
@@ -942,7 +944,8 @@ int seed_launch(int dev, const double* x, int64_t nrec, int64_t rec_stride, int 
     void *qs, *ds_;
     if ((rc = workspace(dev, "qi_seed", (size_t)2 * ndata * nrec * 8, &qs))) return rc;
     if ((rc = workspace(dev, "dc_seed", (size_t)nrec * 8, &ds_))) return rc;
-    auto sk = ndata <= 12 ? dfmi::seed_kernel<12> : ndata <= 16 ? dfmi::seed_kernel<16> : dfmi::seed_kernel<0>;
+    auto sk = ndata <= 12 ? dfmi::seed_kernel<12> : ndata <= 16 ? dfmi::seed_kernel<16>
+              : t_tune.lm_wide ? dfmi::seed_kernel<dfmi::kWideNd> : dfmi::seed_kernel<0>;
     // the many-harmonic demodulation where its geometry holds (16-B rows, 128 <= L <= 256):
     // the bulk's own QI for buffer 0, and a fold with 10 wave loads in flight instead of the
     // cycle-aligned scalar fold against a global basis
@@ -1106,6 +1109,7 @@ const std::map<std::string, Knob>& knobs() {
       {"ekf_pit_tol", {&Tuning::ekf_pit_tol, {}}},
       {"ekf_pit_stall", {&Tuning::ekf_pit_stall, {}}},
       {"ekf_pit_slow_from", {&Tuning::ekf_pit_slow_from, {}}},
+      {"ekf_pit_overlap", {&Tuning::ekf_pit_overlap, {0, 1, 2}}},
       {"ekf_pit_trace", {&Tuning::ekf_pit_trace, {0, 1}}},
       {"ekf_pit_seq", {&Tuning::ekf_pit_seq, {0, 1}}},
       {"ekf_pit_measure", {&Tuning::ekf_pit_measure, {0, 1}}},
@@ -1298,10 +1302,13 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
   std::vector<char> host_handed((size_t)nrec, 0);
   int64_t nh = 0;
   bool side_used = false;
+  hipStream_t side_stream = nullptr;
   std::string seq_name;
   if (handed) HIPCHK(hipMemsetAsync(handed, 0, (size_t)nrec * sizeof(unsigned), st));
+  const int overlap = t_tune.ekf_pit_overlap;
   auto hand_over = [&](const dfmi::PitChan* hc, bool final_) -> int {
     if (!t_tune.ekf_pit_seq) return DFMI_OK;
+    if (!overlap && !final_) return DFMI_OK;  // ekf_pit_overlap 0: every re-run after the passes, on st
     int64_t cnt = 0;
     for (int64_t r = 0; r < nrec; ++r)
       if (!host_handed[r] && (hc[r].status == 2 || (final_ && hc[r].status != 1))) {
@@ -1310,25 +1317,35 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
       }
     if (cnt == 0) return DFMI_OK;
     DeviceState& d = *t_ds;
-    if (!d.ekf_side) {
-      int lo = 0, hi = 0;
-      HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-      HIPCHK(hipStreamCreateWithPriority(&d.ekf_side, hipStreamNonBlocking, hi));
-      HIPCHK(hipEventCreateWithFlags(&d.ev_ekf_in, hipEventDisableTiming));
-      HIPCHK(hipEventCreateWithFlags(&d.ev_ekf_out, hipEventDisableTiming));
+    hipStream_t side = st;
+    if (overlap) {
+      hipStream_t& sref = overlap == 2 ? d.ekf_side : d.ekf_side_lo;
+      if (!sref) {
+        int lo = 0, hi = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(hipStreamCreateWithPriority(&sref, hipStreamNonBlocking, overlap == 2 ? hi : lo));
+      }
+      if (!d.ev_ekf_in) {
+        HIPCHK(hipEventCreateWithFlags(&d.ev_ekf_in, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&d.ev_ekf_out, hipEventDisableTiming));
+      }
+      side = sref;
     }
     hipLaunchKernelGGL(dfmi::ekf_pit_handover_kernel, dim3(1), dim3(64), 0, st, (const dfmi::PitChan*)ch, nrec,
                        (unsigned*)handed, (int*)sidx + nh, final_ ? 1 : 0);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(d.ev_ekf_in, st));
-    HIPCHK(hipStreamWaitEvent(d.ekf_side, d.ev_ekf_in, 0));
+    if (side != st) {
+      HIPCHK(hipEventRecord(d.ev_ekf_in, st));
+      HIPCHK(hipStreamWaitEvent(side, d.ev_ekf_in, 0));
+      side_stream = side;
+      side_used = true;
+    }
     const char* kname;
-    if (int rc = ekf_seq_launch(dx, cnt, rs, n, dx0, dp0, dq, dr, wt, R, nbuf, dstates, d.ekf_side, &kname,
+    if (int rc = ekf_seq_launch(dx, cnt, rs, n, dx0, dp0, dq, dr, wt, R, nbuf, dstates, side, &kname,
                                 (const int*)sidx + nh))
       return rc;
     seq_name = kname;
     nh += cnt;
-    side_used = true;
     return DFMI_OK;
   };
   int cur = 0;
@@ -1387,10 +1404,10 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
   g_last_demod = "ekf_pit (B=" + std::to_string(B) + ", nb=" + std::to_string(nb) + ")";
   if (int rc = hand_over(hc, true)) return rc;  // every channel still not converged
   if (side_used) {  // join: the caller's stream sees the re-run states
-    HIPCHK(hipEventRecord(t_ds->ev_ekf_out, t_ds->ekf_side));
+    HIPCHK(hipEventRecord(t_ds->ev_ekf_out, side_stream));
     HIPCHK(hipStreamWaitEvent(st, t_ds->ev_ekf_out, 0));
-    g_last_demod += std::string(" + ") + seq_name + " x" + std::to_string(nh);
   }
+  if (nh) g_last_demod += std::string(" + ") + seq_name + " x" + std::to_string(nh);
   return DFMI_OK;
 }
 

@@ -1455,77 +1455,136 @@ __device__ __forceinline__ double lm_descend_ladder(Ev&& ev, double (&p)[4], con
 
 // fit.py:260-320 (_find_best_initial_guess). jtab: n_grid rows of J_1..J_ndata(mtry)
 // (psi = 0 exactly: cos(j*0) = 1, -sin(j*0) = -0). Q.qc(i) / Q.qs(i): Q_{i+1}, I_{i+1}.
+// One point of fit.py:260-320's m grid (grid index g): the linear phi / amp estimates at
+// mtry = M_GRID_MIN + g * step and ssqf there; false where the reference `continue`s.
+template <typename QF>
+DFMI_HDI bool m_grid_point(QF&& Q, int ndata, const double* __restrict__ jtab, const LMConst& c, int g,
+                           double& s_out, double (&pt)[3]) {
+  const double mtry = c.grid_min + (double)g * c.grid_delta;
+  const double* jrow = jtab + (int64_t)g * ndata;
+  double sinsum = 0.0, cossum = 0.0;
+  int nsin = 0, ncos = 0;
+  for (int i = 0; i < ndata; ++i) {
+    const int j = i + 1;
+    const double bq = jrow[i] * 1.0;   // jv * cos(j*0)
+    const double bi = jrow[i] * -0.0;  // jv * -sin(j*0)
+    const double dq = Q.qc(i), di = Q.qs(i);
+    if (fabs(bq) > c.bessel_amp_thr) {
+      switch (j & 3) {
+        case 0: cossum += dq / bq; ++ncos; break;
+        case 1: sinsum -= dq / bq; ++nsin; break;
+        case 2: cossum -= dq / bq; ++ncos; break;
+        default: sinsum += dq / bq; ++nsin; break;
+      }
+    }
+    if (fabs(bi) > c.bessel_amp_thr) {
+      switch (j & 3) {
+        case 0: cossum += di / bi; ++ncos; break;
+        case 1: sinsum -= di / bi; ++nsin; break;
+        case 2: cossum -= di / bi; ++ncos; break;
+        default: sinsum += di / bi; ++nsin; break;
+      }
+    }
+  }
+  if (nsin == 0 || ncos == 0) return false;
+  const double ptry = atan2(sinsum / (double)nsin, cossum / (double)ncos);
+  double sp, cp;
+  sincos(ptry, &sp, &cp);
+  double asum = 0.0;
+  int na = 0;
+  for (int i = 0; i < ndata; ++i) {
+    const int j = i + 1;
+    const double sc = quarter_turn(j, cp, sp);  // [cos, -sin, -cos, sin][j % 4]
+    const double bq = jrow[i] * 1.0;
+    const double bi = jrow[i] * -0.0;
+    if (fabs(bq) > c.bessel_amp_thr && fabs(sc) > c.sincos_amp_thr) {
+      asum += Q.qc(i) / (sc * bq);
+      ++na;
+    }
+    if (fabs(bi) > c.bessel_amp_thr && fabs(sc) > c.sincos_amp_thr) {
+      asum += Q.qs(i) / (sc * bi);
+      ++na;
+    }
+  }
+  if (na == 0) return false;
+  const double atry = asum / (double)na;
+  // ssqf at (atry, mtry, ptry, 0): fit.py:152-167 with cos(j*0)=1, sin(j*0)=0
+  double s = 0.0;
+  for (int i = 0; i < ndata; ++i) {
+    const double common = atry * quarter_turn(i + 1, cp, sp) * jrow[i];
+    const double rq = Q.qc(i) - common;
+    const double ri = Q.qs(i) + common * 0.0;
+    s = fma(rq, rq, s);
+    s = fma(ri, ri, s);
+  }
+  s_out = s;
+  pt[0] = atry;
+  pt[1] = mtry;
+  pt[2] = ptry;
+  return true;
+}
+
 template <typename QF>
 DFMI_HDI void m_grid_seed(QF&& Q, int ndata, const double* __restrict__ jtab, const LMConst& c, double (&best)[4]) {
   double best_ssq = 9e99;
   best[0] = best[1] = best[2] = best[3] = 0.0;
   for (int g = 0; g < c.n_grid; ++g) {
-    const double mtry = c.grid_min + (double)g * c.grid_delta;
-    const double* jrow = jtab + (int64_t)g * ndata;
-    double sinsum = 0.0, cossum = 0.0;
-    int nsin = 0, ncos = 0;
-    for (int i = 0; i < ndata; ++i) {
-      const int j = i + 1;
-      const double bq = jrow[i] * 1.0;   // jv * cos(j*0)
-      const double bi = jrow[i] * -0.0;  // jv * -sin(j*0)
-      const double dq = Q.qc(i), di = Q.qs(i);
-      if (fabs(bq) > c.bessel_amp_thr) {
-        switch (j & 3) {
-          case 0: cossum += dq / bq; ++ncos; break;
-          case 1: sinsum -= dq / bq; ++nsin; break;
-          case 2: cossum -= dq / bq; ++ncos; break;
-          default: sinsum += dq / bq; ++nsin; break;
-        }
-      }
-      if (fabs(bi) > c.bessel_amp_thr) {
-        switch (j & 3) {
-          case 0: cossum += di / bi; ++ncos; break;
-          case 1: sinsum -= di / bi; ++nsin; break;
-          case 2: cossum -= di / bi; ++ncos; break;
-          default: sinsum += di / bi; ++nsin; break;
-        }
-      }
-    }
-    if (nsin == 0 || ncos == 0) continue;
-    const double ptry = atan2(sinsum / (double)nsin, cossum / (double)ncos);
-    double sp, cp;
-    sincos(ptry, &sp, &cp);
-    double asum = 0.0;
-    int na = 0;
-    for (int i = 0; i < ndata; ++i) {
-      const int j = i + 1;
-      const double sc = quarter_turn(j, cp, sp);  // [cos, -sin, -cos, sin][j % 4]
-      const double bq = jrow[i] * 1.0;
-      const double bi = jrow[i] * -0.0;
-      if (fabs(bq) > c.bessel_amp_thr && fabs(sc) > c.sincos_amp_thr) {
-        asum += Q.qc(i) / (sc * bq);
-        ++na;
-      }
-      if (fabs(bi) > c.bessel_amp_thr && fabs(sc) > c.sincos_amp_thr) {
-        asum += Q.qs(i) / (sc * bi);
-        ++na;
-      }
-    }
-    if (na == 0) continue;
-    const double atry = asum / (double)na;
-    // ssqf at (atry, mtry, ptry, 0): fit.py:152-167 with cos(j*0)=1, sin(j*0)=0
-    double s = 0.0;
-    for (int i = 0; i < ndata; ++i) {
-      const double common = atry * quarter_turn(i + 1, cp, sp) * jrow[i];
-      const double rq = Q.qc(i) - common;
-      const double ri = Q.qs(i) + common * 0.0;
-      s = fma(rq, rq, s);
-      s = fma(ri, ri, s);
-    }
+    double s, pt[3];
+    if (!m_grid_point(Q, ndata, jtab, c, g, s, pt)) continue;
     if (s < best_ssq) {
       best_ssq = s;
-      best[0] = atry;
-      best[1] = mtry;
-      best[2] = ptry;
+      best[0] = pt[0];
+      best[1] = pt[1];
+      best[2] = pt[2];
       best[3] = 0.0;
     }
   }
 }
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// m_grid_seed with the grid points dealt over the L lanes of a group that runs one fit (the
+// lambda-ladder descents: the seed kernels, lm_ladder_kernel): lane r evaluates points r, r + L,
+// ..., keeps its first strict minimum, and the group reduces (s, g) pairs — the smaller ssq, on a
+// tie the smaller grid index: exactly the serial loop's first strict minimum. Same bits, ~L
+// times shorter (a seed fitted from a far guess, e.g. the quickstart's m = 31.4 from m = 6,
+// always takes this path).
+template <int L, typename QF>
+__device__ __forceinline__ void m_grid_seed_lanes(QF&& Q, int ndata, const double* __restrict__ jtab,
+                                                  const LMConst& c, double (&best)[4]) {
+  const int r = (int)(__lane_id() & (L - 1));
+  double bs = 9e99, bp[3] = {0.0, 0.0, 0.0};
+  int bg = 0x7fffffff;
+  for (int g = r; g < c.n_grid; g += L) {
+    double s, pt[3];
+    if (!m_grid_point(Q, ndata, jtab, c, g, s, pt)) continue;
+    if (s < bs) {
+      bs = s;
+      bg = g;
+      bp[0] = pt[0];
+      bp[1] = pt[1];
+      bp[2] = pt[2];
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < L; o <<= 1) {
+    const int src = (int)__lane_id() ^ o;
+    const double os = shfl_any(bs, src);
+    const int og = shfl_any(bg, src);
+    const double o0 = shfl_any(bp[0], src), o1 = shfl_any(bp[1], src), o2 = shfl_any(bp[2], src);
+    if (os < bs || (os == bs && og < bg)) {
+      bs = os;
+      bg = og;
+      bp[0] = o0;
+      bp[1] = o1;
+      bp[2] = o2;
+    }
+  }
+  best[0] = bp[0];
+  best[1] = bp[1];
+  best[2] = bp[2];
+  best[3] = 0.0;
+}
+#endif
 
 // fit.py:322-361 (fit): LM, status + grid retry, normalisation, phi wrap.
 // Ev: the evaluator (GenSplitEval / SplitEval); FLAT = 0 runs the nested descent
@@ -1552,7 +1611,11 @@ DFMI_HDI int fit_finish_t(Ev&& ev, QF&& Q, int ndata, const double* __restrict__
     status = 0;
   } else {
     double g[4];
-    m_grid_seed(Q, ndata, jtab, c, g);
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (FLAT == 2) m_grid_seed_lanes<kLadderLanes>(Q, ndata, jtab, c, g);
+    else
+#endif
+      m_grid_seed(Q, ndata, jtab, c, g);
     if (!(g[0] == 0.0) || !(g[1] == 0.0) || !(g[2] == 0.0) || !(g[3] == 0.0)) {  // np.any
       const double ssq2 = descend(g);
       if (ssq2 < ssq) {

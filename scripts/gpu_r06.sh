@@ -24,6 +24,9 @@ for step in "$@"; do
     sweepx) for spec in $SWEEPS; do  # SWEEPS="name:key=v+key=v ..."
               timeout -k 10 300 python -u scripts/probe_ndata_sweep.py 100000 "${spec#*:}" > $O/sweep_${spec%%:*}.jsonl 2>> $O/sweep.err || exit 22
             done ;;
+    ekfho) timeout -k 10 300 python -u scripts/probe_ekf_handover.py > $O/ekf_handover.jsonl 2> $O/ekf_handover.err || exit 23
+           MODES=2 REPS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$O/ekfho_prof" -o ho -- python3 scripts/probe_ekf_handover.py > $O/ekf_handover_prof.jsonl 2>> $O/ekf_handover.err || exit 23 ;;
+    wdfmipmc) timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 --output-format csv -d "$PWD/$O/wdfmi_pmc" -o wd -- python3 scripts/bench_wdfmi.py --records 2048 --cpu 0 --reps 1 > $O/wdfmi_pmc.jsonl 2> $O/wdfmi_pmc.err || exit 24 ;;
     lmvec) timeout -k 10 600 $PYT tests/test_gpu_lm_stress.py tests/test_gpu_parity.py tests/test_gpu_numerics.py > $O/lmvec.log 2>&1 || exit 19 ;;
     pitmoves) timeout -k 10 300 python -u scripts/probe_pit_moves.py > $O/pit_moves.jsonl 2> $O/pit_moves.err || exit 20 ;;
     *) echo "unknown step $step"; exit 2 ;;

@@ -665,9 +665,9 @@ def extra_configs(torch, dev, lib, _lib, stream, cfg, cpu_leg):
 def ekf_handover_point(torch, dev, lib, _lib, stream, ns=400_000, nch=1024, n_bad=64):
     """The EKF parallel in time's hand-over (dfmi_capi.hip ekf_pit_run, round 6): channels whose
     iteration does not lock (here m = 20 records fitted from init_m = 6: the filter never
-    locks, moves O(1) every pass) are re-run by the sequential kernel, launched at the host
-    check that first sees them on a stream of their own while the other channels keep passing.
-    One such channel alone: its time against the sequential kernel's alone (the passes before
+    locks, moves O(1) every pass) are re-run in place by the sequential kernel, in one launch
+    after the last pass (ekf_pit_overlap 0; launching at each check beside the passes measured
+    slower). One such channel alone: its time against the sequential kernel's alone (the passes before
     the hand-over are the overhead). A batch of nch config-5 channels with n_bad of those among
     them: its time against the passes alone (the same batch with the re-run switched off,
     ekf_pit_seq 0: diagnostics) and the n_bad channels' sequential run alone."""
@@ -726,6 +726,7 @@ def ekf_handover_point(torch, dev, lib, _lib, stream, ns=400_000, nch=1024, n_ba
              "ms": round(tb * 1e3, 3), "kernel": kb, "passes_alone_ms": round(tp * 1e3, 3),
              "sequential_alone_ms": round(tsq * 1e3, 3), "sequential_kernel": ksq,
              "ratio_to_max_of_parts": round(tb / max(tp, tsq), 4),
+             "ratio_to_sum_of_parts": round(tb / (tp + tsq), 4),
              "handed_states_bit_identical_to_sequential": bool(torch.equal(sb[idx], ss))}
     del sb, ss, xs
     torch.cuda.empty_cache()

@@ -95,8 +95,9 @@ struct Tuning {
                               // (then every ekf_pit_every); config 5's record converges in 5
   int ekf_pit_every = 2;
   int ekf_pit_tol = 13;       // stop rule: distance from the fixed point bounded by 10^-ekf_pit_tol (pit_decide)
-  int ekf_pit_overlap = 2;    // sequential re-runs of handed-over channels: 2 at each host check on a high-priority
-                              // stream beside the passes, 1 the same on a default-priority stream, 0 after the passes
+  int ekf_pit_overlap = 0;    // sequential re-runs of handed-over channels: 0 all in one launch after the passes;
+                              // 3 at each host check on the next of kEkfPool high-priority streams beside the
+                              // passes, 2 on one high-priority stream, 1 on one default-priority stream
   int ekf_pit_slow_from = 16; // pass from which "too slow to meet the bound within the cap" counts (pit_decide)
   int ekf_pit_stall = 3;      // passes in a row not contracting fast enough to meet the bound within the cap
                               // before the sequential kernel (pit_decide)
@@ -180,6 +181,7 @@ struct DeviceState {
   // the EKF parallel in time's hand-over stream: sequential re-runs of channels that stopped
   // contracting run here beside the remaining passes (created on first use)
   hipStream_t ekf_side = nullptr, ekf_side_lo = nullptr;  // high / default priority (ekf_pit_overlap 2 / 1)
+  hipStream_t ekf_pool[3] = {};                           // ekf_pit_overlap 3: one per hand-over, round robin
   hipEvent_t ev_ekf_in = nullptr, ev_ekf_out = nullptr;
 };
 
@@ -1109,7 +1111,7 @@ const std::map<std::string, Knob>& knobs() {
       {"ekf_pit_tol", {&Tuning::ekf_pit_tol, {}}},
       {"ekf_pit_stall", {&Tuning::ekf_pit_stall, {}}},
       {"ekf_pit_slow_from", {&Tuning::ekf_pit_slow_from, {}}},
-      {"ekf_pit_overlap", {&Tuning::ekf_pit_overlap, {0, 1, 2}}},
+      {"ekf_pit_overlap", {&Tuning::ekf_pit_overlap, {0, 1, 2, 3}}},
       {"ekf_pit_trace", {&Tuning::ekf_pit_trace, {0, 1}}},
       {"ekf_pit_seq", {&Tuning::ekf_pit_seq, {0, 1}}},
       {"ekf_pit_measure", {&Tuning::ekf_pit_measure, {0, 1}}},
@@ -1137,6 +1139,13 @@ thread_local std::vector<int32_t> g_pit_passes;
 thread_local std::vector<double> g_pit_hist;
 thread_local int g_pit_hist_n = 0;
 constexpr int kPitNoMem = 1;  // ekf_pit_run: a workspace could not be allocated (nothing launched)
+// Hand-over streams of ekf_pit_overlap 3: successive hand-overs run concurrently on up to this many
+// streams (a process has GPU_MAX_HW_QUEUES = 4 hardware queues by default, the caller's stream holds
+// one). A sequential re-run lasts as long as the record whatever its channel count (63 ms for the
+// 1,024-channel bench batch), so every extra launch costs that again: the batch took 143 ms with one
+// launch after the 80 ms of passes (mode 0, the default), 194 ms over this pool (mode 3) and 432 ms
+// queued in one stream (modes 1 and 2), profiles/r06/ekf_handover_probe.jsonl
+constexpr int kEkfPool = 3;
 
 // Pinned host scratch of the current device (grow-only).
 int pinned(size_t bytes, void** out) {
@@ -1303,6 +1312,8 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
   int64_t nh = 0;
   bool side_used = false;
   hipStream_t side_stream = nullptr;
+  int n_batches = 0;                     // hand-over launches so far
+  hipStream_t used_streams[kEkfPool] = {};  // the streams they went to (pool mode)
   std::string seq_name;
   if (handed) HIPCHK(hipMemsetAsync(handed, 0, (size_t)nrec * sizeof(unsigned), st));
   const int overlap = t_tune.ekf_pit_overlap;
@@ -1318,7 +1329,19 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
     if (cnt == 0) return DFMI_OK;
     DeviceState& d = *t_ds;
     hipStream_t side = st;
-    if (overlap) {
+    if (overlap == 3) {  // a pool of streams: successive hand-overs run concurrently, not queued in one stream
+      hipStream_t& sref = d.ekf_pool[n_batches % kEkfPool];
+      if (!sref) {
+        int lo = 0, hi = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(hipStreamCreateWithPriority(&sref, hipStreamNonBlocking, hi));
+      }
+      if (!d.ev_ekf_in) {
+        HIPCHK(hipEventCreateWithFlags(&d.ev_ekf_in, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&d.ev_ekf_out, hipEventDisableTiming));
+      }
+      side = sref;
+    } else if (overlap) {
       hipStream_t& sref = overlap == 2 ? d.ekf_side : d.ekf_side_lo;
       if (!sref) {
         int lo = 0, hi = 0;
@@ -1339,7 +1362,9 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
       HIPCHK(hipStreamWaitEvent(side, d.ev_ekf_in, 0));
       side_stream = side;
       side_used = true;
+      if (n_batches < kEkfPool) used_streams[n_batches] = side;
     }
+    ++n_batches;
     const char* kname;
     if (int rc = ekf_seq_launch(dx, cnt, rs, n, dx0, dp0, dq, dr, wt, R, nbuf, dstates, side, &kname,
                                 (const int*)sidx + nh))
@@ -1404,8 +1429,12 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
   g_last_demod = "ekf_pit (B=" + std::to_string(B) + ", nb=" + std::to_string(nb) + ")";
   if (int rc = hand_over(hc, true)) return rc;  // every channel still not converged
   if (side_used) {  // join: the caller's stream sees the re-run states
-    HIPCHK(hipEventRecord(t_ds->ev_ekf_out, side_stream));
-    HIPCHK(hipStreamWaitEvent(st, t_ds->ev_ekf_out, 0));
+    for (int i = 0; i < kEkfPool; ++i) {
+      hipStream_t w = overlap == 3 ? used_streams[i] : (i == 0 ? side_stream : nullptr);
+      if (!w) continue;
+      HIPCHK(hipEventRecord(t_ds->ev_ekf_out, w));
+      HIPCHK(hipStreamWaitEvent(st, t_ds->ev_ekf_out, 0));
+    }
   }
   if (nh) g_last_demod += std::string(" + ") + seq_name + " x" + std::to_string(nh);
   return DFMI_OK;

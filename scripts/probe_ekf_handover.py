@@ -1,10 +1,10 @@
 """The EKF parallel in time's hand-over (round 6), by variant: a batch of NCH config-5 channels
 (400,000 samples, m = 6, 40 dB) with NBAD m = 20 channels fitted from init_m = 6 (never lock)
-spread among them. Per ekf_pit_overlap (2: re-runs launched at the host check on a
-high-priority stream beside the passes; 1: a default-priority stream; 0: after the passes, on
-the caller's stream) the batch time, against the passes alone (ekf_pit_seq 0) and the NBAD
+spread among them. Per ekf_pit_overlap (3: re-runs launched at the host check on the next of a
+pool of high-priority streams beside the passes; 2: one high-priority stream; 1: one
+default-priority stream; 0: after the passes, on the caller's stream) the batch time, against the passes alone (ekf_pit_seq 0) and the NBAD
 channels' sequential run alone (ekf_pit 0). One JSON line per measurement.
-env: NCH (1024), NBAD (64), NS (400000), MODES ("2,1,0"), REPS (2)."""
+env: NCH (1024), NBAD (64), NS (400000), MODES ("3,2,0"), REPS (2)."""
 import json
 import os
 import sys
@@ -61,9 +61,9 @@ def main():
         finally:
             for k in tune:
                 _lib.check(lib.dfmi_set_tuning(k.encode(), {"ekf_pit": 1024, "ekf_pit_seq": 1,
-                                                            "ekf_pit_overlap": 2}[k]), k)
+                                                            "ekf_pit_overlap": 0}[k]), k)
     res = {}
-    for mode in [int(v) for v in os.environ.get("MODES", "2,1,0").split(",")]:
+    for mode in [int(v) for v in os.environ.get("MODES", "3,2,0").split(",")]:
         t, kn, out = run(xe, nch, {"ekf_pit_overlap": mode})
         res[mode] = out
         print(json.dumps({"what": "batch", "overlap": mode, "ms": round(t, 3), "kernel": kn}), flush=True)

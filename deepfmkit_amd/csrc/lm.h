@@ -903,7 +903,9 @@ struct SplitEval {  // NDMAX: a register-path variant tag (nd_cap / nd_exact)
 // the reference is gated at full scale (tests/test_gpu_full_scale.py ndata 16..62,
 // tests/test_gpu_quickstart.py).
 // ---------------------------------------------------------------------------
-constexpr int kWideNd = 1 << 9;  // NDMAX tag of the many-harmonic path
+constexpr int kWideNd = 1 << 9;       // NDMAX tag of the many-harmonic path
+constexpr int kWideNdF = kWideNd | 1;  // the same with one walk per trial (WideEval<QF, true>)
+constexpr bool wide_nd(int ndmax) { return (ndmax & ~1) == kWideNd; }
 
 // Component-major QI with the column base uniform across the wave (qi, harmonic h) and the
 // segment index per lane.
@@ -1107,7 +1109,63 @@ DFMI_HDI void wide_accept(const QF& q, int nd, const double (&p)[4], const WideT
   e = Eval{t.ssq, a00, a01, a02, 0.0, a11, a12, 0.0, a22, 0.0, a33, g0, g1, g2, g3};
 }
 
+// ssqf and coeffs at p in ONE walk (WideEval<QF, true>): the bodies of wide_trial and
+// wide_accept together, the same operations on the same walk values, so the same bits as a
+// trial followed by its accept. The LM runs SIMT: a wave pays the accept's walk on every pass
+// where one of its 64 lanes accepts (nearly every pass but the last few), so a trial that
+// carries the coeffs costs ~the accept alone where the split form costs trial + accept.
+struct WideFull {
+  Eval e;
+};
+
 template <typename QF>
+DFMI_HDI double wide_full(const QF& q, int nd, const double (&p)[4], Eval& e, const DfmiTrigK& k) {
+  double sph, cph, s1, c1, sn, cn;
+  dfmi_sincos_auto(p[2], k, &sph, &cph);
+  dfmi_sincos_auto(p[3], k, &s1, &c1);
+  dfmi_sincos_auto((double)nd * p[3], k, &sn, &cn);
+  const double a = p[0];
+  const double ac = a * cph, as = a * sph;
+  const double cph0 = (a != 0.0) ? cph : 0.0, sph0 = (a != 0.0) ? sph : 0.0;
+  double so = 0.0, se = 0.0;
+  double a00 = 0.0, a01 = 0.0, a02 = 0.0, a11 = 0.0, a12 = 0.0, a22 = 0.0, a33 = 0.0;
+  double g0 = 0.0, g1 = 0.0, g2 = 0.0, g3 = 0.0;
+  wide_walk(q, nd, p[1], p[3], c1, s1, cn, sn,
+            [&](int j, double Jm1, double Jj, double Jp1, double cj, double sj, double Q, double I) {
+              const double aP = quarter_turn(j, ac, as), aD = quarter_turn(j + 1, ac, as);
+              const double c = aP * Jj;
+              const double rq = fma(-c, cj, Q);
+              const double ri = fma(c, sj, I);
+              if (j & 1) {
+                so = fma(rq, rq, so);
+                so = fma(ri, ri, so);
+              } else {
+                se = fma(rq, rq, se);
+                se = fma(ri, ri, se);
+              }
+              const double u0 = quarter_turn(j, cph0, sph0) * Jj;
+              const double u1 = aP * (0.5 * (Jm1 - Jp1));
+              const double u2 = aD * Jj;
+              const double A = fma(cj, rq, -(sj * ri));
+              const double B = fma(sj, rq, cj * ri);
+              a00 = fma(u0, u0, a00);
+              a01 = fma(u0, u1, a01);
+              a02 = fma(u0, u2, a02);
+              a11 = fma(u1, u1, a11);
+              a12 = fma(u1, u2, a12);
+              a22 = fma(u2, u2, a22);
+              const double jc = (double)j * c;
+              a33 = fma(jc, jc, a33);
+              g0 = fma(u0, A, g0);
+              g1 = fma(u1, A, g1);
+              g2 = fma(u2, A, g2);
+              g3 = fma(-jc, B, g3);
+            });
+  e = Eval{so + se, a00, a01, a02, 0.0, a11, a12, 0.0, a22, 0.0, a33, g0, g1, g2, g3};
+  return e.ssq;
+}
+
+template <typename QF, bool FUSED = false>
 struct WideEval {
   const QF& q;
   int nd;
@@ -1117,6 +1175,18 @@ struct WideEval {
   DFMI_HDI void accept(const double (&p)[4], const Trial& t, Eval& e) { wide_accept(q, nd, p, t, e); }
   DFMI_HDI void solve(const Eval& e, double lam, double (&dp)[4]) { damped_solve_block(e, lam, dp); }
   DFMI_HDI static double ssq_of(const Trial& t) { return t.ssq; }
+};
+
+template <typename QF>
+struct WideEval<QF, true> {
+  const QF& q;
+  int nd;
+  const DfmiTrigK& k;
+  using Trial = WideFull;
+  DFMI_HDI double trial(const double (&p)[4], Trial& t) { return wide_full(q, nd, p, t.e, k); }
+  DFMI_HDI void accept(const double (&)[4], const Trial& t, Eval& e) { e = t.e; }
+  DFMI_HDI void solve(const Eval& e, double lam, double (&dp)[4]) { damped_solve_block(e, lam, dp); }
+  DFMI_HDI static double ssq_of(const Trial& t) { return t.e.ssq; }
 };
 
 // ---------------------------------------------------------------------------
@@ -1657,8 +1727,8 @@ template <int NDMAX, typename QE, typename QM, int FLAT = 1>
 __host__ __device__ __forceinline__ int fit_segment_q2(const QE& qe, const QM& qm, int ndata,
                                                     const double* __restrict__ jtab, const LMConst& c,
                                                     double (&p)[4], double& ssq_out) {
-  if constexpr (NDMAX == kWideNd) {  // many harmonics: closed form over the lean Miller walk
-    WideEval<QE> ev{qe, ndata, c.trig};
+  if constexpr (wide_nd(NDMAX)) {  // many harmonics: closed form over the lean Miller walk
+    WideEval<QE, NDMAX == kWideNdF> ev{qe, ndata, c.trig};
     return fit_segment_t<FLAT>(ev, qm, ndata, jtab, c, p, ssq_out);
   } else if constexpr (NDMAX > 0) {
     SplitEval<NDMAX, QE> ev{qe, ndata, c.trig};
@@ -1718,7 +1788,7 @@ struct GuessInline {
 // r05as), so it keeps its allocation.
 template <int NDMAX, bool CHAIN, bool ONEPASS = false>
 constexpr int lm_waves() {
-  return (!CHAIN && (NDMAX == 12 || ONEPASS || NDMAX == kWideNd)) ? 2 : 1;  // ONEPASS: 259 VGPRs unbounded
+  return (!CHAIN && (NDMAX == 12 || ONEPASS || wide_nd(NDMAX))) ? 2 : 1;  // ONEPASS: 259 VGPRs unbounded
 }
 // ONEPASS (general path, chunk size 1, component-major): each lane keeps its Bessel recurrence
 // values in dynamic LDS (64 x (ndata + 2) doubles per wave) and walks once per evaluation
@@ -1830,7 +1900,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(lm_waves<NDM
     auto one = [&](int64_t sidx) {
       double ssq;
       int st;
-      if constexpr (NDMAX == kWideNd && QREG && !CHAIN) {
+      if constexpr (wide_nd(NDMAX) && QREG && !CHAIN) {
         // the lane's 2 ndata QI into its own LDS column (no other lane reads it: no barrier),
         // 16 loads in flight
         double* col = lds_q + threadIdx.x;
@@ -1845,10 +1915,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(lm_waves<NDM
             if (c0 + u < nc) col[(c0 + u) * 64] = v[u];
         }
         const QLds ql{col, ndata};
-        st = fit_segment_q<kWideNd, QLds, 1>(ql, ndata, jtab, c, p, ssq);
-      } else if constexpr (NDMAX == kWideNd) {
+        st = fit_segment_q<NDMAX, QLds, 1>(ql, ndata, jtab, c, p, ssq);
+      } else if constexpr (wide_nd(NDMAX)) {
         const QCol qg{qi, (uint32_t)sidx, qi_ld, ndata};
-        st = fit_segment_q<kWideNd, QCol, 1>(qg, ndata, jtab, c, p, ssq);
+        st = fit_segment_q<NDMAX, QCol, 1>(qg, ndata, jtab, c, p, ssq);
       } else if constexpr (kQReg) {
         const QGlobal qg{qi + sidx, qi_ld, ndata};
         QRegs<nd_cap(NDMAX)> qr;

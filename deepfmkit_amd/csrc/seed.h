@@ -73,10 +73,9 @@ __global__ __launch_bounds__(64) void seed_kernel(const double* __restrict__ x, 
   }
   double ssq;
   const QGlobal qs{ndata <= 128 ? qsh : qis + r, ndata <= 128 ? 1 : nrec, ndata};
-  // NDMAX == kWideNd (more than 16 harmonics, lm_wide): the many-harmonic evaluation, as the
-  // bulk LM that this seed's result seeds
-  const int st = fit_segment_q<(NDMAX == kWideNd ? kWideNd : kSeedPath), QGlobal, kSeedFlat>(qs, ndata, jtab, c, p,
-                                                                                                ssq);
+  // NDMAX == kWideNd / kWideNdF (more than 16 harmonics, lm_wide / lm_wide_fused): the
+  // many-harmonic evaluation, as the bulk LM that this seed's result seeds
+  const int st = fit_segment_q<(wide_nd(NDMAX) ? NDMAX : kSeedPath), QGlobal, kSeedFlat>(qs, ndata, jtab, c, p, ssq);
   if (lane != 0) return;
   const int64_t sidx = r * nbuf;
   out[0 * out_ld + sidx] = p[0];

@@ -159,6 +159,9 @@ int hc_fit_segments(const double* qi, long n, int ndata, const double* guess, co
     if (force_general == 3) {  // the many-harmonic path (lm.h kWideNd), any ndata
       const dfmi::QCol qc{qi, (uint32_t)s, n, ndata};
       status_out[s] = dfmi::fit_segment_q<dfmi::kWideNd, dfmi::QCol>(qc, ndata, tab.data(), c, p, ssq);
+    } else if (force_general == 4) {  // the same, one walk per trial (kWideNdF, wide_full)
+      const dfmi::QCol qc{qi, (uint32_t)s, n, ndata};
+      status_out[s] = dfmi::fit_segment_q<dfmi::kWideNdF, dfmi::QCol>(qc, ndata, tab.data(), c, p, ssq);
     } else if (force_general == 2 && ndata <= 12) {  // nested (one-lane) descent: must equal the flattened one
       const dfmi::QGlobal qg{qi + s, n, ndata};
       status_out[s] = dfmi::fit_segment_q<12, dfmi::QGlobal, false>(qg, ndata, tab.data(), c, p, ssq);

@@ -96,6 +96,18 @@ def test_host_lm_vectors(hc, lm_npz, group, force_general):
     check_lm_group(lm_npz, group, st, p, ssq)
 
 
+@pytest.mark.parametrize("group", ["10", "20", "30", "62"])
+def test_host_wide_lm_vectors(hc, lm_npz, group):
+    """The many-harmonic path (lm.h kWideNd, the device's LM from ndata 17) on the golden LM
+    vectors, and its one-walk-per-trial form (kWideNdF, lm_wide_fused) bit for bit equal to it."""
+    qi, g = lm_npz[f"g{group}_qi"], lm_npz[f"g{group}_guess"]
+    split = _fit(hc, qi, g, 3)
+    check_lm_group(lm_npz, group, *split)
+    fused = _fit(hc, qi, g, 4)
+    for x, y in zip(split, fused):
+        np.testing.assert_array_equal(x, y)
+
+
 def test_host_lm_on_reference_qi(hc, records_npz, manifest):
     """LM on the reference's own QI of the config-1 record, chunk size 1, vs the
     reference's _fit_parallel(chunk size 1) outputs: the BASELINE tolerance 1e-9."""

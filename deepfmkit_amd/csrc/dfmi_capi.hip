@@ -100,12 +100,7 @@ struct Tuning {
   int ekf_pit_tol = 13;       // stop rule: distance from the fixed point bounded by 10^-ekf_pit_tol (pit_decide)
   int ekf_pit_overlap = 0;    // sequential re-runs of handed-over channels: 0 all in one launch after the passes;
                               // 3 at each host check on the next of kEkfPool high-priority streams beside the
-                              // passes, 2 on one high-priority stream, 1 on one default-priority stream; 4 the
-                              // race: every channel's sequential run started beside the passes (ekf_race),
-                              // each row stopping once its channel converges (from ekf_pit_race_min channels
-                              // while the row rotation kernel applies; else 0)
-  int ekf_pit_race_min = 64;
-  int ekf_pit_race_prio = 0;  // the race's waves' issue priority (s_setprio; 3 slowed the passes 3x, r06n)
+                              // passes, 2 on one high-priority stream, 1 on one default-priority stream
   int ekf_pit_slow_from = 16; // pass from which "too slow to meet the bound within the cap" counts (pit_decide)
   int ekf_pit_stall = 3;      // passes in a row not contracting fast enough to meet the bound within the cap
                               // before the sequential kernel (pit_decide)
@@ -190,9 +185,6 @@ struct DeviceState {
   // contracting run here beside the remaining passes (created on first use)
   hipStream_t ekf_side = nullptr, ekf_side_lo = nullptr;  // high / default priority (ekf_pit_overlap 2 / 1)
   hipStream_t ekf_pool[3] = {};                           // ekf_pit_overlap 3: one per hand-over, round robin
-  hipStream_t ekf_race = nullptr;                         // ekf_pit_overlap 4 (default priority)
-  int* race_flags = nullptr;                              // its cancel flags (host-coherent pinned, grow-only)
-  size_t race_flags_n = 0;
   hipEvent_t ev_ekf_in = nullptr, ev_ekf_out = nullptr;
 };
 
@@ -1129,9 +1121,7 @@ const std::map<std::string, Knob>& knobs() {
       {"ekf_pit_tol", {&Tuning::ekf_pit_tol, {}}},
       {"ekf_pit_stall", {&Tuning::ekf_pit_stall, {}}},
       {"ekf_pit_slow_from", {&Tuning::ekf_pit_slow_from, {}}},
-      {"ekf_pit_overlap", {&Tuning::ekf_pit_overlap, {0, 1, 2, 3, 4}}},
-      {"ekf_pit_race_min", {&Tuning::ekf_pit_race_min, {}}},
-      {"ekf_pit_race_prio", {&Tuning::ekf_pit_race_prio, {0, 1, 2, 3}}},
+      {"ekf_pit_overlap", {&Tuning::ekf_pit_overlap, {0, 1, 2, 3}}},
       {"ekf_pit_trace", {&Tuning::ekf_pit_trace, {0, 1}}},
       {"ekf_pit_seq", {&Tuning::ekf_pit_seq, {0, 1}}},
       {"ekf_pit_measure", {&Tuning::ekf_pit_measure, {0, 1}}},
@@ -1185,39 +1175,26 @@ int pinned(size_t bytes, void** out) {
 // row each (ekf_rot_kernel with sin / cos by rotation between anchors when R % 4 == 0, else
 // ekf_row_kernel, ~1.7x the per-channel rate), many one lane each (ekf_lane_rot_kernel /
 // ekf_kernel, 16x the channels per instruction). Returns the variant's name in *name.
-// The sequential variant for nrec channels is the row rotation kernel (the one that takes a
-// cancel word, ekf_pit_overlap 4).
-bool ekf_seq_is_row_rot(int64_t nrec, int32_t R) {
-  return t_tune.ekf_row && nrec <= (int64_t)t_tune.ekf_row * t_ds->n_cu * 16 && t_tune.ekf_rot && R % 4 == 0;
-}
-
 int ekf_seq_launch(const double* dx, int64_t nrec, int64_t rs, int64_t n, const double* dx0, const double* dp0,
                    const double* dq, const double* dr, const double* wt, int32_t R, int64_t nbuf, double* dstates,
-                   hipStream_t st, const char** name, const int* idx = nullptr, const int* cancel = nullptr) {
+                   hipStream_t st, const char** name, const int* idx = nullptr) {
   const int block = 64;
   const bool row = t_tune.ekf_row && nrec <= (int64_t)t_tune.ekf_row * t_ds->n_cu * 16;
   const int64_t grid = row ? (nrec + 3) / 4 : (nrec + block - 1) / block;
   // rotation between anchors: groups of 16 (8, 4) samples whose ends carry the snapshots
   const bool rot = t_tune.ekf_rot && R % 4 == 0;
-  if (cancel && !(row && rot)) return fail(DFMI_ERR_ARG, "ekf_seq_launch: cancel word without the row rotation kernel");
-  if (row && rot) {
-    using RK = void (*)(const double*, int64_t, int64_t, int64_t, const double*, const double*, const double*,
-                        const double*, const double*, int, int64_t, double*, DfmiTrigK, const int*, const int*, int);
-    const RK rk = R % DFMI_EKF_ROT_G == 0 ? dfmi::ekf_rot_kernel<DFMI_EKF_ROT_G>
-                  : R % 8 == 0            ? dfmi::ekf_rot_kernel<8>
-                                          : dfmi::ekf_rot_kernel<4>;
-    hipLaunchKernelGGL(rk, dim3((unsigned)grid), dim3(block), 0, st, dx, nrec, rs, n, dx0, dp0, dq, dr, wt, (int)R,
-                       nbuf, dstates, dfmi_trig_k(), idx, cancel, cancel ? t_tune.ekf_pit_race_prio : 0);
-  } else {
-    using EK = void (*)(const double*, int64_t, int64_t, int64_t, const double*, const double*, const double*,
-                        const double*, const double*, int, int64_t, double*, DfmiTrigK, const int*);
-    const EK ek = row    ? dfmi::ekf_row_kernel<DFMI_EKF_SPLIT != 0>
-                  : !rot ? dfmi::ekf_kernel
-                  : R % 8 == 0 ? dfmi::ekf_lane_rot_kernel<8>
-                               : dfmi::ekf_lane_rot_kernel<4>;
-    hipLaunchKernelGGL(ek, dim3((unsigned)grid), dim3(block), 0, st, dx, nrec, rs, n, dx0, dp0, dq, dr, wt, (int)R,
-                       nbuf, dstates, dfmi_trig_k(), idx);
-  }
+  using EK = void (*)(const double*, int64_t, int64_t, int64_t, const double*, const double*, const double*,
+                      const double*, const double*, int, int64_t, double*, DfmiTrigK, const int*);
+  EK ek;
+  if (row)
+    ek = !rot ? dfmi::ekf_row_kernel<DFMI_EKF_SPLIT != 0>
+         : R % DFMI_EKF_ROT_G == 0 ? dfmi::ekf_rot_kernel<DFMI_EKF_ROT_G>
+         : R % 8 == 0              ? dfmi::ekf_rot_kernel<8>
+                                   : dfmi::ekf_rot_kernel<4>;
+  else
+    ek = !rot ? dfmi::ekf_kernel : R % 8 == 0 ? dfmi::ekf_lane_rot_kernel<8> : dfmi::ekf_lane_rot_kernel<4>;
+  hipLaunchKernelGGL(ek, dim3((unsigned)grid), dim3(block), 0, st, dx, nrec, rs, n, dx0, dp0, dq, dr, wt, (int)R, nbuf,
+                     dstates, dfmi_trig_k(), idx);
   HIPCHK(hipGetLastError());
   *name = row ? (rot ? "ekf_rot_kernel" : "ekf_row_kernel") : (rot ? "ekf_lane_rot_kernel" : "ekf_kernel");
   return DFMI_OK;
@@ -1251,10 +1228,7 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
                                             : (int)std::min<int64_t>(256, std::max<int64_t>(48, n / 1600));
   const int hist_n = t_tune.ekf_pit_trace ? cap : 0;
   void *xt, *wtt, *xbar, *conv, *chan, *hst, *done, *hs, *ent = nullptr, *hist = nullptr, *pin;
-  void *sidx = nullptr, *handed = nullptr, *race_states = nullptr;
-  // the race (ekf_pit_overlap 4): every channel's sequential run beside the passes, into p_race
-  const bool race = t_tune.ekf_pit_seq && t_tune.ekf_pit_overlap == 4 && nrec >= t_tune.ekf_pit_race_min &&
-                    nrec <= 65535 && nbuf > 0 && ekf_seq_is_row_rot(nrec, R);
+  void *sidx = nullptr, *handed = nullptr;
   std::vector<double*> lv[2];  // per aggregate buffer: level arrays [r][65][lsz[l]]
   // every allocation before the first launch: a failure leaves the sequential kernels to run
   {
@@ -1284,7 +1258,6 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
       ws("p_sidx", (size_t)nrec * sizeof(int), &sidx);
       ws("p_handed", (size_t)nrec * sizeof(unsigned), &handed);
     }
-    if (race) ws("p_race", (size_t)(nrec * nbuf * 5) * 8, &race_states);
     if (!rc) rc = pinned((size_t)nrec * sizeof(dfmi::PitChan) + 64, &pin);
     if (rc) {
       (void)hipGetLastError();  // clear the failed allocation
@@ -1314,32 +1287,6 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
     hipLaunchKernelGGL(dfmi::ekf_pit_gather_tiled_kernel, dim3((unsigned)((B + 31) / 32), (unsigned)((nb + 63) / 64), nr),
                        dim3(256), 0, st, dx, rs, n, B, nb, w_m, f_samp, (double*)xt, (double*)wtt, ch,
                        (double*)conv, (unsigned*)done);
-  std::string seq_name;
-  if (race) {
-    DeviceState& d = *t_ds;
-    if (d.race_flags_n < (size_t)nrec) {
-      if (d.ekf_race) HIPCHK(hipStreamSynchronize(d.ekf_race));  // no race still reads the old flags
-      if (d.race_flags) HIPCHK(hipHostFree(d.race_flags));
-      d.race_flags = nullptr;
-      d.race_flags_n = 0;
-      HIPCHK(hipHostMalloc((void**)&d.race_flags, (size_t)nrec * sizeof(int), hipHostMallocCoherent | hipHostMallocMapped));
-      d.race_flags_n = (size_t)nrec;
-    }
-    // a previous call's race may still be reading them: it then only stops later
-    memset(d.race_flags, 0, (size_t)nrec * sizeof(int));
-    if (!d.ekf_race) HIPCHK(hipStreamCreateWithFlags(&d.ekf_race, hipStreamNonBlocking));
-    if (!d.ev_ekf_in) {
-      HIPCHK(hipEventCreateWithFlags(&d.ev_ekf_in, hipEventDisableTiming));
-      HIPCHK(hipEventCreateWithFlags(&d.ev_ekf_out, hipEventDisableTiming));
-    }
-    HIPCHK(hipEventRecord(d.ev_ekf_in, st));
-    HIPCHK(hipStreamWaitEvent(d.ekf_race, d.ev_ekf_in, 0));
-    const char* kname;
-    if (int rc = ekf_seq_launch(dx, nrec, rs, n, dx0, dp0, dq, dr, wt, R, nbuf, (double*)race_states, d.ekf_race,
-                                &kname, nullptr, d.race_flags))
-      return rc;
-    seq_name = kname;
-  }
   const dim3 lanes((unsigned)((nb + 63) / 64), nr);
   // scan of one buffer's hierarchy: every level bottom-up, then the fix-ups top-down; the
   // pass kernels read level 0 (prefixes within workgroups) and level 1 (true prefixes)
@@ -1377,24 +1324,11 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
   hipStream_t side_stream = nullptr;
   int n_batches = 0;                     // hand-over launches so far
   hipStream_t used_streams[kEkfPool] = {};  // the streams they went to (pool mode)
+  std::string seq_name;
   if (handed) HIPCHK(hipMemsetAsync(handed, 0, (size_t)nrec * sizeof(unsigned), st));
   const int overlap = t_tune.ekf_pit_overlap;
   auto hand_over = [&](const dfmi::PitChan* hc, bool final_) -> int {
     if (!t_tune.ekf_pit_seq) return DFMI_OK;
-    if (race) {  // the race's run of every channel: the converged ones' rows stop (flags); at the end,
-                 // wait for it and take the states of those not converged
-      for (int64_t r = 0; r < nrec; ++r)
-        if (hc[r].status == 1) __atomic_store_n(t_ds->race_flags + r, 1, __ATOMIC_RELAXED);
-      if (!final_) return DFMI_OK;
-      for (int64_t r = 0; r < nrec; ++r) nh += hc[r].status != 1;
-      HIPCHK(hipEventRecord(t_ds->ev_ekf_out, t_ds->ekf_race));
-      HIPCHK(hipStreamWaitEvent(st, t_ds->ev_ekf_out, 0));
-      if (nh)
-        hipLaunchKernelGGL(dfmi::ekf_pit_take_kernel, dim3((unsigned)((nbuf * 5 + 255) / 256), nr), dim3(256), 0, st,
-                           (const dfmi::PitChan*)ch, nbuf, (const double*)race_states, dstates);
-      HIPCHK(hipGetLastError());
-      return DFMI_OK;
-    }
     if (!overlap && !final_) return DFMI_OK;  // ekf_pit_overlap 0: every re-run after the passes, on st
     int64_t cnt = 0;
     for (int64_t r = 0; r < nrec; ++r)
@@ -1512,7 +1446,7 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
       HIPCHK(hipStreamWaitEvent(st, t_ds->ev_ekf_out, 0));
     }
   }
-  if (nh) g_last_demod += std::string(" + ") + seq_name + (race ? " (race)" : "") + " x" + std::to_string(nh);
+  if (nh) g_last_demod += std::string(" + ") + seq_name + " x" + std::to_string(nh);
   return DFMI_OK;
 }
 
@@ -1759,9 +1693,6 @@ int dfmi_release_workspaces(void) {
   if (t_ds->pin) HIPCHK(hipHostFree(t_ds->pin));
   t_ds->pin = nullptr;
   t_ds->pin_n = 0;
-  if (t_ds->race_flags) HIPCHK(hipHostFree(t_ds->race_flags));
-  t_ds->race_flags = nullptr;
-  t_ds->race_flags_n = 0;
   return DFMI_OK;
 }
 

@@ -529,16 +529,7 @@ __global__ __launch_bounds__(64) void ekf_rot_kernel(const double* __restrict__ 
                                                       const double* __restrict__ rv, const double* __restrict__ wt,
                                                       int R, int64_t nbuf, double* __restrict__ states,
                                                       DfmiTrigK tk,
-    const int* __restrict__ idx, const int* cancel = nullptr, int prio = 0) {
-  // cancel (optional, the race of ekf_pit_overlap 4): host-coherent pinned flags, cancel[rid] =
-  // 1 once the host saw the channel converge in the parallel-in-time passes; the row stops at
-  // the first snapshot after it reads 1 (those states are not taken). (The passes' own status
-  // words are device memory, not coherent across the XCDs' L2s while both kernels run: a row
-  // polling them never saw the change, r06m.) prio (ekf_pit_race_prio): the waves' issue
-  // priority beside the passes' waves.
-  if (prio == 1) __builtin_amdgcn_s_setprio(1);
-  if (prio == 2) __builtin_amdgcn_s_setprio(2);
-  if (prio >= 3) __builtin_amdgcn_s_setprio(3);
+    const int* __restrict__ idx) {
   const int lane = threadIdx.x & 63;
   const int64_t r0 = (int64_t)blockIdx.x * 4 + (lane >> 4);
   const bool live = r0 < nrec;
@@ -611,7 +602,6 @@ __global__ __launch_bounds__(64) void ekf_rot_kernel(const double* __restrict__ 
 #pragma unroll
         for (int i = 0; i < 5; ++i) states[(rid * nbuf + b) * 5 + i] = st[i];
       }
-      if (cancel && __hip_atomic_load(cancel + rid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 1) return;
     }
 #pragma unroll
     for (int u = 0; u < G; ++u) {

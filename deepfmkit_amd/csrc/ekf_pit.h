@@ -36,9 +36,7 @@
 // ekf_pit_every, and stops when none is left. A channel that stops contracting (or reaches
 // the pass cap) is re-run by the sequential row / lane kernel reading the record in place
 // (ekf_pit_handover_kernel's index list; after the passes by default, ekf_pit_overlap in
-// dfmi_capi.hip) or, racing the passes, taken from a sequential run of every channel started
-// beside them (ekf_pit_take_kernel), so the result never depends on the iteration having
-// converged.
+// dfmi_capi.hip), so the result never depends on the iteration having converged.
 //
 // Layouts (all channel-major, blocks fastest so lane b of a wave reads address b):
 //   xt[r][i][b], wtt[i][b] (sample k = b B + i), xbar[r][c][i][b] (the seeded trajectory:
@@ -1167,18 +1165,6 @@ __global__ __launch_bounds__(64) void ekf_pit_handover_kernel(const PitChan* __r
     }
     base += __popcll(m);
   }
-}
-
-// The race (ekf_pit_overlap 4): a sequential run of every channel (ekf_rot_kernel with its
-// cancel word, into `from`) started beside the passes; each channel the passes did not
-// converge takes its nbuf x 5 states from it. Grid (ceil(nbuf·5 / 256), nrec).
-__global__ __launch_bounds__(256) void ekf_pit_take_kernel(const PitChan* __restrict__ ch, int64_t nbuf,
-                                                           const double* __restrict__ from, double* __restrict__ to) {
-  const int64_t per = nbuf * 5;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t r = blockIdx.y;
-  if (i >= per || ch[r].status == 1) return;
-  to[r * per + i] = from[r * per + i];
 }
 
 }  // namespace dfmi

@@ -4,7 +4,7 @@ spread among them. Per ekf_pit_overlap (3: re-runs launched at the host check on
 pool of high-priority streams beside the passes; 2: one high-priority stream; 1: one
 default-priority stream; 0: after the passes, on the caller's stream) the batch time, against the passes alone (ekf_pit_seq 0) and the NBAD
 channels' sequential run alone (ekf_pit 0). One JSON line per measurement.
-env: NCH (1024), NBAD (64), NS (400000), MODES ("3,2,0"), REPS (2), PRIO (ekf_pit_race_prio, 0)."""
+env: NCH (1024), NBAD (64), NS (400000), MODES ("3,2,0"), REPS (2)."""
 import json
 import os
 import sys
@@ -61,13 +61,12 @@ def main():
         finally:
             for k in tune:
                 _lib.check(lib.dfmi_set_tuning(k.encode(), {"ekf_pit": 1024, "ekf_pit_seq": 1,
-                                                            "ekf_pit_overlap": 0, "ekf_pit_race_prio": 0}[k]), k)
+                                                            "ekf_pit_overlap": 0}[k]), k)
     res = {}
-    prio = int(os.environ.get("PRIO", 0))
     for mode in [int(v) for v in os.environ.get("MODES", "3,2,0").split(",")]:
-        t, kn, out = run(xe, nch, {"ekf_pit_overlap": mode, "ekf_pit_race_prio": prio})
+        t, kn, out = run(xe, nch, {"ekf_pit_overlap": mode})
         res[mode] = out
-        print(json.dumps({"what": "batch", "overlap": mode, "race_prio": prio, "channels": nch, "non_locking": nbad,
+        print(json.dumps({"what": "batch", "overlap": mode, "channels": nch, "non_locking": nbad,
                           "ms": round(t, 3), "kernel": kn}), flush=True)
     t, kn, _ = run(xe, nch, {"ekf_pit_seq": 0})
     print(json.dumps({"what": "passes alone (ekf_pit_seq 0)", "ms": round(t, 3), "kernel": kn}), flush=True)

@@ -51,8 +51,7 @@ class _tune:
     """dfmi_set_tuning for the duration of a block, restoring the defaults."""
     DEFAULTS = {"ekf_row": 1, "ekf_rot": 1, "ekf_pit": 1024, "ekf_pit_min": 4096, "ekf_pit_block": 0,
                 "ekf_pit_passes": 0, "ekf_pit_head": 256, "ekf_pit_fused": 1, "ekf_pit_first": 5,
-                "ekf_pit_every": 2, "ekf_pit_tol": 13, "ekf_pit_stall": 3, "ekf_pit_trace": 0, "ekf_pit_seq": 1,
-                "ekf_pit_overlap": 0, "ekf_pit_race_min": 64}
+                "ekf_pit_every": 2, "ekf_pit_tol": 13, "ekf_pit_stall": 3, "ekf_pit_trace": 0, "ekf_pit_seq": 1}
 
     def __init__(self, lib, **kw):
         self.lib, self.kw = lib, kw
@@ -196,31 +195,6 @@ def test_pit_fallback_only_for_unconverged_channels(lib):
     got, kname, passes = _ekf(lib, xs, 4000, 5)
     assert all(p > 0 for p in passes) and "+" not in kname, (kname, passes)
     assert np.abs(got - seq).max() <= 1e-12
-
-
-def test_pit_race_takes_the_sequential_states(lib):
-    """ekf_pit_overlap 4 (the race): every channel's sequential run (ekf_rot_kernel) starts beside
-    the passes and a row stops once its channel converges. Channels the passes converge keep the
-    passes' states (bit for bit those of the default mode); the ones handed over take the race's,
-    bit for bit their own sequential run's: here an m = 20 record fitted from init_m = 6 (the
-    filter never locks) among four that converge, and, with the pass cap at 2, all five."""
-    import deepfmkit_amd as dfm
-    xs = [_raw(dfm, 6.0, 0.1, 31), _raw(dfm, 4.3, 0.1, 32, psi=0.3, phi=0.7), _raw(dfm, 20.0, 0.1, 33),
-          _raw(dfm, 9.0, 0.1, 34, phi=1.3), _raw(dfm, 6.0, 0.1, 35)]
-    with _tune(lib, ekf_pit=0):
-        seq, _, _ = _ekf(lib, xs, 4000, 5)
-    dflt, kd, pd = _ekf(lib, xs, 4000, 5)
-    with _tune(lib, ekf_pit_overlap=4, ekf_pit_race_min=1):
-        got, kname, passes = _ekf(lib, xs, 4000, 5)
-        print("race", kname, passes, "default", kd, pd)
-        assert passes == pd and passes[2] < 0 and all(p > 0 for i, p in enumerate(passes) if i != 2), passes
-        assert kname.endswith("+ ekf_rot_kernel (race) x1"), kname
-        np.testing.assert_array_equal(got, dflt)
-        np.testing.assert_array_equal(got[2], seq[2])
-        with _tune(lib, ekf_pit_passes=2):
-            cap, kc, pc = _ekf(lib, xs, 4000, 5)
-        assert pc == [-2] * 5 and kc.endswith("+ ekf_rot_kernel (race) x5"), (kc, pc)
-        np.testing.assert_array_equal(cap, seq)
 
 
 def test_pit_trace_and_passes_are_host_side(lib, c5):

@@ -62,6 +62,8 @@ struct Tuning {
   int lm_wide_fused = 1;        // many-harmonic LM with QI from L2 (ndata > lm_wide_lds), the ladder and the seed:
                                 // each trial walks once for ssqf AND coeffs (lm.h wide_full, same bits); 0:
                                 // ssqf-only trials + a second walk at accepted points
+  int seed_wave_split = 1;      // the seed beyond 16 harmonics: the wave as 8 rungs x 8 harmonic shares (seed.h
+                                // SFLAT 3); 0: 8 rungs, every 8-lane group the same whole fit
   int lm_wide_lds = 20;         // many-harmonic LM: QI staged in LDS per lane up to this ndata (0: never): while 8
                                 // waves per CU still fit (20 KB per wave); ndata 20 0.076 vs 0.088 ms per 100k
                                 // segments, but 30 / 40 0.151 / 0.179 vs 0.118 / 0.149 at 5 / 3 waves per CU (r06g)
@@ -955,7 +957,9 @@ int seed_launch(int dev, const double* x, int64_t nrec, int64_t rec_stride, int 
     if ((rc = workspace(dev, "qi_seed", (size_t)2 * ndata * nrec * 8, &qs))) return rc;
     if ((rc = workspace(dev, "dc_seed", (size_t)nrec * 8, &ds_))) return rc;
     auto sk = ndata <= 12 ? dfmi::seed_kernel<12> : ndata <= 16 ? dfmi::seed_kernel<16>
-              : t_tune.lm_wide ? (t_tune.lm_wide_fused ? dfmi::seed_kernel<dfmi::kWideNdF> : dfmi::seed_kernel<dfmi::kWideNd>)
+              : t_tune.lm_wide ? (t_tune.seed_wave_split ? dfmi::seed_kernel<dfmi::kWideNdF, 3>
+                                  : t_tune.lm_wide_fused ? dfmi::seed_kernel<dfmi::kWideNdF>
+                                                         : dfmi::seed_kernel<dfmi::kWideNd>)
                                : dfmi::seed_kernel<0>;
     // the many-harmonic demodulation where its geometry holds (16-B rows, 128 <= L <= 256):
     // the bulk's own QI for buffer 0, and a fold with 10 wave loads in flight instead of the
@@ -1103,6 +1107,7 @@ const std::map<std::string, Knob>& knobs() {
       {"lm_wide", {&Tuning::lm_wide, {0, 1}}},
       {"lm_wide_lds", {&Tuning::lm_wide_lds, {}}},
       {"lm_wide_fused", {&Tuning::lm_wide_fused, {0, 1}}},
+      {"seed_wave_split", {&Tuning::seed_wave_split, {0, 1}}},
       {"lm_split", {&Tuning::lm_split, {0, 2, 4}}},
       {"lm_split_from", {&Tuning::lm_split_from, {}}},
       {"demod_wide_half", {&Tuning::demod_wide_half, {0, 1}}},

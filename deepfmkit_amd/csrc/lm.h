@@ -1207,7 +1207,7 @@ struct QLdsG {  // QI of one segment in a wave's LDS tile [component][S segments
   DFMI_HDI double qs(int h) const { return p[(nd + h) * S]; }
 };
 
-// sum of v over the P lanes of a group (P = 1, 2, 4: lanes r = lane % P), the same bits on
+// sum of v over the P lanes of a group (P = 1, 2, 4, 8: lanes r = lane % P), the same bits on
 // every lane of the group (each butterfly level adds two commuted operands)
 template <int P>
 __device__ __forceinline__ double group_sum(double v) {
@@ -1225,7 +1225,14 @@ __device__ __forceinline__ double group_sum(double v) {
     const int hi2 = __builtin_amdgcn_update_dpp(0, hi, 0x4E, 0xF, 0xF, false);
     v += __builtin_bit_cast(double, ((long long)hi2 << 32) | (unsigned)lo2);
   }
-  static_assert(P == 1 || P == 2 || P == 4, "P");
+  if constexpr (P >= 8) {  // the two quads of a half-row: lane i <- 7 - i (the other quad's sum)
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = (int)b, hi = (int)(b >> 32);
+    const int lo3 = __builtin_amdgcn_update_dpp(0, lo, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    const int hi3 = __builtin_amdgcn_update_dpp(0, hi, 0x141, 0xF, 0xF, false);
+    v += __builtin_bit_cast(double, ((long long)hi3 << 32) | (unsigned)lo3);
+  }
+  static_assert(P == 1 || P == 2 || P == 4 || P == 8, "P");
   return v;
 }
 
@@ -1311,6 +1318,63 @@ __device__ __forceinline__ void wide_walk_part(const QF& q, int nd, double m, do
     sj = s2;
   }
 }
+
+// The many-harmonic seed's evaluator (FLAT 3: one record's buffer 0 fitted by a whole wave, 8
+// rungs x P = 8 shares): wide_full's sums over this lane's share of the harmonics, reduced over
+// the P lanes; a trial carries the coeffs (the ladder shuffles the taken rung's Eval, so an
+// accepted trial needs no second walk). A lane's walk is the Miller passes + its share: at
+// ndata 62 ~1/3 of one lane's full walk. Not bit-identical to WideEval (the sums' order).
+template <int P, typename QF>
+struct PartFullEval {
+  const QF& q;
+  int nd;
+  const DfmiTrigK& k;
+  int r;  // this lane's share
+  using Trial = WideFull;
+  __device__ __forceinline__ double trial(const double (&p)[4], Trial& t) {
+    double sph, cph, s1, c1;
+    dfmi_sincos_auto(p[2], k, &sph, &cph);
+    dfmi_sincos_auto(p[3], k, &s1, &c1);
+    const double a = p[0];
+    const double ac = a * cph, as = a * sph;
+    const double cph0 = (a != 0.0) ? cph : 0.0, sph0 = (a != 0.0) ? sph : 0.0;
+    double ss = 0.0, a00 = 0.0, a01 = 0.0, a02 = 0.0, a11 = 0.0, a12 = 0.0, a22 = 0.0, a33 = 0.0;
+    double g0 = 0.0, g1 = 0.0, g2 = 0.0, g3 = 0.0;
+    wide_walk_part<P>(q, nd, p[1], p[3], c1, s1, k, r,
+                      [&](int j, double Jm1, double Jj, double Jp1, double cj, double sj, double Q, double I) {
+                        const double aP = quarter_turn(j, ac, as), aD = quarter_turn(j + 1, ac, as);
+                        const double c = aP * Jj;
+                        const double rq = fma(-c, cj, Q);
+                        const double ri = fma(c, sj, I);
+                        ss = fma(rq, rq, ss);
+                        ss = fma(ri, ri, ss);
+                        const double u0 = quarter_turn(j, cph0, sph0) * Jj;
+                        const double u1 = aP * (0.5 * (Jm1 - Jp1));
+                        const double u2 = aD * Jj;
+                        const double A = fma(cj, rq, -(sj * ri));
+                        const double B = fma(sj, rq, cj * ri);
+                        a00 = fma(u0, u0, a00);
+                        a01 = fma(u0, u1, a01);
+                        a02 = fma(u0, u2, a02);
+                        a11 = fma(u1, u1, a11);
+                        a12 = fma(u1, u2, a12);
+                        a22 = fma(u2, u2, a22);
+                        const double jc = (double)j * c;
+                        a33 = fma(jc, jc, a33);
+                        g0 = fma(u0, A, g0);
+                        g1 = fma(u1, A, g1);
+                        g2 = fma(u2, A, g2);
+                        g3 = fma(-jc, B, g3);
+                      });
+    t.e = Eval{group_sum<P>(ss), group_sum<P>(a00), group_sum<P>(a01), group_sum<P>(a02), 0.0, group_sum<P>(a11),
+               group_sum<P>(a12), 0.0, group_sum<P>(a22), 0.0, group_sum<P>(a33), group_sum<P>(g0),
+               group_sum<P>(g1), group_sum<P>(g2), group_sum<P>(g3)};
+    return t.e.ssq;
+  }
+  __device__ __forceinline__ void accept(const double (&)[4], const Trial& t, Eval& e) { e = t.e; }
+  __device__ __forceinline__ void solve(const Eval& e, double lam, double (&dp)[4]) { damped_solve_block(e, lam, dp); }
+  __device__ __forceinline__ static double ssq_of(const Trial& t) { return t.e.ssq; }
+};
 
 template <int P, typename QF>
 struct PartEval {
@@ -1431,6 +1495,7 @@ __device__ __forceinline__ T shfl_any(T v, int src) {
 }
 
 constexpr int kLadderLanes = 8;  // lanes per segment of the parallel-ladder descent (= the default ladder)
+constexpr int kSeedShares = 8;   // FLAT 3 (the many-harmonic seed): harmonic shares per rung, 8 x 8 = the wave
 
 // fit.py:208-258 (_run_lma_fit) with the lambda ladder evaluated in parallel. The LPS
 // lanes of a lane group (lanes LPS·g .. LPS·g + LPS-1 of the wave) hold the same segment
@@ -1453,16 +1518,20 @@ constexpr int kLadderLanes = 8;  // lanes per segment of the parallel-ladder des
 // rung `base` of the current iteration): lm_descend_ladder's loop. (Round 4 also resumed
 // one-lane descents here that parked at their first rejected rung, lm_park_kernel: same
 // bits, LM 41-45 us against 36 us, removed)
-template <int LPS, typename Ev>
+// P > 1 (the many-harmonic seed, FLAT 3): each rung is evaluated by P adjacent lanes, each over
+// a share of the harmonics (PartFullEval: the P lanes of a rung end with the same bits), so the
+// group is LPS x P lanes: lane = g0 + rung P + share.
+template <int LPS, int P = 1, typename Ev>
 __device__ __forceinline__ double lm_ladder_resume(Ev&& ev, double (&p)[4], const LMConst& c, Eval& e, int it,
                                                    int base, bool live) {
   using Trial = typename std::decay_t<Ev>::Trial;
   constexpr int NT = (int)(sizeof(Trial) / sizeof(double));
   static_assert(sizeof(Trial) == NT * sizeof(double), "trial state: doubles only");
   static_assert(LPS == 2 || LPS == 4 || LPS == 8 || LPS == 16, "LPS");
+  static_assert(P == 1 || (LPS * P <= 64 && (P & (P - 1)) == 0), "P");
   const int lane = (int)__lane_id();
-  const int r = lane & (LPS - 1);
-  const int g0 = lane & ~(LPS - 1);
+  const int r = (lane / P) & (LPS - 1);
+  const int g0 = lane & ~(LPS * P - 1);
   bool active = live && it < c.max_steps && base < c.n_lambda;
   while (__ballot(active) != 0) {
     const int rung = base + r;
@@ -1475,8 +1544,15 @@ __device__ __forceinline__ double lm_ladder_resume(Ev&& ev, double (&p)[4], cons
     bool improved = false;
     if (step) improved = ev.trial(pt, tt) < e.ssq;
     const uint64_t imp = __ballot(improved);
-    const uint64_t gm = (imp >> g0) & ((1ull << LPS) - 1);
-    const int src = gm ? g0 + __builtin_ctzll(gm) : lane;
+    uint64_t gm;
+    if constexpr (P == 1) {
+      gm = (imp >> g0) & ((1ull << LPS) - 1);
+    } else {  // rung k improved: its share-0 lane's bit (its P lanes agree)
+      gm = 0;
+#pragma unroll
+      for (int k = 0; k < LPS; ++k) gm |= ((imp >> (g0 + k * P)) & 1ull) << k;
+    }
+    const int src = gm ? g0 + __builtin_ctzll(gm) * P + (lane & (P - 1)) : lane;
     if (__ballot(gm != 0 && active) != 0) {  // some group accepts: fetch the taken rung's state
 #pragma unroll
       for (int i = 0; i < 4; ++i) pt[i] = shfl_any(pt[i], src);
@@ -1511,7 +1587,7 @@ __device__ __forceinline__ double lm_ladder_resume(Ev&& ev, double (&p)[4], cons
   return e.ssq;
 }
 
-template <int LPS, typename Ev>
+template <int LPS, int P = 1, typename Ev>
 __device__ __forceinline__ double lm_descend_ladder(Ev&& ev, double (&p)[4], const LMConst& c, bool live = true) {
   using Trial = typename std::decay_t<Ev>::Trial;
   Eval e;
@@ -1520,7 +1596,7 @@ __device__ __forceinline__ double lm_descend_ladder(Ev&& ev, double (&p)[4], con
     ev.trial(p, t0);
     ev.accept(p, t0, e);
   }
-  return lm_ladder_resume<LPS>(ev, p, c, e, 0, 0, live);
+  return lm_ladder_resume<LPS, P>(ev, p, c, e, 0, 0, live);
 }
 
 // fit.py:260-320 (_find_best_initial_guess). jtab: n_grid rows of J_1..J_ndata(mtry)
@@ -1664,6 +1740,7 @@ template <int FLAT, typename Ev>
 DFMI_HDI double descend_t(Ev&& ev, double (&pp)[4], const LMConst& c) {
 #if defined(__HIP_DEVICE_COMPILE__)
   if constexpr (FLAT == 2) return lm_descend_ladder<kLadderLanes>(ev, pp, c);
+  else if constexpr (FLAT == 3) return lm_descend_ladder<kLadderLanes, kSeedShares>(ev, pp, c);
   else
 #endif
   if constexpr (FLAT == 1) return lm_descend_flat(ev, pp, c);
@@ -1683,6 +1760,7 @@ DFMI_HDI int fit_finish_t(Ev&& ev, QF&& Q, int ndata, const double* __restrict__
     double g[4];
 #if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (FLAT == 2) m_grid_seed_lanes<kLadderLanes>(Q, ndata, jtab, c, g);
+    else if constexpr (FLAT == 3) m_grid_seed_lanes<kLadderLanes * kSeedShares>(Q, ndata, jtab, c, g);
     else
 #endif
       m_grid_seed(Q, ndata, jtab, c, g);
@@ -1727,6 +1805,12 @@ template <int NDMAX, typename QE, typename QM, int FLAT = 1>
 __host__ __device__ __forceinline__ int fit_segment_q2(const QE& qe, const QM& qm, int ndata,
                                                     const double* __restrict__ jtab, const LMConst& c,
                                                     double (&p)[4], double& ssq_out) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (wide_nd(NDMAX) && FLAT == 3) {  // the many-harmonic seed: a whole wave, harmonic shares
+    PartFullEval<kSeedShares, QE> ev{qe, ndata, c.trig, (int)(__lane_id() & (kSeedShares - 1))};
+    return fit_segment_t<FLAT>(ev, qm, ndata, jtab, c, p, ssq_out);
+  } else
+#endif
   if constexpr (wide_nd(NDMAX)) {  // many harmonics: closed form over the lean Miller walk
     WideEval<QE, NDMAX == kWideNdF> ev{qe, ndata, c.trig};
     return fit_segment_t<FLAT>(ev, qm, ndata, jtab, c, p, ssq_out);

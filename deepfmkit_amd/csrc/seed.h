@@ -34,7 +34,10 @@ constexpr int kSeedFlat = 2;
 // tabT (not null): the many-harmonic demodulation (demod.h wide_seed_segment, basis_table_wide
 // with `no` output slices; dynamic LDS L + 4 doubles): the record's buffer 0 gets the QI the
 // bulk demod_wide_kernel would give it.
-template <int NDMAX>
+// SFLAT: the seed's descent — kSeedFlat (8 rungs by 8-lane groups, every group the same fit) or,
+// beyond 16 harmonics (tuning seed_wave_split), 3: the wave's 64 lanes as 8 rungs x 8 harmonic
+// shares (lm.h PartFullEval), one fit.
+template <int NDMAX, int SFLAT = kSeedFlat>
 __global__ __launch_bounds__(64) void seed_kernel(const double* __restrict__ x, int64_t rec_stride, int R, int L,
                                                   int ndata, double w0, const double* __restrict__ tab,
                                                   double* __restrict__ qis, double* __restrict__ dcs, int64_t nrec,
@@ -75,7 +78,7 @@ __global__ __launch_bounds__(64) void seed_kernel(const double* __restrict__ x, 
   const QGlobal qs{ndata <= 128 ? qsh : qis + r, ndata <= 128 ? 1 : nrec, ndata};
   // NDMAX == kWideNd / kWideNdF (more than 16 harmonics, lm_wide / lm_wide_fused): the
   // many-harmonic evaluation, as the bulk LM that this seed's result seeds
-  const int st = fit_segment_q<(wide_nd(NDMAX) ? NDMAX : kSeedPath), QGlobal, kSeedFlat>(qs, ndata, jtab, c, p, ssq);
+  const int st = fit_segment_q<(wide_nd(NDMAX) ? NDMAX : kSeedPath), QGlobal, SFLAT>(qs, ndata, jtab, c, p, ssq);
   if (lane != 0) return;
   const int64_t sidx = r * nbuf;
   out[0 * out_ld + sidx] = p[0];

@@ -8,7 +8,9 @@ HBM fraction at 8R + 8(2 ndata + 1) bytes per segment, and the status-0 fraction
 The binned demodulation folds each segment into L phase bins (R adds) and contracts the bins
 with the basis (2 ndata L FMAs, L = 200): at ndata 62 that is 24,800 FMAs per 4,000 samples
 read, so the demodulation stays HBM-bound where a per-sample basis product (4 ndata R flops)
-would not; what grows with ndata is the LM (Bessel orders, harmonic sums)."""
+would not; what grows with ndata is the LM (Bessel orders, harmonic sums).
+env: MTRUE (the record's m, 6.0; the step's buffer 0 is fitted from the default guess m = 6 either
+way), NDS (the ndata list)."""
 import json
 import sys
 import os
@@ -32,8 +34,10 @@ def main():
     tune = dict(kv.split("=") for kv in sys.argv[2].split("+")) if len(sys.argv) > 2 and sys.argv[2] else {}
     for k, v in tune.items():  # e.g. lm_onepass=0
         _lib.check(lib.dfmi_set_tuning(k.encode(), int(v)), "tune")
+    m_true = float(os.environ.get("MTRUE", 6.0))  # the record's m (31.4: the reference quickstart's)
+    nds = [int(v) for v in os.environ.get("NDS", "10,12,16,20,30,40,62").split(",")]
     x = torch.empty(nseg * R, dtype=torch.float64, device=dev)
-    bench.gen_shard(torch, dev, 0, nseg, R, seed=bench.SEED, out=x)
+    bench.gen_shard(torch, dev, 0, nseg, R, seed=bench.SEED, m_true=m_true, out=x)
     w0 = w0_of(1000.0, 200000.0)
     cfg = F.lm_config()
     stream = torch.cuda.current_stream()
@@ -52,14 +56,14 @@ def main():
         ev1.synchronize()
         return ev0.elapsed_time(ev1) / n
 
-    for nd in (10, 12, 16, 20, 30, 40, 62):
+    for nd in nds:
         rows = torch.empty((nseg, lib.dfmi_qi_row_stride(nd)), dtype=torch.float64, device=dev)
         qi = torch.empty((2 * nd, nseg), dtype=torch.float64, device=dev)
         dcb = torch.empty(nseg, dtype=torch.float64, device=dev)
         lo = torch.empty((4, nseg), dtype=torch.float64, device=dev)
         ls = torch.empty(nseg, dtype=torch.float64, device=dev)
         lk = torch.empty(nseg, dtype=torch.int32, device=dev)
-        g = torch.tensor([1.0, 6.0, 0.0, 0.0], dtype=torch.float64, device=dev)
+        g = torch.tensor([1.0, m_true, 0.0, 0.0], dtype=torch.float64, device=dev)
 
         def step():
             _lib.check(lib.dfmi_nls_record(x.data_ptr(), 1, nseg * R, nseg, R, nd, w0, 0, _lib.ptr(guess), 1,
@@ -93,7 +97,7 @@ def main():
         lm_ms = timed(lm, 60)
         bytes_seg = 8 * R + 8 * (2 * nd + 1)
         print(json.dumps({
-            "ndata": nd, "segments": nseg, "R": R, "tune": tune,
+            "ndata": nd, "m": m_true, "segments": nseg, "R": R, "tune": tune,
             "step_ms": round(step_ms, 4), "segments_per_s": round(nseg / step_ms * 1e3, 1),
             "step_demod_kernel": step_kernel, "demod_layout": layout, "demod_ms": round(demod_ms, 4), "demod_kernel": demod_kernel,
             "demod_hbm_frac": round(nseg * bytes_seg / (demod_ms * 1e-3) / 8e12, 4),

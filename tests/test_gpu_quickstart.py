@@ -94,3 +94,28 @@ def test_quickstart_fit(quick, nd, mode):
     rep = compare_fit(ours, ref, tol=record_tol(nd, qi, ref), min_status_match=1.0)
     print(f"quickstart ndata {nd} {mode}: max |d| amp {rep['amp']:.2e} m {rep['m']:.2e} phi {rep['phi']:.2e} "
           f"psi {rep['psi']:.2e}")
+
+
+@pytest.mark.parametrize("split", [1, 0])
+def test_quickstart_seed_paths(quick, split):
+    """Buffer 0's fit beyond 16 harmonics by the whole wave as 8 rungs x 8 harmonic shares
+    (seed_wave_split 1, the default: seed.h SFLAT 3, lm.h PartFullEval) and by 8-lane groups
+    each running the whole fit (0): both through the m-grid seed (status 1) and every buffer
+    within the gates of the reference's chunk-size-1 outputs at ndata 62."""
+    meta, npz = quick
+    from deepfmkit_amd import _lib
+    from deepfmkit_amd.fitters import StandardNLSFitter
+    lib = _lib.load()
+    dff, label, _ = quickstart_framework()
+    _lib.check(lib.dfmi_set_tuning(b"seed_wave_split", split), "tune")
+    try:
+        df = StandardNLSFitter({"n": 20}).fit(dff.raws[label], parallel=True, ndata=62)
+    finally:
+        _lib.check(lib.dfmi_set_tuning(b"seed_wave_split", 1), "tune")
+    ours = {k: df[k].to_numpy() for k in COLS}
+    ref = {k: npz[f"nd62_c1_{k}"] for k in COLS}
+    assert ours["fitok"][0] == 1
+    np.testing.assert_array_equal(ours["fitok"], ref["fitok"])
+    rep = compare_fit(ours, ref, tol=record_tol(62, npz["qi62"], ref), min_status_match=1.0)
+    print(f"seed_wave_split {split}: max |d| amp {rep['amp']:.2e} m {rep['m']:.2e} phi {rep['phi']:.2e} "
+          f"psi {rep['psi']:.2e}")

@@ -1319,6 +1319,74 @@ __device__ __forceinline__ void wide_walk_part(const QF& q, int nd, double m, do
   }
 }
 
+// wide_walk_part in ONE Miller pass (the seed's evaluator): the P lanes of a rung walk the same
+// recurrence (the same trial m), so each stores every f_k it forms in the rung's LDS row `fb`
+// while summing the normalisation as pass 1 does, then reads back its share's f_{lo-1} ..
+// f_{hi+1}: the recurrence runs M steps per evaluation instead of M + (M - lo), with the same
+// values (bit for bit wide_walk_part's J). kFbMax bounds M where the lean walk applies
+// (M log2(2M/m + 1) < 590 with M >= 1.1 m: M < 351); beyond, wide_walk_part.
+constexpr int kFbMax = 356;
+template <int P, typename QF, typename Body>
+__device__ __forceinline__ void wide_walk_share(const QF& q, int nd, double m, double psi, double c1, double s1,
+                                                const DfmiTrigK& tk, int r, double* fb, Body&& body) {
+  const int len = (nd + P - 1) / P;
+  const int hi = nd - r * len;
+  const int lo = hi - len + 1 > 1 ? hi - len + 1 : 1;
+  const int M = dfmi_bessel_start(nd + 1, m);
+  const double tox = 2.0 / m;
+  const bool fast = m > 0.0 && m >= DFMI_BES_TINY && m < 1.0e5 && !dfmi_bessel_use_large(m, nd + 1) &&
+                    (float)M * log2f((float)fma((double)M, tox, 1.0)) < (float)(DFMI_BES_BIG_EXP - 10) &&
+                    M + 2 <= kFbMax;
+  if (!fast) {
+    wide_walk_part<P>(q, nd, m, psi, c1, s1, tk, r, body);
+    return;
+  }
+  double fp1 = 0.0, f = 1.0, S = 2.0;
+  double kd = (double)M;
+  fb[M + 1] = 0.0;
+  fb[M] = 1.0;
+  for (int k = M; k > 2; k -= 2) {
+    double fm1 = fma(kd * tox, f, -fp1);
+    fb[k - 1] = fm1;
+    fp1 = f;
+    f = fm1;
+    kd -= 1.0;
+    fm1 = fma(kd * tox, f, -fp1);
+    fb[k - 2] = fm1;
+    fp1 = f;
+    f = fm1;
+    kd -= 1.0;
+    S += 2.0 * f;
+  }
+  {
+    double fm1 = fma(kd * tox, f, -fp1);  // f_1
+    fb[1] = fm1;
+    fp1 = f;
+    f = fm1;
+    kd -= 1.0;
+    fm1 = fma(kd * tox, f, -fp1);  // f_0
+    fb[0] = fm1;
+    S += fm1;
+  }
+  if (hi < 1) return;  // no share (nd < P)
+  const double invS = 1.0 / S;
+  double sn, cn;
+  dfmi_sincos_auto((double)hi * psi, tk, &sn, &cn);
+  double Jp1 = fb[hi + 1] * invS;
+  double J0 = fb[hi] * invS;
+  double cj = cn, sj = sn;
+  for (int j = hi; j >= lo; --j) {
+    const double Jm1 = fb[j - 1] * invS;
+    body(j, Jm1, J0, Jp1, cj, sj, q.qc(j - 1), q.qs(j - 1));
+    Jp1 = J0;
+    J0 = Jm1;
+    const double c2 = fma(cj, c1, sj * s1);
+    const double s2 = fma(sj, c1, -(cj * s1));
+    cj = c2;
+    sj = s2;
+  }
+}
+
 // The many-harmonic seed's evaluator (FLAT 3: one record's buffer 0 fitted by a whole wave, 8
 // rungs x P = 8 shares): wide_full's sums over this lane's share of the harmonics, reduced over
 // the P lanes; a trial carries the coeffs (the ladder shuffles the taken rung's Eval, so an
@@ -1340,7 +1408,10 @@ struct PartFullEval {
     const double cph0 = (a != 0.0) ? cph : 0.0, sph0 = (a != 0.0) ? sph : 0.0;
     double ss = 0.0, a00 = 0.0, a01 = 0.0, a02 = 0.0, a11 = 0.0, a12 = 0.0, a22 = 0.0, a33 = 0.0;
     double g0 = 0.0, g1 = 0.0, g2 = 0.0, g3 = 0.0;
-    wide_walk_part<P>(q, nd, p[1], p[3], c1, s1, k, r,
+    // the rung's LDS row for the one-pass walk (64 / P rungs of P lanes: the whole wave)
+    __shared__ double fbuf[64 / P][kFbMax];
+    double* fb = fbuf[__lane_id() / P];
+    wide_walk_share<P>(q, nd, p[1], p[3], c1, s1, k, r, fb,
                       [&](int j, double Jm1, double Jj, double Jp1, double cj, double sj, double Q, double I) {
                         const double aP = quarter_turn(j, ac, as), aD = quarter_turn(j + 1, ac, as);
                         const double c = aP * Jj;

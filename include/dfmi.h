@@ -330,6 +330,19 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
  * channel keeps its last pass's states instead of the sequential kernel's), "ekf_pit_head"
  * (samples the sequential EKF seeds the trajectory with, default 256), "ekf_pit_fused" (1
  * [default]: the EKF and the next pass's fold in one kernel per pass; 0: separate kernels),
+ * "ekf_pit_slow_from" (pass from which the rule's "too slow to meet the bound within the
+ * cap" extrapolation counts, default 16), "ekf_pit_overlap" (where the sequential re-runs of
+ * handed-over channels go: 0 [default] one launch after the passes on the caller's stream; 3 /
+ * 2 / 1 at each host check on a pool of three / one high- / one default-priority stream beside
+ * the passes — measured slower; same states), "lm_wide" (1 [default]: beyond 16 harmonics the
+ * many-harmonic LM, closed-form sums over a lean Miller walk; 0: the literal general path;
+ * rounding only), "lm_wide_lds" (the largest ndata whose QI the many-harmonic LM stages in LDS
+ * per lane, default 20; same bits), "lm_wide_fused" (1 [default]: one walk per trial for ssqf
+ * and coeffs beyond lm_wide_lds, in the ladder and in the seed; same bits), "lm_split" /
+ * "lm_split_from" (0 [default] / 41: P = 2 or 4 lanes per segment from that ndata — measured
+ * slower; rounding only), "seed_wave_split" (1 [default]: the seed beyond 16 harmonics fitted by
+ * the whole wave as 8 lambda rungs x 8 harmonic shares; 0: 8-lane groups each running the
+ * whole fit; rounding only),
  * "probe" (1 =
  * diagnostics timestamp buffer on the current device, dfmi_probe_read). */
 int dfmi_set_tuning(const char* key, int64_t value);

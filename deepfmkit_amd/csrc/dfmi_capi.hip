@@ -62,6 +62,8 @@ struct Tuning {
   int lm_wide_fused = 1;        // many-harmonic LM with QI from L2 (ndata > lm_wide_lds), the ladder and the seed:
                                 // each trial walks once for ssqf AND coeffs (lm.h wide_full, same bits); 0:
                                 // ssqf-only trials + a second walk at accepted points
+  int lm_ladder_split = 4;      // the ladder beyond 16 harmonics for at most this many items per CU: one wave per
+                                // item as 8 rungs x 8 harmonic shares (lm.h PartFullEval); 0 = 8 lanes per item
   int seed_wave_split = 1;      // the seed beyond 16 harmonics: the wave as 8 rungs x 8 harmonic shares (seed.h
                                 // SFLAT 3); 0: 8 rungs, every 8-lane group the same whole fit
   int lm_wide_lds = 20;         // many-harmonic LM: QI staged in LDS per lane up to this ndata (0: never): while 8
@@ -831,7 +833,13 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
            : nd_sel <= 16 ? dfmi::lm_ladder_kernel<16, false, false>
            : wide && t_tune.lm_wide_fused ? dfmi::lm_ladder_kernel<dfmi::kWideNdF, false, false>
            : wide ? dfmi::lm_ladder_kernel<dfmi::kWideNd, false, false> : dfmi::lm_ladder_kernel<0, false, false>;
-    const int64_t lgrid = (lanes * dfmi::kLadderLanes + block - 1) / block;
+    // beyond 16 harmonics, while at most lm_ladder_split x CUs items: one wave per item, its 64
+    // lanes 8 rungs x 8 harmonic shares (lm.h PartFullEval, as the seed)
+    const bool wsplit = !rows && wide && t_tune.lm_wide_fused && t_tune.lm_ladder_split &&
+                        lanes <= (int64_t)t_tune.lm_ladder_split * t_ds->n_cu;
+    if (wsplit) lk = chain ? dfmi::lm_ladder_kernel<dfmi::kWideNdF, true, false, 64>
+                           : dfmi::lm_ladder_kernel<dfmi::kWideNdF, false, false, 64>;
+    const int64_t lgrid = (lanes * (wsplit ? 64 : dfmi::kLadderLanes) + block - 1) / block;
     hipLaunchKernelGGL(lk, dim3((unsigned)lgrid), dim3(block), 0, st, qi, qi_ld, ndata, nrec, nbuf, first, nitems,
                        nchunk, guess_dev, g_rec, g_comp, ginl, use_inline, jtab, c, out, out_ld, status);
     HIPCHK(hipGetLastError());
@@ -1108,6 +1116,7 @@ const std::map<std::string, Knob>& knobs() {
       {"lm_wide_lds", {&Tuning::lm_wide_lds, {}}},
       {"lm_wide_fused", {&Tuning::lm_wide_fused, {0, 1}}},
       {"seed_wave_split", {&Tuning::seed_wave_split, {0, 1}}},
+      {"lm_ladder_split", {&Tuning::lm_ladder_split, {}}},
       {"lm_split", {&Tuning::lm_split, {0, 2, 4}}},
       {"lm_split_from", {&Tuning::lm_split_from, {}}},
       {"demod_wide_half", {&Tuning::demod_wide_half, {0, 1}}},

@@ -2159,14 +2159,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void lm
 // [first, first + nitems), warm start within a chunk, fitters.py:13-60); ROWS: QI as
 // demodulation rows (chunk size 1; dc copied into out[4] as lm_chunks_kernel does).
 // Lane 0 of each group writes the results. A wave holds 64 / kLadderLanes items.
-template <int NDMAX, bool CHAIN, bool ROWS>
+// LPSI = 64 (many harmonics, the one-walk evaluator: tuning lm_ladder_split): one item per wave,
+// each λ rung evaluated by 8 lanes over harmonic shares (FLAT 3, as the seed), the segment's QI
+// staged in LDS for every fit.
+template <int NDMAX, bool CHAIN, bool ROWS, int LPSI = kLadderLanes>
 __global__ __launch_bounds__(64) void lm_ladder_kernel(
     const double* __restrict__ qi, int64_t qi_ld, int ndata, int64_t nrec, int64_t nbuf, int64_t first,
     int64_t nitems, int64_t nchunk, const double* __restrict__ guess, int64_t g_rec, int64_t g_comp,
     GuessInline ginl, int use_inline, const double* __restrict__ jtab, LMConst c, double* __restrict__ out,
     int64_t out_ld, int32_t* __restrict__ status) {
   static_assert(!(ROWS && CHAIN), "row layout: chunk size 1 only");
-  constexpr int LPS = kLadderLanes;
+  static_assert(LPSI == kLadderLanes || (LPSI == 64 && wide_nd(NDMAX) && !ROWS), "wave-split ladder");
+  constexpr int LPS = LPSI;
+  constexpr int FL = LPSI == 64 ? 3 : 2;
   constexpr bool kQReg = NDMAX > 0 && nd_exact(NDMAX);
   const int64_t id = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPS;
   if (id >= nrec * nchunk) return;  // whole groups leave together
@@ -2198,8 +2203,8 @@ __global__ __launch_bounds__(64) void lm_ladder_kernel(
       qr.load(qm);
       st = fit_segment_q2<NDMAX, QRegs<nd_cap(NDMAX)>, std::decay_t<decltype(qm)>, 2>(qr, qm, ndata, jtab, c, p, ssq);
     } else {
-      st = fit_segment_q2<NDMAX, std::decay_t<decltype(qm)>, std::decay_t<decltype(qm)>, 2>(qm, qm, ndata, jtab, c, p,
-                                                                                          ssq);
+      st = fit_segment_q2<NDMAX, std::decay_t<decltype(qm)>, std::decay_t<decltype(qm)>, FL>(qm, qm, ndata, jtab, c, p,
+                                                                                           ssq);
     }
     if (lead) {
       out[0 * out_ld + sidx] = p[0];
@@ -2261,6 +2266,20 @@ __global__ __launch_bounds__(64) void lm_ladder_kernel(
         out[5 * out_ld + s0 + t] = ssq;
         status[s0 + t] = st;
       }
+    }
+  } else if constexpr (LPSI == 64) {
+    // one segment per wave: its QI into LDS (2 ndata doubles; beyond 128 harmonics from global)
+    __shared__ double qsh[2 * 128];
+    for (int64_t t = 0; t < len; ++t) {
+      if (ndata <= 128) {
+        __builtin_amdgcn_wave_barrier();  // the previous fit's reads are done (one wave, in order)
+        for (int i = (int)threadIdx.x; i < 2 * ndata; i += 64) qsh[i] = qi[(int64_t)i * qi_ld + s0 + t];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      const QGlobal q{ndata <= 128 ? qsh : qi + s0 + t, ndata <= 128 ? 1 : qi_ld, ndata};
+      fit(q, s0 + t);
     }
   } else {
     for (int64_t t = 0; t < len; ++t) {  // warm-start chain (sequential / n_cores); len 1: chunk size 1

@@ -342,7 +342,9 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
  * "lm_split_from" (0 [default] / 41: P = 2 or 4 lanes per segment from that ndata — measured
  * slower; rounding only), "seed_wave_split" (1 [default]: the seed beyond 16 harmonics fitted by
  * the whole wave as 8 lambda rungs x 8 harmonic shares; 0: 8-lane groups each running the
- * whole fit; rounding only),
+ * whole fit; rounding only), "lm_ladder_split" (the ladder beyond 16 harmonics for at most this
+ * many items per CU, default 4: one wave per item as 8 rungs x 8 harmonic shares; 0 = 8 lanes
+ * per item; rounding only),
  * "probe" (1 =
  * diagnostics timestamp buffer on the current device, dfmi_probe_read). */
 int dfmi_set_tuning(const char* key, int64_t value);

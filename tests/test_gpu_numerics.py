@@ -80,6 +80,7 @@ def restore_ladder():
     lib = _lib.load()
     yield lib
     _lib.check(lib.dfmi_set_tuning(b"lm_ladder", 32), "dfmi_set_tuning")
+    _lib.check(lib.dfmi_set_tuning(b"lm_ladder_split", 4), "dfmi_set_tuning")
 
 
 @pytest.mark.parametrize("nd", [10, 7, 30])
@@ -90,7 +91,10 @@ def test_lm_ladder_bit_identical(restore_ladder, nd):
     _fit_sequential and of n_cores chunks, for a small chunk-size-1 record (row layout),
     and for dfmi_lm's per-segment guesses — incl. noise-only buffers that take the m-grid
     retry (status 1/2), the register path (ndata 10 exact, 7 masked) and the general
-    path (ndata 30)."""
+    path (ndata 30). Beyond 16 harmonics the ladder's small batches default to one wave per
+    segment, 8 rungs x 8 harmonic shares (lm_ladder_split): sums in another order, so that form
+    is held to the one-lane descent's status and, on status-0 fits, to 1e-7 (its parity against
+    the reference: tests/test_gpu_quickstart.py), and the bit identity to lm_ladder_split 0."""
     import torch
     from deepfmkit_amd import _lib
     from deepfmkit_amd import fit as F
@@ -110,8 +114,9 @@ def test_lm_ladder_bit_identical(restore_ladder, nd):
     x = torch.stack(recs).contiguous()
     st = torch.cuda.current_stream().cuda_stream
     res = {}
-    for ladder in (32, 0):
+    for ladder, split in ((32, 0), (0, 0), (32, 4)):
         _lib.check(lib.dfmi_set_tuning(b"lm_ladder", ladder), "dfmi_set_tuning")
+        _lib.check(lib.dfmi_set_tuning(b"lm_ladder_split", split), "dfmi_set_tuning")
         out = []
         for kw in (dict(parallel=False), dict(parallel=True, n_cores=4), dict(parallel=True)):
             cols, ok = nls_records(x, 200000.0, 1000.0, R, nbuf, nd, **kw)
@@ -127,10 +132,20 @@ def test_lm_ladder_bit_identical(restore_ladder, nd):
         _lib.check(lib.dfmi_lm(qi.data_ptr(), nbuf, nd, gd.data_ptr(), 1, nbuf, F.lm_config(), p.data_ptr(),
                                ssq.data_ptr(), stt.data_ptr(), _lib.DFMI_MEM_DEVICE, st), "dfmi_lm")
         out += [a.cpu().numpy() for a in (p, ssq, stt)]
-        res[ladder] = out
-    assert any((res[0][i] != 0).any() for i in (1, 3, 5, 8))  # the m-grid retry path ran (status 1/2)
-    for i, (a, b) in enumerate(zip(res[32], res[0])):
+        res[(ladder, split)] = out
+    one, lad, spl = res[(0, 0)], res[(32, 0)], res[(32, 4)]
+    assert any((one[i] != 0).any() for i in (1, 3, 5, 8))  # the m-grid retry path ran (status 1/2)
+    for i, (a, b) in enumerate(zip(lad, one)):
         np.testing.assert_array_equal(a, b, err_msg=f"output {i}")
+    if nd > 16:  # the wave-split ladder: same statuses, status-0 fits within 1e-7
+        for cols_i, ok_i in ((0, 1), (2, 3), (4, 5)):
+            np.testing.assert_array_equal(spl[ok_i], one[ok_i])
+            good = one[ok_i].reshape(-1) == 0
+            d = np.abs(spl[cols_i].reshape(spl[cols_i].shape[0], -1) - one[cols_i].reshape(one[cols_i].shape[0], -1))
+            assert d[:4, good].max() <= 1e-7, d[:4, good].max()
+        np.testing.assert_array_equal(spl[8], one[8])
+        good = one[8] == 0
+        assert np.abs(spl[6][:, good] - one[6][:, good]).max() <= 1e-7
 
 
 def test_init_m_with_parallel_is_accepted():

@@ -101,6 +101,7 @@ struct Tuning {
   int ekf_pit_first = 5;      // passes enqueued before the host first reads how many channels still pass
                               // (then every ekf_pit_every); config 5's record converges in 5
   int ekf_pit_every = 2;
+  int ekf_pit_topfix = 1;     // the scan's top level (<= 4 elements, above level 1) folded by the fix-up below it
   int ekf_pit_tol = 13;       // stop rule: distance from the fixed point bounded by 10^-ekf_pit_tol (pit_decide)
   int ekf_pit_overlap = 0;    // sequential re-runs of handed-over channels: 0 all in one launch after the passes;
                               // 3 at each host check on the next of kEkfPool high-priority streams beside the
@@ -1132,6 +1133,7 @@ const std::map<std::string, Knob>& knobs() {
       {"ekf_pit_passes", {&Tuning::ekf_pit_passes, {}}},
       {"ekf_pit_first", {&Tuning::ekf_pit_first, {}}},
       {"ekf_pit_every", {&Tuning::ekf_pit_every, {}}},
+      {"ekf_pit_topfix", {&Tuning::ekf_pit_topfix, {0, 1}}},
       {"ekf_pit_tol", {&Tuning::ekf_pit_tol, {}}},
       {"ekf_pit_stall", {&Tuning::ekf_pit_stall, {}}},
       {"ekf_pit_slow_from", {&Tuning::ekf_pit_slow_from, {}}},
@@ -1304,15 +1306,19 @@ int ekf_pit_run(int dev, const double* dx, int64_t nrec, int64_t rs, int64_t n, 
   const dim3 lanes((unsigned)((nb + 63) / 64), nr);
   // scan of one buffer's hierarchy: every level bottom-up, then the fix-ups top-down; the
   // pass kernels read level 0 (prefixes within workgroups) and level 1 (true prefixes)
+  // (ekf_pit_topfix: a top level of at most 4 elements above level 1 is not scanned; the
+  // fix-up of the level below folds its prefix itself, ekf_pit_fixup_top_kernel)
+  const bool topfix = t_tune.ekf_pit_topfix && L >= 2 && lsz[L] <= 4;
   auto scan = [&](std::vector<double*>& a) {
-    for (int l = 0; l <= L; ++l)
+    for (int l = 0; l <= L - (topfix ? 1 : 0); ++l)
       hipLaunchKernelGGL(dfmi::ekf_pit_scan_kernel<dfmi::kPitWg>,
                          dim3((unsigned)((lsz[l] + dfmi::kPitWg - 1) / dfmi::kPitWg), nr), dim3(4 * dfmi::kPitWg), 0,
                          st, a[l], lsz[l], lsz[l], l < L ? a[l + 1] : nullptr, (const dfmi::PitChan*)ch);
     for (int l = L - 1; l >= 1; --l)
       if (lsz[l] > dfmi::kPitWg)
-        hipLaunchKernelGGL(dfmi::ekf_pit_fixup_kernel, dim3((unsigned)((lsz[l] - dfmi::kPitWg + 63) / 64), nr), dim3(64),
-                           0, st, a[l], lsz[l], (const double*)a[l + 1], lsz[l + 1], (const dfmi::PitChan*)ch);
+        hipLaunchKernelGGL(topfix && l == L - 1 ? dfmi::ekf_pit_fixup_top_kernel : dfmi::ekf_pit_fixup_kernel,
+                           dim3((unsigned)((lsz[l] - dfmi::kPitWg + 63) / 64), nr), dim3(64), 0, st, a[l], lsz[l],
+                           (const double*)a[l + 1], lsz[l + 1], (const dfmi::PitChan*)ch);
   };
   const double* tops[2] = {L >= 1 ? lv[0][1] : nullptr, L >= 1 ? lv[1][1] : nullptr};
   const int every = std::max(t_tune.ekf_pit_every, 1);

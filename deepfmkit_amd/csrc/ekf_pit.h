@@ -889,6 +889,48 @@ __global__ __launch_bounds__(64) void ekf_pit_fixup_kernel(double* __restrict__ 
     }
 }
 
+// ekf_pit_fixup_kernel for the level below an UNSCANNED top of at most a few elements
+// (ekf_pit_topfix): block k's elements take the prefix up[0] (x) .. (x) up[k], which lane 0
+// folds left to right into LDS (k <= 3 combines) — the top level's scan launch saved.
+__global__ __launch_bounds__(64) void ekf_pit_fixup_top_kernel(double* __restrict__ el, int64_t n_el,
+                                                               const double* __restrict__ up, int64_t n_up,
+                                                               const PitChan* __restrict__ ch) {
+  const int64_t r = blockIdx.y;
+  if (ch[r].status) return;
+  __shared__ double pref[kPitEl];
+  const int64_t k = blockIdx.x;
+  const double* u = up + r * kPitEl * n_up;
+  if (threadIdx.x == 0) {
+    for (int c = 0; c < kPitEl; ++c) pref[c] = u[c * n_up];
+    for (int64_t i = 1; i <= k; ++i) {
+      double o[kPitEl];
+      pit_combine(PitEl{pref, 1}, PitEl{u + i, n_up}, o);
+#pragma unroll
+      for (int c = 0; c < kPitEl; ++c) pref[c] = o[c];
+    }
+  }
+  __syncthreads();
+  const int64_t g = (k + 1) * kPitWg + threadIdx.x;
+  if (g >= n_el) return;
+  double st[5], P[5][5];
+  double* e = el + r * kPitEl * n_el + g;
+  pit_combine_state(PitEl{pref, 1}, PitEl{e, n_el}, st, P);
+#pragma unroll
+  for (int c = 0; c < 25; ++c) e[(kPitA + c) * n_el] = 0.0;
+#pragma unroll
+  for (int c = 0; c < 5; ++c) {
+    e[(kPitB + c) * n_el] = st[c];
+    e[(kPitE + c) * n_el] = 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+#pragma unroll
+    for (int j = i; j < 5; ++j) {
+      e[(kPitC + pit_sy(i, j)) * n_el] = P[i][j];
+      e[(kPitJ + pit_sy(i, j)) * n_el] = 0.0;
+    }
+}
+
 // The state (x, P) entering block b: (x0, P0) for block 0, else the filtered (mean, cov)
 // after block b-1 = the inclusive prefix: agg[b-1] (scanned within its workgroup) preceded by
 // tot[g-1] (the scanned workgroup totals) when b-1 lies past the first workgroup.

@@ -330,7 +330,9 @@ int dfmi_wdfmi_fit(const double* x, int64_t nrec, int64_t rec_stride, int64_t nb
  * channel keeps its last pass's states instead of the sequential kernel's), "ekf_pit_head"
  * (samples the sequential EKF seeds the trajectory with, default 256), "ekf_pit_fused" (1
  * [default]: the EKF and the next pass's fold in one kernel per pass; 0: separate kernels),
- * "ekf_pit_slow_from" (pass from which the rule's "too slow to meet the bound within the
+ * "ekf_pit_topfix" (1 [default]: a scan top level of at most 4 elements is folded by the
+ * fix-up below it instead of its own launch; rounding only), "ekf_pit_slow_from" (pass from
+ * which the rule's "too slow to meet the bound within the
  * cap" extrapolation counts, default 16), "ekf_pit_overlap" (where the sequential re-runs of
  * handed-over channels go: 0 [default] one launch after the passes on the caller's stream; 3 /
  * 2 / 1 at each host check on a pool of three / one high- / one default-priority stream beside

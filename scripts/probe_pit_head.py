@@ -2,7 +2,8 @@
 head length (ekf_pit_head: the samples the sequential EKF runs before the first trajectory is
 formed) and block size: call time (HIP events, median of REPS), passes, and the largest state
 difference from the default's states. One JSON line per setting.
-env: HEADS ("256,128,64,32"), BLOCKS ("0": the default rule), REPS (20)."""
+env: HEADS ("256,128,64,32"), BLOCKS ("0": the default rule), REPS (20), TUNE ("k=v,...": other
+tuning keys for the whole run)."""
 import ctypes
 import json
 import os
@@ -31,6 +32,9 @@ def main():
     st = torch.cuda.current_stream()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     reps = int(os.environ.get("REPS", 20))
+    for kv in filter(None, os.environ.get("TUNE", "").split(",")):  # e.g. ekf_pit_topfix=0
+        k, v = kv.split("=")
+        _lib.check(lib.dfmi_set_tuning(k.encode(), int(v)), k)
 
     def run(head, block):
         out = torch.empty((1, nb5, 5), dtype=torch.float64, device=dev)
@@ -61,7 +65,8 @@ def main():
     for block in [int(v) for v in os.environ.get("BLOCKS", "0").split(",")]:
         for head in [int(v) for v in os.environ.get("HEADS", "256,128,64,32").split(",")]:
             ms, passes, kn, out = run(head, block)
-            print(json.dumps({"head": head, "block": block, "ms": round(ms, 4), "passes": passes, "kernel": kn,
+            print(json.dumps({"head": head, "block": block, "tune": os.environ.get("TUNE", ""), "ms": round(ms, 4),
+                              "passes": passes, "kernel": kn,
                               "max_abs_dstate_vs_default": float((out - ref).abs().max().item())}), flush=True)
 
 

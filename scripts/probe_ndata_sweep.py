@@ -95,6 +95,10 @@ def main():
         demod_kernel = lib.dfmi_last_demod_kernel().decode()
         demod_cm()
         lm_ms = timed(lm, 60)
+        import hashlib  # bit-identity across tuning variants: digests of the step's and the LM's outputs
+        out_sha = hashlib.sha256(out.cpu().numpy().tobytes() + ok.cpu().numpy().tobytes()).hexdigest()[:16]
+        lm_sha = hashlib.sha256(lo.cpu().numpy().tobytes() + ls.cpu().numpy().tobytes()
+                                + lk.cpu().numpy().tobytes()).hexdigest()[:16]
         bytes_seg = 8 * R + 8 * (2 * nd + 1)
         print(json.dumps({
             "ndata": nd, "m": m_true, "segments": nseg, "R": R, "tune": tune,
@@ -102,7 +106,7 @@ def main():
             "step_demod_kernel": step_kernel, "demod_layout": layout, "demod_ms": round(demod_ms, 4), "demod_kernel": demod_kernel,
             "demod_hbm_frac": round(nseg * bytes_seg / (demod_ms * 1e-3) / 8e12, 4),
             "lm_ms": round(lm_ms, 4), "end_to_end_frac": round(nseg * (8 * R + 56) / (step_ms * 1e-3) / 8e12, 4),
-            "status0_frac": float(np.mean(st == 0)), "mean_m": float(np.mean(m[st == 0]))}), flush=True)
+            "status0_frac": float(np.mean(st == 0)), "mean_m": float(np.mean(m[st == 0])), "out_sha16": out_sha, "lm_sha16": lm_sha}), flush=True)
         del rows, qi, dcb, lo, ls, lk
 
 

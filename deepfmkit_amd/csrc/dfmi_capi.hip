@@ -69,8 +69,6 @@ struct Tuning {
   int lm_wide_lds = 20;         // many-harmonic LM: QI staged in LDS per lane up to this ndata (0: never): while 8
                                 // waves per CU still fit (20 KB per wave); ndata 20 0.076 vs 0.088 ms per 100k
                                 // segments, but 30 / 40 0.151 / 0.179 vs 0.118 / 0.149 at 5 / 3 waves per CU (r06g)
-  int lm_wide_part = 0;         // many-harmonic LM beyond lm_wide_lds: the QI of the lowest 20 harmonics staged in
-                                // LDS (lm.h QHyb, 20 KB per wave: 8 waves per CU), the rest from global; 0: none
   int lm_split = 0;             // many-harmonic LM with this many lanes per segment (2 / 4; 0 = one lane): measured
   int lm_split_from = 41;       // slower everywhere (ndata 30 / 62: 0.195 / 0.432 ms at 2 lanes, 0.260 / 0.420 at 4,
                                 // against 0.118 / 0.215 for one lane; r06g), kept for A/B
@@ -877,13 +875,6 @@ int lm_device(int dev, const double* qi, int64_t qi_ld, int ndata, int64_t nrec,
     kern = dfmi::lm_chunks_kernel<dfmi::kWideNd, false, false, true>;
     lds = (size_t)2 * ndata * 64 * sizeof(double);
   }
-  // beyond it, the lowest kWideStageH harmonics' QI staged in LDS, the rest read from global
-  else if (!chain && !rows && nd_sel > dfmi::kWideStageH && nd_sel < 1000 && t_tune.lm_wide && t_tune.lm_wide_part &&
-           (size_t)2 * dfmi::kWideStageH * 64 * sizeof(double) <= t_ds->lds_per_block) {
-    kern = t_tune.lm_wide_fused ? dfmi::lm_chunks_kernel<dfmi::kWideNdF, false, false, true, false, true>
-                                : dfmi::lm_chunks_kernel<dfmi::kWideNd, false, false, true, false, true>;
-    lds = (size_t)2 * dfmi::kWideStageH * 64 * sizeof(double);
-  }
   if (!chain && !rows && nd_sel > 16 && !(t_tune.lm_wide && nd_sel < 1000) && t_tune.lm_onepass &&
       (t_tune.lm_onepass == 2 || (size_t)64 * (ndata + 2) * 8 * 7 <= t_ds->lds_per_block)) {
     kern = dfmi::lm_chunks_kernel<0, false, false, false, true>;
@@ -1125,7 +1116,6 @@ const std::map<std::string, Knob>& knobs() {
       {"lm_wide", {&Tuning::lm_wide, {0, 1}}},
       {"lm_wide_lds", {&Tuning::lm_wide_lds, {}}},
       {"lm_wide_fused", {&Tuning::lm_wide_fused, {0, 1}}},
-      {"lm_wide_part", {&Tuning::lm_wide_part, {0, 1}}},
       {"seed_wave_split", {&Tuning::seed_wave_split, {0, 1}}},
       {"lm_ladder_split", {&Tuning::lm_ladder_split, {}}},
       {"lm_split", {&Tuning::lm_split, {0, 2, 4}}},

@@ -930,24 +930,6 @@ struct QLds {
   DFMI_HDI double qs(int h) const { return p[(nd + h) * 64]; }
 };
 
-// Beyond kWideStageH harmonics (tuning "lm_wide_part"): the lane's QI of harmonics h <
-// kWideStageH staged in LDS as by QLds (2 kWideStageH x 64 doubles = 20 KB per wave, so the 8
-// waves per CU of the two-per-SIMD allocation still fit), the higher harmonics read from
-// global memory as by QCol. The walk's h is uniform across the wave: a scalar branch per value.
-constexpr int kWideStageH = 20;
-struct QHyb {
-  static constexpr int kPre = 0;
-  const double* p;  // the lane's LDS column: [h * 64] cos, [(kWideStageH + h) * 64] sin
-  const double* __restrict__ base;
-  uint32_t off;
-  int64_t ld;
-  int nd;
-  DFMI_HDI double qc(int h) const { return h < kWideStageH ? p[h * 64] : (base + (int64_t)h * ld)[off]; }
-  DFMI_HDI double qs(int h) const {
-    return h < kWideStageH ? p[(kWideStageH + h) * 64] : (base + (int64_t)(nd + h) * ld)[off];
-  }
-};
-
 // Harmonics j = nd .. 1 in descending order: body(j, J_{j-1}, J_j, J_{j+1}, cos j psi, sin j psi,
 // Q_j, I_j). (c1, s1) = (cos, sin) psi, (cn, sn) = (cos, sin)(nd psi).
 template <typename QF, typename Body>
@@ -1966,8 +1948,7 @@ constexpr int lm_waves() {
 // ONEPASS (general path, chunk size 1, component-major): each lane keeps its Bessel recurrence
 // values in dynamic LDS (64 x (ndata + 2) doubles per wave) and walks once per evaluation
 // (harmonic_walk_q); same bits.
-// PART (with QREG, many harmonics, ndata > kWideStageH): the QHyb split of the lane's QI.
-template <int NDMAX, bool CHAIN, bool ROWS = false, bool QREG = false, bool ONEPASS = false, bool PART = false>
+template <int NDMAX, bool CHAIN, bool ROWS = false, bool QREG = false, bool ONEPASS = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(lm_waves<NDMAX, CHAIN, ONEPASS>()))) void lm_chunks_kernel(
     const double* __restrict__ qi, int64_t qi_ld, int ndata, int64_t nrec, int64_t nbuf, int64_t first,
     int64_t nitems, int64_t nchunk, const double* __restrict__ guess, int64_t g_rec, int64_t g_comp,
@@ -2074,27 +2055,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(lm_waves<NDM
     auto one = [&](int64_t sidx) {
       double ssq;
       int st;
-      if constexpr (wide_nd(NDMAX) && QREG && PART && !CHAIN) {
-        // harmonics below kWideStageH into the lane's LDS column (cos then sin), 16 loads in
-        // flight; the rest stay in global memory (QHyb)
-        double* col = lds_q + threadIdx.x;
-        const double* __restrict__ src = qi + sidx;
-        constexpr int S = kWideStageH;
-#pragma unroll
-        for (int c0 = 0; c0 < 2 * S; c0 += 16) {
-          double v[16];
-#pragma unroll
-          for (int u = 0; u < 16; ++u) {
-            const int cc = c0 + u;
-            v[u] = cc < 2 * S ? src[(int64_t)(cc < S ? cc : ndata + cc - S) * qi_ld] : 0.0;
-          }
-#pragma unroll
-          for (int u = 0; u < 16; ++u)
-            if (c0 + u < 2 * S) col[(c0 + u) * 64] = v[u];
-        }
-        const QHyb qh{col, qi, (uint32_t)sidx, qi_ld, ndata};
-        st = fit_segment_q<NDMAX, QHyb, 1>(qh, ndata, jtab, c, p, ssq);
-      } else if constexpr (wide_nd(NDMAX) && QREG && !CHAIN) {
+      if constexpr (wide_nd(NDMAX) && QREG && !CHAIN) {
         // the lane's 2 ndata QI into its own LDS column (no other lane reads it: no barrier),
         // 16 loads in flight
         double* col = lds_q + threadIdx.x;
